@@ -1,0 +1,50 @@
+"""Oracle-side episode / single-search drivers producing the fixture record format.
+
+TEST INFRASTRUCTURE (see ``oracle/__init__.py``).
+"""
+from oracle.driving import DrivingModel
+from oracle.episode import belief_digest, fhex, run_episode
+from oracle.pomcp import OracleConfig, OraclePOMCP
+from oracle.rng import Streams
+
+
+def oracle_record(p: OraclePOMCP, searched, action):
+    rec = {"searched": searched, "action": int(action)}
+    if not searched:
+        return rec
+    st = p.stats
+    parts = st["belief"]
+    rec["belief_size"] = len(parts)
+    rec["belief_digest"] = belief_digest(parts)
+    rec["num_sims"] = int(st.get("num_sims", 0))
+    if rec["num_sims"] > 0:
+        rec["search_depth"] = st["search_depth"]
+        rec["root_visits"] = st["root_visits"]
+        rec["child_visits"] = list(st["child_visits"])
+        rec["child_values"] = [fhex(v) for v in st["child_values"]]
+        rec["child_totals"] = [fhex(v) for v in st["child_totals"]]
+        rec["min_value"] = fhex(st["min_value"])
+        rec["max_value"] = fhex(st["max_value"])
+    return rec
+
+
+def make_oracle(cfg_kwargs, num_sims, ego="0", grid="14x14RoundAbout", tree=0):
+    streams = Streams(cfg_kwargs.get("seed") or 0, tree)
+    model = DrivingModel(streams, grid=grid)
+    cfg = OracleConfig(num_sims=num_sims, **cfg_kwargs)
+    return OraclePOMCP(model, ego, cfg, streams)
+
+
+def oracle_episode(cfg_kwargs, num_sims, env_seed, ego="0", grid="14x14RoundAbout", tree=0,
+                   max_steps=50):
+    p = make_oracle(cfg_kwargs, num_sims, ego=ego, grid=grid, tree=tree)
+    records = []
+
+    def step(obs):
+        searched = not p.on_abs[p.root]
+        a = p.step(obs)
+        records.append(oracle_record(p, searched, a))
+        return a
+
+    trace = run_episode(step, env_seed, ego=ego, grid=grid, max_steps=max_steps)
+    return trace, records

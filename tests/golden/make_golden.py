@@ -1,0 +1,94 @@
+"""Generate the golden fixtures under tests/golden/ (container-only).
+
+Runs the REAL reference planner (``oracle/ref_harness.py``: stub-imported
+``posggym_baselines.planning``, injected RNG streams, fake clock) on the build's
+Driving-v1 restatement and writes its per-step records.  Every case is also
+run through the oracle restatement (``oracle/pomcp.py``) and the script aborts
+if the two disagree anywhere, so the committed fixtures pin the oracle.
+
+Usage:  python tests/golden/make_golden.py
+"""
+import json
+import math
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+from oracle.ref_harness import import_reference, reference_available, reference_episode  # noqa: E402
+from oracle.run import oracle_episode  # noqa: E402
+
+SQRT2 = math.sqrt(2)
+# tests/planning/test_pomcp.py:38-50 (config 1 of BASELINE.json)
+TEST_CFG = dict(discount=0.95, search_time_limit=0.1, c=SQRT2, truncated=False,
+                action_selection="ucb", pucb_exploration_fraction=0.25, known_bounds=None,
+                step_limit=None, epsilon=0.92, seed=0, state_belief_only=True)
+
+CASES = {
+    # name: (cfg overrides, num_sims, [(planner seed, env seed)], ego, max_steps)
+    "c1_ucb": ({}, 128, [(0, 0), (1, 1), (2, 2)], "0", 50),
+    "c1_pucb": ({"action_selection": "pucb"}, 128, [(0, 3), (4, 4)], "0", 50),
+    "uniform": ({"action_selection": "uniform"}, 64, [(5, 5)], "0", 50),
+    "deep_ucb": ({"discount": 0.99, "epsilon": 0.01}, 48, [(6, 2)], "0", 50),
+    "known_bounds": ({"known_bounds": (-1.0, 1.0)}, 96, [(7, 7)], "0", 50),
+    "ego1_ucb": ({}, 96, [(8, 8)], "1", 50),
+    "large_first_step": ({}, 2048, [(9, 9), (10, 10)], "0", 1),
+}
+
+
+def run_case(name):
+    over, num_sims, pairs, ego, max_steps = CASES[name]
+    out = {"case": name, "num_sims": num_sims, "ego": ego, "episodes": []}
+    for seed, env_seed in pairs:
+        cfg = dict(TEST_CFG)
+        cfg.update(over)
+        cfg["seed"] = seed
+        tr, rr = reference_episode(cfg, num_sims, env_seed, ego=ego, max_steps=max_steps)
+        to, ro = oracle_episode(cfg, num_sims, env_seed, ego=ego, max_steps=max_steps)
+        if tr != to or rr != ro:
+            raise SystemExit(f"oracle disagrees with reference in case {name} seed {seed}")
+        cfg_json = dict(cfg)
+        if cfg_json["known_bounds"] is not None:
+            cfg_json["known_bounds"] = list(cfg_json["known_bounds"])
+        out["episodes"].append({"config": cfg_json, "env_seed": env_seed,
+                                "trace": tr, "records": rr})
+    return out
+
+
+def config_kats():
+    """MCTSConfig derived fields (config.py:461-469) from the reference itself."""
+    P = import_reference()
+    rows = []
+    for T in (0.1, 0.5, 1.0, 5.0, 20.0):
+        for g, eps in ((0.95, 0.92), (0.99, 0.01), (0.9, 0.5), (0.0, 0.5), (1.0, 0.3)):
+            for prop in (1.0 / 16, 0.0, 0.5):
+                row = {"search_time_limit": T, "discount": g, "epsilon": eps,
+                       "extra_particles_prop": prop}
+                try:
+                    c = P.MCTSConfig(discount=g, search_time_limit=T, c=1.0, truncated=False,
+                                     epsilon=eps, extra_particles_prop=prop)
+                    row.update(num_particles=c.num_particles, extra_particles=c.extra_particles,
+                               depth_limit=c.depth_limit)
+                except Exception as ex:  # e.g. discount == 1.0 -> log(1) == 0
+                    row["raises"] = type(ex).__name__
+                rows.append(row)
+    return rows
+
+
+def main():
+    if not reference_available():
+        raise SystemExit("reference not available (container-only script)")
+    for name in CASES:
+        data = run_case(name)
+        with open(os.path.join(HERE, f"{name}.json"), "w") as f:
+            json.dump(data, f, separators=(",", ":"))
+        n = sum(len(e["records"]) for e in data["episodes"])
+        print(f"{name}: {len(data['episodes'])} episodes, {n} records")
+    with open(os.path.join(HERE, "config_kats.json"), "w") as f:
+        json.dump(config_kats(), f, separators=(",", ":"))
+    print("config_kats written")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,70 @@
+"""Oracle pinning: the CPU restatement against the reference's golden vectors."""
+import pytest
+
+from golden_util import EPISODE_CASES, cfg_kwargs, load
+from oracle.pomcp import OracleConfig
+from oracle.rng import Streams, StreamRandom, philox4x32_10
+from oracle.run import oracle_episode
+
+
+def test_philox_known_answers():
+    # Random123 kat_vectors for philox4x32_10
+    assert philox4x32_10(0, 0, 0, 0, 0, 0) == (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)
+    m = 0xFFFFFFFF
+    assert philox4x32_10(m, m, m, m, m, m) == (0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD)
+    assert philox4x32_10(0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344,
+                         0xA4093822, 0x299F31D0) == (0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1)
+
+
+def test_stream_layout():
+    s = Streams(5, 3)
+    words = [s.u32(1) for _ in range(6)]
+    b0 = philox4x32_10(0, 0, 1, 0, 5, 3)
+    b1 = philox4x32_10(1, 0, 1, 0, 5, 3)
+    assert words == list(b0) + list(b1[:2])
+    assert s.counters() == {1: 6}
+    # randint is a multiply-shift of one word
+    s2 = Streams(5, 3)
+    assert [s2.randint(1, 7) for _ in range(6)] == [(w * 7) >> 32 for w in words]
+
+
+def test_stream_random_choices_matches_cpython_arithmetic():
+    """random.choices: cum_weights via accumulate, bisect(cum, random()*total, 0, n-1)."""
+    import bisect
+    import itertools
+
+    w = [0.2] * 5
+    cum = list(itertools.accumulate(w))
+    sr = StreamRandom(Streams(1, 2), 1)
+    ref = Streams(1, 2)
+    for _ in range(200):
+        got = sr.choices(list(range(5)), weights=w, k=1)[0]
+        exp = bisect.bisect(cum, ref.random(1) * (cum[-1] + 0.0), 0, 4)
+        assert got == exp
+
+
+def test_config_kats():
+    for row in load("config_kats"):
+        kw = dict(discount=row["discount"], search_time_limit=row["search_time_limit"], c=1.0,
+                  epsilon=row["epsilon"], extra_particles_prop=row["extra_particles_prop"])
+        if "raises" in row:
+            with pytest.raises(ZeroDivisionError):
+                OracleConfig(num_sims=1, **kw)
+            continue
+        c = OracleConfig(num_sims=1, **kw)
+        assert (c.num_particles, c.extra_particles, c.depth_limit) == (
+            row["num_particles"], row["extra_particles"], row["depth_limit"])
+
+
+@pytest.mark.parametrize("case", EPISODE_CASES)
+def test_oracle_matches_reference_goldens(case):
+    data = load(case)
+    for ep in data["episodes"]:
+        kw = cfg_kwargs(ep["config"])
+        max_steps = 1 if case == "large_first_step" else 50
+        trace, records = oracle_episode(kw, data["num_sims"], ep["env_seed"], ego=data["ego"],
+                                        max_steps=max_steps)
+        assert trace == ep["trace"]
+        assert len(records) == len(ep["records"])
+        for t, (got, exp) in enumerate(zip(records, ep["records"])):
+            assert got == exp, f"{case} step {t}"
