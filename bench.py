@@ -1,0 +1,209 @@
+"""POMCP simulation throughput on MI355X (BASELINE.json metric).
+
+One step = one exact-mode POMCP search (``get_action``, mcts.py:269-306) of
+``--sims`` simulations on each of ``--trees`` synthetic Driving-v1 roots
+(tree b's root is the ego's belief after the initial update for
+an environment sampled under seed 1000 + b), followed by the root-parallel
+exchange: one all-reduce (RCCL over xGMI) of every tree's (visit count, total
+value) per root action and the merged action choice.  Ranks search the same
+roots with different RNG keys (seed ^ rank << 32); per-GPU work is fixed as N
+grows (weak scaling).  Inputs are resident in HBM before timing starts; each
+timed step restores the post-update root state (a few KB per tree) and
+re-searches it.
+
+    python bench.py [--gpus N --steps K --warmup W --trees B --sims S]
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "posggym-baselines_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+# algorithmic HBM bytes (DESIGN.md "Algorithmic bytes"): per simulation, per
+# tree level stepped, per leaf expansion, per obs node created
+B_SIM, B_LEVEL, B_EXPAND, B_NEW_NODE = 16, 168, 144, 28
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--trees", type=int, default=4096)
+    ap.add_argument("--sims", type=int, default=65536)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-sims", type=int, default=4096)
+    ap.add_argument("--cpu-sample-trees", type=int, default=3)
+    return ap.parse_args()
+
+
+TEST_CFG = dict(discount=0.95, search_time_limit=0.1, c=math.sqrt(2), truncated=False,
+                action_selection="ucb", pucb_exploration_fraction=0.25, known_bounds=None,
+                step_limit=None, epsilon=0.92, state_belief_only=True)
+
+
+class _DevArray:
+    """__cuda_array_interface__ view of a device pointer owned by the engine."""
+
+    def __init__(self, ptr, n):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<f8", "data": (ptr, False),
+                                         "version": 3}
+
+
+def cpu_baseline(sims, trees, seed):
+    """The oracle (pure-Python restatement of the reference planner, pinned to it by
+    tests/golden) timed on one host core over a bounded sample of the same workload."""
+    from oracle.episode import run_episode
+    from oracle.run import make_oracle
+    cfg = dict(TEST_CFG, seed=seed)
+    t_search = 0.0
+    for b in range(trees):
+        p = make_oracle(cfg, sims, tree=b)
+
+        def step(obs, p=p):
+            nonlocal t_search
+            p.update(None, obs)
+            t0 = time.perf_counter()
+            a = p.get_action()
+            t_search += time.perf_counter() - t0
+            return a
+
+        run_episode(step, 1000 + b, max_steps=1)
+    return {"value": sims * trees / t_search, "unit": "simulations/s", "cores": 1, "kind": "port",
+            "sample": f"{trees} roots x {sims} sims (get_action only), oracle/pomcp.py, 1 thread"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+
+    from posggym_baselines_amd import build as nb
+    if rank == 0:
+        nb.build()
+    if world > 1:
+        dist.barrier()
+    from posggym_baselines_amd.envs import DrivingModel
+    from posggym_baselines_amd.planning import BatchedPOMCP, MCTSConfig
+    from posggym_baselines_amd.planning.engine import plan_capacities
+
+    B, S = args.trees, args.sims
+    cfg = MCTSConfig(seed=args.seed, num_sims=S, **TEST_CFG)
+    model = DrivingModel()
+    caps = plan_capacities(cfg, model.spec.max_episode_steps, S, 1, reroot=False,
+                           max_blocks=min(S + 64, 16384), max_obs_nodes=min(S + 64, 65536 + 64))
+    stream = torch.cuda.Stream(device=dev)
+    bp = BatchedPOMCP(model, "0", cfg, B, S, capacities=caps, stream=stream.cuda_stream,
+                      device=dev)
+    bp.init_synthetic(1000)
+    bp.engine.rekey(args.seed ^ (rank << 32))
+    A = bp.engine.A
+    merge = torch.as_tensor(_DevArray(bp.engine.merge_buffer_ptr(), B * A * 2), device=f"cuda:{dev}")
+
+    def step(events=None):
+        with torch.cuda.stream(stream):
+            bp.restore()
+            if events is not None:
+                events[0].record(stream)
+            bp.search(fetch=False)
+            if events is not None:
+                events[1].record(stream)
+            m = merge.view(B, A, 2)
+            if world > 1:
+                dist.all_reduce(merge)
+            vis, tot = m[..., 0], m[..., 1]
+            val = torch.where(vis > 0, tot / vis.clamp_min(1), torch.full_like(tot, -math.inf))
+            return torch.argmax(val, dim=-1)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    st = bp.engine.root_stats()   # raises on any per-tree error (arena overflow, ...)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(ev[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    if world > 1:
+        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=f"cuda:{dev}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kernel_ms = float(t[0]), float(t[1])
+    st = bp.engine.root_stats()
+    sims = sum(s.num_sims for s in st)
+    levels = sum(s.n_levels for s in st)
+    expands = sum(s.n_expansions for s in st)
+    new_nodes = sum(s.n_new_nodes for s in st)
+    alg_bytes = B_SIM * sims + B_LEVEL * levels + B_EXPAND * expands + B_NEW_NODE * new_nodes
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    total_sims = world * B * S * args.steps
+    value = total_sims / elapsed
+    traffic = None
+    prof = os.path.join(ROOT, "profiles", "pmc_search.json")
+    if os.path.exists(prof):
+        try:
+            pm = json.load(open(prof))
+            if pm.get("trees") == B and pm.get("sims") == S:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    out = {
+        "metric": "MCTS simulations/sec on Driving-v1 (POMCP exact search)",
+        "value": value,
+        "unit": "simulations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic Driving-v1 belief states (env seed 1000+b), build's Driving-v1 restatement",
+        "config": {"workload": f"POMCP Driving-v1 14x14RoundAbout exact search, {B} roots x {S} "
+                               f"sims per GPU, ucb c=sqrt2 gamma=0.95 depth_limit=2, root-parallel "
+                               f"all-reduce over {world} GPU(s)",
+                   "trees_per_gpu": B, "sims_per_tree": S, "depth_limit": cfg.depth_limit,
+                   "parallelism": f"root-parallel x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "k_search", "kernel_ms": kernel_ms,
+                     "alg_bytes_per_launch": alg_bytes},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_sample_sims, args.cpu_sample_trees, args.seed)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    bp.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

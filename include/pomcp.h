@@ -1,0 +1,183 @@
+/* pomcp.h — C ABI of the MI355X-native POMCP engine (libpomcp_hip.so).
+ *
+ * Drop-in boundary for the hot path of posggym_baselines.planning
+ * (SURVEY §8(b)).  Plain pointers and sizes only; no torch types.  Every entry
+ * point replaces a piece of the reference planner, cited per function below
+ * (paths relative to posggym_baselines/planning/ in the reference).
+ *
+ * Threading: a context is not thread-safe (the reference planner objects are
+ * single-threaded).  Host buffers are copied synchronously unless noted.
+ * Return codes: POMCP_OK (0) or a negative pomcp_status; pomcp_last_error()
+ * gives the message.
+ */
+#ifndef POMCP_H_
+#define POMCP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define POMCP_ABI_VERSION 1
+#define POMCP_MAX_ACTIONS 8
+
+typedef enum pomcp_status {
+  POMCP_OK = 0,
+  POMCP_E_INVALID = -1,      /* bad argument / config (MCTSConfig.__post_init__ asserts) */
+  POMCP_E_HIP = -2,          /* HIP runtime error */
+  POMCP_E_ARENA = -3,        /* per-tree arena capacity exceeded */
+  POMCP_E_STATE = -4,        /* call out of order (e.g. search before update) */
+  POMCP_E_UNSUPPORTED = -5,  /* model / option not implemented on the GPU */
+  POMCP_E_NOT_FOUND = -6,    /* node.py:58-63 AssertionError: root has no child for action */
+  POMCP_E_NO_DEVICE = -7
+} pomcp_status;
+
+typedef enum pomcp_selection {
+  POMCP_SEL_PUCB = 0,     /* mcts.py:492-527 + max_visit final (565-581) */
+  POMCP_SEL_UCB = 1,      /* mcts.py:529-546 + max_value final (583-600) */
+  POMCP_SEL_UNIFORM = 2   /* mcts.py:548-563 + max_value final */
+} pomcp_selection;
+
+typedef enum pomcp_env { POMCP_ENV_DRIVING = 1 } pomcp_env;
+
+/* Driving-v1 grid tables (16-wide row stride). */
+typedef struct pomcp_grid {
+  uint8_t wall[256];
+  uint8_t dist[8][256];
+  uint8_t loc_x[8], loc_y[8], loc_dir[8];
+  int32_t width, height, num_locs;
+  int32_t obs_front, obs_back, obs_side;
+  int32_t pad[2];
+} pomcp_grid;
+
+/* MCTSConfig (config.py:8-55) after __post_init__, plus engine sizing. */
+typedef struct pomcp_config {
+  int32_t abi_version;          /* = POMCP_ABI_VERSION */
+  int32_t env_id;               /* pomcp_env */
+  int32_t num_agents;           /* model.possible_agents (2) */
+  int32_t ego_agent;            /* index of agent_id in possible_agents */
+  int32_t num_actions;          /* model.action_spaces[agent_id].n */
+  int32_t action_selection;     /* pomcp_selection */
+  int32_t depth_limit;          /* config.py:464-469 */
+  int32_t step_limit;           /* mcts.py:53-58; INT32_MAX = unbounded */
+  int32_t num_particles;        /* config.py:461 */
+  int32_t extra_particles;      /* config.py:462 */
+  int32_t has_known_bounds;
+  int32_t num_trees;            /* independent planners (batched roots) */
+  double discount;
+  double c;
+  double pucb_exploration_fraction;
+  double reinvigoration_sample_limit_factor;
+  double known_min, known_max;
+  uint64_t seed;                /* MCTSConfig.seed -> stream key (seed, tree) */
+  uint32_t tree_key_base;       /* tree t uses key tree_key_base + t */
+  int32_t pad0;
+  /* per-tree arena capacities */
+  int64_t max_obs_nodes;
+  int64_t max_blocks;           /* expanded obs nodes (A action nodes each) */
+  int64_t max_particles;        /* particle log records */
+  int64_t max_belief;           /* root belief records */
+  int64_t hash_slots;           /* power of two, multiple of 16 */
+  /* host-computed FP64 tables (Python's own math.log / float.__pow__) */
+  const double* log_table;      /* log_table[n] = math.log(n), n >= 1 */
+  int64_t log_table_size;
+  const double* discount_pow;   /* discount ** k */
+  int64_t discount_pow_size;
+  pomcp_grid grid;
+} pomcp_config;
+
+/* Per-tree result of the last search (MCTS.step_statistics + root children). */
+typedef struct pomcp_root_stats {
+  int32_t action;               /* _final_action_selection(root) */
+  int32_t num_sims;
+  int32_t search_depth;
+  int32_t root_visits;
+  int32_t root_absorbing;
+  int32_t belief_size;
+  int32_t error;                /* pomcp_status of this tree */
+  int32_t num_children;
+  int32_t child_visits[POMCP_MAX_ACTIONS];
+  double child_values[POMCP_MAX_ACTIONS];
+  double child_totals[POMCP_MAX_ACTIONS];
+  double min_value, max_value;  /* MinMaxStats (utils.py:15-42) */
+  /* work counters (algorithmic-byte accounting) */
+  int64_t n_levels;             /* tree levels stepped (mcts.py:330-381) */
+  int64_t n_expansions;         /* leaf expansions (mcts.py:318-321) */
+  int64_t n_new_nodes;          /* obs nodes created (mcts.py:369) */
+  int64_t n_rollout_steps;      /* model steps in _rollout (mcts.py:414-450) */
+  int64_t n_probes;             /* obs-child hash bucket probes */
+  int32_t n_obs_nodes, n_blocks, n_log, pad;
+} pomcp_root_stats;
+
+typedef struct pomcp_ctx pomcp_ctx;
+
+/* Library / ABI identity. */
+int32_t pomcp_abi_version(void);
+
+/* MCTS.__init__ (mcts.py:29-91): allocate all per-tree device state.
+ * `hip_stream` is a hipStream_t (NULL = the library's own stream). */
+int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomcp_ctx** out);
+void pomcp_destroy(pomcp_ctx* ctx);
+const char* pomcp_last_error(const pomcp_ctx* ctx);
+int pomcp_set_stream(pomcp_ctx* ctx, void* hip_stream);
+
+/* MCTS.reset (mcts.py:123-138) for every tree: fresh root, t=0; RNG
+ * counters persist (the reference's generators are not reseeded). */
+int pomcp_reset(pomcp_ctx* ctx);
+
+/* MCTS.update (mcts.py:159-263) for every tree: at t == 0 the initial
+ * belief (_initial_update, mcts.py:175-227), else re-root to child
+ * (action, obs) and reinvigorate (mcts.py:651-700, belief.py:145-194).
+ * obs_keys: packed ego observations (driving.h).  root_absorbing_out may be NULL. */
+int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_keys,
+                 int32_t* root_absorbing_out);
+
+/* MCTS.get_action (mcts.py:269-306) for every tree with exactly num_sims
+ * simulations each (the time-bounded loop of mcts.py:285 becomes a count).
+ * actions_out (host, [num_trees]) may be NULL: results stay on device. */
+int pomcp_search(pomcp_ctx* ctx, int32_t num_sims, int32_t* actions_out);
+
+/* Copy every tree's pomcp_root_stats of the last search to host. */
+int pomcp_get_root_stats(pomcp_ctx* ctx, pomcp_root_stats* out);
+
+/* Root belief particles of one tree as (t, v0, v1) u32 triples (belief.py:47-64). */
+int pomcp_get_root_belief(pomcp_ctx* ctx, int32_t tree, uint32_t* out, int32_t capacity,
+                          int32_t* count);
+
+/* Root-parallel search: re-key every tree's streams to `seed`
+ * keeping counters (rank g uses seed ^ (g << 32)). */
+int pomcp_rekey(pomcp_ctx* ctx, uint64_t seed);
+
+/* Device pointer of the merge buffer written by pomcp_search:
+ * double[num_trees][num_actions][2] = (child visits, child total value),
+ * the operand of the RCCL all-reduce at action-selection time. */
+int pomcp_root_merge_buffer(pomcp_ctx* ctx, void** device_ptr);
+
+/* Bench / batch helpers: synthetic Driving-v1 roots.  Tree b samples s0 from
+ * the model's b0 under env key (env_seed_base + b, 0x40000000) and the ego's
+ * initial obs is written to obs_keys_out (host, [num_trees], may be NULL). */
+int pomcp_synthetic_obs(pomcp_ctx* ctx, uint64_t env_seed_base, uint64_t* obs_keys_out);
+/* Save / restore the complete post-update root state (headers, root nodes,
+ * root belief, RNG counters) so a timed loop can re-search the same roots. */
+int pomcp_snapshot(pomcp_ctx* ctx);
+int pomcp_restore(pomcp_ctx* ctx);
+
+/* ---- Host (CPU) Driving-v1 model from the same header (driving.h) -------
+ * The environment side of the episode loop (env.step in
+ * tests/planning/test_pomcp.py:23-29); not on the planner's hot path. */
+int pomcp_driving_sample_initial_state(const pomcp_grid* g, uint64_t seed, uint32_t tree,
+                                       uint32_t* model_ctr, uint32_t state_out[2]);
+/* One joint step; draws the execution-order shuffle from the model stream
+ * (seed, tree) at counter *model_ctr (advanced). */
+int pomcp_driving_step(const pomcp_grid* g, uint64_t seed, uint32_t tree, uint32_t* model_ctr,
+                       const uint32_t state[2], const int32_t actions[2], uint32_t next_out[2],
+                       double rewards_out[2], int32_t terminated_out[2],
+                       uint64_t obs_keys_out[2]);
+int pomcp_driving_obs(const pomcp_grid* g, const uint32_t state[2], uint64_t obs_keys_out[2]);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* POMCP_H_ */

@@ -1,0 +1,14 @@
+/* pomcp_debug.h — diagnostics of libpomcp_hip.so (not part of the drop-in ABI). */
+#ifndef POMCP_DEBUG_H_
+#define POMCP_DEBUG_H_
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* out[4*i + k] = {sqrt(a), a / b, a + 0.95 * b, (a - b) / (a + b)} computed on
+ * device 0 in FP64 (checks the device FP64 path is correctly rounded). */
+int pomcp_debug_fp_selftest(const double* a, const double* b, int32_t n, double* out);
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,502 @@
+// C-ABI host side of libpomcp_hip.so (include/pomcp.h).
+//
+// Owns every device allocation of a planner batch, validates the
+// MCTSConfig-derived parameters (config.py:447-469 asserts) and launches the
+// kernels of pomcp_kernels.hip on one HIP stream.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+// Single translation unit: the kernels are compiled together with their launchers.
+#include "pomcp_kernels.hip"
+#include "../../include/pomcp_debug.h"
+
+using namespace pb;
+
+static_assert(sizeof(pomcp_grid) == sizeof(DrvGrid), "grid layout");
+static_assert(sizeof(Slot) == 16, "slot layout");
+static_assert(sizeof(ActRec) == 32, "action record layout");
+
+struct pomcp_ctx {
+  pomcp_config cfg;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  DevParams dp{};
+  std::vector<void*> allocs;
+  std::string err;
+  bool have_snapshot = false;
+  TreeHdr* snap_hdr = nullptr;
+  int2* snap_root = nullptr;
+  std::vector<int32_t> host_upd;
+  std::vector<pomcp_root_stats> host_stats;
+};
+
+#define HIP_TRY(ctx, expr)                                                          \
+  do {                                                                              \
+    hipError_t e_ = (expr);                                                         \
+    if (e_ != hipSuccess) {                                                         \
+      (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);              \
+      return POMCP_E_HIP;                                                           \
+    }                                                                               \
+  } while (0)
+
+static int fail(pomcp_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  return code;
+}
+
+static int dev_alloc(pomcp_ctx* ctx, void** out, size_t bytes) {
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, bytes ? bytes : 16);
+  if (e != hipSuccess) {
+    ctx->err = "hipMalloc(" + std::to_string(bytes) + " B): " + hipGetErrorString(e);
+    return POMCP_E_HIP;
+  }
+  ctx->allocs.push_back(p);
+  *out = p;
+  return POMCP_OK;
+}
+
+static unsigned grid_blocks(int B) { return (unsigned)((B + kTreesPerBlock - 1) / kTreesPerBlock); }
+
+extern "C" {
+
+int32_t pomcp_abi_version(void) { return POMCP_ABI_VERSION; }
+
+const char* pomcp_last_error(const pomcp_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int pomcp_set_stream(pomcp_ctx* ctx, void* hip_stream) {
+  if (!ctx) return POMCP_E_INVALID;
+  if (hip_stream) {
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
+    ctx->stream = (hipStream_t)hip_stream;
+    ctx->own_stream = false;
+  }
+  return POMCP_OK;
+}
+
+static int validate(const pomcp_config* c, std::string* why) {
+  auto bad = [&](const char* m) {
+    *why = m;
+    return POMCP_E_INVALID;
+  };
+  if (c->abi_version != POMCP_ABI_VERSION) return bad("ABI version mismatch");
+  if (c->env_id != POMCP_ENV_DRIVING) { *why = "only Driving-v1 is implemented"; return POMCP_E_UNSUPPORTED; }
+  if (c->num_agents != 2) { *why = "Driving-v1 engine supports 2 agents"; return POMCP_E_UNSUPPORTED; }
+  if (c->ego_agent < 0 || c->ego_agent >= c->num_agents) return bad("ego_agent out of range");
+  if (c->num_actions < 1 || c->num_actions > POMCP_MAX_ACTIONS) return bad("num_actions");
+  if (c->action_selection < 0 || c->action_selection > 2) return bad("action_selection");
+  if (!(c->discount >= 0.0 && c->discount <= 1.0)) return bad("discount in [0,1]");
+  if (!(c->c > 0.0)) return bad("c > 0");
+  if (!(c->pucb_exploration_fraction >= 0.0 && c->pucb_exploration_fraction <= 1.0))
+    return bad("pucb_exploration_fraction in [0,1]");
+  if (!(c->reinvigoration_sample_limit_factor >= 1.0)) return bad("sample_limit_factor >= 1");
+  if (c->depth_limit < 0 || c->step_limit < 0) return bad("depth/step limit");
+  if (c->num_particles < 1 || c->extra_particles < 0) return bad("num_particles");
+  if (c->num_trees < 1) return bad("num_trees >= 1");
+  if (c->max_obs_nodes < 4 || c->max_obs_nodes > INT32_MAX) return bad("max_obs_nodes");
+  if (c->max_blocks < 1 || c->max_blocks * c->num_actions > INT32_MAX) return bad("max_blocks");
+  if (c->max_particles < 1 || c->max_particles > INT32_MAX) return bad("max_particles");
+  if (c->max_belief < 2 * (c->num_particles + c->extra_particles)) return bad("max_belief too small");
+  if (c->hash_slots < kBucket || (c->hash_slots & (c->hash_slots - 1)) != 0)
+    return bad("hash_slots must be a power of two >= 16");
+  if (!c->log_table || c->log_table_size < 2) return bad("log_table");
+  if (!c->discount_pow || c->discount_pow_size < 1) return bad("discount_pow");
+  const pomcp_grid& g = c->grid;
+  if (g.width < 1 || g.width > 16 || g.height < 1 || g.height > 16) return bad("grid size");
+  if (g.num_locs < 2 || g.num_locs > 8) return bad("grid locations");
+  const int ncells = (g.obs_front + g.obs_back + 1) * (2 * g.obs_side + 1);
+  if (g.obs_front < 0 || g.obs_back < 0 || g.obs_side < 0 || ncells > 15)
+    return bad("obs window must have <= 15 cells");
+  return POMCP_OK;
+}
+
+int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomcp_ctx** out) {
+  if (!cfg || !out) return POMCP_E_INVALID;
+  *out = nullptr;
+  auto* ctx = new pomcp_ctx();
+  ctx->cfg = *cfg;
+  std::string why;
+  int rc = validate(cfg, &why);
+  if (rc != POMCP_OK) {
+    std::fprintf(stderr, "pomcp_create: %s\n", why.c_str());
+    delete ctx;
+    return rc;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) {
+    delete ctx;
+    return POMCP_E_NO_DEVICE;
+  }
+  ctx->device = device;
+  if (hipSetDevice(device) != hipSuccess) {
+    delete ctx;
+    return POMCP_E_NO_DEVICE;
+  }
+  if (hip_stream) {
+    ctx->stream = (hipStream_t)hip_stream;
+  } else {
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+      delete ctx;
+      return POMCP_E_HIP;
+    }
+    ctx->own_stream = true;
+  }
+  const pomcp_config& c = *cfg;
+  DevParams& d = ctx->dp;
+  d.B = c.num_trees;
+  d.A = c.num_actions;
+  d.ego = c.ego_agent;
+  d.other = 1 - c.ego_agent;
+  d.sel = c.action_selection;
+  d.depth_limit = c.depth_limit;
+  d.step_limit = c.step_limit;
+  d.n_target = c.num_particles + c.extra_particles;
+  d.has_kb = c.has_known_bounds;
+  d.ncells = (c.grid.obs_front + c.grid.obs_back + 1) * (2 * c.grid.obs_side + 1);
+  d.discount = c.discount;
+  d.c = c.c;
+  d.pucb_f = c.pucb_exploration_fraction;
+  d.limit_factor = c.reinvigoration_sample_limit_factor;
+  d.kb_min = c.known_min;
+  d.kb_max = c.known_max;
+  d.No = c.max_obs_nodes;
+  d.Nb = c.max_blocks;
+  d.Np = c.max_particles;
+  d.Nr = c.max_belief;
+  d.H = c.hash_slots;
+  d.bucket_mask = (uint32_t)(c.hash_slots / kBucket - 1);
+  const int64_t B = c.num_trees;
+  void* p;
+#define ALLOC(field, type, count)                                               \
+  do {                                                                          \
+    if ((rc = dev_alloc(ctx, &p, sizeof(type) * (size_t)(count))) != POMCP_OK) {\
+      pomcp_destroy(ctx);                                                       \
+      return rc;                                                                \
+    }                                                                           \
+    d.field = reinterpret_cast<decltype(d.field)>(p);                           \
+  } while (0)
+  ALLOC(hdr, TreeHdr, B);
+  ALLOC(onode, int2, B * d.No);
+  ALLOC(ometa, int32_t, B * d.No);
+  ALLOC(an, ActRec, B * d.Nb * d.A);
+  ALLOC(hash, Slot, B * d.H);
+  ALLOC(plog, uint4, B * d.Np);
+  ALLOC(belief, uint4, B * 2 * d.Nr);
+  ALLOC(logtab, double, c.log_table_size);
+  ALLOC(dpow, double, c.discount_pow_size);
+  ALLOC(grid, DrvGrid, 1);
+  ALLOC(stats, pomcp_root_stats, B);
+  ALLOC(merge, double, B * d.A * 2);
+  ALLOC(upd_out, int32_t, B * 2);
+  ALLOC(in_actions, int32_t, B);
+  ALLOC(in_obs, uint64_t, B);
+  ALLOC(out_obs, uint64_t, B);
+#undef ALLOC
+  d.logtab_n = c.log_table_size;
+  d.dpow_n = (int32_t)(c.discount_pow_size > INT32_MAX ? INT32_MAX : c.discount_pow_size);
+  hipStream_t s = ctx->stream;
+  // zero: hash epoch 0 is never valid, headers start empty
+  if (hipMemsetAsync(d.hash, 0, sizeof(Slot) * (size_t)(B * d.H), s) != hipSuccess ||
+      hipMemsetAsync(d.hdr, 0, sizeof(TreeHdr) * (size_t)B, s) != hipSuccess ||
+      hipMemsetAsync(d.stats, 0, sizeof(pomcp_root_stats) * (size_t)B, s) != hipSuccess ||
+      hipMemcpyAsync((void*)d.logtab, c.log_table, sizeof(double) * c.log_table_size,
+                     hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync((void*)d.dpow, c.discount_pow, sizeof(double) * c.discount_pow_size,
+                     hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync((void*)d.grid, &c.grid, sizeof(DrvGrid), hipMemcpyHostToDevice, s) !=
+          hipSuccess) {
+    ctx->err = "initial upload failed";
+    pomcp_destroy(ctx);
+    return POMCP_E_HIP;
+  }
+  // headers: keys and counters
+  std::vector<TreeHdr> h((size_t)B);
+  for (int64_t t = 0; t < B; ++t) {
+    std::memset(&h[t], 0, sizeof(TreeHdr));
+    h[t].seed = c.seed;
+    h[t].tree_key = c.tree_key_base + (uint32_t)t;
+  }
+  if (hipMemcpy(d.hdr, h.data(), sizeof(TreeHdr) * (size_t)B, hipMemcpyHostToDevice) !=
+      hipSuccess) {
+    ctx->err = "header upload failed";
+    pomcp_destroy(ctx);
+    return POMCP_E_HIP;
+  }
+  ctx->host_upd.resize((size_t)(2 * B));
+  ctx->host_stats.resize((size_t)B);
+  // the tables were copied asynchronously from caller memory: finish before returning
+  if (hipStreamSynchronize(s) != hipSuccess) {
+    pomcp_destroy(ctx);
+    return POMCP_E_HIP;
+  }
+  rc = pomcp_reset(ctx);
+  if (rc != POMCP_OK) {
+    pomcp_destroy(ctx);
+    return rc;
+  }
+  *out = ctx;
+  return POMCP_OK;
+}
+
+void pomcp_destroy(pomcp_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  for (void* p : ctx->allocs) (void)hipFree(p);
+  if (ctx->snap_hdr) (void)hipFree(ctx->snap_hdr);
+  if (ctx->snap_root) (void)hipFree(ctx->snap_root);
+  if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int pomcp_reset(pomcp_ctx* ctx) {
+  if (!ctx) return POMCP_E_INVALID;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(k_reset, dim3(grid_blocks(ctx->dp.B)), dim3(256), 0, ctx->stream, ctx->dp);
+  HIP_TRY(ctx, hipGetLastError());
+  ctx->have_snapshot = false;
+  return POMCP_OK;
+}
+
+static int first_tree_error(pomcp_ctx* ctx, const int32_t* codes, int stride, int off,
+                            const char* what) {
+  for (int t = 0; t < ctx->dp.B; ++t) {
+    const int e = codes[(size_t)t * stride + off];
+    if (e != 0) {
+      const char* kind = e == POMCP_E_ARENA ? "arena capacity exceeded"
+                         : e == POMCP_E_NOT_FOUND ? "root has no child node for action"
+                         : e == POMCP_E_STATE ? "call out of order"
+                         : e == POMCP_E_INVALID ? "invalid observation"
+                                                : "error";
+      return fail(ctx, e, std::string(what) + ": tree " + std::to_string(t) + ": " + kind);
+    }
+  }
+  return POMCP_OK;
+}
+
+int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_keys,
+                 int32_t* root_absorbing_out) {
+  if (!ctx || !obs_keys) return POMCP_E_INVALID;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  const int B = ctx->dp.B;
+  std::vector<int32_t> acts((size_t)B, -1);
+  if (actions) std::memcpy(acts.data(), actions, sizeof(int32_t) * (size_t)B);
+  HIP_TRY(ctx, hipMemcpyAsync((void*)ctx->dp.in_actions, acts.data(), sizeof(int32_t) * B,
+                              hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync((void*)ctx->dp.in_obs, obs_keys, sizeof(uint64_t) * B,
+                              hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(k_update, dim3(grid_blocks(B)), dim3(256), 0, ctx->stream, ctx->dp);
+  HIP_TRY(ctx, hipGetLastError());
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->host_upd.data(), ctx->dp.upd_out, sizeof(int32_t) * 2 * B,
+                              hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  if (root_absorbing_out)
+    for (int t = 0; t < B; ++t) root_absorbing_out[t] = ctx->host_upd[2 * t];
+  return first_tree_error(ctx, ctx->host_upd.data(), 2, 1, "update");
+}
+
+int pomcp_search(pomcp_ctx* ctx, int32_t num_sims, int32_t* actions_out) {
+  if (!ctx || num_sims < 0) return POMCP_E_INVALID;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(k_search, dim3(grid_blocks(ctx->dp.B)), dim3(256), 0, ctx->stream,
+                     ctx->dp, (int)num_sims);
+  HIP_TRY(ctx, hipGetLastError());
+  if (!actions_out) return POMCP_OK;
+  const int rc = pomcp_get_root_stats(ctx, ctx->host_stats.data());
+  if (rc != POMCP_OK) return rc;
+  for (int t = 0; t < ctx->dp.B; ++t) actions_out[t] = ctx->host_stats[t].action;
+  return POMCP_OK;
+}
+
+int pomcp_get_root_stats(pomcp_ctx* ctx, pomcp_root_stats* out) {
+  if (!ctx || !out) return POMCP_E_INVALID;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  HIP_TRY(ctx, hipMemcpyAsync(out, ctx->dp.stats, sizeof(pomcp_root_stats) * ctx->dp.B,
+                              hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  for (int t = 0; t < ctx->dp.B; ++t)
+    if (out[t].error != 0) {
+      std::vector<int32_t> codes((size_t)ctx->dp.B);
+      for (int k = 0; k < ctx->dp.B; ++k) codes[k] = out[k].error;
+      return first_tree_error(ctx, codes.data(), 1, 0, "search");
+    }
+  return POMCP_OK;
+}
+
+int pomcp_get_root_belief(pomcp_ctx* ctx, int32_t tree, uint32_t* out, int32_t capacity,
+                          int32_t* count) {
+  if (!ctx || !count || tree < 0 || tree >= ctx->dp.B) return POMCP_E_INVALID;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  TreeHdr h;
+  HIP_TRY(ctx, hipMemcpyAsync(&h, ctx->dp.hdr + tree, sizeof(TreeHdr), hipMemcpyDeviceToHost,
+                              ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  *count = h.belief_size;
+  if (!out || capacity <= 0) return POMCP_OK;
+  const int n = h.belief_size < capacity ? h.belief_size : capacity;
+  std::vector<uint4> tmp((size_t)n);
+  const uint4* src = ctx->dp.belief + (int64_t)tree * 2 * ctx->dp.Nr + (int64_t)h.belief_sel * ctx->dp.Nr;
+  if (n > 0) {
+    HIP_TRY(ctx, hipMemcpyAsync(tmp.data(), src, sizeof(uint4) * n, hipMemcpyDeviceToHost,
+                                ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  for (int i = 0; i < n; ++i) {
+    out[3 * i + 0] = tmp[i].x;
+    out[3 * i + 1] = tmp[i].y;
+    out[3 * i + 2] = tmp[i].z;
+  }
+  return POMCP_OK;
+}
+
+int pomcp_rekey(pomcp_ctx* ctx, uint64_t seed) {
+  if (!ctx) return POMCP_E_INVALID;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  std::vector<TreeHdr> h((size_t)ctx->dp.B);
+  HIP_TRY(ctx, hipMemcpyAsync(h.data(), ctx->dp.hdr, sizeof(TreeHdr) * h.size(),
+                              hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  for (auto& x : h) x.seed = seed;
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->dp.hdr, h.data(), sizeof(TreeHdr) * h.size(),
+                              hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return POMCP_OK;
+}
+
+int pomcp_root_merge_buffer(pomcp_ctx* ctx, void** device_ptr) {
+  if (!ctx || !device_ptr) return POMCP_E_INVALID;
+  *device_ptr = ctx->dp.merge;
+  return POMCP_OK;
+}
+
+int pomcp_synthetic_obs(pomcp_ctx* ctx, uint64_t env_seed_base, uint64_t* obs_keys_out) {
+  if (!ctx) return POMCP_E_INVALID;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(k_synthetic_obs, dim3(grid_blocks(ctx->dp.B)), dim3(256), 0, ctx->stream,
+                     ctx->dp, env_seed_base);
+  HIP_TRY(ctx, hipGetLastError());
+  if (obs_keys_out) {
+    HIP_TRY(ctx, hipMemcpyAsync(obs_keys_out, ctx->dp.out_obs, sizeof(uint64_t) * ctx->dp.B,
+                                hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  return POMCP_OK;
+}
+
+int pomcp_snapshot(pomcp_ctx* ctx) {
+  if (!ctx) return POMCP_E_INVALID;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  const int B = ctx->dp.B;
+  std::vector<TreeHdr> h((size_t)B);
+  HIP_TRY(ctx, hipMemcpyAsync(h.data(), ctx->dp.hdr, sizeof(TreeHdr) * B, hipMemcpyDeviceToHost,
+                              ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  std::vector<int2> roots((size_t)B);
+  for (int t = 0; t < B; ++t) {
+    // only the post-initial-update state (empty obs-child map) can be restored by
+    // bumping the map generation
+    if (h[t].root_t != 1 || h[t].n_blocks != 0 || h[t].n_log != 0 || h[t].error != 0)
+      return fail(ctx, POMCP_E_STATE, "snapshot: every tree must be right after its initial update");
+    roots[t] = make_int2(-1, 0);
+  }
+  if (!ctx->snap_hdr) {
+    HIP_TRY(ctx, hipMalloc(&ctx->snap_hdr, sizeof(TreeHdr) * B));
+    HIP_TRY(ctx, hipMalloc(&ctx->snap_root, sizeof(int2) * B));
+  }
+  for (int t = 0; t < B; ++t) {
+    int2 r;
+    HIP_TRY(ctx, hipMemcpy(&r, ctx->dp.onode + (int64_t)t * ctx->dp.No + h[t].root, sizeof(int2),
+                           hipMemcpyDeviceToHost));
+    roots[t] = r;
+  }
+  HIP_TRY(ctx, hipMemcpy(ctx->snap_hdr, h.data(), sizeof(TreeHdr) * B, hipMemcpyHostToDevice));
+  HIP_TRY(ctx, hipMemcpy(ctx->snap_root, roots.data(), sizeof(int2) * B, hipMemcpyHostToDevice));
+  ctx->have_snapshot = true;
+  return POMCP_OK;
+}
+
+int pomcp_restore(pomcp_ctx* ctx) {
+  if (!ctx) return POMCP_E_INVALID;
+  if (!ctx->have_snapshot) return fail(ctx, POMCP_E_STATE, "restore without snapshot");
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(k_restore, dim3(grid_blocks(ctx->dp.B)), dim3(256), 0, ctx->stream, ctx->dp,
+                     ctx->snap_hdr, ctx->snap_root);
+  HIP_TRY(ctx, hipGetLastError());
+  return POMCP_OK;
+}
+
+// ---------------------------------------------------------------- host model
+
+int pomcp_driving_sample_initial_state(const pomcp_grid* g, uint64_t seed, uint32_t tree,
+                                       uint32_t* model_ctr, uint32_t state_out[2]) {
+  if (!g || !model_ctr || !state_out) return POMCP_E_INVALID;
+  const DrvGrid& gg = *reinterpret_cast<const DrvGrid*>(g);
+  Streams s;
+  s.seed = seed;
+  s.tree = tree;
+  for (int k = 0; k < 5; ++k) s.ctr[k] = 0;
+  s.ctr[2] = *model_ctr;
+  drv_sample_initial_state2(gg, [&](uint32_t n) { return s.model(n); }, &state_out[0],
+                            &state_out[1]);
+  *model_ctr = s.ctr[2];
+  return POMCP_OK;
+}
+
+int pomcp_driving_step(const pomcp_grid* g, uint64_t seed, uint32_t tree, uint32_t* model_ctr,
+                       const uint32_t state[2], const int32_t actions[2], uint32_t next_out[2],
+                       double rewards_out[2], int32_t terminated_out[2],
+                       uint64_t obs_keys_out[2]) {
+  if (!g || !model_ctr || !state || !actions || !next_out) return POMCP_E_INVALID;
+  const DrvGrid& gg = *reinterpret_cast<const DrvGrid*>(g);
+  Streams s;
+  s.seed = seed;
+  s.tree = tree;
+  for (int k = 0; k < 5; ++k) s.ctr[k] = 0;
+  s.ctr[2] = *model_ctr;
+  const uint32_t j = s.model(2);   // execution-order shuffle
+  *model_ctr = s.ctr[2];
+  drv_step2(gg, state[0], state[1], actions[0], actions[1], j, &next_out[0], &next_out[1]);
+  for (int i = 0; i < 2; ++i) {
+    if (rewards_out) rewards_out[i] = drv_reward(state[i], next_out[i]);
+    if (terminated_out) terminated_out[i] = veh_done(next_out[i]) ? 1 : 0;
+  }
+  if (obs_keys_out) {
+    obs_keys_out[0] = obs_key_serial(gg, next_out[0], next_out[1]);
+    obs_keys_out[1] = obs_key_serial(gg, next_out[1], next_out[0]);
+  }
+  return POMCP_OK;
+}
+
+int pomcp_driving_obs(const pomcp_grid* g, const uint32_t state[2], uint64_t obs_keys_out[2]) {
+  if (!g || !state || !obs_keys_out) return POMCP_E_INVALID;
+  const DrvGrid& gg = *reinterpret_cast<const DrvGrid*>(g);
+  obs_keys_out[0] = obs_key_serial(gg, state[0], state[1]);
+  obs_keys_out[1] = obs_key_serial(gg, state[1], state[0]);
+  return POMCP_OK;
+}
+
+// Debug: FP64 sqrt / div / add-mul on the device, for bit-exactness checks
+// against the host (include/pomcp_debug.h).
+int pomcp_debug_fp_selftest(const double* a, const double* b, int32_t n, double* out) {
+  if (!a || !b || !out || n <= 0) return POMCP_E_INVALID;
+  double *da = nullptr, *db = nullptr, *dout = nullptr;
+  if (hipMalloc(&da, sizeof(double) * n) != hipSuccess) return POMCP_E_HIP;
+  (void)hipMalloc(&db, sizeof(double) * n);
+  (void)hipMalloc(&dout, sizeof(double) * 4 * n);
+  (void)hipMemcpy(da, a, sizeof(double) * n, hipMemcpyHostToDevice);
+  (void)hipMemcpy(db, b, sizeof(double) * n, hipMemcpyHostToDevice);
+  hipLaunchKernelGGL(k_fp_selftest, dim3((n + 255) / 256), dim3(256), 0, 0, da, db, n, dout);
+  hipError_t e = hipMemcpy(out, dout, sizeof(double) * 4 * n, hipMemcpyDeviceToHost);
+  (void)hipFree(da);
+  (void)hipFree(db);
+  (void)hipFree(dout);
+  return e == hipSuccess ? POMCP_OK : POMCP_E_HIP;
+}
+
+}  // extern "C"

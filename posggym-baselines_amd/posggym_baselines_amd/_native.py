@@ -1,0 +1,188 @@
+"""ctypes binding of libpomcp_hip.so (include/pomcp.h).
+
+The structs below mirror the C declarations field for field.  The library is
+built in-tree by ``posggym_baselines_amd.build`` (hipcc, gfx950) and loaded
+from ``posggym_baselines_amd/_lib/``; there is no fallback: if the shared
+object is missing, importing the planner raises.
+"""
+import ctypes as C
+import os
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
+LIB_PATH = os.path.join(LIB_DIR, "libpomcp_hip.so")
+
+POMCP_ABI_VERSION = 1
+POMCP_MAX_ACTIONS = 8
+
+POMCP_OK = 0
+POMCP_E_INVALID = -1
+POMCP_E_HIP = -2
+POMCP_E_ARENA = -3
+POMCP_E_STATE = -4
+POMCP_E_UNSUPPORTED = -5
+POMCP_E_NOT_FOUND = -6
+POMCP_E_NO_DEVICE = -7
+
+SEL_PUCB, SEL_UCB, SEL_UNIFORM = 0, 1, 2
+ENV_DRIVING = 1
+
+STATUS_NAMES = {
+    POMCP_E_INVALID: "POMCP_E_INVALID",
+    POMCP_E_HIP: "POMCP_E_HIP",
+    POMCP_E_ARENA: "POMCP_E_ARENA",
+    POMCP_E_STATE: "POMCP_E_STATE",
+    POMCP_E_UNSUPPORTED: "POMCP_E_UNSUPPORTED",
+    POMCP_E_NOT_FOUND: "POMCP_E_NOT_FOUND",
+    POMCP_E_NO_DEVICE: "POMCP_E_NO_DEVICE",
+}
+
+
+class PomcpGrid(C.Structure):
+    _fields_ = [
+        ("wall", C.c_uint8 * 256),
+        ("dist", (C.c_uint8 * 256) * 8),
+        ("loc_x", C.c_uint8 * 8),
+        ("loc_y", C.c_uint8 * 8),
+        ("loc_dir", C.c_uint8 * 8),
+        ("width", C.c_int32),
+        ("height", C.c_int32),
+        ("num_locs", C.c_int32),
+        ("obs_front", C.c_int32),
+        ("obs_back", C.c_int32),
+        ("obs_side", C.c_int32),
+        ("pad", C.c_int32 * 2),
+    ]
+
+
+class PomcpConfig(C.Structure):
+    _fields_ = [
+        ("abi_version", C.c_int32),
+        ("env_id", C.c_int32),
+        ("num_agents", C.c_int32),
+        ("ego_agent", C.c_int32),
+        ("num_actions", C.c_int32),
+        ("action_selection", C.c_int32),
+        ("depth_limit", C.c_int32),
+        ("step_limit", C.c_int32),
+        ("num_particles", C.c_int32),
+        ("extra_particles", C.c_int32),
+        ("has_known_bounds", C.c_int32),
+        ("num_trees", C.c_int32),
+        ("discount", C.c_double),
+        ("c", C.c_double),
+        ("pucb_exploration_fraction", C.c_double),
+        ("reinvigoration_sample_limit_factor", C.c_double),
+        ("known_min", C.c_double),
+        ("known_max", C.c_double),
+        ("seed", C.c_uint64),
+        ("tree_key_base", C.c_uint32),
+        ("pad0", C.c_int32),
+        ("max_obs_nodes", C.c_int64),
+        ("max_blocks", C.c_int64),
+        ("max_particles", C.c_int64),
+        ("max_belief", C.c_int64),
+        ("hash_slots", C.c_int64),
+        ("log_table", C.POINTER(C.c_double)),
+        ("log_table_size", C.c_int64),
+        ("discount_pow", C.POINTER(C.c_double)),
+        ("discount_pow_size", C.c_int64),
+        ("grid", PomcpGrid),
+    ]
+
+
+class PomcpRootStats(C.Structure):
+    _fields_ = [
+        ("action", C.c_int32),
+        ("num_sims", C.c_int32),
+        ("search_depth", C.c_int32),
+        ("root_visits", C.c_int32),
+        ("root_absorbing", C.c_int32),
+        ("belief_size", C.c_int32),
+        ("error", C.c_int32),
+        ("num_children", C.c_int32),
+        ("child_visits", C.c_int32 * POMCP_MAX_ACTIONS),
+        ("child_values", C.c_double * POMCP_MAX_ACTIONS),
+        ("child_totals", C.c_double * POMCP_MAX_ACTIONS),
+        ("min_value", C.c_double),
+        ("max_value", C.c_double),
+        ("n_levels", C.c_int64),
+        ("n_expansions", C.c_int64),
+        ("n_new_nodes", C.c_int64),
+        ("n_rollout_steps", C.c_int64),
+        ("n_probes", C.c_int64),
+        ("n_obs_nodes", C.c_int32),
+        ("n_blocks", C.c_int32),
+        ("n_log", C.c_int32),
+        ("pad", C.c_int32),
+    ]
+
+
+# (name, restype, argtypes) for every symbol include/pomcp.h declares.
+_CTX = C.c_void_p
+_P32 = C.POINTER(C.c_int32)
+_PU32 = C.POINTER(C.c_uint32)
+_PU64 = C.POINTER(C.c_uint64)
+_PD = C.POINTER(C.c_double)
+SIGNATURES = [
+    ("pomcp_abi_version", C.c_int32, []),
+    ("pomcp_create", C.c_int, [C.POINTER(PomcpConfig), C.c_int32, C.c_void_p, C.POINTER(_CTX)]),
+    ("pomcp_destroy", None, [_CTX]),
+    ("pomcp_last_error", C.c_char_p, [_CTX]),
+    ("pomcp_set_stream", C.c_int, [_CTX, C.c_void_p]),
+    ("pomcp_reset", C.c_int, [_CTX]),
+    ("pomcp_update", C.c_int, [_CTX, _P32, _PU64, _P32]),
+    ("pomcp_search", C.c_int, [_CTX, C.c_int32, _P32]),
+    ("pomcp_get_root_stats", C.c_int, [_CTX, C.POINTER(PomcpRootStats)]),
+    ("pomcp_get_root_belief", C.c_int, [_CTX, C.c_int32, _PU32, C.c_int32, _P32]),
+    ("pomcp_rekey", C.c_int, [_CTX, C.c_uint64]),
+    ("pomcp_root_merge_buffer", C.c_int, [_CTX, C.POINTER(C.c_void_p)]),
+    ("pomcp_synthetic_obs", C.c_int, [_CTX, C.c_uint64, _PU64]),
+    ("pomcp_snapshot", C.c_int, [_CTX]),
+    ("pomcp_restore", C.c_int, [_CTX]),
+    ("pomcp_driving_sample_initial_state", C.c_int,
+     [C.POINTER(PomcpGrid), C.c_uint64, C.c_uint32, _PU32, _PU32]),
+    ("pomcp_driving_step", C.c_int,
+     [C.POINTER(PomcpGrid), C.c_uint64, C.c_uint32, _PU32, _PU32, _P32, _PU32, _PD, _P32, _PU64]),
+    ("pomcp_driving_obs", C.c_int, [C.POINTER(PomcpGrid), _PU32, _PU64]),
+]
+DEBUG_SIGNATURES = [
+    ("pomcp_debug_fp_selftest", C.c_int, [_PD, _PD, C.c_int32, _PD]),
+]
+
+_lib = None
+
+
+class PomcpError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{STATUS_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+def load():
+    """Load the in-tree shared object (raises if it was never built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -m posggym_baselines_amd.build` "
+            "(or __graft_entry__.build()); there is no CPU fallback for the planner")
+    lib = C.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES + DEBUG_SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.pomcp_abi_version() != POMCP_ABI_VERSION:
+        raise ImportError("libpomcp_hip.so ABI version mismatch; rebuild")
+    _lib = lib
+    return lib
+
+
+def check(rc, ctx=None, what=""):
+    if rc != POMCP_OK:
+        msg = what
+        if ctx is not None:
+            err = load().pomcp_last_error(ctx)
+            if err:
+                msg = f"{what}: {err.decode()}"
+        raise PomcpError(rc, msg)

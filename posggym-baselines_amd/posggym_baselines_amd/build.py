@@ -1,0 +1,50 @@
+"""Build libpomcp_hip.so in-tree with hipcc for gfx950.
+
+    python -m posggym_baselines_amd.build
+
+``-ffp-contract=off`` is required: the reference's FP64 arithmetic (UCB,
+Welford, discounting) has no fused multiply-adds and parity is bit-exact.
+"""
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+PROJECT = os.path.dirname(PKG)                       # posggym-baselines_amd/
+REPO = os.path.dirname(PROJECT)
+CSRC = os.path.join(PROJECT, "csrc")
+INCLUDE = os.path.join(REPO, "include")
+OUT = os.path.join(PKG, "_lib", "libpomcp_hip.so")
+SOURCES = [os.path.join(CSRC, "pomcp_capi.hip")]
+DEPS = SOURCES + [os.path.join(CSRC, f) for f in
+                  ("pomcp_kernels.hip", "pomcp_device.h", "driving.h", "philox.h")] + [
+    os.path.join(INCLUDE, "pomcp.h"), os.path.join(INCLUDE, "pomcp_debug.h")]
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("POMCP_OFFLOAD_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC",
+         "-shared", f"-I{INCLUDE}", "-Wall", "-Wno-unused-function"]
+
+
+def up_to_date() -> bool:
+    if not os.path.exists(OUT):
+        return False
+    t = os.path.getmtime(OUT)
+    return all(os.path.getmtime(d) <= t for d in DEPS if os.path.exists(d))
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    if not force and up_to_date():
+        return OUT
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    tmp = OUT + ".tmp"
+    cmd = [HIPCC] + FLAGS + ["-o", tmp] + SOURCES
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,6 @@
+from posggym_baselines_amd.envs.driving import (  # noqa: F401
+    GRIDS,
+    DrivingModel,
+    pack_obs,
+    unpack_obs,
+)

@@ -1,0 +1,17 @@
+"""Drop-in for ``posggym_baselines.planning`` (``planning/__init__.py:1-18``):
+the POMCP hot path on MI355X."""
+from posggym_baselines_amd.planning.config import MCTSConfig  # noqa: F401
+from posggym_baselines_amd.planning.other_policy import (  # noqa: F401
+    OtherAgentPolicy,
+    RandomOtherAgentPolicy,
+)
+from posggym_baselines_amd.planning.pomcp import POMCP, BatchedPOMCP, uct_merge  # noqa: F401
+from posggym_baselines_amd.planning.search_policy import (  # noqa: F401
+    RandomSearchPolicy,
+    SearchPolicy,
+)
+from posggym_baselines_amd.planning.utils import (  # noqa: F401
+    KnownBounds,
+    MinMaxStats,
+    PlanningStatTracker,
+)

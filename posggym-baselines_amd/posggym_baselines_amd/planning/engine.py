@@ -1,0 +1,211 @@
+"""Python handle on one ``pomcp_ctx`` (a batch of independent search trees on
+one GPU).  Builds the C config from a model + ``MCTSConfig``, sizes the
+per-tree HBM arenas, and exposes update / search / statistics as numpy.
+"""
+import ctypes as C
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+from posggym_baselines_amd import _native as N
+
+INT32_MAX = 2**31 - 1
+
+
+@dataclass
+class Capacities:
+    max_obs_nodes: int
+    max_blocks: int
+    max_particles: int
+    max_belief: int
+    hash_slots: int
+    log_table_size: int
+    discount_pow_size: int
+
+    def bytes_per_tree(self, num_actions: int) -> int:
+        return (self.max_obs_nodes * 12 + self.max_blocks * num_actions * 32
+                + self.hash_slots * 16 + self.max_particles * 16 + 2 * self.max_belief * 16)
+
+
+def _next_pow2(n: int) -> int:
+    return 1 << max(4, (int(n) - 1).bit_length())
+
+
+def plan_capacities(config, step_limit: int, num_sims: int, searches: int = 1,
+                    reroot: bool = True, max_blocks: int = None, max_obs_nodes: int = None):
+    """Worst-case arena sizes for ``searches`` searches of ``num_sims`` each.
+
+    Every simulation creates at most one obs node and expands at most one leaf
+    (mcts.py:318-328, 369) and appends one particle per tree level stepped
+    (mcts.py:371), at most min(depth_limit, step_limit) + 1 levels.
+    """
+    levels = min(config.depth_limit, step_limit) + 1
+    n_target = config.num_particles + config.extra_particles
+    total = num_sims * searches
+    no = total + 2 * searches + 16 if max_obs_nodes is None else max_obs_nodes
+    nb = no if max_blocks is None else max_blocks
+    np_ = total * min(levels, 64) + searches * 2 * n_target + 64
+    nr = (np_ + 2 * n_target + 64) if reroot else (4 * n_target + 64)
+    return Capacities(
+        max_obs_nodes=no, max_blocks=nb, max_particles=np_, max_belief=nr,
+        hash_slots=_next_pow2(2 * no), log_table_size=total + 2,
+        discount_pow_size=min(levels, 4096) + 2)
+
+
+class PomcpEngine:
+    SELECTION = {"pucb": N.SEL_PUCB, "ucb": N.SEL_UCB, "uniform": N.SEL_UNIFORM}
+
+    def __init__(self, model, agent_id, config, num_trees=1, capacities=None, num_sims=None,
+                 searches=None, device=None, stream=None, tree_key_base=0, seed=None):
+        lib = N.load()
+        if not hasattr(model, "pomcp_grid"):
+            raise NotImplementedError(
+                f"{type(model).__name__} has no GPU generative model; the engine implements "
+                "Driving-v1 (posggym_baselines_amd.envs.DrivingModel)")
+        if config.truncated and not config.use_rollout_if_no_value:
+            raise NotImplementedError("truncated search needs a value function (none on GPU)")
+        self.model = model
+        self.config = config
+        self.num_trees = int(num_trees)
+        self.ego = model.possible_agents.index(agent_id)
+        self.A = model.action_spaces[agent_id].n
+        if config.step_limit is not None:
+            step_limit = int(config.step_limit)
+        elif getattr(model, "spec", None) is not None and model.spec.max_episode_steps:
+            step_limit = int(model.spec.max_episode_steps)
+        else:
+            step_limit = INT32_MAX
+        self.step_limit = step_limit
+        if capacities is None:
+            sims = num_sims if num_sims is not None else (config.num_sims or 4096)
+            budget = searches if searches is not None else (
+                (step_limit if step_limit < INT32_MAX else 100) + 1)
+            capacities = plan_capacities(config, step_limit, sims, budget)
+        self.capacities = capacities
+        c = N.PomcpConfig()
+        c.abi_version = N.POMCP_ABI_VERSION
+        c.env_id = N.ENV_DRIVING
+        c.num_agents = len(model.possible_agents)
+        c.ego_agent = self.ego
+        c.num_actions = self.A
+        c.action_selection = self.SELECTION[config.action_selection]
+        c.depth_limit = min(config.depth_limit, INT32_MAX)
+        c.step_limit = step_limit
+        c.num_particles = config.num_particles
+        c.extra_particles = config.extra_particles
+        kb = config.known_bounds
+        c.has_known_bounds = 1 if kb else 0
+        if kb:
+            c.known_min, c.known_max = float(kb[0]), float(kb[1])
+        c.num_trees = self.num_trees
+        c.discount = config.discount
+        c.c = config.c
+        c.pucb_exploration_fraction = config.pucb_exploration_fraction
+        c.reinvigoration_sample_limit_factor = config.reinvigoration_sample_limit_factor
+        s = config.seed if seed is None else seed
+        if s is None:
+            s = int(np.random.SeedSequence().entropy) & (2**63 - 1)
+        c.seed = int(s) & (2**64 - 1)
+        c.tree_key_base = int(tree_key_base)
+        c.max_obs_nodes = capacities.max_obs_nodes
+        c.max_blocks = capacities.max_blocks
+        c.max_particles = capacities.max_particles
+        c.max_belief = capacities.max_belief
+        c.hash_slots = capacities.hash_slots
+        # FP64 tables from Python's own math.log and float ** int (bit-exact with
+        # mcts.py:534 and mcts.py:421)
+        self._logtab = np.array([0.0] + [math.log(n) for n in range(1, capacities.log_table_size)],
+                                dtype=np.float64)
+        self._dpow = np.array([config.discount ** k for k in range(capacities.discount_pow_size)],
+                              dtype=np.float64)
+        c.log_table = self._logtab.ctypes.data_as(C.POINTER(C.c_double))
+        c.log_table_size = len(self._logtab)
+        c.discount_pow = self._dpow.ctypes.data_as(C.POINTER(C.c_double))
+        c.discount_pow_size = len(self._dpow)
+        c.grid = model.pomcp_grid()
+        self._cfg = c
+        dev = config.device if device is None else device
+        ctx = C.c_void_p()
+        rc = lib.pomcp_create(C.byref(c), int(dev), stream, C.byref(ctx))
+        if rc != N.POMCP_OK:
+            raise N.PomcpError(rc, "pomcp_create failed (no GPU, bad config or out of memory)")
+        self._ctx = ctx
+        self._lib = lib
+        self._stats = (N.PomcpRootStats * self.num_trees)()
+
+    # ------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self._lib.pomcp_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        N.check(rc, self._ctx, what)
+
+    def reset(self):
+        self._check(self._lib.pomcp_reset(self._ctx), "reset")
+
+    def update(self, actions, obs_keys):
+        B = self.num_trees
+        a = np.ascontiguousarray(np.broadcast_to(np.asarray(actions, dtype=np.int32), (B,)))
+        o = np.ascontiguousarray(np.broadcast_to(np.asarray(obs_keys, dtype=np.uint64), (B,)))
+        absorbing = np.zeros(B, dtype=np.int32)
+        self._check(self._lib.pomcp_update(
+            self._ctx, a.ctypes.data_as(C.POINTER(C.c_int32)),
+            o.ctypes.data_as(C.POINTER(C.c_uint64)),
+            absorbing.ctypes.data_as(C.POINTER(C.c_int32))), "update")
+        return absorbing.astype(bool)
+
+    def search(self, num_sims, fetch=True):
+        if not fetch:
+            self._check(self._lib.pomcp_search(self._ctx, int(num_sims), None), "search")
+            return None
+        out = np.zeros(self.num_trees, dtype=np.int32)
+        self._check(self._lib.pomcp_search(self._ctx, int(num_sims),
+                                           out.ctypes.data_as(C.POINTER(C.c_int32))), "search")
+        return out
+
+    def root_stats(self):
+        self._check(self._lib.pomcp_get_root_stats(self._ctx, self._stats), "get_root_stats")
+        return self._stats
+
+    def root_belief(self, tree=0):
+        n = C.c_int32()
+        self._check(self._lib.pomcp_get_root_belief(self._ctx, tree, None, 0, C.byref(n)),
+                    "get_root_belief")
+        buf = np.zeros(3 * max(n.value, 1), dtype=np.uint32)
+        self._check(self._lib.pomcp_get_root_belief(
+            self._ctx, tree, buf.ctypes.data_as(C.POINTER(C.c_uint32)), n.value, C.byref(n)),
+            "get_root_belief")
+        return buf[:3 * n.value].reshape(-1, 3)
+
+    def rekey(self, seed):
+        self._check(self._lib.pomcp_rekey(self._ctx, int(seed) & (2**64 - 1)), "rekey")
+
+    def merge_buffer_ptr(self) -> int:
+        p = C.c_void_p()
+        self._check(self._lib.pomcp_root_merge_buffer(self._ctx, C.byref(p)), "merge_buffer")
+        return p.value
+
+    def synthetic_obs(self, env_seed_base):
+        out = np.zeros(self.num_trees, dtype=np.uint64)
+        self._check(self._lib.pomcp_synthetic_obs(
+            self._ctx, int(env_seed_base), out.ctypes.data_as(C.POINTER(C.c_uint64))),
+            "synthetic_obs")
+        return out
+
+    def snapshot(self):
+        self._check(self._lib.pomcp_snapshot(self._ctx), "snapshot")
+
+    def restore(self):
+        self._check(self._lib.pomcp_restore(self._ctx), "restore")
+
+    def set_stream(self, stream):
+        self._check(self._lib.pomcp_set_stream(self._ctx, stream), "set_stream")

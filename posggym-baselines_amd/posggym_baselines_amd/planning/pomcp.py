@@ -1,0 +1,230 @@
+"""POMCP drop-in: the reference's ``POMCP`` API (``pomcp.py:9-35`` on top of
+``mcts.py:22-739``) with the search, the tree, the particle beliefs and the
+generative model on the GPU.
+
+Public surface kept from the reference: ``POMCP(model, agent_id, config,
+search_policy)``, ``step(obs)``, ``reset()``, ``update(action, obs)``,
+``get_action()``, ``close()``, and the attributes ``model``, ``agent_id``,
+``config``, ``other_agent_policies``, ``search_policy``, ``step_statistics``,
+``stat_tracker``, ``root``.
+
+``BatchedPOMCP`` runs many independent planners (one tree each) in one kernel
+launch; it is what the bench and batch experiments use.
+"""
+import dataclasses
+import logging
+import math
+import time
+from typing import Optional
+
+import numpy as np
+import psutil
+
+from posggym_baselines_amd.planning.config import MCTSConfig
+from posggym_baselines_amd.planning.engine import PomcpEngine
+from posggym_baselines_amd.planning.other_policy import RandomOtherAgentPolicy
+from posggym_baselines_amd.planning.search_policy import RandomSearchPolicy, SearchPolicy
+from posggym_baselines_amd.planning.utils import PlanningStatTracker
+
+
+@dataclasses.dataclass
+class RootView:
+    """Read-only view of the GPU root node (``ObsNode`` fields the callers use)."""
+
+    t: int = 0
+    is_absorbing: bool = False
+    visits: int = 0
+    child_visits: tuple = ()
+    child_values: tuple = ()
+    child_totals: tuple = ()
+    belief_size: int = 0
+
+
+class POMCP:
+    """Partially Observable Monte-Carlo Planning, GPU-resident tree.
+
+    Only the uniform random search policy is executed on the device
+    (``RandomSearchPolicy``), matching the reference's POMCP test setup
+    (``tests/planning/test_pomcp.py:36-74``); other agents are random
+    (``pomcp.py:28-31``).
+    """
+
+    def __init__(self, model, agent_id: str, config: MCTSConfig, search_policy: SearchPolicy,
+                 *, num_sims: Optional[int] = None):
+        if not isinstance(search_policy, RandomSearchPolicy):
+            raise NotImplementedError(
+                "the GPU POMCP engine runs the uniform random rollout policy in-kernel; "
+                f"{type(search_policy).__name__} is not supported")
+        if not config.state_belief_only:
+            # pomcp.py:32-34 calls config.replace(...), which does not exist on the
+            # dataclass (AttributeError in the reference); dataclasses.replace is
+            # what it means.  Recorded in DESIGN.md.
+            config = dataclasses.replace(config, state_belief_only=True)
+        self.model = model
+        self.agent_id = agent_id
+        self.config = config
+        self.search_policy = search_policy
+        self.other_agent_policies = {
+            i: RandomOtherAgentPolicy(model, i) for i in model.possible_agents if i != agent_id}
+        self.num_agents = len(model.possible_agents)
+        self.action_space = list(range(model.action_spaces[agent_id].n))
+        self._num_sims = num_sims if num_sims is not None else config.num_sims
+        self._engine = PomcpEngine(model, agent_id, config, num_trees=1,
+                                   num_sims=self._num_sims or 4096)
+        self.step_limit = self._engine.step_limit
+        self._logger = logging.getLogger()
+        self._last_action = None
+        self._step_num = 0
+        self.root = RootView()
+        self.step_statistics = {}
+        self._reset_step_statistics()
+        self.stat_tracker = PlanningStatTracker(self)
+
+    # ---------------------------------------------------------------- step
+    def step(self, obs):
+        """``mcts.py:97-117``."""
+        assert self.root.t <= self.step_limit
+        if self.root.is_absorbing:
+            for k in self.step_statistics:
+                self.step_statistics[k] = np.nan
+            return self._last_action
+        self._reset_step_statistics()
+        self.update(self._last_action, obs)
+        self._last_action = self.get_action()
+        self._step_num += 1
+        self.step_statistics["mem_usage"] = psutil.Process().memory_info().rss / 1024**2
+        self.stat_tracker.step()
+        return self._last_action
+
+    def reset(self):
+        """``mcts.py:123-138``."""
+        self.stat_tracker.reset_episode()
+        self._step_num = 0
+        self._engine.reset()
+        self.root = RootView()
+        self._min_value, self._max_value = self._initial_bounds()
+        self._reset_step_statistics()
+        self._last_action = None
+
+    def _initial_bounds(self):
+        kb = self.config.known_bounds
+        return (kb[0], kb[1]) if kb else (float("inf"), -float("inf"))
+
+    def _reset_step_statistics(self):
+        if not hasattr(self, "_min_value"):
+            self._min_value, self._max_value = self._initial_bounds()
+        self.step_statistics = {
+            "search_time": 0.0, "update_time": 0.0, "reinvigoration_time": 0.0,
+            "evaluation_time": 0.0, "policy_calls": 0, "inference_time": 0.0,
+            "search_depth": 0, "num_sims": 0, "mem_usage": 0,
+            "min_value": self._min_value, "max_value": self._max_value,
+        }
+
+    # -------------------------------------------------------------- update
+    def update(self, action, obs):
+        """``mcts.py:159-263``: initial belief at t == 0, else re-root + reinvigorate."""
+        if self.root.is_absorbing:
+            return
+        start = time.time()
+        if self.root.t == 0:
+            self._last_action = None
+            a = -1
+        else:
+            a = int(action)
+        key = self.model.obs_key(obs)
+        absorbing = self._engine.update([a], [key])
+        self.root = dataclasses.replace(self.root, t=self.root.t + 1,
+                                        is_absorbing=bool(absorbing[0]))
+        self.step_statistics["update_time"] = time.time() - start
+
+    # -------------------------------------------------------------- search
+    def get_action(self):
+        """``mcts.py:269-306`` (fixed ``num_sims``, or chunks until the time limit)."""
+        if self.root.is_absorbing:
+            return self.action_space[0]
+        start = time.time()
+        if self._num_sims is not None:
+            self._engine.search(self._num_sims, fetch=False)
+            n_sims = self._num_sims
+        else:
+            n_sims, chunk = 0, 16
+            while time.time() - start < self.config.search_time_limit:
+                self._engine.search(chunk, fetch=False)
+                self._engine.root_stats()          # synchronises
+                n_sims += chunk
+                chunk = min(chunk * 2, 4096)
+        st = self._engine.root_stats()[0]
+        search_time = time.time() - start
+        A = len(self.action_space)
+        self._min_value, self._max_value = st.min_value, st.max_value
+        self.root = dataclasses.replace(
+            self.root, visits=st.root_visits, belief_size=st.belief_size,
+            child_visits=tuple(st.child_visits[:A]), child_values=tuple(st.child_values[:A]),
+            child_totals=tuple(st.child_totals[:A]))
+        self.step_statistics.update(
+            search_time=search_time, search_depth=st.search_depth, num_sims=n_sims,
+            min_value=st.min_value, max_value=st.max_value)
+        if self._num_sims is None:
+            # the time-bounded loop ran several launches; the last one chose the action
+            pass
+        return int(st.action)
+
+    def root_belief(self):
+        """Root particles as (t, v0, v1) packed u32 rows."""
+        return self._engine.root_belief(0)
+
+    def close(self):
+        self.search_policy.close()
+        for p in self.other_agent_policies.values():
+            p.close()
+        self._engine.close()
+
+    def __str__(self):
+        return "POMCP"
+
+
+class BatchedPOMCP:
+    """``num_trees`` independent POMCP planners searched by one launch.
+
+    Tree ``b`` uses RNG key ``(seed, tree_key_base + b)``; each tree is
+    bit-identical to a single ``POMCP`` (and to the oracle) with that key.
+    """
+
+    def __init__(self, model, agent_id, config: MCTSConfig, num_trees: int, num_sims: int,
+                 *, searches: int = 1, reroot: bool = False, capacities=None, stream=None,
+                 tree_key_base: int = 0, device: Optional[int] = None):
+        from posggym_baselines_amd.planning.engine import plan_capacities
+        if capacities is None:
+            step_limit = config.step_limit or model.spec.max_episode_steps
+            capacities = plan_capacities(config, step_limit, num_sims, searches, reroot=reroot)
+        self.num_trees = num_trees
+        self.num_sims = num_sims
+        self.engine = PomcpEngine(model, agent_id, config, num_trees=num_trees,
+                                  capacities=capacities, stream=stream,
+                                  tree_key_base=tree_key_base, device=device)
+        self.engine.reset()
+
+    def init_synthetic(self, env_seed_base: int = 1000):
+        """Synthetic Driving-v1 roots: per tree an env b0 sample and
+        the initial belief update; snapshot so ``restore()`` can re-search them."""
+        keys = self.engine.synthetic_obs(env_seed_base)
+        self.engine.update(np.full(self.num_trees, -1, dtype=np.int32), keys)
+        self.engine.snapshot()
+        return keys
+
+    def search(self, fetch=True):
+        return self.engine.search(self.num_sims, fetch=fetch)
+
+    def restore(self):
+        self.engine.restore()
+
+    def close(self):
+        self.engine.close()
+
+
+def uct_merge(visits: np.ndarray, totals: np.ndarray) -> np.ndarray:
+    """Root-parallel decision from summed (visits, total value) per action:
+    argmax of mean value, lowest index on ties."""
+    with np.errstate(invalid="ignore", divide="ignore"):
+        v = np.where(visits > 0, totals / np.maximum(visits, 1), -math.inf)
+    return np.argmax(v, axis=-1)

@@ -1,0 +1,69 @@
+"""Search (rollout / prior) policies — ``search_policy.py:16-185``.
+
+The GPU engine implements the uniform random rollout policy in-kernel
+(``RandomSearchPolicy``: ``sample_action`` = ``Discrete.sample``, uniform
+``get_pi``, no value).  Neural / posggym.agents search policies are out of
+scope for this build and are rejected by ``POMCP``.
+"""
+import abc
+from typing import Dict, Optional
+
+
+class SearchPolicy(abc.ABC):
+    def __init__(self, model, agent_id: str, policy_id: str):
+        self.model = model
+        self.agent_id = agent_id
+        self.policy_id = policy_id
+
+    @abc.abstractmethod
+    def get_initial_state(self):
+        ...
+
+    @abc.abstractmethod
+    def get_next_state(self, action, obs, state):
+        ...
+
+    @abc.abstractmethod
+    def sample_action(self, state):
+        ...
+
+    @abc.abstractmethod
+    def get_pi(self, state) -> Dict[int, float]:
+        ...
+
+    @abc.abstractmethod
+    def get_value(self, state) -> float:
+        ...
+
+    def get_state_from_history(self, initial_state, history):
+        state = initial_state
+        for a, o in history:
+            state = self.get_next_state(a, o, state)
+        return state
+
+    def close(self):
+        pass
+
+
+class RandomSearchPolicy(SearchPolicy):
+    """Uniform random rollout policy (runs inside the search kernel)."""
+
+    def __init__(self, model, agent_id: str):
+        super().__init__(model, agent_id, "RandomSearchPolicy")
+        self._action_space = model.action_spaces[agent_id]
+
+    def get_initial_state(self):
+        return {}
+
+    def get_next_state(self, action: Optional[int], obs, state):
+        return {}
+
+    def sample_action(self, state) -> int:
+        return self._action_space.sample()
+
+    def get_pi(self, state) -> Dict[int, float]:
+        n = self._action_space.n
+        return {a: 1.0 / n for a in range(n)}
+
+    def get_value(self, state) -> float:
+        raise NotImplementedError("RandomSearchPolicy does not support value estimates.")

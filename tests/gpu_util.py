@@ -1,0 +1,65 @@
+"""Drive the product (GPU) planner in the oracle's record format."""
+from oracle.episode import belief_digest, fhex, run_episode
+from oracle.driving import unpack_vehicle
+
+
+def product_config(cfg_kwargs, num_sims):
+    from posggym_baselines_amd.planning import KnownBounds, MCTSConfig
+    kw = dict(cfg_kwargs)
+    if kw.get("known_bounds") is not None:
+        kw["known_bounds"] = KnownBounds(*kw["known_bounds"])
+    return MCTSConfig(num_sims=num_sims, **kw)
+
+
+def rows_digest(rows):
+    parts = [((unpack_vehicle(int(v0)), unpack_vehicle(int(v1))), int(t)) for t, v0, v1 in rows]
+    return len(parts), belief_digest(parts)
+
+
+def stats_record(st, A, searched, action, rows):
+    rec = {"searched": searched, "action": int(action)}
+    if not searched:
+        return rec
+    rec["belief_size"], rec["belief_digest"] = rows_digest(rows)
+    rec["num_sims"] = int(st.num_sims)
+    if rec["num_sims"] > 0:
+        rec["search_depth"] = int(st.search_depth)
+        rec["root_visits"] = int(st.root_visits)
+        rec["child_visits"] = [int(x) for x in st.child_visits[:A]]
+        rec["child_values"] = [fhex(x) for x in st.child_values[:A]]
+        rec["child_totals"] = [fhex(x) for x in st.child_totals[:A]]
+        rec["min_value"] = fhex(st.min_value)
+        rec["max_value"] = fhex(st.max_value)
+    return rec
+
+
+def gpu_episode(cfg_kwargs, num_sims, env_seed, ego="0", max_steps=50):
+    from posggym_baselines_amd.envs import DrivingModel
+    from posggym_baselines_amd.planning import POMCP, RandomSearchPolicy
+    model = DrivingModel()
+    planner = POMCP(model, ego, product_config(cfg_kwargs, num_sims),
+                    RandomSearchPolicy(model, ego))
+    planner.reset()
+    records = []
+    A = model.action_spaces[ego].n
+
+    def step(obs):
+        searched = not planner.root.is_absorbing
+        a = planner.step(obs)
+        if not searched:
+            records.append({"searched": False, "action": int(a)})
+            return a
+        rows = planner.root_belief()
+        st = planner._engine.root_stats()[0]
+        rec = stats_record(st, A, True, a, rows)
+        rec["num_sims"] = int(planner.step_statistics["num_sims"])
+        if rec["num_sims"] == 0:
+            for k in ("search_depth", "root_visits", "child_visits", "child_values",
+                      "child_totals", "min_value", "max_value"):
+                rec.pop(k, None)
+        records.append(rec)
+        return a
+
+    trace = run_episode(step, env_seed, ego=ego, max_steps=max_steps)
+    planner.close()
+    return trace, records

@@ -1,0 +1,49 @@
+"""The host build of csrc/driving.h (through the C ABI) against the oracle's
+Python Driving-v1 restatement: same RNG stream, same states, rewards, obs."""
+import pytest
+
+from oracle.driving import DrivingModel as OracleDriving
+from oracle.driving import pack_obs, pack_vehicle
+from oracle.episode import ENV_TREE_BASE
+from oracle.rng import Streams
+from posggym_baselines_amd.envs import DrivingModel, pack_obs as product_pack_obs
+
+
+@pytest.mark.parametrize("grid", ["14x14RoundAbout", "7x7RoundAbout"])
+def test_host_model_matches_oracle(grid):
+    for seed in range(40):
+        o_streams = Streams(seed, ENV_TREE_BASE)
+        om = OracleDriving(o_streams, grid=grid)
+        pm = DrivingModel(grid=grid, seed=seed)
+        os_ = om.sample_initial_state()
+        ps = pm.sample_initial_state()
+        assert ps == (pack_vehicle(os_[0]), pack_vehicle(os_[1]))
+        oo = om.sample_initial_obs(os_)
+        po = pm.sample_initial_obs(ps)
+        assert {k: pack_obs(v) for k, v in oo.items()} == {k: product_pack_obs(v) for k, v in po.items()}
+        act_streams = Streams(seed + 777, 5)
+        for t in range(50):
+            acts = {"0": act_streams.randint(8, 5), "1": act_streams.randint(9, 5)}
+            ots = om.step(os_, acts)
+            pts = pm.step(ps, acts)
+            assert pts.state == (pack_vehicle(ots.state[0]), pack_vehicle(ots.state[1])), (seed, t)
+            assert pts.rewards == ots.rewards
+            assert pts.terminations == ots.terminations
+            assert pts.all_done == ots.all_done
+            for a in ("0", "1"):
+                assert product_pack_obs(pts.observations[a]) == pack_obs(ots.observations[a])
+                assert pts.observations[a] == ots.observations[a]
+            os_, ps = ots.state, pts.state
+            if ots.all_done:
+                break
+
+
+def test_grid_tables_match_oracle():
+    from oracle.driving import Grid, GRIDS as OG
+    from posggym_baselines_amd.envs.driving import GRIDS, build_grid_tables
+    assert GRIDS == OG
+    for name, rows in GRIDS.items():
+        w, h, wall, locs, dirs, dist = build_grid_tables(rows)
+        g = Grid(rows)
+        assert (w, h, locs, dirs) == (g.width, g.height, g.locs, g.init_dir)
+        assert dist == g.dist

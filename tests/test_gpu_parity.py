@@ -1,0 +1,137 @@
+"""GPU parity: the HIP engine through the C ABI against the reference goldens
+and the oracle (bit-exact: actions, visit counts, FP64 values, particles)."""
+import math
+
+import numpy as np
+import pytest
+
+from golden_util import EPISODE_CASES, cfg_kwargs, load
+from gpu_util import gpu_episode, product_config, stats_record
+from oracle.episode import run_episode
+from oracle.run import make_oracle, oracle_record
+
+pytestmark = pytest.mark.gpu
+
+SQRT2 = math.sqrt(2)
+TEST_CFG = dict(discount=0.95, search_time_limit=0.1, c=SQRT2, truncated=False,
+                action_selection="ucb", pucb_exploration_fraction=0.25, known_bounds=None,
+                step_limit=None, epsilon=0.92, seed=0, state_belief_only=True)
+
+
+def test_device_fp64_is_correctly_rounded():
+    import ctypes as C
+    from posggym_baselines_amd import _native as N
+    rng = np.random.default_rng(0)
+    n = 1 << 16
+    a = np.concatenate([rng.random(n // 2) * 10, np.exp(rng.normal(0, 20, n // 2))])
+    b = np.concatenate([rng.random(n // 2) + 1e-3, np.exp(rng.normal(0, 20, n // 2))])
+    out = np.zeros(4 * n)
+    P = C.POINTER(C.c_double)
+    assert N.load().pomcp_debug_fp_selftest(a.ctypes.data_as(P), b.ctypes.data_as(P), n,
+                                            out.ctypes.data_as(P)) == 0
+    out = out.reshape(n, 4)
+    assert np.array_equal(out[:, 0], np.sqrt(a))
+    assert np.array_equal(out[:, 1], a / b)
+    assert np.array_equal(out[:, 2], a + 0.95 * b)
+    assert np.array_equal(out[:, 3], (a - b) / (a + b))
+
+
+@pytest.mark.parametrize("case", EPISODE_CASES)
+def test_gpu_matches_reference_goldens(case):
+    data = load(case)
+    for ep in data["episodes"]:
+        kw = cfg_kwargs(ep["config"])
+        max_steps = 1 if case == "large_first_step" else 50
+        trace, records = gpu_episode(kw, data["num_sims"], ep["env_seed"], ego=data["ego"],
+                                     max_steps=max_steps)
+        assert len(records) == len(ep["records"])
+        for t, (got, exp) in enumerate(zip(records, ep["records"])):
+            assert got == exp, f"{case} step {t}"
+        assert trace == ep["trace"]
+
+
+def _oracle_first_step(cfg, num_sims, tree, env_seed, rekey=None):
+    p = make_oracle(cfg, num_sims, tree=tree)
+    recs = []
+
+    def step(obs):
+        p.update(None, obs)
+        if rekey is not None:
+            p.s.rekey(rekey)
+        a = p.get_action()
+        p.stats["searched"] = True
+        recs.append(oracle_record(p, True, a))
+        return a
+
+    run_episode(step, env_seed, max_steps=1)
+    return recs[0]
+
+
+def _batched_vs_oracle(cfg, num_trees, num_sims, check_trees, rekey=None):
+    from posggym_baselines_amd.envs import DrivingModel
+    from posggym_baselines_amd.planning import BatchedPOMCP
+    model = DrivingModel()
+    bp = BatchedPOMCP(model, "0", product_config(cfg, num_sims), num_trees, num_sims)
+    bp.init_synthetic(1000)
+    if rekey is not None:
+        bp.engine.rekey(rekey)
+    actions = bp.search()
+    stats = bp.engine.root_stats()
+    for b in check_trees:
+        exp = _oracle_first_step(cfg, num_sims, b, 1000 + b, rekey=rekey)
+        got = stats_record(stats[b], 5, True, actions[b], bp.engine.root_belief(b))
+        assert got == exp, f"tree {b}"
+    bp.close()
+    return stats
+
+
+def test_batched_synthetic_roots_ucb():
+    _batched_vs_oracle(TEST_CFG, 37, 256, range(37))
+
+
+def test_batched_synthetic_roots_pucb_deep():
+    cfg = dict(TEST_CFG, action_selection="pucb", discount=0.99, epsilon=0.01, seed=3)
+    _batched_vs_oracle(cfg, 9, 128, range(9))
+
+
+def test_root_parallel_rekey():
+    seed = TEST_CFG["seed"]
+    _batched_vs_oracle(TEST_CFG, 6, 200, range(6), rekey=seed ^ (3 << 32))
+
+
+def test_full_size_65536_sims():
+    """BASELINE config 2 size: 65,536 simulations from one root, bit-exact."""
+    stats = _batched_vs_oracle(TEST_CFG, 2, 65536, [0])
+    # size-independent properties on the other tree
+    st = stats[1]
+    assert st.num_sims == 65536 and st.root_visits == 65536
+    assert sum(st.child_visits[:5]) == 65536
+
+
+def test_many_trees_properties():
+    """Large batch: invariants that hold for every tree (visit conservation,
+    Welford totals, action = argmax value)."""
+    from posggym_baselines_amd.envs import DrivingModel
+    from posggym_baselines_amd.planning import BatchedPOMCP
+    model = DrivingModel()
+    B, S = 2048, 512
+    bp = BatchedPOMCP(model, "0", product_config(TEST_CFG, S), B, S)
+    bp.init_synthetic(5000)
+    actions = bp.search()
+    stats = bp.engine.root_stats()
+    for b in range(B):
+        st = stats[b]
+        v = np.array(st.child_visits[:5])
+        assert st.error == 0 and st.num_sims == S and st.root_visits == S and v.sum() == S
+        vals = np.array(st.child_values[:5])
+        tot = np.array(st.child_totals[:5])
+        assert np.allclose(vals[v > 0], tot[v > 0] / v[v > 0], rtol=1e-9, atol=1e-12)
+        assert vals[actions[b]] == vals.max()
+    # determinism: restore + search reproduces every tree bit for bit
+    first = [(s.action, tuple(s.child_visits), tuple(s.child_values)) for s in stats]
+    bp.restore()
+    bp.search()
+    again = [(s.action, tuple(s.child_visits), tuple(s.child_values))
+             for s in bp.engine.root_stats()]
+    assert first == again
+    bp.close()
