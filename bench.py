@@ -40,8 +40,8 @@ def parse():
     ap.add_argument("--sims", type=int, default=65536)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-sims", type=int, default=4096)
-    ap.add_argument("--cpu-sample-trees", type=int, default=3)
+    ap.add_argument("--cpu-sample-sims", type=int, default=16384)
+    ap.add_argument("--cpu-sample-trees", type=int, default=4)
     return ap.parse_args()
 
 
@@ -110,7 +110,7 @@ def main():
     cfg = MCTSConfig(seed=args.seed, num_sims=S, **TEST_CFG)
     model = DrivingModel()
     caps = plan_capacities(cfg, model.spec.max_episode_steps, S, 1, reroot=False,
-                           max_blocks=min(S + 64, 16384), max_obs_nodes=min(S + 64, 65536 + 64))
+                           max_blocks=min(S + 64, 4096), overflow_slots=1024)
     stream = torch.cuda.Stream(device=dev)
     bp = BatchedPOMCP(model, "0", cfg, B, S, capacities=caps, stream=stream.cuda_stream,
                       device=dev)

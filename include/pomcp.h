@@ -74,11 +74,10 @@ typedef struct pomcp_config {
   uint32_t tree_key_base;       /* tree t uses key tree_key_base + t */
   int32_t pad0;
   /* per-tree arena capacities */
-  int64_t max_obs_nodes;
-  int64_t max_blocks;           /* expanded obs nodes (A action nodes each) */
-  int64_t max_particles;        /* particle log records */
-  int64_t max_belief;           /* root belief records */
-  int64_t hash_slots;           /* power of two, multiple of 16 */
+  int64_t max_blocks;           /* expanded obs nodes: A x 128 B action nodes each */
+  int64_t max_particles;        /* particle log records (16 B) */
+  int64_t max_belief;           /* root belief records (16 B), x2 ping-pong */
+  int64_t overflow_slots;       /* children beyond 6 per action node; power of two >= 16 */
   /* host-computed FP64 tables (Python's own math.log / float.__pow__) */
   const double* log_table;      /* log_table[n] = math.log(n), n >= 1 */
   int64_t log_table_size;

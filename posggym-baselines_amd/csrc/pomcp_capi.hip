@@ -18,8 +18,8 @@
 using namespace pb;
 
 static_assert(sizeof(pomcp_grid) == sizeof(DrvGrid), "grid layout");
-static_assert(sizeof(Slot) == 16, "slot layout");
-static_assert(sizeof(ActRec) == 32, "action record layout");
+static_assert(sizeof(ActNode) == 128, "action node layout");
+static_assert(sizeof(OvfSlot) == 32, "overflow slot layout");
 
 struct pomcp_ctx {
   pomcp_config cfg;
@@ -31,7 +31,6 @@ struct pomcp_ctx {
   std::string err;
   bool have_snapshot = false;
   TreeHdr* snap_hdr = nullptr;
-  int2* snap_root = nullptr;
   std::vector<int32_t> host_upd;
   std::vector<pomcp_root_stats> host_stats;
 };
@@ -99,12 +98,12 @@ static int validate(const pomcp_config* c, std::string* why) {
   if (c->depth_limit < 0 || c->step_limit < 0) return bad("depth/step limit");
   if (c->num_particles < 1 || c->extra_particles < 0) return bad("num_particles");
   if (c->num_trees < 1) return bad("num_trees >= 1");
-  if (c->max_obs_nodes < 4 || c->max_obs_nodes > INT32_MAX) return bad("max_obs_nodes");
-  if (c->max_blocks < 1 || c->max_blocks * c->num_actions > INT32_MAX) return bad("max_blocks");
+  if (c->max_blocks < 1 || c->max_blocks > INT32_MAX / 64) return bad("max_blocks");
   if (c->max_particles < 1 || c->max_particles > INT32_MAX) return bad("max_particles");
   if (c->max_belief < 2 * (c->num_particles + c->extra_particles)) return bad("max_belief too small");
-  if (c->hash_slots < kBucket || (c->hash_slots & (c->hash_slots - 1)) != 0)
-    return bad("hash_slots must be a power of two >= 16");
+  if (c->overflow_slots < kBucket || (c->overflow_slots & (c->overflow_slots - 1)) != 0 ||
+      c->overflow_slots > (1ll << 28))
+    return bad("overflow_slots must be a power of two in [16, 2^28]");
   if (!c->log_table || c->log_table_size < 2) return bad("log_table");
   if (!c->discount_pow || c->discount_pow_size < 1) return bad("discount_pow");
   const pomcp_grid& g = c->grid;
@@ -165,12 +164,12 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
   d.limit_factor = c.reinvigoration_sample_limit_factor;
   d.kb_min = c.known_min;
   d.kb_max = c.known_max;
-  d.No = c.max_obs_nodes;
   d.Nb = c.max_blocks;
   d.Np = c.max_particles;
   d.Nr = c.max_belief;
-  d.H = c.hash_slots;
-  d.bucket_mask = (uint32_t)(c.hash_slots / kBucket - 1);
+  d.H = c.overflow_slots;
+  d.bucket_mask = (uint32_t)(c.overflow_slots / kBucket - 1);
+  d.ovf_base = (uint32_t)(c.max_blocks * c.num_actions * kSlots + 1);
   const int64_t B = c.num_trees;
   void* p;
 #define ALLOC(field, type, count)                                               \
@@ -182,10 +181,8 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
     d.field = reinterpret_cast<decltype(d.field)>(p);                           \
   } while (0)
   ALLOC(hdr, TreeHdr, B);
-  ALLOC(onode, int2, B * d.No);
-  ALLOC(ometa, int32_t, B * d.No);
-  ALLOC(an, ActRec, B * d.Nb * d.A);
-  ALLOC(hash, Slot, B * d.H);
+  ALLOC(an, ActNode, B * d.Nb * d.A);
+  ALLOC(ovf, OvfSlot, B * d.H);
   ALLOC(plog, uint4, B * d.Np);
   ALLOC(belief, uint4, B * 2 * d.Nr);
   ALLOC(logtab, double, c.log_table_size);
@@ -202,7 +199,7 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
   d.dpow_n = (int32_t)(c.discount_pow_size > INT32_MAX ? INT32_MAX : c.discount_pow_size);
   hipStream_t s = ctx->stream;
   // zero: hash epoch 0 is never valid, headers start empty
-  if (hipMemsetAsync(d.hash, 0, sizeof(Slot) * (size_t)(B * d.H), s) != hipSuccess ||
+  if (hipMemsetAsync(d.ovf, 0, sizeof(OvfSlot) * (size_t)(B * d.H), s) != hipSuccess ||
       hipMemsetAsync(d.hdr, 0, sizeof(TreeHdr) * (size_t)B, s) != hipSuccess ||
       hipMemsetAsync(d.stats, 0, sizeof(pomcp_root_stats) * (size_t)B, s) != hipSuccess ||
       hipMemcpyAsync((void*)d.logtab, c.log_table, sizeof(double) * c.log_table_size,
@@ -250,7 +247,6 @@ void pomcp_destroy(pomcp_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   for (void* p : ctx->allocs) (void)hipFree(p);
   if (ctx->snap_hdr) (void)hipFree(ctx->snap_hdr);
-  if (ctx->snap_root) (void)hipFree(ctx->snap_root);
   if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -397,26 +393,14 @@ int pomcp_snapshot(pomcp_ctx* ctx) {
   HIP_TRY(ctx, hipMemcpyAsync(h.data(), ctx->dp.hdr, sizeof(TreeHdr) * B, hipMemcpyDeviceToHost,
                               ctx->stream));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-  std::vector<int2> roots((size_t)B);
   for (int t = 0; t < B; ++t) {
-    // only the post-initial-update state (empty obs-child map) can be restored by
-    // bumping the map generation
+    // only the post-initial-update state (no blocks, no log, empty overflow map)
+    // is restorable by resetting the header and bumping the map generation
     if (h[t].root_t != 1 || h[t].n_blocks != 0 || h[t].n_log != 0 || h[t].error != 0)
       return fail(ctx, POMCP_E_STATE, "snapshot: every tree must be right after its initial update");
-    roots[t] = make_int2(-1, 0);
   }
-  if (!ctx->snap_hdr) {
-    HIP_TRY(ctx, hipMalloc(&ctx->snap_hdr, sizeof(TreeHdr) * B));
-    HIP_TRY(ctx, hipMalloc(&ctx->snap_root, sizeof(int2) * B));
-  }
-  for (int t = 0; t < B; ++t) {
-    int2 r;
-    HIP_TRY(ctx, hipMemcpy(&r, ctx->dp.onode + (int64_t)t * ctx->dp.No + h[t].root, sizeof(int2),
-                           hipMemcpyDeviceToHost));
-    roots[t] = r;
-  }
+  if (!ctx->snap_hdr) HIP_TRY(ctx, hipMalloc(&ctx->snap_hdr, sizeof(TreeHdr) * B));
   HIP_TRY(ctx, hipMemcpy(ctx->snap_hdr, h.data(), sizeof(TreeHdr) * B, hipMemcpyHostToDevice));
-  HIP_TRY(ctx, hipMemcpy(ctx->snap_root, roots.data(), sizeof(int2) * B, hipMemcpyHostToDevice));
   ctx->have_snapshot = true;
   return POMCP_OK;
 }
@@ -426,7 +410,7 @@ int pomcp_restore(pomcp_ctx* ctx) {
   if (!ctx->have_snapshot) return fail(ctx, POMCP_E_STATE, "restore without snapshot");
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   hipLaunchKernelGGL(k_restore, dim3(grid_blocks(ctx->dp.B)), dim3(256), 0, ctx->stream, ctx->dp,
-                     ctx->snap_hdr, ctx->snap_root);
+                     ctx->snap_hdr);
   HIP_TRY(ctx, hipGetLastError());
   return POMCP_OK;
 }

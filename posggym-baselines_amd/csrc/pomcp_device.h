@@ -1,12 +1,15 @@
 // Device-side data layout and wave-level helpers of the POMCP engine.
 //
 // One 64-lane wavefront owns one search tree (one planner).  Serial parts of
-// the reference's per-simulation loop run wave-uniform (every lane holds the
-// same value), the data-parallel parts are spread over lanes:
-//   * UCB / PUCB scores of the A action children  -> lanes 0..A-1
-//   * the ego observation window (15 cells)       -> lanes 0..14, 2 ballots
-//   * obs-child lookup (16-slot hash bucket)      -> lanes 0..15, 1 ballot
-//   * belief extraction at re-root                -> 64 log records / step
+// the reference's per-simulation loop run wave-uniform (scalar registers where
+// the compiler can keep them), the data-parallel parts are spread over lanes:
+//   * one tree level = one coalesced 640 B load of an action block
+//     (5 action nodes x 128 B, lane l holds bytes [16 l, 16 l + 16))
+//   * UCB / PUCB scores of the A children     -> lanes 8a (stats part 0)
+//   * obs-child lookup among 6 inline slots    -> lanes 8a+2 .. 8a+7, 1 ballot
+//   * the ego observation window (15 cells)   -> lanes 0..14, 2 ballots
+//   * belief extraction at re-root            -> 64 log records / step
+//   * RNG: each lane computes one Philox block, a draw is a readlane
 // A tree is touched by exactly one wave, so no atomics are needed.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -19,51 +22,69 @@
 namespace pb {
 
 constexpr int kWave = 64;
-constexpr int kTreesPerBlock = 4;        // 256-thread workgroups, one tree per wave
-constexpr int kBucket = 16;              // hash bucket = 16 slots = 256 B
-constexpr int kEpochShift = 50;          // obs keys use bits 0..49
+constexpr int kTreesPerBlock = 4;      // 256-thread workgroups, one tree per wave
+constexpr int kSlots = 6;              // inline obs children per action node
+constexpr int kLanesPerAct = 8;        // 128 B action node = 8 x 16 B
+constexpr int kBucket = 16;            // overflow map bucket (16 x 32 B)
+constexpr int kEpochShift = 50;        // obs keys use bits 0..49
 constexpr uint32_t kEpochMask = 0x3FFF;
-constexpr int kMaxPath = 64;             // tree levels per simulation (one VGPR lane each)
+constexpr uint64_t kObsMask = (1ull << 50) - 1;
+constexpr uint64_t kValidBit = 1ull << 62;
+constexpr uint64_t kAbsorbBit = 1ull << 63;
+constexpr int kMaxPath = 64;           // tree levels per simulation (one lane each)
+constexpr uint32_t kRootId = 0;        // obs node id of a root created by the initial update
 
-// Action node: ActionNode.{visits, value, total_value, agg} (node.py:120-178).
-struct ActRec {
+// Action node (node.py:120-178) with its obs children inline (node.py:144-160).
+// 128 B: part 0 {visits, pad, value}, part 1 {total, agg}, parts 2..7 children.
+struct ChildSlot {
+  uint64_t key;     // obs key | valid << 62 | is_absorbing << 63
+  int32_t block;    // action block of the child obs node (-1 = leaf)
+  int32_t visits;   // ObsNode.visits
+};
+struct ActNode {
   int32_t visits;
   int32_t pad;
   double value;
   double total;
   double agg;
+  ChildSlot child[kSlots];
 };
 
-// obs-child map entry: (action node, observation) -> obs node (node.py:144-160).
-struct Slot {
-  uint64_t key;      // obs key | epoch << 50
-  uint32_t an;       // action node index
-  uint32_t child;    // obs node index
+// Overflow children (> kSlots per action node): open-addressing map keyed by
+// (action node, obs).  32 B entries; valid when key's epoch matches.
+struct OvfSlot {
+  uint64_t key;     // obs | epoch << 50
+  uint32_t an;      // action node index
+  uint32_t flags;   // bit 0: is_absorbing
+  int32_t block;
+  int32_t visits;
+  uint64_t pad;
 };
 
 // Per-tree header (device resident between calls).
 struct TreeHdr {
-  int32_t root, n_obs, n_blocks, n_log;
-  int32_t belief_size, belief_sel, epoch, error;
-  int32_t root_t, root_abs, pad0, pad1;
+  int32_t n_blocks, n_log, n_nodes, error;
+  int32_t belief_size, belief_sel, epoch, root_t;
+  uint32_t root_id;
+  int32_t root_blk, root_visits, root_abs;
   double mm_min, mm_max;
   uint64_t seed;
   uint32_t tree_key;
-  uint32_t ctr[5];
+  uint32_t ctr[5];     // belief, select, model, act0, act1
+  int32_t pad[2];
 };
 
 struct DevParams {
   int32_t B, A, ego, other, sel, depth_limit, step_limit, n_target, has_kb, ncells;
   double discount, c, pucb_f, limit_factor, kb_min, kb_max;
-  int64_t No, Nb, Np, Nr, H;
+  int64_t Nb, Np, Nr, H;
   uint32_t bucket_mask;
+  uint32_t ovf_base;    // node ids >= ovf_base are overflow entries
   TreeHdr* hdr;
-  int2* onode;          // {block, visits}
-  int32_t* ometa;       // t << 1 | is_absorbing
-  ActRec* an;
-  Slot* hash;
-  uint4* plog;          // {obs node, t, v0, v1}
-  uint4* belief;        // 2 x Nr per tree: {t, v0, v1, 0}
+  ActNode* an;          // [B][Nb][A]
+  OvfSlot* ovf;         // [B][H]
+  uint4* plog;          // [B][Np] {obs node id, t, v0, v1}
+  uint4* belief;        // [B][2][Nr] {t, v0, v1, 0}
   const double* logtab;
   int64_t logtab_n;
   const double* dpow;
@@ -80,6 +101,9 @@ struct DevParams {
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 __device__ __forceinline__ int rl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ uint32_t rlu(uint32_t v, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
 
 __device__ __forceinline__ double rl_d(double v, int l) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
@@ -88,6 +112,15 @@ __device__ __forceinline__ double rl_d(double v, int l) {
 }
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t uniu(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return (uint64_t)uniu((uint32_t)v) | ((uint64_t)uniu((uint32_t)(v >> 32)) << 32);
+}
+__device__ __forceinline__ double uni_d(double v) {
+  return __hiloint2double(uni(__double2hiint(v)), uni(__double2loint(v)));
+}
 
 __device__ __forceinline__ uint32_t spread16(uint32_t x) {
   x &= 0xFFFFu;
@@ -106,10 +139,10 @@ __device__ __forceinline__ uint64_t obs_key_wave(const DrvGrid& g, uint32_t self
   const uint64_t b0 = __ballot(cell & 1);
   const uint64_t b1 = __ballot(cell & 2);
   const uint64_t cells = (uint64_t)(spread16((uint32_t)b0) | (spread16((uint32_t)b1) << 1));
-  return cells | obs_tail(g, self);
+  return uni64(cells | obs_tail(g, self));
 }
 
-__device__ __forceinline__ uint32_t slot_hash(uint32_t an, uint64_t key) {
+__device__ __forceinline__ uint32_t ovf_hash(uint32_t an, uint64_t key) {
   uint64_t h = key ^ ((uint64_t)an * 0x9E3779B97F4A7C15ull);
   h ^= h >> 33;
   h *= 0xFF51AFD7ED558CCDull;
@@ -118,5 +151,27 @@ __device__ __forceinline__ uint32_t slot_hash(uint32_t an, uint64_t key) {
   h ^= h >> 33;
   return (uint32_t)h;
 }
+
+// Wave-cached Philox stream: lane i holds the 4 words of block (page * 64 + i),
+// so 256 consecutive draws are readlanes; the wave refills the page in one
+// pass (64 blocks in parallel).  Same words as philox_word() (philox.h).
+struct CachedStream {
+  uint32_t w0, w1, w2, w3;   // per-lane
+  __device__ __forceinline__ void refill(uint64_t seed, uint32_t tree, uint32_t stream,
+                                         uint32_t page) {
+    uint32_t c[4] = {page * 64u + (uint32_t)lane_id(), 0u, stream, (uint32_t)(seed >> 32)};
+    philox4x32_10(c, (uint32_t)seed, tree);
+    w0 = c[0];
+    w1 = c[1];
+    w2 = c[2];
+    w3 = c[3];
+  }
+  __device__ __forceinline__ uint32_t get(uint32_t j) const {
+    const int l = (int)((j >> 2) & 63u);
+    const uint32_t a = rlu(w0, l), b = rlu(w1, l), c = rlu(w2, l), d = rlu(w3, l);
+    const uint32_t r = j & 3u;
+    return (r & 2u) ? ((r & 1u) ? d : c) : ((r & 1u) ? b : a);
+  }
+};
 
 }  // namespace pb

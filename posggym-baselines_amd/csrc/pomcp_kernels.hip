@@ -2,9 +2,10 @@
 //
 // Replaces posggym_baselines/planning/mcts.py:269-452 (get_action, _simulate,
 // _rollout, UCB/PUCB/min-visit selection, final action choice),
-// node.py (ObsNode/ActionNode -> SoA arena), belief.py (ParticleBelief ->
-// particle log + root belief buffer, BeliefRejectionSampler -> k_update) and
-// utils.py:15-42 (MinMaxStats -> two registers).  One wavefront per tree.
+// node.py (ObsNode/ActionNode -> 128 B action records with inline children),
+// belief.py (ParticleBelief -> particle log + root belief buffer,
+// BeliefRejectionSampler -> k_update) and utils.py:15-42 (MinMaxStats -> two
+// registers).  One wavefront per tree; see pomcp_device.h for the lane map.
 //
 // FP64 arithmetic follows the reference's operation order exactly and is built
 // with -ffp-contract=off; log(N) and discount**k come from host tables computed
@@ -22,140 +23,151 @@ __device__ __forceinline__ void stage_grid(const DrvGrid* src, DrvGrid& dst) {
   __syncthreads();
 }
 
-// Everything one wave needs about its tree, header fields held in registers.
+__device__ __forceinline__ double hilo(uint32_t lo, uint32_t hi) {
+  return __hiloint2double((int)hi, (int)lo);
+}
+__device__ __forceinline__ uint4 pack_stats0(int visits, double value) {
+  return make_uint4((uint32_t)visits, 0u, (uint32_t)__double2loint(value),
+                    (uint32_t)__double2hiint(value));
+}
+__device__ __forceinline__ uint4 pack_stats1(double total, double agg) {
+  return make_uint4((uint32_t)__double2loint(total), (uint32_t)__double2hiint(total),
+                    (uint32_t)__double2loint(agg), (uint32_t)__double2hiint(agg));
+}
+
+// Result of looking up / inserting an obs child (ActionNode.children[obs]).
+struct ChildRef {
+  uint32_t id;        // obs node id (particle log key)
+  int blk;            // action block of the child (-1 = leaf)
+  int visits;         // ObsNode.visits after this visit
+  int absorbing;
+  int lane;           // lane holding the inline slot in the level registers (-1: overflow)
+  int32_t* blk_ptr;   // where the child's block index lives (for expansion)
+};
+
 struct Tree {
   const DevParams& p;
   const DrvGrid& g;
   int tree, lane;
-  int2* onode;
-  int32_t* ometa;
-  ActRec* an;
-  uint4* hash;
+  ActNode* an;
+  OvfSlot* ovf;
   uint4* plog;
-  uint4* bel;          // 2 * Nr records
-  int root, n_obs, n_blocks, n_log, bsize, bsel, epoch, err, root_t, root_abs;
+  uint4* bel;
+  int n_blocks, n_log, n_nodes, err, bsize, bsel, epoch, root_t;
+  uint32_t root_id;
+  int root_blk, root_visits, root_abs;
   double mm_min, mm_max;
-  Streams rs;
+  uint64_t seed;
+  uint32_t tkey;
+  uint32_t c_belief, c_select, c_model, c_act0, c_act1;
+  CachedStream r_belief, r_model, r_act0, r_act1;
   int64_t c_levels, c_expand, c_new, c_rollout, c_probes;
 
   __device__ Tree(const DevParams& pp, const DrvGrid& gg, int t) : p(pp), g(gg), tree(t) {
     lane = lane_id();
-    onode = p.onode + (int64_t)t * p.No;
-    ometa = p.ometa + (int64_t)t * p.No;
     an = p.an + (int64_t)t * p.Nb * p.A;
-    hash = reinterpret_cast<uint4*>(p.hash + (int64_t)t * p.H);
+    ovf = p.ovf + (int64_t)t * p.H;
     plog = p.plog + (int64_t)t * p.Np;
     bel = p.belief + (int64_t)t * 2 * p.Nr;
     const TreeHdr h = p.hdr[t];
-    root = uni(h.root);
-    n_obs = uni(h.n_obs);
     n_blocks = uni(h.n_blocks);
     n_log = uni(h.n_log);
+    n_nodes = uni(h.n_nodes);
+    err = uni(h.error);
     bsize = uni(h.belief_size);
     bsel = uni(h.belief_sel);
     epoch = uni(h.epoch);
-    err = uni(h.error);
     root_t = uni(h.root_t);
+    root_id = uniu(h.root_id);
+    root_blk = uni(h.root_blk);
+    root_visits = uni(h.root_visits);
     root_abs = uni(h.root_abs);
-    mm_min = h.mm_min;
-    mm_max = h.mm_max;
-    rs.seed = h.seed;
-    rs.tree = h.tree_key;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) rs.ctr[k] = (uint32_t)uni((int)h.ctr[k]);
+    mm_min = uni_d(h.mm_min);
+    mm_max = uni_d(h.mm_max);
+    seed = uni64(h.seed);
+    tkey = uniu(h.tree_key);
+    c_belief = uniu(h.ctr[0]);
+    c_select = uniu(h.ctr[1]);
+    c_model = uniu(h.ctr[2]);
+    c_act0 = uniu(h.ctr[3]);
+    c_act1 = uniu(h.ctr[4]);
     c_levels = c_expand = c_new = c_rollout = c_probes = 0;
+  }
+
+  __device__ void warm_rng() {
+    r_belief.refill(seed, tkey, S_BELIEF, c_belief >> 8);
+    r_model.refill(seed, tkey, S_MODEL, c_model >> 8);
+    r_act0.refill(seed, tkey, S_ACT_BASE, c_act0 >> 8);
+    r_act1.refill(seed, tkey, S_ACT_BASE + 1, c_act1 >> 8);
   }
 
   __device__ void store_header() {
     if (lane != 0) return;
     TreeHdr h;
-    h.root = root;
-    h.n_obs = n_obs;
     h.n_blocks = n_blocks;
     h.n_log = n_log;
+    h.n_nodes = n_nodes;
+    h.error = err;
     h.belief_size = bsize;
     h.belief_sel = bsel;
     h.epoch = epoch;
-    h.error = err;
     h.root_t = root_t;
+    h.root_id = root_id;
+    h.root_blk = root_blk;
+    h.root_visits = root_visits;
     h.root_abs = root_abs;
-    h.pad0 = h.pad1 = 0;
     h.mm_min = mm_min;
     h.mm_max = mm_max;
-    h.seed = rs.seed;
-    h.tree_key = rs.tree;
-    for (int k = 0; k < 5; ++k) h.ctr[k] = rs.ctr[k];
+    h.seed = seed;
+    h.tree_key = tkey;
+    h.ctr[0] = c_belief;
+    h.ctr[1] = c_select;
+    h.ctr[2] = c_model;
+    h.ctr[3] = c_act0;
+    h.ctr[4] = c_act1;
+    h.pad[0] = h.pad[1] = 0;
     p.hdr[tree] = h;
+  }
+
+  // ------------------------------------------------------------- RNG draws
+  __device__ __forceinline__ uint32_t draw(CachedStream& cs, uint32_t& ctr, uint32_t stream) {
+    const uint32_t j = ctr++;
+    if ((j & 255u) == 0u) cs.refill(seed, tkey, stream, j >> 8);
+    return cs.get(j);
+  }
+  __device__ uint32_t d_belief(uint32_t n) { return uniform_int(draw(r_belief, c_belief, S_BELIEF), n); }
+  __device__ uint32_t d_model(uint32_t n) { return uniform_int(draw(r_model, c_model, S_MODEL), n); }
+  __device__ uint32_t d_act(int agent, uint32_t n) {
+    return agent == 0 ? uniform_int(draw(r_act0, c_act0, S_ACT_BASE), n)
+                      : uniform_int(draw(r_act1, c_act1, S_ACT_BASE + 1), n);
+  }
+  __device__ uint32_t d_select(uint32_t n) {
+    return uniform_int(uniu(philox_word(seed, tkey, S_SELECT, c_select++)), n);
+  }
+  __device__ double d_select_float() {
+    return uniform_float(uniu(philox_word(seed, tkey, S_SELECT, c_select++)));
   }
 
   __device__ uint4* root_belief() { return bel + (int64_t)bsel * p.Nr; }
   __device__ uint4* other_belief() { return bel + (int64_t)(bsel ^ 1) * p.Nr; }
 
-  // ObsNode(...) (node.py:32-56)
-  __device__ int new_obs_node(int t, int visits, int absorbing) {
-    if (n_obs >= p.No) {
-      err = POMCP_E_ARENA;
-      return -1;
-    }
-    const int i = n_obs++;
-    if (lane == 0) {
-      onode[i] = make_int2(-1, visits);
-      ometa[i] = (t << 1) | absorbing;
-    }
-    ++c_new;
-    return i;
+  __device__ uint4 load_block(int blk) const {
+    uint4 q = make_uint4(0, 0, 0, 0);
+    if (lane < kLanesPerAct * p.A) q = reinterpret_cast<const uint4*>(an + (int64_t)blk * p.A)[lane];
+    return q;
   }
 
-  // ObsNode.add_child for every action (mcts.py:279-281, 318-321).
-  __device__ int expand(int node) {
+  // ObsNode.add_child for every action (mcts.py:279-281, 318-321): zeroed block.
+  __device__ int alloc_block() {
     if (n_blocks >= p.Nb) {
       err = POMCP_E_ARENA;
       return -1;
     }
     const int b = n_blocks++;
-    if (lane < p.A) {
-      ActRec z;
-      z.visits = 0;
-      z.pad = 0;
-      z.value = 0.0;
-      z.total = 0.0;
-      z.agg = 0.0;
-      an[(int64_t)b * p.A + lane] = z;
-    }
-    if (lane == 0) onode[node].x = b;
+    if (lane < kLanesPerAct * p.A)
+      reinterpret_cast<uint4*>(an + (int64_t)b * p.A)[lane] = make_uint4(0, 0, 0, 0);
     ++c_expand;
     return b;
-  }
-
-  // ActionNode.children[obs] lookup, inserting a new ObsNode when absent.
-  __device__ int find_or_insert(uint32_t ani, uint64_t okey, bool insert, int t_child,
-                                int visits, int absorbing, bool* is_new) {
-    const uint64_t key = okey | ((uint64_t)epoch << kEpochShift);
-    uint32_t b = slot_hash(ani, okey) & p.bucket_mask;
-    *is_new = false;
-    for (uint32_t probe = 0; probe <= p.bucket_mask; ++probe) {
-      ++c_probes;
-      uint4 s = make_uint4(0, 0, 0, 0);
-      if (lane < kBucket) s = hash[(int64_t)b * kBucket + lane];
-      const uint64_t skey = (uint64_t)s.x | ((uint64_t)s.y << 32);
-      const bool valid = lane < kBucket && (uint32_t)(skey >> kEpochShift) == (uint32_t)epoch;
-      const uint64_t m = __ballot(valid && skey == key && s.z == ani);
-      if (m) return rl((int)s.w, __ffsll((long long)m) - 1);
-      const uint64_t e = __ballot(lane < kBucket && !valid);
-      if (e) {
-        if (!insert) return -1;
-        const int c = new_obs_node(t_child, visits, absorbing);
-        if (c < 0) return -1;
-        if (lane == __ffsll((long long)e) - 1)
-          hash[(int64_t)b * kBucket + lane] =
-              make_uint4((uint32_t)key, (uint32_t)(key >> 32), ani, (uint32_t)c);
-        *is_new = true;
-        return c;
-      }
-      b = (b + 1) & p.bucket_mask;
-    }
-    err = POMCP_E_ARENA;
-    return -1;
   }
 
   __device__ void mm_update(double v) {     // utils.py:29-32
@@ -168,68 +180,14 @@ struct Tree {
     return v;
   }
 
-  // Joint step with random other agent; returns the packed next state.
   __device__ void joint_step(uint32_t s0, uint32_t s1, int ego_a, int oth_a, uint32_t* n0,
                              uint32_t* n1) {
-    const uint32_t j = rs.model(2);   // Python random.shuffle of the exec order
+    const uint32_t j = d_model(2);   // Python random.shuffle of the exec order
     const int a0 = p.ego == 0 ? ego_a : oth_a;
     const int a1 = p.ego == 0 ? oth_a : ego_a;
     drv_step2(g, s0, s1, a0, a1, j, n0, n1);
-  }
-
-  // _search_action_selection (mcts.py:492-563); lanes 0..A-1 score children.
-  __device__ int select(int blk, int visits) {
-    const int A = p.A;
-    // (PUCB with visits == 0 is handled by pucb_prior_draw before this call.)
-    if (visits == 0) return (int)rs.select((uint32_t)A);   // mcts.py:532, 555
-    const ActRec* rec = an + (int64_t)blk * A;
-    int n = 0;
-    double v = 0.0;
-    if (lane < A) {
-      const int4 q = *reinterpret_cast<const int4*>(rec + lane);   // {visits, pad, value}
-      n = q.x;
-      v = __hiloint2double(q.w, q.z);
-    }
-    if (p.sel == POMCP_SEL_UNIFORM) {   // min_visit_action_selection
-      int min_n = visits + 1, best = 0;
-      for (int a = 0; a < A; ++a) {
-        const int na = rl(n, a);
-        if (na < min_n) {
-          min_n = na;
-          best = a;
-        }
-      }
-      return best;
-    }
-    double score = -__builtin_inf();
-    if (p.sel == POMCP_SEL_UCB) {
-      const uint64_t unv = __ballot(lane < A && n == 0);   // mcts.py:539-540
-      if (unv) return __ffsll((long long)unv) - 1;
-      if (visits >= p.logtab_n) {
-        err = POMCP_E_ARENA;
-        return 0;
-      }
-      const double log_n = p.logtab[visits];
-      if (lane < A) score = normalize(v) + p.c * sqrt(log_n / (double)n);   // mcts.py:541-542
-    } else {   // PUCB, mcts.py:502-527
-      const double noise = 1.0 / (double)A;
-      const double prior = (1.0 / (double)A) * (1.0 - p.pucb_f) + p.pucb_f * noise;
-      const double sqrt_n = sqrt((double)visits);
-      if (lane < A) {
-        const double explore = p.c * prior * (sqrt_n / (double)(1 + n));
-        score = (n > 0 ? normalize(v) : 0.0) + explore;
-      }
-    }
-    double best_v = -__builtin_inf();
-    int best = 0;
-    for (int a = 0; a < A; ++a) {   // strict '>' in action order
-      const double sa = rl_d(score, a);
-      if (sa > best_v) {
-        best_v = sa;
-        best = a;
-      }
-    }
-    return best;
+    *n0 = uniu(*n0);
+    *n1 = uniu(*n1);
   }
 
   // PUCB with N == 0 (mcts.py:494-500): random.choices(actions, weights=prior),
@@ -244,27 +202,69 @@ struct Tree {
       acc = acc + w;
       cum[k] = acc;
     }
-    const double total = cum[A - 1] + 0.0;
-    const double x = rs.select_float() * total;
-    for (int k = 0; k < A - 1; ++k)   // bisect_right(cum, x, 0, A-1)
+    const double x = d_select_float() * (cum[A - 1] + 0.0);
+    for (int k = 0; k < A - 1; ++k)
       if (x < cum[k]) return k;
     return A - 1;
   }
 
-  __device__ int choose_action(int blk, int visits) {
+  // _search_action_selection (mcts.py:492-563) on a block held in registers.
+  __device__ int choose(const uint4& q, int visits) {
+    const int A = p.A;
     if (p.sel == POMCP_SEL_PUCB && visits == 0) return pucb_prior_draw();
-    return select(blk, visits);
+    if (visits == 0) return (int)d_select((uint32_t)A);   // mcts.py:532, 555
+    const bool head = (lane & 7) == 0 && lane < kLanesPerAct * A;
+    const int n = head ? (int)q.x : 0;
+    const double v = head ? hilo(q.z, q.w) : 0.0;
+    if (p.sel == POMCP_SEL_UNIFORM) {   // min_visit_action_selection
+      int min_n = visits + 1, best = 0;
+      for (int a = 0; a < A; ++a) {
+        const int na = rl(n, 8 * a);
+        if (na < min_n) {
+          min_n = na;
+          best = a;
+        }
+      }
+      return best;
+    }
+    double score = -__builtin_inf();
+    if (p.sel == POMCP_SEL_UCB) {
+      const uint64_t unv = __ballot(head && n == 0);   // mcts.py:539-540
+      if (unv) return (__ffsll((long long)unv) - 1) >> 3;
+      if (visits >= p.logtab_n) {
+        err = POMCP_E_ARENA;
+        return 0;
+      }
+      const double log_n = p.logtab[visits];
+      if (head) score = normalize(v) + p.c * sqrt(log_n / (double)n);   // mcts.py:541-542
+    } else {   // PUCB, mcts.py:502-527
+      const double noise = 1.0 / (double)A;
+      const double prior = (1.0 / (double)A) * (1.0 - p.pucb_f) + p.pucb_f * noise;
+      const double sqrt_n = sqrt((double)visits);
+      if (head) score = (n > 0 ? normalize(v) : 0.0) + p.c * prior * (sqrt_n / (double)(1 + n));
+    }
+    double best_v = -__builtin_inf();
+    int best = 0;
+    for (int a = 0; a < A; ++a) {   // strict '>' in action order
+      const double sa = rl_d(score, 8 * a);
+      if (sa > best_v) {
+        best_v = sa;
+        best = a;
+      }
+    }
+    return best;
   }
 
-  // _final_action_selection (mcts.py:565-600).
-  __device__ int final_action(int blk, int visits) {
+  // _final_action_selection (mcts.py:565-600) on the root block registers.
+  __device__ int final_action(const uint4& q, int visits) {
     const int A = p.A;
+    uint32_t ties = 0;
+    int nt = 0;
     if (p.sel == POMCP_SEL_PUCB) {
-      if (visits == 0) return (int)rs.select((uint32_t)A);
-      int mx = 0, nt = 0;
-      uint32_t ties = 0;
+      if (visits == 0) return (int)d_select((uint32_t)A);
+      int mx = 0;
       for (int a = 0; a < A; ++a) {
-        const int na = an[(int64_t)blk * A + a].visits;
+        const int na = rl((int)q.x, 8 * a);
         if (na == mx) {
           ties |= 1u << a;
           ++nt;
@@ -274,24 +274,139 @@ struct Tree {
           nt = 1;
         }
       }
-      return kth_bit(ties, rs.select((uint32_t)nt));
-    }
-    if (blk < 0) return (int)rs.select((uint32_t)A);
-    double mx = -__builtin_inf();
-    int nt = 0;
-    uint32_t ties = 0;
-    for (int a = 0; a < A; ++a) {
-      const double va = an[(int64_t)blk * A + a].value;
-      if (va == mx) {
-        ties |= 1u << a;
-        ++nt;
-      } else if (va > mx) {
-        mx = va;
-        ties = 1u << a;
-        nt = 1;
+    } else {
+      double mx = -__builtin_inf();
+      for (int a = 0; a < A; ++a) {
+        const double va = hilo(rlu(q.z, 8 * a), rlu(q.w, 8 * a));
+        if (va == mx) {
+          ties |= 1u << a;
+          ++nt;
+        } else if (va > mx) {
+          mx = va;
+          ties = 1u << a;
+          nt = 1;
+        }
       }
     }
-    return kth_bit(ties, rs.select((uint32_t)nt));
+    return kth_bit(ties, d_select((uint32_t)nt));
+  }
+
+  // Overflow map (children beyond the kSlots inline ones).
+  __device__ bool ovf_lookup(uint32_t ani, uint64_t okey, bool insert, int init_visits,
+                             int absorbing, ChildRef* c, bool* is_new) {
+    const uint64_t key = okey | ((uint64_t)epoch << kEpochShift);
+    uint32_t b = ovf_hash(ani, okey) & p.bucket_mask;
+    *is_new = false;
+    for (uint32_t probe = 0; probe <= p.bucket_mask; ++probe) {
+      ++c_probes;
+      uint4 s = make_uint4(0, 0, 0, 0), s2 = make_uint4(0, 0, 0, 0);
+      OvfSlot* e = ovf + (int64_t)b * kBucket + (lane & (kBucket - 1));
+      if (lane < kBucket) {
+        s = reinterpret_cast<const uint4*>(e)[0];
+        s2 = reinterpret_cast<const uint4*>(e)[1];
+      }
+      const uint64_t skey = (uint64_t)s.x | ((uint64_t)s.y << 32);
+      const bool valid = lane < kBucket && (uint32_t)(skey >> kEpochShift) == (uint32_t)epoch;
+      const uint64_t m = __ballot(valid && skey == key && s.z == ani);
+      const uint32_t base = (uint32_t)(b * kBucket);
+      if (m) {
+        const int L = __ffsll((long long)m) - 1;
+        c->id = p.ovf_base + base + (uint32_t)L;
+        c->blk = rl((int)s2.x, L);
+        c->visits = rl((int)s2.y, L);
+        c->absorbing = rl((int)s.w, L) & 1;
+        c->lane = -1;
+        c->blk_ptr = &(ovf + (int64_t)b * kBucket + L)->block;
+        return true;
+      }
+      const uint64_t em = __ballot(lane < kBucket && !valid);
+      if (em) {
+        if (!insert) return false;
+        const int L = __ffsll((long long)em) - 1;
+        if (lane == L) {
+          reinterpret_cast<uint4*>(e)[0] =
+              make_uint4((uint32_t)key, (uint32_t)(key >> 32), ani, (uint32_t)absorbing);
+          reinterpret_cast<uint4*>(e)[1] = make_uint4((uint32_t)-1, (uint32_t)init_visits, 0u, 0u);
+        }
+        c->id = p.ovf_base + base + (uint32_t)L;
+        c->blk = -1;
+        c->visits = init_visits;
+        c->absorbing = absorbing;
+        c->lane = -1;
+        c->blk_ptr = &(ovf + (int64_t)b * kBucket + L)->block;
+        *is_new = true;
+        ++n_nodes;
+        ++c_new;
+        return true;
+      }
+      b = (b + 1) & p.bucket_mask;
+    }
+    err = POMCP_E_ARENA;
+    return false;
+  }
+
+  // ActionNode.children lookup for action a of the block `blk` held in q.
+  // Search path (visit): visits += 1 / new child with init_visits=1, is_absorbing
+  // overwritten (mcts.py:358-370).  Update path: no visit count change; new
+  // child with init_visits=0 and the root's absorbing flag (mcts.py:240-247).
+  __device__ bool child_ref(uint4& q, int blk, int a, uint64_t okey, bool visit, int done,
+                            ChildRef* c) {
+    const uint32_t ani = (uint32_t)(blk * p.A + a);
+    const int lo = kLanesPerAct * a + 2;
+    const bool cl = lane >= lo && lane < lo + kSlots;
+    const uint64_t skey = (uint64_t)q.x | ((uint64_t)q.y << 32);
+    const bool valid = cl && (skey & kValidBit) != 0;
+    const uint64_t m = __ballot(valid && (skey & kObsMask) == okey);
+    uint4* slots = reinterpret_cast<uint4*>(an + (int64_t)ani) + 2;
+    int L;
+    bool is_new = false;
+    if (m) {
+      L = __ffsll((long long)m) - 1;
+      c->blk = rl((int)q.z, L);
+      c->visits = rl((int)q.w, L);
+      c->absorbing = (int)(rlu(q.y, L) >> 31);
+    } else {
+      const uint64_t em = __ballot(cl && (skey & kValidBit) == 0);
+      if (!em) {   // all inline slots taken: overflow map
+        bool nw;
+        if (!ovf_lookup(ani, okey, true, visit ? 1 : 0, done, c, &nw)) return false;
+        if (!nw && visit) {
+          c->visits += 1;
+          c->absorbing = done;
+          OvfSlot* e = ovf + (int64_t)(c->id - p.ovf_base);
+          if (lane == 0) {
+            e->visits = c->visits;
+            e->flags = (uint32_t)done;
+          }
+        }
+        return true;
+      }
+      L = __ffsll((long long)em) - 1;
+      c->blk = -1;
+      c->visits = 0;
+      c->absorbing = done;
+      is_new = true;
+      ++n_nodes;
+      ++c_new;
+    }
+    const int k = L - lo;
+    if (visit) {
+      c->visits += 1;
+      c->absorbing = done;
+    }
+    if (visit || is_new) {
+      const uint64_t nk = okey | kValidBit | ((uint64_t)c->absorbing << 63);
+      const uint4 ns = make_uint4((uint32_t)nk, (uint32_t)(nk >> 32), (uint32_t)c->blk,
+                                  (uint32_t)c->visits);
+      if (lane == L) {
+        slots[k] = ns;
+        q = ns;
+      }
+    }
+    c->id = ani * kSlots + (uint32_t)k + 1u;
+    c->lane = L;
+    c->blk_ptr = reinterpret_cast<int32_t*>(slots + k) + 2;
+    return true;
   }
 
   // MCTS._rollout (mcts.py:405-452), random search policy.
@@ -299,8 +414,8 @@ struct Tree {
     double ret = 0.0;
     int k = 0;
     while (depth <= p.depth_limit && t <= p.step_limit) {
-      const int ae = (int)rs.act(p.ego, (uint32_t)p.A);     // search_policy.py:177
-      const int ao = (int)rs.act(p.other, (uint32_t)p.A);   // other_policy.py:151
+      const int ae = (int)d_act(p.ego, (uint32_t)p.A);     // search_policy.py:177
+      const int ao = (int)d_act(p.other, (uint32_t)p.A);   // other_policy.py:151
       uint32_t n0, n1;
       joint_step(s0, s1, ae, ao, &n0, &n1);
       const uint32_t e0 = p.ego == 0 ? s0 : s1, e1 = p.ego == 0 ? n0 : n1;
@@ -322,25 +437,34 @@ struct Tree {
   }
 
   // One simulation from the root (mcts.py:286-290 + _simulate 308-382).
-  __device__ int simulate(int root_blk, int root_visits) {
-    const uint32_t k = rs.belief((uint32_t)bsize);   // belief.py:55
+  // qr: the root block held in registers (lane l: bytes [16l, 16l+16)).
+  __device__ int simulate(uint4& qr) {
+    const uint32_t k = d_belief((uint32_t)bsize);   // belief.py:55
     const uint4 pr = root_belief()[k];
-    int t = (int)pr.x;
-    uint32_t s0 = pr.y, s1 = pr.z;
-    int node = root, depth = 0, plen = 0;
-    int blk = root_blk, nvis = root_visits;
+    int t = uni((int)pr.x);
+    uint32_t s0 = uniu(pr.y), s1 = uniu(pr.z);
+    int blk = root_blk, nvis = root_visits, depth = 0, plen = 0;
+    int32_t* leaf_blk_ptr = nullptr;
+    int leaf_lane = -1;
     double leaf = 0.0;
-    int p_an = 0, p_done = 0;
-    double p_r = 0.0;
+    // path registers: lane i holds tree level i
+    uint32_t p_an = 0;
+    int p_done = 0, p_n = 0;
+    double p_r = 0.0, p_v = 0.0, p_tot = 0.0, p_agg = 0.0;
+    uint4 q = qr;
     while (true) {
       if (depth > p.depth_limit || t > p.step_limit) break;   // mcts.py:315
       if (blk < 0) {                                            // mcts.py:318-328
-        if (expand(node) < 0) return -1;
+        const int b = alloc_block();
+        if (b < 0) return -1;
+        if (lane == 0) *leaf_blk_ptr = b;
+        if (depth == 1 && lane == leaf_lane) qr.z = (uint32_t)b;   // root child slot
         leaf = rollout(s0, s1, t, depth);
         break;
       }
-      const int a = choose_action(blk, nvis);                  // mcts.py:330
-      const int ao = (int)rs.act(p.other, (uint32_t)p.A);      // mcts.py:331
+      if (depth > 0) q = load_block(blk);
+      const int a = choose(q, nvis);                            // mcts.py:330
+      const int ao = (int)d_act(p.other, (uint32_t)p.A);       // mcts.py:331
       uint32_t n0, n1;
       joint_step(s0, s1, a, ao, &n0, &n1);                     // mcts.py:333
       const uint32_t e0 = p.ego == 0 ? s0 : s1;
@@ -349,30 +473,29 @@ struct Tree {
       const double r = drv_reward(e0, e1);
       const int done = (veh_done(e1) || (veh_done(n0) && veh_done(n1))) ? 1 : 0;
       const uint64_t okey = obs_key_wave(g, e1, o1, p.ncells);
-      const uint32_t ani = (uint32_t)(blk * p.A + a);
-      bool is_new;
-      const int child = find_or_insert(ani, okey, true, t + 1, 1, done, &is_new);
-      if (child < 0) return -1;
-      int cvis = 1, cblk = -1;
-      if (!is_new) {                                            // mcts.py:358-367
-        const int2 cn = onode[child];
-        cvis = cn.y + 1;
-        cblk = cn.x;
-        if (lane == 0) {
-          onode[child].y = cvis;
-          ometa[child] = ((t + 1) << 1) | done;                 // mcts.py:370
-        }
-      }
+      // the chosen action node's statistics, before the child's slot changes q
+      const int hl = kLanesPerAct * a;
+      const int an_vis = rl((int)q.x, hl);
+      const double an_val = hilo(rlu(q.z, hl), rlu(q.w, hl));
+      const double an_tot = hilo(rlu(q.x, hl + 1), rlu(q.y, hl + 1));
+      const double an_agg = hilo(rlu(q.z, hl + 1), rlu(q.w, hl + 1));
+      ChildRef c;
+      if (!child_ref(q, blk, a, okey, true, done, &c)) return -1;   // mcts.py:356-370
+      if (depth == 0 && c.lane >= 0 && lane == c.lane) qr = q;
       if (n_log >= p.Np) {
         err = POMCP_E_ARENA;
         return -1;
       }
-      if (lane == 0) plog[n_log] = make_uint4((uint32_t)child, (uint32_t)(t + 1), n0, n1);
+      if (lane == 0) plog[n_log] = make_uint4(c.id, (uint32_t)(t + 1), n0, n1);
       ++n_log;                                                  // mcts.py:371
       if (lane == plen) {
-        p_an = (int)ani;
+        p_an = (uint32_t)(blk * p.A + a);
         p_r = r;
         p_done = done;
+        p_n = an_vis;
+        p_v = an_val;
+        p_tot = an_tot;
+        p_agg = an_agg;
       }
       ++plen;
       ++c_levels;
@@ -381,32 +504,35 @@ struct Tree {
         err = POMCP_E_ARENA;
         return -1;
       }
-      node = child;
+      blk = c.blk;
+      nvis = c.visits;
+      leaf_blk_ptr = c.blk_ptr;
+      leaf_lane = c.lane;
       s0 = n0;
       s1 = n1;
       ++t;
       ++depth;
-      nvis = cvis;
-      blk = cblk;
     }
     // backup, deepest level first (mcts.py:374-381, node.py:166-178)
     double gr = leaf;
     for (int i = plen - 1; i >= 0; --i) {
-      const int ani = rl(p_an, i);
+      const uint32_t ani = rlu(p_an, i);
       const double r = rl_d(p_r, i);
       gr = rl(p_done, i) ? r : r + p.discount * gr;
-      ActRec rec = an[ani];
-      const int n = rec.visits + 1;
-      const double total = rec.total + gr;
-      const double delta = gr - rec.value;
-      const double value = rec.value + delta / (double)n;
-      const double agg = rec.agg + delta * (gr - value);
-      if (lane == 0) {
-        rec.visits = n;
-        rec.value = value;
-        rec.total = total;
-        rec.agg = agg;
-        an[ani] = rec;
+      const int n = rl(p_n, i) + 1;
+      const double value0 = rl_d(p_v, i);
+      const double total = rl_d(p_tot, i) + gr;
+      const double delta = gr - value0;
+      const double value = value0 + delta / (double)n;
+      const double agg = rl_d(p_agg, i) + delta * (gr - value);
+      const uint4 w0 = pack_stats0(n, value), w1 = pack_stats1(total, agg);
+      uint4* rec = reinterpret_cast<uint4*>(an + (int64_t)ani);
+      if (lane == 0) rec[0] = w0;
+      if (lane == 1) rec[1] = w1;
+      if (i == 0) {   // root level: keep the register copy current
+        const int hl = kLanesPerAct * (int)(ani - (uint32_t)(root_blk * p.A));
+        if (lane == hl) qr = w0;
+        if (lane == hl + 1) qr = w1;
       }
       mm_update(value);
     }
@@ -424,10 +550,10 @@ struct Tree {
     uint32_t ov = 0;
     for (int tr = 0; tr < 64; ++tr) {
       const uint32_t av = all & ~(1u << eloc);
-      const int s = kth_bit(av, rs.model((uint32_t)popc8(av)));
+      const int s = kth_bit(av, d_model((uint32_t)popc8(av)));
       const uint32_t avd = all & ~(1u << edest) & ~(1u << s);
-      const int d = kth_bit(avd, rs.model((uint32_t)popc8(avd)));
-      ov = make_vehicle(g, s, d);
+      const int d = kth_bit(avd, d_model((uint32_t)popc8(avd)));
+      ov = uniu(make_vehicle(g, s, d));
       if (obs_key_wave(g, ev, ov, p.ncells) == obs) break;
     }
     *s0 = p.ego == 0 ? ev : ov;
@@ -438,32 +564,36 @@ struct Tree {
 
 // ---------------------------------------------------------------- kernels
 
+__device__ void clear_ovf(const DevParams& p, int tree, int lane) {
+  uint4* hs = reinterpret_cast<uint4*>(p.ovf + (int64_t)tree * p.H);
+  for (int64_t i = lane; i < 2 * p.H; i += kWave) hs[i] = make_uint4(0, 0, 0, 0);
+}
+
 __global__ __launch_bounds__(256) void k_reset(DevParams p) {
   const int tree = blockIdx.x * kTreesPerBlock + (threadIdx.x >> 6);
   if (tree >= p.B) return;
   const int lane = lane_id();
   TreeHdr h = p.hdr[tree];
   int epoch = (h.epoch + 1) & (int)kEpochMask;
-  if (epoch == 0) {   // generation counter wrapped: clear this tree's map
-    uint4* hs = reinterpret_cast<uint4*>(p.hash + (int64_t)tree * p.H);
-    for (int64_t i = lane; i < p.H; i += kWave) hs[i] = make_uint4(0, 0, 0, 0);
+  if (epoch == 0) {   // generation counter wrapped: clear this tree's overflow map
+    clear_ovf(p, tree, lane);
     epoch = 1;
   }
   if (lane == 0) {
-    h.root = 0;
-    h.n_obs = 1;
     h.n_blocks = 0;
     h.n_log = 0;
+    h.n_nodes = 1;
+    h.error = 0;
     h.belief_size = 0;
     h.epoch = epoch;
-    h.error = 0;
     h.root_t = 0;
+    h.root_id = kRootId;
+    h.root_blk = -1;
+    h.root_visits = 0;
     h.root_abs = 0;
     h.mm_max = p.has_kb ? p.kb_max : -__builtin_inf();   // utils.py:21-27
     h.mm_min = p.has_kb ? p.kb_min : __builtin_inf();
     p.hdr[tree] = h;
-    p.onode[(int64_t)tree * p.No] = make_int2(-1, 0);
-    p.ometa[(int64_t)tree * p.No] = 0;
   }
 }
 
@@ -473,14 +603,14 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
   const int tree = blockIdx.x * kTreesPerBlock + (threadIdx.x >> 6);
   if (tree >= p.B) return;
   Tree T(p, sg, tree);
+  T.warm_rng();
   const int lane = T.lane;
   if (T.err == 0 && !T.root_abs) {   // mcts.py:161-162
-    const uint64_t obs = p.in_obs[tree];
+    const uint64_t obs = uni64(p.in_obs[tree]);
     if (T.root_t == 0) {
-      // _initial_update (mcts.py:175-227)
-      const int node = T.new_obs_node(T.root_t + 1, 0, 0);
+      // _initial_update (mcts.py:175-227): root -> None -> obs node (visits 0)
       uint32_t s0, s1;
-      if (node >= 0 && !T.sample_agent_initial(obs, &s0, &s1)) T.err = POMCP_E_INVALID;  // probe
+      if (!T.sample_agent_initial(obs, &s0, &s1)) T.err = POMCP_E_INVALID;   // probe
       uint4* nb = T.other_belief();
       int n = 0;
       while (T.err == 0 && n < p.n_target) {
@@ -493,25 +623,24 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
         ++n;
       }
       if (T.err == 0) {
-        T.root = node;
+        T.root_id = kRootId;
+        T.root_blk = -1;
+        T.root_visits = 0;
         T.root_t = 1;
         T.root_abs = 0;
         T.bsel ^= 1;
         T.bsize = n;
+        ++T.n_nodes;
       }
     } else {
       // _update (mcts.py:229-263)
-      const int action = p.in_actions[tree];
-      const int blk = T.onode[T.root].x;
-      if (blk < 0 || action < 0 || action >= p.A) {
+      const int action = uni(p.in_actions[tree]);
+      if (T.root_blk < 0 || action < 0 || action >= p.A) {
         T.err = POMCP_E_NOT_FOUND;
       } else {
-        const uint32_t ani = (uint32_t)(blk * p.A + action);
-        bool is_new;
-        const int child =
-            T.find_or_insert(ani, obs, true, T.root_t + 1, 0, T.root_abs, &is_new);
-        if (child >= 0) {
-          const int cabs = T.ometa[child] & 1;
+        uint4 q = T.load_block(T.root_blk);
+        ChildRef c;
+        if (T.child_ref(q, T.root_blk, action, obs, false, T.root_abs, &c)) {
           // the child's belief: its particles from the log, insertion order
           uint4* nb = T.other_belief();
           int n = 0;
@@ -519,7 +648,7 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
             const int i = base + lane;
             uint4 rec = make_uint4(0xFFFFFFFFu, 0, 0, 0);
             if (i < T.n_log) rec = T.plog[i];
-            const bool m = i < T.n_log && rec.x == (uint32_t)child;
+            const bool m = i < T.n_log && rec.x == c.id;
             const uint64_t mask = __ballot(m);
             const int pos = n + (int)__popcll(mask & ((1ull << lane) - 1ull));
             if (m && pos < p.Nr) nb[pos] = make_uint4(rec.y, rec.z, rec.w, 0u);
@@ -528,22 +657,22 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
           if (n > p.Nr) T.err = POMCP_E_ARENA;
           // _reinvigorate (mcts.py:651-700) -> BeliefRejectionSampler (belief.py:145-194)
           const int need = p.n_target - n;
-          if (T.err == 0 && !cabs && need > 0) {
+          if (T.err == 0 && !c.absorbing && need > 0) {
             if (n + 2 * need > p.Nr) {
               T.err = POMCP_E_ARENA;
             } else {
-              const uint4* pb_ = T.root_belief();
+              const uint4* pbel = T.root_belief();
               const double limit = p.limit_factor * (double)need;
               int got = 0, tries = 0, nrej = 0;
               while (got < need && (double)tries < limit) {
                 ++tries;
-                const uint4 hp = pb_[T.rs.belief((uint32_t)T.bsize)];
-                const int ao = (int)T.rs.act(p.other, (uint32_t)p.A);
+                const uint4 hp = pbel[T.d_belief((uint32_t)T.bsize)];
+                const int ao = (int)T.d_act(p.other, (uint32_t)p.A);
                 uint32_t n0, n1;
-                T.joint_step(hp.y, hp.z, action, ao, &n0, &n1);
+                T.joint_step(uniu(hp.y), uniu(hp.z), action, ao, &n0, &n1);
                 const uint32_t e1 = p.ego == 0 ? n0 : n1, o1 = p.ego == 0 ? n1 : n0;
                 const uint64_t k = obs_key_wave(sg, e1, o1, p.ncells);
-                const uint4 rec = make_uint4(hp.x + 1u, n0, n1, 0u);
+                const uint4 rec = make_uint4(uniu(hp.x) + 1u, n0, n1, 0u);
                 if (k == obs) {
                   if (lane == 0) nb[n + got] = rec;
                   ++got;
@@ -554,15 +683,17 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
               }
               int fill = need - got;
               if (fill > nrej) fill = nrej;
-              for (int q = 0; q < fill; ++q)
-                if (lane == 0) nb[n + got + q] = nb[n + need + q];
+              for (int q2 = 0; q2 < fill; ++q2)
+                if (lane == 0) nb[n + got + q2] = nb[n + need + q2];
               n += got + fill;
             }
           }
           if (T.err == 0) {
-            T.root = child;
+            T.root_id = c.id;
+            T.root_blk = c.blk;
+            T.root_visits = c.visits;
             T.root_t += 1;
-            T.root_abs = cabs;
+            T.root_abs = c.absorbing;
             T.bsel ^= 1;
             T.bsize = n;
           }
@@ -583,50 +714,51 @@ __global__ __launch_bounds__(256) void k_search(DevParams p, int num_sims) {
   const int tree = blockIdx.x * kTreesPerBlock + (threadIdx.x >> 6);
   if (tree >= p.B) return;
   Tree T(p, sg, tree);
+  T.warm_rng();
   const int lane = T.lane;
-  int action = 0, max_depth = 0, sims = 0, blk = -1, visits = 0;
+  int action = 0, max_depth = 0, sims = 0;
+  uint4 qr = make_uint4(0, 0, 0, 0);
   if (T.err == 0 && T.root_t == 0) T.err = POMCP_E_STATE;
   if (T.err == 0 && !T.root_abs) {   // mcts.py:270-272
-    const int2 rn = T.onode[T.root];
-    blk = rn.x;
-    visits = rn.y;
-    if (blk < 0) blk = T.expand(T.root);   // mcts.py:279-281
-    if (blk >= 0 && T.bsize <= 0) T.err = POMCP_E_STATE;
+    if (T.root_blk < 0) T.root_blk = T.alloc_block();   // mcts.py:279-281
+    if (T.root_blk >= 0 && T.bsize <= 0) T.err = POMCP_E_STATE;
+    if (T.err == 0) qr = T.load_block(T.root_blk);
     for (int s = 0; s < num_sims && T.err == 0; ++s) {
-      const int d = T.simulate(blk, visits);
+      const int d = T.simulate(qr);
       if (d < 0) break;
-      ++visits;                               // mcts.py:288
+      ++T.root_visits;                              // mcts.py:288
       max_depth = d > max_depth ? d : max_depth;
       ++sims;
     }
-    if (T.err == 0) action = T.final_action(blk, visits);
-    if (lane == 0 && blk >= 0) T.onode[T.root] = make_int2(blk, visits);
+    if (T.err == 0) action = T.final_action(qr, T.root_visits);
   }
   T.store_header();
   // root statistics: MCTS.step_statistics + root children
   pomcp_root_stats* st = p.stats + tree;
   const int A = p.A;
-  if (lane < A) {
-    ActRec r;
-    r.visits = 0;
-    r.value = 0.0;
-    r.total = 0.0;
-    if (blk >= 0) r = T.an[(int64_t)blk * A + lane];
-    st->child_visits[lane] = r.visits;
-    st->child_values[lane] = r.value;
-    st->child_totals[lane] = r.total;
-    p.merge[((int64_t)tree * A + lane) * 2] = (double)r.visits;
-    p.merge[((int64_t)tree * A + lane) * 2 + 1] = r.total;
+  const bool have = T.root_blk >= 0 && !T.root_abs;
+  for (int a = 0; a < A; ++a) {
+    const int hl = kLanesPerAct * a;
+    const int nv = have ? rl((int)qr.x, hl) : 0;
+    const double va = have ? hilo(rlu(qr.z, hl), rlu(qr.w, hl)) : 0.0;
+    const double tot = have ? hilo(rlu(qr.x, hl + 1), rlu(qr.y, hl + 1)) : 0.0;
+    if (lane == a) {
+      st->child_visits[a] = nv;
+      st->child_values[a] = va;
+      st->child_totals[a] = tot;
+      p.merge[((int64_t)tree * A + a) * 2] = (double)nv;
+      p.merge[((int64_t)tree * A + a) * 2 + 1] = tot;
+    }
   }
   if (lane == 0) {
     st->action = action;
     st->num_sims = sims;
     st->search_depth = max_depth;
-    st->root_visits = visits;
+    st->root_visits = T.root_visits;
     st->root_absorbing = T.root_abs;
     st->belief_size = T.bsize;
     st->error = T.err;
-    st->num_children = blk >= 0 ? A : 0;
+    st->num_children = have ? A : 0;
     st->min_value = T.mm_min;
     st->max_value = T.mm_max;
     st->n_levels = T.c_levels;
@@ -634,7 +766,7 @@ __global__ __launch_bounds__(256) void k_search(DevParams p, int num_sims) {
     st->n_new_nodes = T.c_new;
     st->n_rollout_steps = T.c_rollout;
     st->n_probes = T.c_probes;
-    st->n_obs_nodes = T.n_obs;
+    st->n_obs_nodes = T.n_nodes;
     st->n_blocks = T.n_blocks;
     st->n_log = T.n_log;
     st->pad = 0;
@@ -659,23 +791,20 @@ __global__ __launch_bounds__(256) void k_synthetic_obs(DevParams p, uint64_t env
   if (lane_id() == 0) p.out_obs[tree] = key;
 }
 
-// Snapshot / restore of the post-initial-update root state.
-__global__ __launch_bounds__(256) void k_restore(DevParams p, const TreeHdr* snap,
-                                                 const int2* snap_root) {
+// Restore of the post-initial-update root state (see pomcp_snapshot).
+__global__ __launch_bounds__(256) void k_restore(DevParams p, const TreeHdr* snap) {
   const int tree = blockIdx.x * kTreesPerBlock + (threadIdx.x >> 6);
   if (tree >= p.B) return;
   const int lane = lane_id();
   int epoch = (p.hdr[tree].epoch + 1) & (int)kEpochMask;
   if (epoch == 0) {
-    uint4* hs = reinterpret_cast<uint4*>(p.hash + (int64_t)tree * p.H);
-    for (int64_t i = lane; i < p.H; i += kWave) hs[i] = make_uint4(0, 0, 0, 0);
+    clear_ovf(p, tree, lane);
     epoch = 1;
   }
   if (lane == 0) {
     TreeHdr h = snap[tree];
     h.epoch = epoch;
     p.hdr[tree] = h;
-    p.onode[(int64_t)tree * p.No + h.root] = snap_root[tree];
   }
 }
 

@@ -77,11 +77,10 @@ class PomcpConfig(C.Structure):
         ("seed", C.c_uint64),
         ("tree_key_base", C.c_uint32),
         ("pad0", C.c_int32),
-        ("max_obs_nodes", C.c_int64),
         ("max_blocks", C.c_int64),
         ("max_particles", C.c_int64),
         ("max_belief", C.c_int64),
-        ("hash_slots", C.c_int64),
+        ("overflow_slots", C.c_int64),
         ("log_table", C.POINTER(C.c_double)),
         ("log_table_size", C.c_int64),
         ("discount_pow", C.POINTER(C.c_double)),

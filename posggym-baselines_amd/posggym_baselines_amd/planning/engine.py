@@ -15,17 +15,16 @@ INT32_MAX = 2**31 - 1
 
 @dataclass
 class Capacities:
-    max_obs_nodes: int
-    max_blocks: int
-    max_particles: int
-    max_belief: int
-    hash_slots: int
+    max_blocks: int           # expanded obs nodes (each A x 128 B action nodes)
+    max_particles: int        # particle log records (16 B)
+    max_belief: int           # root belief records (16 B), two ping-pong buffers
+    overflow_slots: int       # obs children beyond 6 per action node (32 B)
     log_table_size: int
     discount_pow_size: int
 
     def bytes_per_tree(self, num_actions: int) -> int:
-        return (self.max_obs_nodes * 12 + self.max_blocks * num_actions * 32
-                + self.hash_slots * 16 + self.max_particles * 16 + 2 * self.max_belief * 16)
+        return (self.max_blocks * num_actions * 128 + self.overflow_slots * 32
+                + self.max_particles * 16 + 2 * self.max_belief * 16)
 
 
 def _next_pow2(n: int) -> int:
@@ -33,24 +32,25 @@ def _next_pow2(n: int) -> int:
 
 
 def plan_capacities(config, step_limit: int, num_sims: int, searches: int = 1,
-                    reroot: bool = True, max_blocks: int = None, max_obs_nodes: int = None):
+                    reroot: bool = True, max_blocks: int = None, overflow_slots: int = None):
     """Worst-case arena sizes for ``searches`` searches of ``num_sims`` each.
 
-    Every simulation creates at most one obs node and expands at most one leaf
-    (mcts.py:318-328, 369) and appends one particle per tree level stepped
-    (mcts.py:371), at most min(depth_limit, step_limit) + 1 levels.
+    Every simulation expands at most one leaf (mcts.py:318-328) and appends one
+    particle per tree level stepped (mcts.py:371), at most
+    min(depth_limit, step_limit) + 1 levels.  Pass smaller ``max_blocks`` /
+    ``overflow_slots`` to trade worst-case guarantees for memory: overflow is
+    detected and reported (POMCP_E_ARENA), never silent.
     """
     levels = min(config.depth_limit, step_limit) + 1
     n_target = config.num_particles + config.extra_particles
     total = num_sims * searches
-    no = total + 2 * searches + 16 if max_obs_nodes is None else max_obs_nodes
-    nb = no if max_blocks is None else max_blocks
+    nb = total + 2 * searches + 16 if max_blocks is None else max_blocks
+    ovf = _next_pow2(max(64, total // 8)) if overflow_slots is None else overflow_slots
     np_ = total * min(levels, 64) + searches * 2 * n_target + 64
     nr = (np_ + 2 * n_target + 64) if reroot else (4 * n_target + 64)
     return Capacities(
-        max_obs_nodes=no, max_blocks=nb, max_particles=np_, max_belief=nr,
-        hash_slots=_next_pow2(2 * no), log_table_size=total + 2,
-        discount_pow_size=min(levels, 4096) + 2)
+        max_blocks=nb, max_particles=np_, max_belief=nr, overflow_slots=ovf,
+        log_table_size=total + 2, discount_pow_size=min(levels, 4096) + 2)
 
 
 class PomcpEngine:
@@ -108,11 +108,10 @@ class PomcpEngine:
             s = int(np.random.SeedSequence().entropy) & (2**63 - 1)
         c.seed = int(s) & (2**64 - 1)
         c.tree_key_base = int(tree_key_base)
-        c.max_obs_nodes = capacities.max_obs_nodes
         c.max_blocks = capacities.max_blocks
         c.max_particles = capacities.max_particles
         c.max_belief = capacities.max_belief
-        c.hash_slots = capacities.hash_slots
+        c.overflow_slots = capacities.overflow_slots
         # FP64 tables from Python's own math.log and float ** int (bit-exact with
         # mcts.py:534 and mcts.py:421)
         self._logtab = np.array([0.0] + [math.log(n) for n in range(1, capacities.log_table_size)],
