@@ -240,3 +240,133 @@ PB_HD int loc_index(const G& g, int x, int y) {
 }
 
 }  // namespace pb
+
+namespace pb {
+
+// ---------------------------------------------------------------------------
+// Table-driven fast path (identical results to the functions above; the CPU
+// tests compare the host build of these against oracle/driving.py).
+//   nbr[cell * 4 + dir]      : neighbouring free cell (y << 4 | x) or 0xFF
+//   win_wall[cell * 4 + dir] : bit c set when window cell c is a wall / outside
+struct DrvModel {
+  DrvGrid g;
+  uint16_t win_wall[1024];
+  uint8_t nbr[1024];
+};
+
+template <class G>
+PB_HD void build_model_tables(const G& g, DrvModel* m) {
+  const int ncells = (g.obs_front + g.obs_back + 1) * (2 * g.obs_side + 1);
+  for (int cell = 0; cell < 256; ++cell) {
+    const int x = cell & 15, y = cell >> 4;
+    for (int d = 0; d < 4; ++d) {
+      const int nx = x + dir_dx(d), ny = y + dir_dy(d);
+      m->nbr[cell * 4 + d] = grid_free(g, nx, ny) ? (uint8_t)((ny << 4) | nx) : (uint8_t)0xFF;
+      uint32_t w = 0;
+      const uint32_t self = (uint32_t)x | ((uint32_t)y << 4) | ((uint32_t)d << 8);
+      for (int c = 0; c < ncells; ++c) {
+        const int W = 2 * g.obs_side + 1;
+        const int fwd = g.obs_front - c / W;
+        const int side = c % W - g.obs_side;
+        const int r = (d + 1) & 3;
+        const int cx = x + fwd * dir_dx(d) + side * dir_dx(r);
+        const int cy = y + fwd * dir_dy(d) + side * dir_dy(r);
+        if (!grid_free(g, cx, cy)) w |= 1u << c;
+      }
+      (void)self;
+      m->win_wall[cell * 4 + d] = (uint16_t)w;
+    }
+  }
+}
+
+// Window index of absolute cell (tx, ty) seen from (x, y) facing d, or -1.
+PB_HD int window_index(const DrvGrid& g, int x, int y, int d, int tx, int ty) {
+  const int rx = tx - x, ry = ty - y;
+  const int r = (d + 1) & 3;
+  const int fwd = rx * dir_dx(d) + ry * dir_dy(d);
+  const int side = rx * dir_dx(r) + ry * dir_dy(r);
+  if (fwd < -g.obs_back || fwd > g.obs_front || side < -g.obs_side || side > g.obs_side) return -1;
+  return (g.obs_front - fwd) * (2 * g.obs_side + 1) + (side + g.obs_side);
+}
+
+PB_HD uint32_t spread_bits16(uint32_t x) {
+  x &= 0xFFFFu;
+  x = (x | (x << 8)) & 0x00FF00FFu;
+  x = (x | (x << 4)) & 0x0F0F0F0Fu;
+  x = (x | (x << 2)) & 0x33333333u;
+  x = (x | (x << 1)) & 0x55555555u;
+  return x;
+}
+
+// Ego observation key without per-cell work: walls from the window table,
+// then the destination cell (11) and the other vehicle (00) patched in.
+PB_HD uint64_t obs_key_fast(const DrvModel& m, uint32_t self, uint32_t other) {
+  const DrvGrid& g = m.g;
+  const int ncells = (g.obs_front + g.obs_back + 1) * (2 * g.obs_side + 1);
+  const uint32_t full = (1u << ncells) - 1u;
+  const int x = self & 15, y = (self >> 4) & 15, d = (self >> 8) & 3;
+  const uint32_t wall = m.win_wall[(((y << 4) | x) << 2) | d];
+  uint32_t cells = spread_bits16(wall) | (spread_bits16(~wall & full) << 1);
+  const int dest = (self >> 12) & 7;
+  const int cd = window_index(g, x, y, d, g.loc_x[dest], g.loc_y[dest]);
+  if (cd >= 0 && !((wall >> cd) & 1u)) cells |= 3u << (2 * cd);
+  const int cv = window_index(g, x, y, d, (int)(other & 15), (int)((other >> 4) & 15));
+  if (cv >= 0 && !((wall >> cv) & 1u)) cells &= ~(3u << (2 * cv));
+  return (uint64_t)cells | obs_tail(g, self);
+}
+
+// One vehicle's move on packed state (same semantics as move_vehicle).
+PB_HD uint32_t move_vehicle_fast(const DrvModel& m, uint32_t self, uint32_t other, int action,
+                                 bool* hit) {
+  *hit = false;
+  if (veh_done(self)) return self;
+  int d = (self >> 8) & 3, speed = (self >> 10) & 3;
+  if (action == TURN_RIGHT) d = (d + 1) & 3;
+  else if (action == TURN_LEFT) d = (d + 3) & 3;
+  else if (action == ACCELERATE) speed = speed + 1 < FORWARD_FAST ? speed + 1 : FORWARD_FAST;
+  else if (action == DECELERATE) speed = speed - 1 > REVERSE ? speed - 1 : REVERSE;
+  const int move = speed != REVERSE ? d : ((d + 2) & 3);
+  const int cells = speed > STOPPED ? speed - STOPPED : STOPPED - speed;
+  const int ocell = (int)(other & 0xFF);
+  int cell = (int)(self & 0xFF);
+  for (int k = 0; k < cells; ++k) {
+    const int n = m.nbr[(cell << 2) | move];
+    if (n == 0xFF) {
+      speed = STOPPED;
+      break;
+    }
+    if (n == ocell) {
+      *hit = true;
+      speed = STOPPED;
+      break;
+    }
+    cell = n;
+  }
+  const int dest = (self >> 12) & 7;
+  const int dist = m.g.dist[dest][cell];
+  const int mind0 = (self >> 17) & 127;
+  const int mind = mind0 < dist ? mind0 : dist;
+  return (self & 0x7F007000u) | (uint32_t)cell | ((uint32_t)d << 8) | ((uint32_t)speed << 10) |
+         ((uint32_t)(dist == 0) << 15) | ((uint32_t)(*hit) << 16) | ((uint32_t)mind << 17);
+}
+
+PB_HD void drv_step2_fast(const DrvModel& m, uint32_t s0, uint32_t s1, int a0, int a1, uint32_t j,
+                          uint32_t* o0, uint32_t* o1) {
+  uint32_t v0 = s0, v1 = s1;
+  bool hit;
+  if (j == 0) {   // shuffle swapped: agent 1 moves first
+    v1 = move_vehicle_fast(m, v1, v0, a1, &hit);
+    if (hit && !veh_done(v0)) v0 |= 1u << 16;
+    v0 = move_vehicle_fast(m, v0, v1, a0, &hit);
+    if (hit && !veh_done(v1)) v1 |= 1u << 16;
+  } else {
+    v0 = move_vehicle_fast(m, v0, v1, a0, &hit);
+    if (hit && !veh_done(v1)) v1 |= 1u << 16;
+    v1 = move_vehicle_fast(m, v1, v0, a1, &hit);
+    if (hit && !veh_done(v0)) v0 |= 1u << 16;
+  }
+  *o0 = v0;
+  *o1 = v1;
+}
+
+}  // namespace pb

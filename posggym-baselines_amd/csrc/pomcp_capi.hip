@@ -33,7 +33,13 @@ struct pomcp_ctx {
   TreeHdr* snap_hdr = nullptr;
   std::vector<int32_t> host_upd;
   std::vector<pomcp_root_stats> host_stats;
+  DrvModel host_model;
 };
+
+static void make_model(const pomcp_grid* g, DrvModel* m) {
+  std::memcpy(&m->g, g, sizeof(DrvGrid));
+  build_model_tables(m->g, m);
+}
 
 #define HIP_TRY(ctx, expr)                                                          \
   do {                                                                              \
@@ -147,6 +153,7 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
     ctx->own_stream = true;
   }
   const pomcp_config& c = *cfg;
+  make_model(&c.grid, &ctx->host_model);
   DevParams& d = ctx->dp;
   d.B = c.num_trees;
   d.A = c.num_actions;
@@ -187,7 +194,7 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
   ALLOC(belief, uint4, B * 2 * d.Nr);
   ALLOC(logtab, double, c.log_table_size);
   ALLOC(dpow, double, c.discount_pow_size);
-  ALLOC(grid, DrvGrid, 1);
+  ALLOC(model, DrvModel, 1);
   ALLOC(stats, pomcp_root_stats, B);
   ALLOC(merge, double, B * d.A * 2);
   ALLOC(upd_out, int32_t, B * 2);
@@ -206,8 +213,8 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
                      hipMemcpyHostToDevice, s) != hipSuccess ||
       hipMemcpyAsync((void*)d.dpow, c.discount_pow, sizeof(double) * c.discount_pow_size,
                      hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemcpyAsync((void*)d.grid, &c.grid, sizeof(DrvGrid), hipMemcpyHostToDevice, s) !=
-          hipSuccess) {
+      hipMemcpyAsync((void*)d.model, &ctx->host_model, sizeof(DrvModel), hipMemcpyHostToDevice,
+                     s) != hipSuccess) {
     ctx->err = "initial upload failed";
     pomcp_destroy(ctx);
     return POMCP_E_HIP;
@@ -300,8 +307,18 @@ int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_key
 int pomcp_search(pomcp_ctx* ctx, int32_t num_sims, int32_t* actions_out) {
   if (!ctx || num_sims < 0) return POMCP_E_INVALID;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
-  hipLaunchKernelGGL(k_search, dim3(grid_blocks(ctx->dp.B)), dim3(256), 0, ctx->stream,
-                     ctx->dp, (int)num_sims);
+  const dim3 grid(grid_blocks(ctx->dp.B)), block(256);
+  switch (ctx->dp.sel) {
+    case POMCP_SEL_PUCB:
+      hipLaunchKernelGGL(k_search<POMCP_SEL_PUCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims);
+      break;
+    case POMCP_SEL_UCB:
+      hipLaunchKernelGGL(k_search<POMCP_SEL_UCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims);
+      break;
+    default:
+      hipLaunchKernelGGL(k_search<POMCP_SEL_UNIFORM>, grid, block, 0, ctx->stream, ctx->dp,
+                         (int)num_sims);
+  }
   HIP_TRY(ctx, hipGetLastError());
   if (!actions_out) return POMCP_OK;
   const int rc = pomcp_get_root_stats(ctx, ctx->host_stats.data());
@@ -437,7 +454,8 @@ int pomcp_driving_step(const pomcp_grid* g, uint64_t seed, uint32_t tree, uint32
                        double rewards_out[2], int32_t terminated_out[2],
                        uint64_t obs_keys_out[2]) {
   if (!g || !model_ctr || !state || !actions || !next_out) return POMCP_E_INVALID;
-  const DrvGrid& gg = *reinterpret_cast<const DrvGrid*>(g);
+  DrvModel m;
+  make_model(g, &m);
   Streams s;
   s.seed = seed;
   s.tree = tree;
@@ -445,23 +463,24 @@ int pomcp_driving_step(const pomcp_grid* g, uint64_t seed, uint32_t tree, uint32
   s.ctr[2] = *model_ctr;
   const uint32_t j = s.model(2);   // execution-order shuffle
   *model_ctr = s.ctr[2];
-  drv_step2(gg, state[0], state[1], actions[0], actions[1], j, &next_out[0], &next_out[1]);
+  drv_step2_fast(m, state[0], state[1], actions[0], actions[1], j, &next_out[0], &next_out[1]);
   for (int i = 0; i < 2; ++i) {
     if (rewards_out) rewards_out[i] = drv_reward(state[i], next_out[i]);
     if (terminated_out) terminated_out[i] = veh_done(next_out[i]) ? 1 : 0;
   }
   if (obs_keys_out) {
-    obs_keys_out[0] = obs_key_serial(gg, next_out[0], next_out[1]);
-    obs_keys_out[1] = obs_key_serial(gg, next_out[1], next_out[0]);
+    obs_keys_out[0] = obs_key_fast(m, next_out[0], next_out[1]);
+    obs_keys_out[1] = obs_key_fast(m, next_out[1], next_out[0]);
   }
   return POMCP_OK;
 }
 
 int pomcp_driving_obs(const pomcp_grid* g, const uint32_t state[2], uint64_t obs_keys_out[2]) {
   if (!g || !state || !obs_keys_out) return POMCP_E_INVALID;
-  const DrvGrid& gg = *reinterpret_cast<const DrvGrid*>(g);
-  obs_keys_out[0] = obs_key_serial(gg, state[0], state[1]);
-  obs_keys_out[1] = obs_key_serial(gg, state[1], state[0]);
+  DrvModel m;
+  make_model(g, &m);
+  obs_keys_out[0] = obs_key_fast(m, state[0], state[1]);
+  obs_keys_out[1] = obs_key_fast(m, state[1], state[0]);
   return POMCP_OK;
 }
 

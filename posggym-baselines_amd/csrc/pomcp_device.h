@@ -89,7 +89,7 @@ struct DevParams {
   int64_t logtab_n;
   const double* dpow;
   int32_t dpow_n;
-  const DrvGrid* grid;
+  const DrvModel* model;
   pomcp_root_stats* stats;
   double* merge;        // [B][A][2]
   int32_t* upd_out;     // [B][2] {root_abs, error}
@@ -152,26 +152,20 @@ __device__ __forceinline__ uint32_t ovf_hash(uint32_t an, uint64_t key) {
   return (uint32_t)h;
 }
 
-// Wave-cached Philox stream: lane i holds the 4 words of block (page * 64 + i),
-// so 256 consecutive draws are readlanes; the wave refills the page in one
-// pass (64 blocks in parallel).  Same words as philox_word() (philox.h).
-struct CachedStream {
-  uint32_t w0, w1, w2, w3;   // per-lane
+// Wave-cached Philox stream in LDS: a page of 256 consecutive draws (64 Philox
+// blocks, one per lane, written with one ds_write_b128) is refilled by the
+// wave in one pass; a draw is one broadcast LDS read.  Same words as
+// philox_word() (philox.h).
+struct LdsStream {
+  uint32_t* page;   // this wave's 256-word LDS page
   __device__ __forceinline__ void refill(uint64_t seed, uint32_t tree, uint32_t stream,
-                                         uint32_t page) {
-    uint32_t c[4] = {page * 64u + (uint32_t)lane_id(), 0u, stream, (uint32_t)(seed >> 32)};
+                                         uint32_t pg) {
+    const uint32_t lane = (uint32_t)lane_id();
+    uint32_t c[4] = {pg * 64u + lane, 0u, stream, (uint32_t)(seed >> 32)};
     philox4x32_10(c, (uint32_t)seed, tree);
-    w0 = c[0];
-    w1 = c[1];
-    w2 = c[2];
-    w3 = c[3];
+    reinterpret_cast<uint4*>(page)[lane] = make_uint4(c[0], c[1], c[2], c[3]);
   }
-  __device__ __forceinline__ uint32_t get(uint32_t j) const {
-    const int l = (int)((j >> 2) & 63u);
-    const uint32_t a = rlu(w0, l), b = rlu(w1, l), c = rlu(w2, l), d = rlu(w3, l);
-    const uint32_t r = j & 3u;
-    return (r & 2u) ? ((r & 1u) ? d : c) : ((r & 1u) ? b : a);
-  }
+  __device__ __forceinline__ uint32_t get(uint32_t j) const { return uniu(page[j & 255u]); }
 };
 
 }  // namespace pb

@@ -16,10 +16,11 @@
 
 namespace pb {
 
-__device__ __forceinline__ void stage_grid(const DrvGrid* src, DrvGrid& dst) {
+__device__ __forceinline__ void stage_model(const DrvModel* src, DrvModel& dst) {
+  static_assert(sizeof(DrvModel) % 4 == 0, "model size");
   const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
   uint32_t* d = reinterpret_cast<uint32_t*>(&dst);
-  for (int i = threadIdx.x; i < (int)(sizeof(DrvGrid) / 4); i += blockDim.x) d[i] = s[i];
+  for (int i = threadIdx.x; i < (int)(sizeof(DrvModel) / 4); i += blockDim.x) d[i] = s[i];
   __syncthreads();
 }
 
@@ -47,6 +48,7 @@ struct ChildRef {
 
 struct Tree {
   const DevParams& p;
+  const DrvModel& m;
   const DrvGrid& g;
   int tree, lane;
   ActNode* an;
@@ -60,10 +62,10 @@ struct Tree {
   uint64_t seed;
   uint32_t tkey;
   uint32_t c_belief, c_select, c_model, c_act0, c_act1;
-  CachedStream r_belief, r_model, r_act0, r_act1;
+  LdsStream r_belief, r_model, r_act0, r_act1;
   int64_t c_levels, c_expand, c_new, c_rollout, c_probes;
 
-  __device__ Tree(const DevParams& pp, const DrvGrid& gg, int t) : p(pp), g(gg), tree(t) {
+  __device__ Tree(const DevParams& pp, const DrvModel& mm, int t) : p(pp), m(mm), g(mm.g), tree(t) {
     lane = lane_id();
     an = p.an + (int64_t)t * p.Nb * p.A;
     ovf = p.ovf + (int64_t)t * p.H;
@@ -94,7 +96,11 @@ struct Tree {
     c_levels = c_expand = c_new = c_rollout = c_probes = 0;
   }
 
-  __device__ void warm_rng() {
+  __device__ void warm_rng(uint32_t* lds) {   // lds: 4 x 256 words for this wave
+    r_belief.page = lds;
+    r_model.page = lds + 256;
+    r_act0.page = lds + 512;
+    r_act1.page = lds + 768;
     r_belief.refill(seed, tkey, S_BELIEF, c_belief >> 8);
     r_model.refill(seed, tkey, S_MODEL, c_model >> 8);
     r_act0.refill(seed, tkey, S_ACT_BASE, c_act0 >> 8);
@@ -130,7 +136,7 @@ struct Tree {
   }
 
   // ------------------------------------------------------------- RNG draws
-  __device__ __forceinline__ uint32_t draw(CachedStream& cs, uint32_t& ctr, uint32_t stream) {
+  __device__ __forceinline__ uint32_t draw(LdsStream& cs, uint32_t& ctr, uint32_t stream) {
     const uint32_t j = ctr++;
     if ((j & 255u) == 0u) cs.refill(seed, tkey, stream, j >> 8);
     return cs.get(j);
@@ -185,7 +191,7 @@ struct Tree {
     const uint32_t j = d_model(2);   // Python random.shuffle of the exec order
     const int a0 = p.ego == 0 ? ego_a : oth_a;
     const int a1 = p.ego == 0 ? oth_a : ego_a;
-    drv_step2(g, s0, s1, a0, a1, j, n0, n1);
+    drv_step2_fast(m, s0, s1, a0, a1, j, n0, n1);
     *n0 = uniu(*n0);
     *n1 = uniu(*n1);
   }
@@ -195,28 +201,27 @@ struct Tree {
   __device__ int pucb_prior_draw() {
     const int A = p.A;
     const double w = 1.0 / (double)A;
-    double cum[POMCP_MAX_ACTIONS];
+    double total = w;
+    for (int k = 1; k < A; ++k) total = total + w;
+    const double x = d_select_float() * (total + 0.0);
     double acc = w;
-    cum[0] = acc;
-    for (int k = 1; k < A; ++k) {
+    for (int k = 0; k < A - 1; ++k) {   // bisect_right over the running sums
+      if (x < acc) return k;
       acc = acc + w;
-      cum[k] = acc;
     }
-    const double x = d_select_float() * (cum[A - 1] + 0.0);
-    for (int k = 0; k < A - 1; ++k)
-      if (x < cum[k]) return k;
     return A - 1;
   }
 
   // _search_action_selection (mcts.py:492-563) on a block held in registers.
+  template <int SEL>
   __device__ int choose(const uint4& q, int visits) {
     const int A = p.A;
-    if (p.sel == POMCP_SEL_PUCB && visits == 0) return pucb_prior_draw();
+    if (SEL == POMCP_SEL_PUCB && visits == 0) return pucb_prior_draw();
     if (visits == 0) return (int)d_select((uint32_t)A);   // mcts.py:532, 555
     const bool head = (lane & 7) == 0 && lane < kLanesPerAct * A;
     const int n = head ? (int)q.x : 0;
     const double v = head ? hilo(q.z, q.w) : 0.0;
-    if (p.sel == POMCP_SEL_UNIFORM) {   // min_visit_action_selection
+    if (SEL == POMCP_SEL_UNIFORM) {   // min_visit_action_selection
       int min_n = visits + 1, best = 0;
       for (int a = 0; a < A; ++a) {
         const int na = rl(n, 8 * a);
@@ -228,7 +233,7 @@ struct Tree {
       return best;
     }
     double score = -__builtin_inf();
-    if (p.sel == POMCP_SEL_UCB) {
+    if (SEL == POMCP_SEL_UCB) {
       const uint64_t unv = __ballot(head && n == 0);   // mcts.py:539-540
       if (unv) return (__ffsll((long long)unv) - 1) >> 3;
       if (visits >= p.logtab_n) {
@@ -256,11 +261,12 @@ struct Tree {
   }
 
   // _final_action_selection (mcts.py:565-600) on the root block registers.
+  template <int SEL>
   __device__ int final_action(const uint4& q, int visits) {
     const int A = p.A;
     uint32_t ties = 0;
     int nt = 0;
-    if (p.sel == POMCP_SEL_PUCB) {
+    if (SEL == POMCP_SEL_PUCB) {
       if (visits == 0) return (int)d_select((uint32_t)A);
       int mx = 0;
       for (int a = 0; a < A; ++a) {
@@ -438,6 +444,7 @@ struct Tree {
 
   // One simulation from the root (mcts.py:286-290 + _simulate 308-382).
   // qr: the root block held in registers (lane l: bytes [16l, 16l+16)).
+  template <int SEL>
   __device__ int simulate(uint4& qr) {
     const uint32_t k = d_belief((uint32_t)bsize);   // belief.py:55
     const uint4 pr = root_belief()[k];
@@ -449,8 +456,8 @@ struct Tree {
     double leaf = 0.0;
     // path registers: lane i holds tree level i
     uint32_t p_an = 0;
-    int p_done = 0, p_n = 0;
-    double p_r = 0.0, p_v = 0.0, p_tot = 0.0, p_agg = 0.0;
+    int p_done = 0;
+    double p_r = 0.0;
     uint4 q = qr;
     while (true) {
       if (depth > p.depth_limit || t > p.step_limit) break;   // mcts.py:315
@@ -463,7 +470,7 @@ struct Tree {
         break;
       }
       if (depth > 0) q = load_block(blk);
-      const int a = choose(q, nvis);                            // mcts.py:330
+      const int a = choose<SEL>(q, nvis);                       // mcts.py:330
       const int ao = (int)d_act(p.other, (uint32_t)p.A);       // mcts.py:331
       uint32_t n0, n1;
       joint_step(s0, s1, a, ao, &n0, &n1);                     // mcts.py:333
@@ -472,13 +479,7 @@ struct Tree {
       const uint32_t o1 = p.ego == 0 ? n1 : n0;
       const double r = drv_reward(e0, e1);
       const int done = (veh_done(e1) || (veh_done(n0) && veh_done(n1))) ? 1 : 0;
-      const uint64_t okey = obs_key_wave(g, e1, o1, p.ncells);
-      // the chosen action node's statistics, before the child's slot changes q
-      const int hl = kLanesPerAct * a;
-      const int an_vis = rl((int)q.x, hl);
-      const double an_val = hilo(rlu(q.z, hl), rlu(q.w, hl));
-      const double an_tot = hilo(rlu(q.x, hl + 1), rlu(q.y, hl + 1));
-      const double an_agg = hilo(rlu(q.z, hl + 1), rlu(q.w, hl + 1));
+      const uint64_t okey = uni64(obs_key_fast(m, e1, o1));
       ChildRef c;
       if (!child_ref(q, blk, a, okey, true, done, &c)) return -1;   // mcts.py:356-370
       if (depth == 0 && c.lane >= 0 && lane == c.lane) qr = q;
@@ -492,10 +493,6 @@ struct Tree {
         p_an = (uint32_t)(blk * p.A + a);
         p_r = r;
         p_done = done;
-        p_n = an_vis;
-        p_v = an_val;
-        p_tot = an_tot;
-        p_agg = an_agg;
       }
       ++plen;
       ++c_levels;
@@ -513,18 +510,36 @@ struct Tree {
       ++t;
       ++depth;
     }
-    // backup, deepest level first (mcts.py:374-381, node.py:166-178)
+    // backup, deepest level first (mcts.py:374-381, node.py:166-178).  The
+    // statistics of every level's action node are fetched together (lane i:
+    // level i, 32 B); the root level comes from the register copy.
+    uint4 s0v = make_uint4(0, 0, 0, 0), s1v = make_uint4(0, 0, 0, 0);
+    if (lane > 0 && lane < plen) {
+      const uint4* rec = reinterpret_cast<const uint4*>(an + (int64_t)p_an);
+      s0v = rec[0];
+      s1v = rec[1];
+    }
+    if (plen > 0) {
+      const int hl = kLanesPerAct * (int)(rl((int)p_an, 0) - (uint32_t)(root_blk * p.A));
+      const uint4 r0 = make_uint4(rlu(qr.x, hl), rlu(qr.y, hl), rlu(qr.z, hl), rlu(qr.w, hl));
+      const uint4 r1 = make_uint4(rlu(qr.x, hl + 1), rlu(qr.y, hl + 1), rlu(qr.z, hl + 1),
+                                  rlu(qr.w, hl + 1));
+      if (lane == 0) {
+        s0v = r0;
+        s1v = r1;
+      }
+    }
     double gr = leaf;
     for (int i = plen - 1; i >= 0; --i) {
       const uint32_t ani = rlu(p_an, i);
       const double r = rl_d(p_r, i);
       gr = rl(p_done, i) ? r : r + p.discount * gr;
-      const int n = rl(p_n, i) + 1;
-      const double value0 = rl_d(p_v, i);
-      const double total = rl_d(p_tot, i) + gr;
+      const int n = rl((int)s0v.x, i) + 1;
+      const double value0 = hilo(rlu(s0v.z, i), rlu(s0v.w, i));
+      const double total = hilo(rlu(s1v.x, i), rlu(s1v.y, i)) + gr;
       const double delta = gr - value0;
       const double value = value0 + delta / (double)n;
-      const double agg = rl_d(p_agg, i) + delta * (gr - value);
+      const double agg = hilo(rlu(s1v.z, i), rlu(s1v.w, i)) + delta * (gr - value);
       const uint4 w0 = pack_stats0(n, value), w1 = pack_stats1(total, agg);
       uint4* rec = reinterpret_cast<uint4*>(an + (int64_t)ani);
       if (lane == 0) rec[0] = w0;
@@ -554,7 +569,7 @@ struct Tree {
       const uint32_t avd = all & ~(1u << edest) & ~(1u << s);
       const int d = kth_bit(avd, d_model((uint32_t)popc8(avd)));
       ov = uniu(make_vehicle(g, s, d));
-      if (obs_key_wave(g, ev, ov, p.ncells) == obs) break;
+      if (uni64(obs_key_fast(m, ev, ov)) == obs) break;
     }
     *s0 = p.ego == 0 ? ev : ov;
     *s1 = p.ego == 0 ? ov : ev;
@@ -598,12 +613,13 @@ __global__ __launch_bounds__(256) void k_reset(DevParams p) {
 }
 
 __global__ __launch_bounds__(256) void k_update(DevParams p) {
-  __shared__ DrvGrid sg;
-  stage_grid(p.grid, sg);
+  __shared__ DrvModel sm;
+  stage_model(p.model, sm);
   const int tree = blockIdx.x * kTreesPerBlock + (threadIdx.x >> 6);
   if (tree >= p.B) return;
-  Tree T(p, sg, tree);
-  T.warm_rng();
+  __shared__ uint32_t rng_lds[kTreesPerBlock][1024];
+  Tree T(p, sm, tree);
+  T.warm_rng(rng_lds[threadIdx.x >> 6]);
   const int lane = T.lane;
   if (T.err == 0 && !T.root_abs) {   // mcts.py:161-162
     const uint64_t obs = uni64(p.in_obs[tree]);
@@ -671,7 +687,7 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
                 uint32_t n0, n1;
                 T.joint_step(uniu(hp.y), uniu(hp.z), action, ao, &n0, &n1);
                 const uint32_t e1 = p.ego == 0 ? n0 : n1, o1 = p.ego == 0 ? n1 : n0;
-                const uint64_t k = obs_key_wave(sg, e1, o1, p.ncells);
+                const uint64_t k = uni64(obs_key_fast(sm, e1, o1));
                 const uint4 rec = make_uint4(uniu(hp.x) + 1u, n0, n1, 0u);
                 if (k == obs) {
                   if (lane == 0) nb[n + got] = rec;
@@ -708,13 +724,18 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_search(DevParams p, int num_sims) {
-  __shared__ DrvGrid sg;
-  stage_grid(p.grid, sg);
+#ifndef POMCP_SEARCH_WAVES_PER_SIMD
+#define POMCP_SEARCH_WAVES_PER_SIMD 1
+#endif
+template <int SEL>
+__global__ __launch_bounds__(256, POMCP_SEARCH_WAVES_PER_SIMD) void k_search(DevParams p, int num_sims) {
+  __shared__ DrvModel sm;
+  stage_model(p.model, sm);
   const int tree = blockIdx.x * kTreesPerBlock + (threadIdx.x >> 6);
   if (tree >= p.B) return;
-  Tree T(p, sg, tree);
-  T.warm_rng();
+  __shared__ uint32_t rng_lds[kTreesPerBlock][1024];
+  Tree T(p, sm, tree);
+  T.warm_rng(rng_lds[threadIdx.x >> 6]);
   const int lane = T.lane;
   int action = 0, max_depth = 0, sims = 0;
   uint4 qr = make_uint4(0, 0, 0, 0);
@@ -724,13 +745,13 @@ __global__ __launch_bounds__(256) void k_search(DevParams p, int num_sims) {
     if (T.root_blk >= 0 && T.bsize <= 0) T.err = POMCP_E_STATE;
     if (T.err == 0) qr = T.load_block(T.root_blk);
     for (int s = 0; s < num_sims && T.err == 0; ++s) {
-      const int d = T.simulate(qr);
+      const int d = T.simulate<SEL>(qr);
       if (d < 0) break;
       ++T.root_visits;                              // mcts.py:288
       max_depth = d > max_depth ? d : max_depth;
       ++sims;
     }
-    if (T.err == 0) action = T.final_action(qr, T.root_visits);
+    if (T.err == 0) action = T.final_action<SEL>(qr, T.root_visits);
   }
   T.store_header();
   // root statistics: MCTS.step_statistics + root children
@@ -773,11 +794,15 @@ __global__ __launch_bounds__(256) void k_search(DevParams p, int num_sims) {
   }
 }
 
+template __global__ void k_search<POMCP_SEL_PUCB>(DevParams, int);
+template __global__ void k_search<POMCP_SEL_UCB>(DevParams, int);
+template __global__ void k_search<POMCP_SEL_UNIFORM>(DevParams, int);
+
 // Synthetic Driving-v1 roots: env b0 sample for tree b under key
 // (env_seed_base + b, 0x40000000), ego's initial observation.
 __global__ __launch_bounds__(256) void k_synthetic_obs(DevParams p, uint64_t env_seed_base) {
-  __shared__ DrvGrid sg;
-  stage_grid(p.grid, sg);
+  __shared__ DrvModel sm;
+  stage_model(p.model, sm);
   const int tree = blockIdx.x * kTreesPerBlock + (threadIdx.x >> 6);
   if (tree >= p.B) return;
   Streams env;
@@ -785,9 +810,9 @@ __global__ __launch_bounds__(256) void k_synthetic_obs(DevParams p, uint64_t env
   env.tree = 0x40000000u;
   for (int k = 0; k < 5; ++k) env.ctr[k] = 0;
   uint32_t s0, s1;
-  drv_sample_initial_state2(sg, [&](uint32_t n) { return env.model(n); }, &s0, &s1);
+  drv_sample_initial_state2(sm.g, [&](uint32_t n) { return env.model(n); }, &s0, &s1);
   const uint32_t e = p.ego == 0 ? s0 : s1, o = p.ego == 0 ? s1 : s0;
-  const uint64_t key = obs_key_wave(sg, e, o, p.ncells);
+  const uint64_t key = obs_key_fast(sm, e, o);
   if (lane_id() == 0) p.out_obs[tree] = key;
 }
 

@@ -9,7 +9,7 @@ import ctypes as C
 import os
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
-LIB_PATH = os.path.join(LIB_DIR, "libpomcp_hip.so")
+LIB_PATH = os.environ.get("POMCP_LIB_PATH") or os.path.join(LIB_DIR, "libpomcp_hip.so")
 
 POMCP_ABI_VERSION = 1
 POMCP_MAX_ACTIONS = 8
