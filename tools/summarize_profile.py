@@ -1,0 +1,81 @@
+"""Summarize a tools/profile.sh run (gpurun_out/prof_TAG) into profiles/.
+
+Writes
+  profiles/<TAG>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
+  profiles/<TAG>_summary.json       bench line + per-launch kernel time + PMC traffic
+  profiles/pmc_search.json          (with --current) the figure bench.py reports as
+                                    roofline.traffic for the same trees/sims
+
+HBM bytes per k_search launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: FETCH_SIZE and
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts half the bytes of wide reads, so it
+is doubled (MI355X_MICROARCH.md "HBM"); WRITE_SIZE is exact for 16-B stores.
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def read_counter(path, name, kernel="k_search"):
+    vals = []
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if kernel in row["Kernel_Name"] and row["Counter_Name"] == name:
+                vals.append(float(row["Counter_Value"]))
+    return vals
+
+
+def bench_line(log):
+    with open(log) as f:
+        for line in f:
+            if line.startswith("{"):
+                return json.loads(line)
+    return None
+
+
+def main():
+    tag = sys.argv[1]
+    current = "--current" in sys.argv
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    out = os.path.join(ROOT, "profiles")
+    os.makedirs(out, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
+                os.path.join(out, f"{tag}_kernel_stats.csv"))
+    stats = {}
+    with open(os.path.join(src, "trace", "run_kernel_stats.csv")) as f:
+        for row in csv.DictReader(f):
+            if "k_search" in row["Name"]:
+                stats = {"name": row["Name"], "calls": int(row["Calls"]),
+                         "avg_ms": float(row["AverageNs"]) / 1e6,
+                         "min_ms": float(row["MinNs"]) / 1e6, "max_ms": float(row["MaxNs"]) / 1e6}
+    fetch = read_counter(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = read_counter(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    # skip the warmup launch: every timed launch re-searches the same restored roots
+    f_avg = sum(fetch[1:]) / max(1, len(fetch) - 1) if len(fetch) > 1 else fetch[0]
+    w_avg = sum(write[1:]) / max(1, len(write) - 1) if len(write) > 1 else write[0]
+    hbm = (2 * f_avg + w_avg) * 1024
+    b = bench_line(os.path.join(src, "bench_trace.log"))
+    cfg = b["config"]
+    summary = {
+        "tag": tag, "bench": b, "k_search": stats,
+        "pmc": {"FETCH_SIZE_KiB_per_launch": f_avg, "WRITE_SIZE_KiB_per_launch": w_avg,
+                "hbm_bytes_per_launch": hbm,
+                "hbm_GBps": hbm / (stats["avg_ms"] * 1e-3) / 1e9,
+                "alg_bytes_per_launch": b["roofline"]["alg_bytes_per_launch"]},
+        "bench_kernel_ms_vs_rocprof_avg_ms": [b["roofline"]["kernel_ms"], stats["avg_ms"]],
+    }
+    with open(os.path.join(out, f"{tag}_summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    if current:
+        with open(os.path.join(out, "pmc_search.json"), "w") as f:
+            json.dump({"tag": tag, "trees": cfg["trees_per_gpu"], "sims": cfg["sims_per_tree"],
+                       "hbm_bytes_per_launch": hbm,
+                       "source": f"profiles/{tag}_summary.json"}, f, indent=1)
+    print(json.dumps(summary["pmc"], indent=1), stats)
+
+
+if __name__ == "__main__":
+    main()
