@@ -50,14 +50,6 @@ TEST_CFG = dict(discount=0.95, search_time_limit=0.1, c=math.sqrt(2), truncated=
                 step_limit=None, epsilon=0.92, state_belief_only=True)
 
 
-class _DevArray:
-    """__cuda_array_interface__ view of a device pointer owned by the engine."""
-
-    def __init__(self, ptr, n):
-        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<f8", "data": (ptr, False),
-                                         "version": 3}
-
-
 def cpu_baseline(sims, trees, seed):
     """The oracle (pure-Python restatement of the reference planner, pinned to it by
     tests/golden) timed on one host core over a bounded sample of the same workload."""
@@ -105,6 +97,7 @@ def main():
     from posggym_baselines_amd.envs import DrivingModel
     from posggym_baselines_amd.planning import BatchedPOMCP, MCTSConfig
     from posggym_baselines_amd.planning.engine import plan_capacities
+    from posggym_baselines_amd.planning.parallel import merge_buffer_tensor, root_parallel_merge
 
     B, S = args.trees, args.sims
     cfg = MCTSConfig(seed=args.seed, num_sims=S, **TEST_CFG)
@@ -117,7 +110,7 @@ def main():
     bp.init_synthetic(1000)
     bp.engine.rekey(args.seed ^ (rank << 32))
     A = bp.engine.A
-    merge = torch.as_tensor(_DevArray(bp.engine.merge_buffer_ptr(), B * A * 2), device=f"cuda:{dev}")
+    merge = merge_buffer_tensor(bp.engine, f"cuda:{dev}")
 
     def step(events=None):
         with torch.cuda.stream(stream):
@@ -127,12 +120,7 @@ def main():
             bp.search(fetch=False)
             if events is not None:
                 events[1].record(stream)
-            m = merge.view(B, A, 2)
-            if world > 1:
-                dist.all_reduce(merge)
-            vis, tot = m[..., 0], m[..., 1]
-            val = torch.where(vis > 0, tot / vis.clamp_min(1), torch.full_like(tot, -math.inf))
-            return torch.argmax(val, dim=-1)
+            return root_parallel_merge(merge, A, world)
 
     for _ in range(args.warmup):
         step()

@@ -48,3 +48,22 @@ def oracle_episode(cfg_kwargs, num_sims, env_seed, ego="0", grid="14x14RoundAbou
 
     trace = run_episode(step, env_seed, ego=ego, grid=grid, max_steps=max_steps)
     return trace, records
+
+
+def oracle_first_step(cfg_kwargs, num_sims, tree, env_seed, rekey=None):
+    """Record of the first planner step of an episode (synthetic root), optionally
+    with the search streams re-keyed after the initial update (root-parallel)."""
+    p = make_oracle(cfg_kwargs, num_sims, tree=tree)
+    recs = []
+
+    def step(obs):
+        p.update(None, obs)
+        if rekey is not None:
+            p.s.rekey(rekey)
+        a = p.get_action()
+        p.stats["searched"] = True
+        recs.append(oracle_record(p, True, a))
+        return a
+
+    run_episode(step, env_seed, max_steps=1)
+    return recs[0], p
