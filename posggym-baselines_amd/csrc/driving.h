@@ -245,13 +245,17 @@ namespace pb {
 
 // ---------------------------------------------------------------------------
 // Table-driven fast path (identical results to the functions above; the CPU
-// tests compare the host build of these against oracle/driving.py).
-//   nbr[cell * 4 + dir]      : neighbouring free cell (y << 4 | x) or 0xFF
+// tests compare the host build of these against oracle/driving.py and the GPU
+// tests the device build against the reference goldens).
+//   nbr2[cell * 4 + dir]     : low byte = next free cell in dir (or 0xFF), high
+//                              byte = the cell after it (or 0xFF)
 //   win_wall[cell * 4 + dir] : bit c set when window cell c is a wall / outside
+//   prog[k * 128 + initd]    : (0.5 * k) / initd for progress k = 1, 2 (k = 0 -> 0.0)
 struct DrvModel {
   DrvGrid g;
   uint16_t win_wall[1024];
-  uint8_t nbr[1024];
+  uint16_t nbr2[1024];
+  double prog[3 * 128];
 };
 
 template <class G>
@@ -261,22 +265,29 @@ PB_HD void build_model_tables(const G& g, DrvModel* m) {
     const int x = cell & 15, y = cell >> 4;
     for (int d = 0; d < 4; ++d) {
       const int nx = x + dir_dx(d), ny = y + dir_dy(d);
-      m->nbr[cell * 4 + d] = grid_free(g, nx, ny) ? (uint8_t)((ny << 4) | nx) : (uint8_t)0xFF;
+      int n1 = 0xFF, n2 = 0xFF;
+      if (grid_free(g, nx, ny)) {
+        n1 = (ny << 4) | nx;
+        const int mx = nx + dir_dx(d), my = ny + dir_dy(d);
+        if (grid_free(g, mx, my)) n2 = (my << 4) | mx;
+      }
+      m->nbr2[cell * 4 + d] = (uint16_t)(n1 | (n2 << 8));
       uint32_t w = 0;
-      const uint32_t self = (uint32_t)x | ((uint32_t)y << 4) | ((uint32_t)d << 8);
+      const int W = 2 * g.obs_side + 1;
+      const int r = (d + 1) & 3;
       for (int c = 0; c < ncells; ++c) {
-        const int W = 2 * g.obs_side + 1;
         const int fwd = g.obs_front - c / W;
         const int side = c % W - g.obs_side;
-        const int r = (d + 1) & 3;
         const int cx = x + fwd * dir_dx(d) + side * dir_dx(r);
         const int cy = y + fwd * dir_dy(d) + side * dir_dy(r);
         if (!grid_free(g, cx, cy)) w |= 1u << c;
       }
-      (void)self;
       m->win_wall[cell * 4 + d] = (uint16_t)w;
     }
   }
+  for (int k = 0; k < 3; ++k)
+    for (int i = 0; i < 128; ++i)
+      m->prog[k * 128 + i] = i == 0 ? 0.0 : (0.5 * (double)k) / (double)i;
 }
 
 // Window index of absolute cell (tx, ty) seen from (x, y) facing d, or -1.
@@ -315,58 +326,110 @@ PB_HD uint64_t obs_key_fast(const DrvModel& m, uint32_t self, uint32_t other) {
   return (uint64_t)cells | obs_tail(g, self);
 }
 
-// One vehicle's move on packed state (same semantics as move_vehicle).
-PB_HD uint32_t move_vehicle_fast(const DrvModel& m, uint32_t self, uint32_t other, int action,
-                                 bool* hit) {
-  *hit = false;
-  if (veh_done(self)) return self;
+// A vehicle's intended move before collision resolution.
+struct MovePlan {
+  uint32_t self;   // packed state before the move
+  int d, speed, cells;
+  uint32_t path;   // nbr2 entry along the move direction
+  bool done;
+};
+
+PB_HD MovePlan plan_move(const DrvModel& m, uint32_t self, int action) {
+  MovePlan p;
+  p.self = self;
+  p.done = veh_done(self);
   int d = (self >> 8) & 3, speed = (self >> 10) & 3;
   if (action == TURN_RIGHT) d = (d + 1) & 3;
   else if (action == TURN_LEFT) d = (d + 3) & 3;
   else if (action == ACCELERATE) speed = speed + 1 < FORWARD_FAST ? speed + 1 : FORWARD_FAST;
   else if (action == DECELERATE) speed = speed - 1 > REVERSE ? speed - 1 : REVERSE;
   const int move = speed != REVERSE ? d : ((d + 2) & 3);
-  const int cells = speed > STOPPED ? speed - STOPPED : STOPPED - speed;
-  const int ocell = (int)(other & 0xFF);
-  int cell = (int)(self & 0xFF);
-  for (int k = 0; k < cells; ++k) {
-    const int n = m.nbr[(cell << 2) | move];
-    if (n == 0xFF) {
-      speed = STOPPED;
-      break;
-    }
-    if (n == ocell) {
+  p.d = d;
+  p.speed = speed;
+  p.cells = speed > STOPPED ? speed - STOPPED : STOPPED - speed;
+  p.path = m.nbr2[((self & 0xFF) << 2) | (uint32_t)move];
+  return p;
+}
+
+// Resolve a planned move against the other vehicle's current cell; returns the
+// final cell, updates *speed and *hit.
+PB_HD int resolve_move(const MovePlan& p, int ocell, int* speed, bool* hit) {
+  int cell = (int)(p.self & 0xFF);
+  *speed = p.speed;
+  *hit = false;
+  if (p.cells >= 1) {
+    const int c1 = (int)(p.path & 0xFF);
+    if (c1 == 0xFF) {
+      *speed = STOPPED;
+    } else if (c1 == ocell) {
       *hit = true;
-      speed = STOPPED;
-      break;
+      *speed = STOPPED;
+    } else {
+      cell = c1;
+      if (p.cells >= 2) {
+        const int c2 = (int)(p.path >> 8);
+        if (c2 == 0xFF) {
+          *speed = STOPPED;
+        } else if (c2 == ocell) {
+          *hit = true;
+          *speed = STOPPED;
+        } else {
+          cell = c2;
+        }
+      }
     }
-    cell = n;
   }
+  return cell;
+}
+
+PB_HD uint32_t finish_move(const DrvModel& m, const MovePlan& p, int cell, int speed, bool hit) {
+  const uint32_t self = p.self;
   const int dest = (self >> 12) & 7;
   const int dist = m.g.dist[dest][cell];
   const int mind0 = (self >> 17) & 127;
   const int mind = mind0 < dist ? mind0 : dist;
-  return (self & 0x7F007000u) | (uint32_t)cell | ((uint32_t)d << 8) | ((uint32_t)speed << 10) |
-         ((uint32_t)(dist == 0) << 15) | ((uint32_t)(*hit) << 16) | ((uint32_t)mind << 17);
+  return (self & 0x7F007000u) | (uint32_t)cell | ((uint32_t)p.d << 8) | ((uint32_t)speed << 10) |
+         ((uint32_t)(dist == 0) << 15) | ((uint32_t)hit << 16) | ((uint32_t)mind << 17);
 }
 
+// Joint step for 2 agents (same semantics as drv_step2): both plans (one table
+// read each) first, then collisions in execution order.
 PB_HD void drv_step2_fast(const DrvModel& m, uint32_t s0, uint32_t s1, int a0, int a1, uint32_t j,
                           uint32_t* o0, uint32_t* o1) {
-  uint32_t v0 = s0, v1 = s1;
-  bool hit;
-  if (j == 0) {   // shuffle swapped: agent 1 moves first
-    v1 = move_vehicle_fast(m, v1, v0, a1, &hit);
-    if (hit && !veh_done(v0)) v0 |= 1u << 16;
-    v0 = move_vehicle_fast(m, v0, v1, a0, &hit);
-    if (hit && !veh_done(v1)) v1 |= 1u << 16;
-  } else {
-    v0 = move_vehicle_fast(m, v0, v1, a0, &hit);
-    if (hit && !veh_done(v1)) v1 |= 1u << 16;
-    v1 = move_vehicle_fast(m, v1, v0, a1, &hit);
-    if (hit && !veh_done(v0)) v0 |= 1u << 16;
+  const MovePlan p0 = plan_move(m, s0, a0);
+  const MovePlan p1 = plan_move(m, s1, a1);
+  const bool first1 = j == 0;   // shuffle swapped: agent 1 moves first
+  const MovePlan& pf = first1 ? p1 : p0;
+  const MovePlan& ps = first1 ? p0 : p1;
+  uint32_t vf = pf.self, vs = ps.self;
+  int cf = (int)(vf & 0xFF), cs = (int)(vs & 0xFF);
+  int spf = 0, sps = 0;
+  bool hf = false, hs = false, sec_crashed = false, fst_crashed = false;
+  bool movedf = false, moveds = false;
+  if (!pf.done) {
+    cf = resolve_move(pf, cs, &spf, &hf);
+    movedf = true;
+    if (hf && !ps.done) sec_crashed = true;
   }
-  *o0 = v0;
-  *o1 = v1;
+  if (!ps.done && !sec_crashed) {
+    cs = resolve_move(ps, cf, &sps, &hs);
+    moveds = true;
+    if (hs) fst_crashed = true;   // the first mover is hit (it may be done: no effect then)
+  }
+  if (movedf) vf = finish_move(m, pf, cf, spf, hf);
+  if (moveds) vs = finish_move(m, ps, cs, sps, hs);
+  if (sec_crashed) vs |= 1u << 16;
+  if (fst_crashed && !veh_done(vf)) vf |= 1u << 16;
+  *o0 = first1 ? vs : vf;
+  *o1 = first1 ? vf : vs;
+}
+
+// Ego reward for prev -> next (drv_reward), the division from the table.
+PB_HD double drv_reward_fast(const DrvModel& m, uint32_t prev, uint32_t next) {
+  if (veh_done(prev)) return 0.0;
+  const double base = ((next >> 16) & 1) ? -1.0 : (((next >> 15) & 1) ? 0.5 : 0.0);
+  const int progress = (int)((prev >> 17) & 127) - (int)((next >> 17) & 127);
+  return base + m.prog[progress * 128 + (int)((prev >> 24) & 127)];
 }
 
 }  // namespace pb

@@ -465,7 +465,7 @@ int pomcp_driving_step(const pomcp_grid* g, uint64_t seed, uint32_t tree, uint32
   *model_ctr = s.ctr[2];
   drv_step2_fast(m, state[0], state[1], actions[0], actions[1], j, &next_out[0], &next_out[1]);
   for (int i = 0; i < 2; ++i) {
-    if (rewards_out) rewards_out[i] = drv_reward(state[i], next_out[i]);
+    if (rewards_out) rewards_out[i] = drv_reward_fast(m, state[i], next_out[i]);
     if (terminated_out) terminated_out[i] = veh_done(next_out[i]) ? 1 : 0;
   }
   if (obs_keys_out) {

@@ -152,20 +152,25 @@ __device__ __forceinline__ uint32_t ovf_hash(uint32_t an, uint64_t key) {
   return (uint32_t)h;
 }
 
-// Wave-cached Philox stream in LDS: a page of 256 consecutive draws (64 Philox
-// blocks, one per lane, written with one ds_write_b128) is refilled by the
-// wave in one pass; a draw is one broadcast LDS read.  Same words as
-// philox_word() (philox.h).
+// Wave-cached Philox stream in LDS: a page of kRngPage consecutive draws
+// (kRngPage / 4 Philox blocks, one per lane, each written with one
+// ds_write_b128) is refilled by the wave in one pass; a draw is one broadcast
+// LDS read.  Same words as philox_word() (philox.h).
+constexpr uint32_t kRngPage = 128;
 struct LdsStream {
-  uint32_t* page;   // this wave's 256-word LDS page
+  uint32_t* page;   // this wave's kRngPage-word LDS page
   __device__ __forceinline__ void refill(uint64_t seed, uint32_t tree, uint32_t stream,
                                          uint32_t pg) {
     const uint32_t lane = (uint32_t)lane_id();
-    uint32_t c[4] = {pg * 64u + lane, 0u, stream, (uint32_t)(seed >> 32)};
-    philox4x32_10(c, (uint32_t)seed, tree);
-    reinterpret_cast<uint4*>(page)[lane] = make_uint4(c[0], c[1], c[2], c[3]);
+    if (lane < kRngPage / 4) {
+      uint32_t c[4] = {pg * (kRngPage / 4) + lane, 0u, stream, (uint32_t)(seed >> 32)};
+      philox4x32_10(c, (uint32_t)seed, tree);
+      reinterpret_cast<uint4*>(page)[lane] = make_uint4(c[0], c[1], c[2], c[3]);
+    }
   }
-  __device__ __forceinline__ uint32_t get(uint32_t j) const { return uniu(page[j & 255u]); }
+  __device__ __forceinline__ uint32_t get(uint32_t j) const {
+    return uniu(page[j & (kRngPage - 1)]);
+  }
 };
 
 }  // namespace pb

@@ -13,6 +13,7 @@
 #pragma clang fp contract(off)
 
 #include "pomcp_device.h"
+#include "driving_vec.h"
 
 namespace pb {
 
@@ -96,15 +97,15 @@ struct Tree {
     c_levels = c_expand = c_new = c_rollout = c_probes = 0;
   }
 
-  __device__ void warm_rng(uint32_t* lds) {   // lds: 4 x 256 words for this wave
+  __device__ void warm_rng(uint32_t* lds) {   // lds: 4 x kRngPage words for this wave
     r_belief.page = lds;
-    r_model.page = lds + 256;
-    r_act0.page = lds + 512;
-    r_act1.page = lds + 768;
-    r_belief.refill(seed, tkey, S_BELIEF, c_belief >> 8);
-    r_model.refill(seed, tkey, S_MODEL, c_model >> 8);
-    r_act0.refill(seed, tkey, S_ACT_BASE, c_act0 >> 8);
-    r_act1.refill(seed, tkey, S_ACT_BASE + 1, c_act1 >> 8);
+    r_model.page = lds + kRngPage;
+    r_act0.page = lds + 2 * kRngPage;
+    r_act1.page = lds + 3 * kRngPage;
+    r_belief.refill(seed, tkey, S_BELIEF, c_belief / kRngPage);
+    r_model.refill(seed, tkey, S_MODEL, c_model / kRngPage);
+    r_act0.refill(seed, tkey, S_ACT_BASE, c_act0 / kRngPage);
+    r_act1.refill(seed, tkey, S_ACT_BASE + 1, c_act1 / kRngPage);
   }
 
   __device__ void store_header() {
@@ -138,7 +139,7 @@ struct Tree {
   // ------------------------------------------------------------- RNG draws
   __device__ __forceinline__ uint32_t draw(LdsStream& cs, uint32_t& ctr, uint32_t stream) {
     const uint32_t j = ctr++;
-    if ((j & 255u) == 0u) cs.refill(seed, tkey, stream, j >> 8);
+    if ((j & (kRngPage - 1)) == 0u) cs.refill(seed, tkey, stream, j / kRngPage);
     return cs.get(j);
   }
   __device__ uint32_t d_belief(uint32_t n) { return uniform_int(draw(r_belief, c_belief, S_BELIEF), n); }
@@ -146,6 +147,25 @@ struct Tree {
   __device__ uint32_t d_act(int agent, uint32_t n) {
     return agent == 0 ? uniform_int(draw(r_act0, c_act0, S_ACT_BASE), n)
                       : uniform_int(draw(r_act1, c_act1, S_ACT_BASE + 1), n);
+  }
+  // vector-ALU variants: the word stays in a VGPR (see driving_vec.h)
+  __device__ uint32_t v_draw(LdsStream& cs, uint32_t& ctr, uint32_t stream) {
+    const uint32_t j = ctr++;
+    if ((j & (kRngPage - 1)) == 0u) cs.refill(seed, tkey, stream, j / kRngPage);
+    return vary(cs.page[j & (kRngPage - 1)]);
+  }
+  __device__ uint32_t v_model(uint32_t n) { return uniform_int(v_draw(r_model, c_model, S_MODEL), n); }
+  __device__ uint32_t v_act(int agent, uint32_t n) {
+    return agent == 0 ? uniform_int(v_draw(r_act0, c_act0, S_ACT_BASE), n)
+                      : uniform_int(v_draw(r_act1, c_act1, S_ACT_BASE + 1), n);
+  }
+  // joint step on the vector ALU (tree and rollout steps)
+  __device__ void joint_step_vec(uint32_t s0, uint32_t s1, uint32_t ego_a, uint32_t oth_a,
+                                 uint32_t* n0, uint32_t* n1) {
+    const uint32_t j = v_model(2);   // Python random.shuffle of the exec order
+    const uint32_t a0 = p.ego == 0 ? ego_a : oth_a;
+    const uint32_t a1 = p.ego == 0 ? oth_a : ego_a;
+    drv_step2_vec(m, s0, s1, a0, a1, j, n0, n1);
   }
   __device__ uint32_t d_select(uint32_t n) {
     return uniform_int(uniu(philox_word(seed, tkey, S_SELECT, c_select++)), n);
@@ -420,19 +440,21 @@ struct Tree {
     double ret = 0.0;
     int k = 0;
     while (depth <= p.depth_limit && t <= p.step_limit) {
-      const int ae = (int)d_act(p.ego, (uint32_t)p.A);     // search_policy.py:177
-      const int ao = (int)d_act(p.other, (uint32_t)p.A);   // other_policy.py:151
+      const uint32_t ae = v_act(p.ego, (uint32_t)p.A);     // search_policy.py:177
+      const uint32_t ao = v_act(p.other, (uint32_t)p.A);   // other_policy.py:151
       uint32_t n0, n1;
-      joint_step(s0, s1, ae, ao, &n0, &n1);
+      joint_step_vec(s0, s1, ae, ao, &n0, &n1);
       const uint32_t e0 = p.ego == 0 ? s0 : s1, e1 = p.ego == 0 ? n0 : n1;
-      const double r = drv_reward(e0, e1);
+      const double r = drv_reward_vec(m, e0, e1);
       if (k >= p.dpow_n) {
         err = POMCP_E_ARENA;
         break;
       }
       ret += p.dpow[k] * r;   // mcts.py:420-422
       ++c_rollout;
-      if (veh_done(e1) || (veh_done(n0) && veh_done(n1))) break;
+      const bool done = ((e1 >> 15) & 3u) != 0u ||
+                        (((n0 >> 15) & 3u) != 0u && ((n1 >> 15) & 3u) != 0u);
+      if (uni(done ? 1 : 0)) break;
       s0 = n0;
       s1 = n1;
       ++t;
@@ -449,7 +471,7 @@ struct Tree {
     const uint32_t k = d_belief((uint32_t)bsize);   // belief.py:55
     const uint4 pr = root_belief()[k];
     int t = uni((int)pr.x);
-    uint32_t s0 = uniu(pr.y), s1 = uniu(pr.z);
+    uint32_t s0 = vary(pr.y), s1 = vary(pr.z);
     int blk = root_blk, nvis = root_visits, depth = 0, plen = 0;
     int32_t* leaf_blk_ptr = nullptr;
     int leaf_lane = -1;
@@ -471,15 +493,16 @@ struct Tree {
       }
       if (depth > 0) q = load_block(blk);
       const int a = choose<SEL>(q, nvis);                       // mcts.py:330
-      const int ao = (int)d_act(p.other, (uint32_t)p.A);       // mcts.py:331
+      const uint32_t ao = v_act(p.other, (uint32_t)p.A);        // mcts.py:331
       uint32_t n0, n1;
-      joint_step(s0, s1, a, ao, &n0, &n1);                     // mcts.py:333
+      joint_step_vec(s0, s1, (uint32_t)a, ao, &n0, &n1);       // mcts.py:333
       const uint32_t e0 = p.ego == 0 ? s0 : s1;
       const uint32_t e1 = p.ego == 0 ? n0 : n1;
       const uint32_t o1 = p.ego == 0 ? n1 : n0;
-      const double r = drv_reward(e0, e1);
-      const int done = (veh_done(e1) || (veh_done(n0) && veh_done(n1))) ? 1 : 0;
-      const uint64_t okey = uni64(obs_key_fast(m, e1, o1));
+      const double r = drv_reward_vec(m, e0, e1);
+      const int done = uni((((e1 >> 15) & 3u) != 0u ||
+                            (((n0 >> 15) & 3u) != 0u && ((n1 >> 15) & 3u) != 0u)) ? 1 : 0);
+      const uint64_t okey = obs_key_vec(m, e1, o1);
       ChildRef c;
       if (!child_ref(q, blk, a, okey, true, done, &c)) return -1;   // mcts.py:356-370
       if (depth == 0 && c.lane >= 0 && lane == c.lane) qr = q;
@@ -617,7 +640,7 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
   stage_model(p.model, sm);
   const int tree = blockIdx.x * kTreesPerBlock + (threadIdx.x >> 6);
   if (tree >= p.B) return;
-  __shared__ uint32_t rng_lds[kTreesPerBlock][1024];
+  __shared__ uint32_t rng_lds[kTreesPerBlock][4 * kRngPage];
   Tree T(p, sm, tree);
   T.warm_rng(rng_lds[threadIdx.x >> 6]);
   const int lane = T.lane;
@@ -725,7 +748,7 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
 }
 
 #ifndef POMCP_SEARCH_WAVES_PER_SIMD
-#define POMCP_SEARCH_WAVES_PER_SIMD 1
+#define POMCP_SEARCH_WAVES_PER_SIMD 6
 #endif
 template <int SEL>
 __global__ __launch_bounds__(256, POMCP_SEARCH_WAVES_PER_SIMD) void k_search(DevParams p, int num_sims) {
@@ -733,7 +756,7 @@ __global__ __launch_bounds__(256, POMCP_SEARCH_WAVES_PER_SIMD) void k_search(Dev
   stage_model(p.model, sm);
   const int tree = blockIdx.x * kTreesPerBlock + (threadIdx.x >> 6);
   if (tree >= p.B) return;
-  __shared__ uint32_t rng_lds[kTreesPerBlock][1024];
+  __shared__ uint32_t rng_lds[kTreesPerBlock][4 * kRngPage];
   Tree T(p, sm, tree);
   T.warm_rng(rng_lds[threadIdx.x >> 6]);
   const int lane = T.lane;
