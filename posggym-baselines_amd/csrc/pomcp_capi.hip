@@ -13,6 +13,7 @@
 
 // Single translation unit: the kernels are compiled together with their launchers.
 #include "pomcp_kernels.hip"
+#include "pomcp_search.hip"
 #include "../../include/pomcp_debug.h"
 
 using namespace pb;
@@ -68,6 +69,9 @@ static int dev_alloc(pomcp_ctx* ctx, void** out, size_t bytes) {
 }
 
 static unsigned grid_blocks(int B) { return (unsigned)((B + kTreesPerBlock - 1) / kTreesPerBlock); }
+static unsigned search_blocks(int B) {
+  return (unsigned)((B + kGroupsPerBlock - 1) / kGroupsPerBlock);
+}
 
 extern "C" {
 
@@ -104,7 +108,8 @@ static int validate(const pomcp_config* c, std::string* why) {
   if (c->depth_limit < 0 || c->step_limit < 0) return bad("depth/step limit");
   if (c->num_particles < 1 || c->extra_particles < 0) return bad("num_particles");
   if (c->num_trees < 1) return bad("num_trees >= 1");
-  if (c->max_blocks < 1 || c->max_blocks > INT32_MAX / 64) return bad("max_blocks");
+  if (c->max_blocks < 1 || c->max_blocks * c->num_actions * 128 > INT32_MAX) return bad("max_blocks");
+  if (c->num_actions > 6) { *why = "the search kernel supports at most 6 actions"; return POMCP_E_UNSUPPORTED; }
   if (c->max_particles < 1 || c->max_particles > INT32_MAX) return bad("max_particles");
   if (c->max_belief < 2 * (c->num_particles + c->extra_particles)) return bad("max_belief too small");
   if (c->overflow_slots < kBucket || (c->overflow_slots & (c->overflow_slots - 1)) != 0 ||
@@ -307,7 +312,7 @@ int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_key
 int pomcp_search(pomcp_ctx* ctx, int32_t num_sims, int32_t* actions_out) {
   if (!ctx || num_sims < 0) return POMCP_E_INVALID;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
-  const dim3 grid(grid_blocks(ctx->dp.B)), block(256);
+  const dim3 grid(search_blocks(ctx->dp.B)), block(256);
   switch (ctx->dp.sel) {
     case POMCP_SEL_PUCB:
       hipLaunchKernelGGL(k_search<POMCP_SEL_PUCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims);

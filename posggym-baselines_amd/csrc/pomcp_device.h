@@ -21,6 +21,10 @@
 
 namespace pb {
 
+#ifndef POMCP_SEARCH_WAVES_PER_SIMD
+#define POMCP_SEARCH_WAVES_PER_SIMD 1
+#endif
+
 constexpr int kWave = 64;
 constexpr int kTreesPerBlock = 4;      // 256-thread workgroups, one tree per wave
 constexpr int kSlots = 6;              // inline obs children per action node
@@ -34,8 +38,11 @@ constexpr uint64_t kAbsorbBit = 1ull << 63;
 constexpr int kMaxPath = 64;           // tree levels per simulation (one lane each)
 constexpr uint32_t kRootId = 0;        // obs node id of a root created by the initial update
 
-// Action node (node.py:120-178) with its obs children inline (node.py:144-160).
-// 128 B: part 0 {visits, pad, value}, part 1 {total, agg}, parts 2..7 children.
+// Action nodes (node.py:120-178) with their obs children inline (node.py:144-160).
+// An expanded obs node owns a block of A x 128 B, laid out in 16 B parts:
+//   part a: {visits, pad, value} of action a; part A + a: {total, agg};
+//   part 2A + 6a + k: child slot k of action a.
+// `ActNode` is the 128 B allocation unit (its fields describe the sizes only).
 struct ChildSlot {
   uint64_t key;     // obs key | valid << 62 | is_absorbing << 63
   int32_t block;    // action block of the child obs node (-1 = leaf)
@@ -109,6 +116,10 @@ __device__ __forceinline__ double rl_d(double v, int l) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
   const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
   return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double hilo_d(uint32_t lo, uint32_t hi) {
+  return __hiloint2double((int)hi, (int)lo);
 }
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }

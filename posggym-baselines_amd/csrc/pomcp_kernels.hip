@@ -148,25 +148,6 @@ struct Tree {
     return agent == 0 ? uniform_int(draw(r_act0, c_act0, S_ACT_BASE), n)
                       : uniform_int(draw(r_act1, c_act1, S_ACT_BASE + 1), n);
   }
-  // vector-ALU variants: the word stays in a VGPR (see driving_vec.h)
-  __device__ uint32_t v_draw(LdsStream& cs, uint32_t& ctr, uint32_t stream) {
-    const uint32_t j = ctr++;
-    if ((j & (kRngPage - 1)) == 0u) cs.refill(seed, tkey, stream, j / kRngPage);
-    return vary(cs.page[j & (kRngPage - 1)]);
-  }
-  __device__ uint32_t v_model(uint32_t n) { return uniform_int(v_draw(r_model, c_model, S_MODEL), n); }
-  __device__ uint32_t v_act(int agent, uint32_t n) {
-    return agent == 0 ? uniform_int(v_draw(r_act0, c_act0, S_ACT_BASE), n)
-                      : uniform_int(v_draw(r_act1, c_act1, S_ACT_BASE + 1), n);
-  }
-  // joint step on the vector ALU (tree and rollout steps)
-  __device__ void joint_step_vec(uint32_t s0, uint32_t s1, uint32_t ego_a, uint32_t oth_a,
-                                 uint32_t* n0, uint32_t* n1) {
-    const uint32_t j = v_model(2);   // Python random.shuffle of the exec order
-    const uint32_t a0 = p.ego == 0 ? ego_a : oth_a;
-    const uint32_t a1 = p.ego == 0 ? oth_a : ego_a;
-    drv_step2_vec(m, s0, s1, a0, a1, j, n0, n1);
-  }
   __device__ uint32_t d_select(uint32_t n) {
     return uniform_int(uniu(philox_word(seed, tkey, S_SELECT, c_select++)), n);
   }
@@ -214,107 +195,6 @@ struct Tree {
     drv_step2_fast(m, s0, s1, a0, a1, j, n0, n1);
     *n0 = uniu(*n0);
     *n1 = uniu(*n1);
-  }
-
-  // PUCB with N == 0 (mcts.py:494-500): random.choices(actions, weights=prior),
-  // cum_weights by itertools.accumulate, bisect(cum, random() * total, 0, A-1).
-  __device__ int pucb_prior_draw() {
-    const int A = p.A;
-    const double w = 1.0 / (double)A;
-    double total = w;
-    for (int k = 1; k < A; ++k) total = total + w;
-    const double x = d_select_float() * (total + 0.0);
-    double acc = w;
-    for (int k = 0; k < A - 1; ++k) {   // bisect_right over the running sums
-      if (x < acc) return k;
-      acc = acc + w;
-    }
-    return A - 1;
-  }
-
-  // _search_action_selection (mcts.py:492-563) on a block held in registers.
-  template <int SEL>
-  __device__ int choose(const uint4& q, int visits) {
-    const int A = p.A;
-    if (SEL == POMCP_SEL_PUCB && visits == 0) return pucb_prior_draw();
-    if (visits == 0) return (int)d_select((uint32_t)A);   // mcts.py:532, 555
-    const bool head = (lane & 7) == 0 && lane < kLanesPerAct * A;
-    const int n = head ? (int)q.x : 0;
-    const double v = head ? hilo(q.z, q.w) : 0.0;
-    if (SEL == POMCP_SEL_UNIFORM) {   // min_visit_action_selection
-      int min_n = visits + 1, best = 0;
-      for (int a = 0; a < A; ++a) {
-        const int na = rl(n, 8 * a);
-        if (na < min_n) {
-          min_n = na;
-          best = a;
-        }
-      }
-      return best;
-    }
-    double score = -__builtin_inf();
-    if (SEL == POMCP_SEL_UCB) {
-      const uint64_t unv = __ballot(head && n == 0);   // mcts.py:539-540
-      if (unv) return (__ffsll((long long)unv) - 1) >> 3;
-      if (visits >= p.logtab_n) {
-        err = POMCP_E_ARENA;
-        return 0;
-      }
-      const double log_n = p.logtab[visits];
-      if (head) score = normalize(v) + p.c * sqrt(log_n / (double)n);   // mcts.py:541-542
-    } else {   // PUCB, mcts.py:502-527
-      const double noise = 1.0 / (double)A;
-      const double prior = (1.0 / (double)A) * (1.0 - p.pucb_f) + p.pucb_f * noise;
-      const double sqrt_n = sqrt((double)visits);
-      if (head) score = (n > 0 ? normalize(v) : 0.0) + p.c * prior * (sqrt_n / (double)(1 + n));
-    }
-    double best_v = -__builtin_inf();
-    int best = 0;
-    for (int a = 0; a < A; ++a) {   // strict '>' in action order
-      const double sa = rl_d(score, 8 * a);
-      if (sa > best_v) {
-        best_v = sa;
-        best = a;
-      }
-    }
-    return best;
-  }
-
-  // _final_action_selection (mcts.py:565-600) on the root block registers.
-  template <int SEL>
-  __device__ int final_action(const uint4& q, int visits) {
-    const int A = p.A;
-    uint32_t ties = 0;
-    int nt = 0;
-    if (SEL == POMCP_SEL_PUCB) {
-      if (visits == 0) return (int)d_select((uint32_t)A);
-      int mx = 0;
-      for (int a = 0; a < A; ++a) {
-        const int na = rl((int)q.x, 8 * a);
-        if (na == mx) {
-          ties |= 1u << a;
-          ++nt;
-        } else if (na > mx) {
-          mx = na;
-          ties = 1u << a;
-          nt = 1;
-        }
-      }
-    } else {
-      double mx = -__builtin_inf();
-      for (int a = 0; a < A; ++a) {
-        const double va = hilo(rlu(q.z, 8 * a), rlu(q.w, 8 * a));
-        if (va == mx) {
-          ties |= 1u << a;
-          ++nt;
-        } else if (va > mx) {
-          mx = va;
-          ties = 1u << a;
-          nt = 1;
-        }
-      }
-    }
-    return kth_bit(ties, d_select((uint32_t)nt));
   }
 
   // Overflow map (children beyond the kSlots inline ones).
@@ -378,12 +258,12 @@ struct Tree {
   __device__ bool child_ref(uint4& q, int blk, int a, uint64_t okey, bool visit, int done,
                             ChildRef* c) {
     const uint32_t ani = (uint32_t)(blk * p.A + a);
-    const int lo = kLanesPerAct * a + 2;
+    const int lo = 2 * p.A + kSlots * a;   // block layout: see pomcp_search.hip
     const bool cl = lane >= lo && lane < lo + kSlots;
     const uint64_t skey = (uint64_t)q.x | ((uint64_t)q.y << 32);
     const bool valid = cl && (skey & kValidBit) != 0;
     const uint64_t m = __ballot(valid && (skey & kObsMask) == okey);
-    uint4* slots = reinterpret_cast<uint4*>(an + (int64_t)ani) + 2;
+    uint4* slots = reinterpret_cast<uint4*>(an + (int64_t)blk * p.A) + lo;
     int L;
     bool is_new = false;
     if (m) {
@@ -433,148 +313,6 @@ struct Tree {
     c->lane = L;
     c->blk_ptr = reinterpret_cast<int32_t*>(slots + k) + 2;
     return true;
-  }
-
-  // MCTS._rollout (mcts.py:405-452), random search policy.
-  __device__ double rollout(uint32_t s0, uint32_t s1, int t, int depth) {
-    double ret = 0.0;
-    int k = 0;
-    while (depth <= p.depth_limit && t <= p.step_limit) {
-      const uint32_t ae = v_act(p.ego, (uint32_t)p.A);     // search_policy.py:177
-      const uint32_t ao = v_act(p.other, (uint32_t)p.A);   // other_policy.py:151
-      uint32_t n0, n1;
-      joint_step_vec(s0, s1, ae, ao, &n0, &n1);
-      const uint32_t e0 = p.ego == 0 ? s0 : s1, e1 = p.ego == 0 ? n0 : n1;
-      const double r = drv_reward_vec(m, e0, e1);
-      if (k >= p.dpow_n) {
-        err = POMCP_E_ARENA;
-        break;
-      }
-      ret += p.dpow[k] * r;   // mcts.py:420-422
-      ++c_rollout;
-      const bool done = ((e1 >> 15) & 3u) != 0u ||
-                        (((n0 >> 15) & 3u) != 0u && ((n1 >> 15) & 3u) != 0u);
-      if (uni(done ? 1 : 0)) break;
-      s0 = n0;
-      s1 = n1;
-      ++t;
-      ++depth;
-      ++k;
-    }
-    return ret;
-  }
-
-  // One simulation from the root (mcts.py:286-290 + _simulate 308-382).
-  // qr: the root block held in registers (lane l: bytes [16l, 16l+16)).
-  template <int SEL>
-  __device__ int simulate(uint4& qr) {
-    const uint32_t k = d_belief((uint32_t)bsize);   // belief.py:55
-    const uint4 pr = root_belief()[k];
-    int t = uni((int)pr.x);
-    uint32_t s0 = vary(pr.y), s1 = vary(pr.z);
-    int blk = root_blk, nvis = root_visits, depth = 0, plen = 0;
-    int32_t* leaf_blk_ptr = nullptr;
-    int leaf_lane = -1;
-    double leaf = 0.0;
-    // path registers: lane i holds tree level i
-    uint32_t p_an = 0;
-    int p_done = 0;
-    double p_r = 0.0;
-    uint4 q = qr;
-    while (true) {
-      if (depth > p.depth_limit || t > p.step_limit) break;   // mcts.py:315
-      if (blk < 0) {                                            // mcts.py:318-328
-        const int b = alloc_block();
-        if (b < 0) return -1;
-        if (lane == 0) *leaf_blk_ptr = b;
-        if (depth == 1 && lane == leaf_lane) qr.z = (uint32_t)b;   // root child slot
-        leaf = rollout(s0, s1, t, depth);
-        break;
-      }
-      if (depth > 0) q = load_block(blk);
-      const int a = choose<SEL>(q, nvis);                       // mcts.py:330
-      const uint32_t ao = v_act(p.other, (uint32_t)p.A);        // mcts.py:331
-      uint32_t n0, n1;
-      joint_step_vec(s0, s1, (uint32_t)a, ao, &n0, &n1);       // mcts.py:333
-      const uint32_t e0 = p.ego == 0 ? s0 : s1;
-      const uint32_t e1 = p.ego == 0 ? n0 : n1;
-      const uint32_t o1 = p.ego == 0 ? n1 : n0;
-      const double r = drv_reward_vec(m, e0, e1);
-      const int done = uni((((e1 >> 15) & 3u) != 0u ||
-                            (((n0 >> 15) & 3u) != 0u && ((n1 >> 15) & 3u) != 0u)) ? 1 : 0);
-      const uint64_t okey = obs_key_vec(m, e1, o1);
-      ChildRef c;
-      if (!child_ref(q, blk, a, okey, true, done, &c)) return -1;   // mcts.py:356-370
-      if (depth == 0 && c.lane >= 0 && lane == c.lane) qr = q;
-      if (n_log >= p.Np) {
-        err = POMCP_E_ARENA;
-        return -1;
-      }
-      if (lane == 0) plog[n_log] = make_uint4(c.id, (uint32_t)(t + 1), n0, n1);
-      ++n_log;                                                  // mcts.py:371
-      if (lane == plen) {
-        p_an = (uint32_t)(blk * p.A + a);
-        p_r = r;
-        p_done = done;
-      }
-      ++plen;
-      ++c_levels;
-      if (done) break;
-      if (plen >= kMaxPath) {
-        err = POMCP_E_ARENA;
-        return -1;
-      }
-      blk = c.blk;
-      nvis = c.visits;
-      leaf_blk_ptr = c.blk_ptr;
-      leaf_lane = c.lane;
-      s0 = n0;
-      s1 = n1;
-      ++t;
-      ++depth;
-    }
-    // backup, deepest level first (mcts.py:374-381, node.py:166-178).  The
-    // statistics of every level's action node are fetched together (lane i:
-    // level i, 32 B); the root level comes from the register copy.
-    uint4 s0v = make_uint4(0, 0, 0, 0), s1v = make_uint4(0, 0, 0, 0);
-    if (lane > 0 && lane < plen) {
-      const uint4* rec = reinterpret_cast<const uint4*>(an + (int64_t)p_an);
-      s0v = rec[0];
-      s1v = rec[1];
-    }
-    if (plen > 0) {
-      const int hl = kLanesPerAct * (int)(rl((int)p_an, 0) - (uint32_t)(root_blk * p.A));
-      const uint4 r0 = make_uint4(rlu(qr.x, hl), rlu(qr.y, hl), rlu(qr.z, hl), rlu(qr.w, hl));
-      const uint4 r1 = make_uint4(rlu(qr.x, hl + 1), rlu(qr.y, hl + 1), rlu(qr.z, hl + 1),
-                                  rlu(qr.w, hl + 1));
-      if (lane == 0) {
-        s0v = r0;
-        s1v = r1;
-      }
-    }
-    double gr = leaf;
-    for (int i = plen - 1; i >= 0; --i) {
-      const uint32_t ani = rlu(p_an, i);
-      const double r = rl_d(p_r, i);
-      gr = rl(p_done, i) ? r : r + p.discount * gr;
-      const int n = rl((int)s0v.x, i) + 1;
-      const double value0 = hilo(rlu(s0v.z, i), rlu(s0v.w, i));
-      const double total = hilo(rlu(s1v.x, i), rlu(s1v.y, i)) + gr;
-      const double delta = gr - value0;
-      const double value = value0 + delta / (double)n;
-      const double agg = hilo(rlu(s1v.z, i), rlu(s1v.w, i)) + delta * (gr - value);
-      const uint4 w0 = pack_stats0(n, value), w1 = pack_stats1(total, agg);
-      uint4* rec = reinterpret_cast<uint4*>(an + (int64_t)ani);
-      if (lane == 0) rec[0] = w0;
-      if (lane == 1) rec[1] = w1;
-      if (i == 0) {   // root level: keep the register copy current
-        const int hl = kLanesPerAct * (int)(ani - (uint32_t)(root_blk * p.A));
-        if (lane == hl) qr = w0;
-        if (lane == hl + 1) qr = w1;
-      }
-      mm_update(value);
-    }
-    return depth;
   }
 
   // sample_agent_initial_state (oracle/driving.py): ego from its obs, the other
@@ -746,80 +484,6 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
     p.upd_out[2 * tree + 1] = T.err;
   }
 }
-
-#ifndef POMCP_SEARCH_WAVES_PER_SIMD
-#define POMCP_SEARCH_WAVES_PER_SIMD 6
-#endif
-template <int SEL>
-__global__ __launch_bounds__(256, POMCP_SEARCH_WAVES_PER_SIMD) void k_search(DevParams p, int num_sims) {
-  __shared__ DrvModel sm;
-  stage_model(p.model, sm);
-  const int tree = blockIdx.x * kTreesPerBlock + (threadIdx.x >> 6);
-  if (tree >= p.B) return;
-  __shared__ uint32_t rng_lds[kTreesPerBlock][4 * kRngPage];
-  Tree T(p, sm, tree);
-  T.warm_rng(rng_lds[threadIdx.x >> 6]);
-  const int lane = T.lane;
-  int action = 0, max_depth = 0, sims = 0;
-  uint4 qr = make_uint4(0, 0, 0, 0);
-  if (T.err == 0 && T.root_t == 0) T.err = POMCP_E_STATE;
-  if (T.err == 0 && !T.root_abs) {   // mcts.py:270-272
-    if (T.root_blk < 0) T.root_blk = T.alloc_block();   // mcts.py:279-281
-    if (T.root_blk >= 0 && T.bsize <= 0) T.err = POMCP_E_STATE;
-    if (T.err == 0) qr = T.load_block(T.root_blk);
-    for (int s = 0; s < num_sims && T.err == 0; ++s) {
-      const int d = T.simulate<SEL>(qr);
-      if (d < 0) break;
-      ++T.root_visits;                              // mcts.py:288
-      max_depth = d > max_depth ? d : max_depth;
-      ++sims;
-    }
-    if (T.err == 0) action = T.final_action<SEL>(qr, T.root_visits);
-  }
-  T.store_header();
-  // root statistics: MCTS.step_statistics + root children
-  pomcp_root_stats* st = p.stats + tree;
-  const int A = p.A;
-  const bool have = T.root_blk >= 0 && !T.root_abs;
-  for (int a = 0; a < A; ++a) {
-    const int hl = kLanesPerAct * a;
-    const int nv = have ? rl((int)qr.x, hl) : 0;
-    const double va = have ? hilo(rlu(qr.z, hl), rlu(qr.w, hl)) : 0.0;
-    const double tot = have ? hilo(rlu(qr.x, hl + 1), rlu(qr.y, hl + 1)) : 0.0;
-    if (lane == a) {
-      st->child_visits[a] = nv;
-      st->child_values[a] = va;
-      st->child_totals[a] = tot;
-      p.merge[((int64_t)tree * A + a) * 2] = (double)nv;
-      p.merge[((int64_t)tree * A + a) * 2 + 1] = tot;
-    }
-  }
-  if (lane == 0) {
-    st->action = action;
-    st->num_sims = sims;
-    st->search_depth = max_depth;
-    st->root_visits = T.root_visits;
-    st->root_absorbing = T.root_abs;
-    st->belief_size = T.bsize;
-    st->error = T.err;
-    st->num_children = have ? A : 0;
-    st->min_value = T.mm_min;
-    st->max_value = T.mm_max;
-    st->n_levels = T.c_levels;
-    st->n_expansions = T.c_expand;
-    st->n_new_nodes = T.c_new;
-    st->n_rollout_steps = T.c_rollout;
-    st->n_probes = T.c_probes;
-    st->n_obs_nodes = T.n_nodes;
-    st->n_blocks = T.n_blocks;
-    st->n_log = T.n_log;
-    st->pad = 0;
-  }
-}
-
-template __global__ void k_search<POMCP_SEL_PUCB>(DevParams, int);
-template __global__ void k_search<POMCP_SEL_UCB>(DevParams, int);
-template __global__ void k_search<POMCP_SEL_UNIFORM>(DevParams, int);
 
 // Synthetic Driving-v1 roots: env b0 sample for tree b under key
 // (env_seed_base + b, 0x40000000), ego's initial observation.
