@@ -231,7 +231,9 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
     h[t].seed = c.seed;
     h[t].tree_key = c.tree_key_base + (uint32_t)t;
   }
-  if (hipMemcpy(d.hdr, h.data(), sizeof(TreeHdr) * (size_t)B, hipMemcpyHostToDevice) !=
+  // same stream as the zeroing memset above (the engine stream is non-blocking:
+  // a null-stream copy would not be ordered after it)
+  if (hipMemcpyAsync(d.hdr, h.data(), sizeof(TreeHdr) * (size_t)B, hipMemcpyHostToDevice, s) !=
       hipSuccess) {
     ctx->err = "header upload failed";
     pomcp_destroy(ctx);
@@ -239,7 +241,8 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
   }
   ctx->host_upd.resize((size_t)(2 * B));
   ctx->host_stats.resize((size_t)B);
-  // the tables were copied asynchronously from caller memory: finish before returning
+  // tables and headers were copied asynchronously from caller / local memory:
+  // finish before returning
   if (hipStreamSynchronize(s) != hipSuccess) {
     pomcp_destroy(ctx);
     return POMCP_E_HIP;
@@ -422,7 +425,9 @@ int pomcp_snapshot(pomcp_ctx* ctx) {
       return fail(ctx, POMCP_E_STATE, "snapshot: every tree must be right after its initial update");
   }
   if (!ctx->snap_hdr) HIP_TRY(ctx, hipMalloc(&ctx->snap_hdr, sizeof(TreeHdr) * B));
-  HIP_TRY(ctx, hipMemcpy(ctx->snap_hdr, h.data(), sizeof(TreeHdr) * B, hipMemcpyHostToDevice));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->snap_hdr, h.data(), sizeof(TreeHdr) * B, hipMemcpyHostToDevice,
+                              ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   ctx->have_snapshot = true;
   return POMCP_OK;
 }

@@ -384,6 +384,28 @@ __global__ __launch_bounds__(256, POMCP_SEARCH_WAVES_PER_SIMD) void k_search(Dev
   T.warm_rng();
   const bool any_sims = num_sims > 0;
   if (!any_sims && S.phase != PH_DONE) S.phase = PH_DONE;
+  // Arrival at an obs node (start of _simulate, mcts.py:315-328): depth/step
+  // cutoff -> back up 0; unexpanded -> expand and roll out; else select there.
+  auto arrive = [&]() {
+    if (S.depth > p.depth_limit || S.t > p.step_limit) {     // mcts.py:315
+      S.ret = 0.0;
+      S.phase = PH_BACKUP;
+    } else if (S.blk < 0) {                                   // mcts.py:318-328
+      const int b = T.alloc_block();
+      if (b < 0) {
+        S.phase = PH_DONE;
+      } else {
+        if (i == 0) *S.leaf_ptr = b;
+        S.ret = 0.0;
+        S.k = 0;
+        S.rdepth = S.depth;   // the rollout's own depth counter (mcts.py:449)
+        S.phase = PH_ROLL;
+      }
+    }
+  };
+  // Loop iteration = one step of every tree: start a simulation (and select at
+  // the root), one tree level, one rollout step, the backup (in this order, so a
+  // depth-2 search takes 3 iterations per simulation).
   while (__ballot(S.phase != PH_DONE)) {
     // ---------------------------------------------------------- start a simulation
     if (S.phase == PH_START) {
@@ -400,25 +422,12 @@ __global__ __launch_bounds__(256, POMCP_SEARCH_WAVES_PER_SIMD) void k_search(Dev
         S.depth = 0;
         S.plen = 0;
         S.phase = PH_LEVEL;
+        arrive();
       }
     }
     // ---------------------------------------------------------- one tree level
     if (S.phase == PH_LEVEL) {
-      if (S.depth > p.depth_limit || S.t > p.step_limit) {   // mcts.py:315
-        S.ret = 0.0;
-        S.phase = PH_BACKUP;
-      } else if (S.blk < 0) {                                 // mcts.py:318-328
-        const int b = T.alloc_block();
-        if (b < 0) {
-          S.phase = PH_DONE;
-        } else {
-          if (i == 0) *S.leaf_ptr = b;
-          S.ret = 0.0;
-          S.k = 0;
-          S.rdepth = S.depth;   // the rollout's own depth counter (mcts.py:449)
-          S.phase = PH_ROLL;
-        }
-      } else {
+      {
         uint4 q0, q1, q2;
         T.load_block(S.blk, &q0, &q1, &q2);
         const int a = T.choose<SEL>(q0, S.nvis);                      // mcts.py:330
@@ -504,6 +513,7 @@ __global__ __launch_bounds__(256, POMCP_SEARCH_WAVES_PER_SIMD) void k_search(Dev
             S.s1 = n1;
             ++S.t;
             ++S.depth;
+            arrive();
           }
         }
       }

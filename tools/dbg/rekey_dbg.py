@@ -1,0 +1,22 @@
+import sys
+sys.path.insert(0, "tests"); sys.path.insert(0, "."); sys.path.insert(0, "posggym-baselines_amd")
+from test_gpu_parity import TEST_CFG, _oracle_first_step
+from gpu_util import product_config, stats_record, rows_digest
+from posggym_baselines_amd.envs import DrivingModel
+from posggym_baselines_amd.planning import BatchedPOMCP
+seed = TEST_CFG["seed"]
+for rekey in (None, seed ^ (3 << 32)):
+    for rep in range(2):
+        bp = BatchedPOMCP(DrivingModel(), "0", product_config(TEST_CFG, 200), 6, 200)
+        bp.init_synthetic(1000)
+        pre = [rows_digest(bp.engine.root_belief(b))[1][:8] for b in range(6)]
+        if rekey is not None:
+            bp.engine.rekey(rekey)
+        acts = bp.search()
+        st = bp.engine.root_stats()
+        post = [rows_digest(bp.engine.root_belief(b))[1][:8] for b in range(6)]
+        print(rekey, rep, pre, post, [list(st[b].child_visits[:5]) for b in range(6)])
+        bp.close()
+    for b in range(6):
+        e = _oracle_first_step(TEST_CFG, 200, b, 1000 + b, rekey=rekey)
+        print("oracle", b, e["belief_digest"][:8], e["child_visits"])
