@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--trees", type=int, default=8192)
     ap.add_argument("--sims", type=int, default=65536)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--max-blocks", type=int, default=None,
+                    help="per-tree action-block arena (default min(sims + 64, 4096))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-sims", type=int, default=16384)
     ap.add_argument("--cpu-sample-trees", type=int, default=4)
@@ -103,7 +105,8 @@ def main():
     cfg = MCTSConfig(seed=args.seed, num_sims=S, **TEST_CFG)
     model = DrivingModel()
     caps = plan_capacities(cfg, model.spec.max_episode_steps, S, 1, reroot=False,
-                           max_blocks=min(S + 64, 4096), overflow_slots=1024)
+                           max_blocks=args.max_blocks or min(S + 64, 4096),
+                           overflow_slots=1024)
     stream = torch.cuda.Stream(device=dev)
     bp = BatchedPOMCP(model, "0", cfg, B, S, capacities=caps, stream=stream.cuda_stream,
                       device=dev)
@@ -178,7 +181,11 @@ def main():
                                f"sims per GPU, ucb c=sqrt2 gamma=0.95 depth_limit=2, root-parallel "
                                f"all-reduce over {world} GPU(s)",
                    "trees_per_gpu": B, "sims_per_tree": S, "depth_limit": cfg.depth_limit,
-                   "parallelism": f"root-parallel x{world}"},
+                   "parallelism": f"root-parallel x{world}",
+                   "arena": {"max_blocks": caps.max_blocks,
+                             "max_blocks_used": max(s.n_blocks for s in st),
+                             "max_particles": caps.max_particles,
+                             "max_particles_used": max(s.n_log for s in st)}},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "k_search", "kernel_ms": kernel_ms,

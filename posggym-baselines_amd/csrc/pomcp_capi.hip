@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -14,6 +15,7 @@
 // Single translation unit: the kernels are compiled together with their launchers.
 #include "pomcp_kernels.hip"
 #include "pomcp_search.hip"
+#include "pomcp_search_t.hip"
 #include "../../include/pomcp_debug.h"
 
 using namespace pb;
@@ -71,6 +73,12 @@ static int dev_alloc(pomcp_ctx* ctx, void** out, size_t bytes) {
 static unsigned grid_blocks(int B) { return (unsigned)((B + kTreesPerBlock - 1) / kTreesPerBlock); }
 static unsigned search_blocks(int B) {
   return (unsigned)((B + kGroupsPerBlock - 1) / kGroupsPerBlock);
+}
+static unsigned search_t_blocks(int B) { return (unsigned)((B + kTPB - 1) / kTPB); }
+// POMCP_SEARCH_KERNEL=g4 selects the 16-lanes-per-tree kernel (A/B measurements)
+static bool use_g4_kernel() {
+  const char* e = std::getenv("POMCP_SEARCH_KERNEL");
+  return e && std::strcmp(e, "g4") == 0;
 }
 
 extern "C" {
@@ -197,6 +205,7 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
   ALLOC(ovf, OvfSlot, B * d.H);
   ALLOC(plog, uint4, B * d.Np);
   ALLOC(belief, uint4, B * 2 * d.Nr);
+  ALLOC(path, uint4, B * 3 * kMaxPath);
   ALLOC(logtab, double, c.log_table_size);
   ALLOC(dpow, double, c.discount_pow_size);
   ALLOC(model, DrvModel, 1);
@@ -315,17 +324,32 @@ int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_key
 int pomcp_search(pomcp_ctx* ctx, int32_t num_sims, int32_t* actions_out) {
   if (!ctx || num_sims < 0) return POMCP_E_INVALID;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
-  const dim3 grid(search_blocks(ctx->dp.B)), block(256);
-  switch (ctx->dp.sel) {
-    case POMCP_SEL_PUCB:
-      hipLaunchKernelGGL(k_search<POMCP_SEL_PUCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims);
-      break;
-    case POMCP_SEL_UCB:
-      hipLaunchKernelGGL(k_search<POMCP_SEL_UCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims);
-      break;
-    default:
-      hipLaunchKernelGGL(k_search<POMCP_SEL_UNIFORM>, grid, block, 0, ctx->stream, ctx->dp,
-                         (int)num_sims);
+  if (use_g4_kernel()) {
+    const dim3 grid(search_blocks(ctx->dp.B)), block(256);
+    switch (ctx->dp.sel) {
+      case POMCP_SEL_PUCB:
+        hipLaunchKernelGGL(k_search<POMCP_SEL_PUCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims);
+        break;
+      case POMCP_SEL_UCB:
+        hipLaunchKernelGGL(k_search<POMCP_SEL_UCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims);
+        break;
+      default:
+        hipLaunchKernelGGL(k_search<POMCP_SEL_UNIFORM>, grid, block, 0, ctx->stream, ctx->dp,
+                           (int)num_sims);
+    }
+  } else {
+    const dim3 grid(search_t_blocks(ctx->dp.B)), block(kTPB);
+    switch (ctx->dp.sel) {
+      case POMCP_SEL_PUCB:
+        hipLaunchKernelGGL(k_search_t<POMCP_SEL_PUCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims);
+        break;
+      case POMCP_SEL_UCB:
+        hipLaunchKernelGGL(k_search_t<POMCP_SEL_UCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims);
+        break;
+      default:
+        hipLaunchKernelGGL(k_search_t<POMCP_SEL_UNIFORM>, grid, block, 0, ctx->stream, ctx->dp,
+                           (int)num_sims);
+    }
   }
   HIP_TRY(ctx, hipGetLastError());
   if (!actions_out) return POMCP_OK;

@@ -92,6 +92,7 @@ struct DevParams {
   OvfSlot* ovf;         // [B][H]
   uint4* plog;          // [B][Np] {obs node id, t, v0, v1}
   uint4* belief;        // [B][2][Nr] {t, v0, v1, 0}
+  uint4* path;          // [B][3 * kMaxPath] search path of the running simulation
   const double* logtab;
   int64_t logtab_n;
   const double* dpow;

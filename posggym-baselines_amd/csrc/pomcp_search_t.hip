@@ -1,0 +1,502 @@
+// k_search_t: the POMCP simulation loop with ONE tree per lane.
+//
+// Replaces posggym_baselines/planning/mcts.py:269-452 (get_action, _simulate,
+// _rollout, the three selection rules, the final action choice) and the
+// search-side parts of node.py / belief.py / utils.py:15-42.
+//
+// Why one tree per lane: the per-simulation work of a tree is a serial chain
+// (select -> step -> observe -> descend -> back up) with almost no data
+// parallelism inside one tree (A = 5 children).  Spreading one tree over 16
+// lanes (k_search, pomcp_search.hip) made every instruction of the chain do
+// the same group-uniform work 16 times; here each lane runs its own tree and
+// every VALU instruction advances 64 trees.  The kernel is then bound by the
+// dependent memory round trips of a simulation (two per tree level: the
+// node's action statistics, then the chosen action's child slots), which the
+// other 63 lanes' trees and the other waves on the SIMD hide.
+//
+// Each loop iteration runs one step of every phase (start a simulation and
+// select at the root, one tree level, one rollout step, the backup) for the
+// lanes in it, so a depth-2 simulation takes three iterations.
+//
+// Block layout (one expanded obs node, A action nodes, A x 128 B), as in
+// pomcp_device.h:
+//   part a            : stats0 of action a {visits, pad, value}
+//   part A + a        : stats1 of action a {total, agg}
+//   part 2A + 6a + k  : child slot k of action a {obs key|valid|absorbing, block, visits}
+// Path entry of level l (3 x 16 B in p.path): {stats byte offset | done << 31,
+// visits before, r}, {value before, total before}, {agg before, -} -- the
+// statistics are captured on the way down (a node appears once per path and
+// only this lane writes this tree), so the backup reads only the path.
+#pragma clang fp contract(off)
+
+namespace pb {
+
+constexpr int kMaxA = 6;
+constexpr int kTPB = 256;   // trees (lanes) per workgroup
+
+enum : int { TP_LEVEL = 0, TP_ROLL = 1, TP_BACKUP = 2, TP_START = 3, TP_DONE = 4 };
+
+template <int SEL>
+__global__ __launch_bounds__(kTPB) void k_search_t(DevParams p, int num_sims) {
+  __shared__ DrvModel sm;
+  stage_model(p.model, sm);
+  const int tree = blockIdx.x * kTPB + threadIdx.x;
+  const bool valid = tree < p.B;
+  const int tt = valid ? tree : 0;
+  const int A = p.A;
+  char* const an = reinterpret_cast<char*>(p.an + (int64_t)tt * p.Nb * A);
+  uint4* const plog = p.plog + (int64_t)tt * p.Np;
+  OvfSlot* const ovf = p.ovf + (int64_t)tt * p.H;
+  uint4* const path = p.path + (int64_t)tt * 3 * kMaxPath;
+  const TreeHdr* const h = p.hdr + tt;
+  const uint4* const rbel = p.belief + (int64_t)tt * 2 * p.Nr + (int64_t)h->belief_sel * p.Nr;
+  int root_blk = h->root_blk, root_visits = h->root_visits;
+  int n_blocks = h->n_blocks, n_log = h->n_log, n_nodes = h->n_nodes;
+  const int bsize = h->belief_size, epoch = h->epoch, root_abs = h->root_abs;
+  int err = h->error;
+  double mm_min = h->mm_min, mm_max = h->mm_max;
+  const uint64_t seed = h->seed;
+  const uint32_t tkey = h->tree_key;
+  uint32_t c_bel = h->ctr[0], c_sel = h->ctr[1], c_mod = h->ctr[2], c_a0 = h->ctr[3],
+           c_a1 = h->ctr[4];
+  const int log0 = n_log, blocks0 = n_blocks, nodes0 = n_nodes;
+  int c_rollout = 0, c_probes = 0;
+
+  // ---- RNG streams (philox.h): one stateless Philox block per draw
+  auto d_belief = [&](uint32_t n) { return uniform_int(philox_word(seed, tkey, S_BELIEF, c_bel++), n); };
+  auto d_model = [&](uint32_t n) { return uniform_int(philox_word(seed, tkey, S_MODEL, c_mod++), n); };
+  auto d_select = [&](uint32_t n) { return uniform_int(philox_word(seed, tkey, S_SELECT, c_sel++), n); };
+  auto d_act = [&](int agent, uint32_t n) {
+    return agent == 0 ? uniform_int(philox_word(seed, tkey, S_ACT_BASE, c_a0++), n)
+                      : uniform_int(philox_word(seed, tkey, S_ACT_BASE + 1, c_a1++), n);
+  };
+  // ObsNode.add_child for every action (mcts.py:279-281, 318-321): zeroed block
+  auto alloc_block = [&]() -> int {
+    if (n_blocks >= p.Nb) {
+      err = POMCP_E_ARENA;
+      return -1;
+    }
+    const int b = n_blocks++;
+    uint4* d = reinterpret_cast<uint4*>(an + (int64_t)b * A * 128);
+    for (int k = 0; k < kLanesPerAct * A; ++k) d[k] = make_uint4(0, 0, 0, 0);
+    return b;
+  };
+  auto normalize = [&](double v) {   // utils.py:34-39
+    return mm_max > mm_min ? (v - mm_min) / (mm_max - mm_min) : v;
+  };
+
+  int phase = TP_START, sims = 0, max_depth = 0;
+  int t = 0, depth = 0, plen = 0, blk = 0, nvis = 0, k = 0, rdepth = 0;
+  uint32_t s0 = 0, s1 = 0;
+  int32_t* leaf_ptr = nullptr;
+  double ret = 0.0;
+
+  if (!valid || err != 0 || root_abs) phase = TP_DONE;   // mcts.py:270-272
+  if (phase != TP_DONE && h->root_t == 0) {
+    err = POMCP_E_STATE;
+    phase = TP_DONE;
+  }
+  if (phase != TP_DONE) {
+    if (root_blk < 0) root_blk = alloc_block();   // mcts.py:279-281
+    if (root_blk < 0 || bsize <= 0) {
+      if (err == 0) err = POMCP_E_STATE;
+      phase = TP_DONE;
+    }
+  }
+  if (num_sims <= 0) phase = TP_DONE;
+
+  // Arrival at an obs node (start of _simulate, mcts.py:315-328): depth/step
+  // cutoff -> back up 0; unexpanded -> expand and roll out; else select there.
+  auto arrive = [&]() {
+    if (depth > p.depth_limit || t > p.step_limit) {   // mcts.py:315
+      ret = 0.0;
+      phase = TP_BACKUP;
+    } else if (blk < 0) {                               // mcts.py:318-328
+      const int b = alloc_block();
+      if (b < 0) {
+        phase = TP_DONE;
+      } else {
+        *leaf_ptr = b;
+        ret = 0.0;
+        k = 0;
+        rdepth = depth;   // the rollout's own depth counter (mcts.py:449)
+        phase = TP_ROLL;
+      }
+    }
+  };
+
+  while (phase != TP_DONE) {
+    // ------------------------------------------------------ start a simulation
+    if (phase == TP_START) {
+      if (sims >= num_sims) {
+        phase = TP_DONE;
+      } else {
+        const uint4 pr = rbel[d_belief((uint32_t)bsize)];   // belief.py:55
+        t = (int)pr.x;
+        s0 = pr.y;
+        s1 = pr.z;
+        blk = root_blk;
+        nvis = root_visits;
+        depth = 0;
+        plen = 0;
+        phase = TP_LEVEL;
+        arrive();
+      }
+    }
+    // ------------------------------------------------------ one tree level
+    if (phase == TP_LEVEL) {
+      char* const bp = an + (int64_t)blk * A * 128;
+      uint4 st[kMaxA];
+#pragma unroll
+      for (int a = 0; a < kMaxA; ++a)
+        st[a] = a < A ? reinterpret_cast<const uint4*>(bp)[a] : make_uint4(0, 0, 0, 0);
+      // _search_action_selection (mcts.py:492-563)
+      int a = 0;
+      if (SEL == POMCP_SEL_PUCB && nvis == 0) {   // random.choices over the uniform prior
+        const double w = 1.0 / (double)A;
+        double total = w;
+        for (int q = 1; q < A; ++q) total = total + w;
+        const double x = uniform_float(philox_word(seed, tkey, S_SELECT, c_sel++)) * (total + 0.0);
+        double acc = w;
+        a = A - 1;
+        for (int q = 0; q < A - 1; ++q) {
+          if (x < acc) {
+            a = q;
+            break;
+          }
+          acc = acc + w;
+        }
+      } else if (nvis == 0) {
+        a = (int)d_select((uint32_t)A);
+      } else if (SEL == POMCP_SEL_UNIFORM) {   // min_visit_action_selection
+        int min_n = nvis + 1;
+#pragma unroll
+        for (int q = 0; q < kMaxA; ++q) {
+          if (q < A && (int)st[q].x < min_n) {
+            min_n = (int)st[q].x;
+            a = q;
+          }
+        }
+      } else if (SEL == POMCP_SEL_UCB) {
+        int unv = -1;   // mcts.py:539-540: first unvisited child
+#pragma unroll
+        for (int q = kMaxA - 1; q >= 0; --q)
+          if (q < A && st[q].x == 0u) unv = q;
+        if (unv >= 0) {
+          a = unv;
+        } else {
+          const double log_n = p.logtab[nvis < p.logtab_n ? nvis : 0];
+          if (nvis >= p.logtab_n) err = POMCP_E_ARENA;
+          double best = -__builtin_inf();
+#pragma unroll
+          for (int q = 0; q < kMaxA; ++q) {
+            if (q < A) {   // mcts.py:541-542, strict '>' in action order
+              const double s = normalize(hilo_d(st[q].z, st[q].w)) +
+                               p.c * sqrt(log_n / (double)(int)st[q].x);
+              if (s > best) {
+                best = s;
+                a = q;
+              }
+            }
+          }
+        }
+      } else {   // PUCB, mcts.py:502-527
+        const double noise = 1.0 / (double)A;
+        const double prior = (1.0 / (double)A) * (1.0 - p.pucb_f) + p.pucb_f * noise;
+        const double sqrt_n = sqrt((double)nvis);
+        double best = -__builtin_inf();
+#pragma unroll
+        for (int q = 0; q < kMaxA; ++q) {
+          if (q < A) {
+            const int n = (int)st[q].x;
+            const double s = (n > 0 ? normalize(hilo_d(st[q].z, st[q].w)) : 0.0) +
+                             p.c * prior * (sqrt_n / (double)(1 + n));
+            if (s > best) {
+              best = s;
+              a = q;
+            }
+          }
+        }
+      }
+      uint4 sa = st[0];
+#pragma unroll
+      for (int q = 1; q < kMaxA; ++q)
+        if (q == a) sa = st[q];
+      // the chosen action's stats1 and child slots (second round trip)
+      const uint4* const ap = reinterpret_cast<const uint4*>(bp);
+      const uint4 s1a = ap[A + a];
+      uint4 sl[kSlots];
+#pragma unroll
+      for (int q = 0; q < kSlots; ++q) sl[q] = ap[2 * A + kSlots * a + q];
+      const uint32_t ao = d_act(p.other, (uint32_t)A);   // mcts.py:331
+      const uint32_t j = d_model(2);                     // exec-order shuffle
+      uint32_t n0, n1;
+      drv_step2_vec(sm, s0, s1, p.ego == 0 ? (uint32_t)a : ao, p.ego == 0 ? ao : (uint32_t)a, j,
+                    &n0, &n1);
+      const uint32_t e0 = p.ego == 0 ? s0 : s1;
+      const uint32_t e1 = p.ego == 0 ? n0 : n1;
+      const uint32_t o1 = p.ego == 0 ? n1 : n0;
+      const double r = drv_reward_vec(sm, e0, e1);
+      const int done = (((e1 >> 15) & 3u) != 0u ||
+                        (((n0 >> 15) & 3u) != 0u && ((n1 >> 15) & 3u) != 0u)) ? 1 : 0;
+      const uint64_t okey = obs_key_vec(sm, e1, o1);
+      // ActionNode.children[obs] among the inline slots (mcts.py:356-370):
+      // filled in order, so the first invalid slot is the insertion point
+      int ks = -1;
+      bool match = false;
+#pragma unroll
+      for (int q = kSlots - 1; q >= 0; --q) {
+        const uint64_t sk = (uint64_t)sl[q].x | ((uint64_t)sl[q].y << 32);
+        const bool vb = (sk & kValidBit) != 0;
+        if (!vb || (sk & kObsMask) == okey) {
+          ks = q;
+          match = vb;
+        }
+      }
+      const uint32_t ani = (uint32_t)(blk * A + a);
+      uint32_t cid = 0;
+      int cblk = -1, cvis = 1;
+      int32_t* cptr = nullptr;
+      if (ks >= 0) {
+        uint4 sk = sl[0];
+#pragma unroll
+        for (int q = 1; q < kSlots; ++q)
+          if (q == ks) sk = sl[q];
+        if (match) {
+          cblk = (int)sk.z;
+          cvis = (int)sk.w + 1;
+        } else {
+          ++n_nodes;
+        }
+        const uint64_t nk = okey | kValidBit | ((uint64_t)done << 63);
+        uint4* slot = const_cast<uint4*>(ap) + 2 * A + kSlots * a + ks;
+        *slot = make_uint4((uint32_t)nk, (uint32_t)(nk >> 32), (uint32_t)cblk, (uint32_t)cvis);
+        cid = ani * kSlots + (uint32_t)ks + 1u;
+        cptr = reinterpret_cast<int32_t*>(slot) + 2;
+      } else {
+        // overflow map: open addressing over 16-entry buckets
+        const uint64_t key = okey | ((uint64_t)epoch << kEpochShift);
+        uint32_t b = ovf_hash(ani, okey) & p.bucket_mask;
+        bool found = false;
+        for (uint32_t probe = 0; probe <= p.bucket_mask && !found; ++probe) {
+          ++c_probes;
+          for (int e = 0; e < kBucket; ++e) {
+            OvfSlot* ep = ovf + (int64_t)b * kBucket + e;
+            const uint4 w0 = reinterpret_cast<const uint4*>(ep)[0];
+            const uint64_t skey = (uint64_t)w0.x | ((uint64_t)w0.y << 32);
+            const bool live = (uint32_t)(skey >> kEpochShift) == (uint32_t)epoch;
+            if (!live || (skey == key && w0.z == ani)) {
+              if (live) {
+                const uint4 w1 = reinterpret_cast<const uint4*>(ep)[1];
+                cblk = (int)w1.x;
+                cvis = (int)w1.y + 1;
+              } else {
+                ++n_nodes;
+              }
+              reinterpret_cast<uint4*>(ep)[0] =
+                  make_uint4((uint32_t)key, (uint32_t)(key >> 32), ani, (uint32_t)done);
+              reinterpret_cast<uint4*>(ep)[1] = make_uint4((uint32_t)cblk, (uint32_t)cvis, 0u, 0u);
+              cid = p.ovf_base + b * kBucket + (uint32_t)e;
+              cptr = &ep->block;
+              found = true;
+              break;
+            }
+          }
+          b = (b + 1) & p.bucket_mask;
+        }
+        if (!found) err = POMCP_E_ARENA;
+      }
+      if (err != 0 || n_log >= p.Np || plen >= kMaxPath) {
+        if (err == 0) err = POMCP_E_ARENA;
+        phase = TP_DONE;
+      } else {
+        plog[n_log++] = make_uint4(cid, (uint32_t)(t + 1), n0, n1);   // mcts.py:371
+        const uint32_t off = (uint32_t)(blk * A * 128 + a * 16);
+        uint4* pe = path + 3 * plen;
+        pe[0] = make_uint4(off | ((uint32_t)done << 31), sa.x, (uint32_t)__double2loint(r),
+                           (uint32_t)__double2hiint(r));
+        pe[1] = make_uint4(sa.z, sa.w, s1a.x, s1a.y);
+        pe[2] = make_uint4(s1a.z, s1a.w, 0u, 0u);
+        ++plen;
+        if (done) {
+          ret = 0.0;
+          phase = TP_BACKUP;
+        } else {
+          blk = cblk;
+          nvis = cvis;
+          leaf_ptr = cptr;
+          s0 = n0;
+          s1 = n1;
+          ++t;
+          ++depth;
+          arrive();
+        }
+      }
+    }
+    // ------------------------------------------------------ one rollout step
+    if (phase == TP_ROLL) {                                  // mcts.py:414-450
+      if (!(rdepth <= p.depth_limit && t <= p.step_limit)) {
+        phase = TP_BACKUP;
+      } else {
+        const uint32_t ae = d_act(p.ego, (uint32_t)A);       // search_policy.py:177
+        const uint32_t ao = d_act(p.other, (uint32_t)A);     // other_policy.py:151
+        const uint32_t j = d_model(2);
+        uint32_t n0, n1;
+        drv_step2_vec(sm, s0, s1, p.ego == 0 ? ae : ao, p.ego == 0 ? ao : ae, j, &n0, &n1);
+        const uint32_t e0 = p.ego == 0 ? s0 : s1, e1 = p.ego == 0 ? n0 : n1;
+        const double r = drv_reward_vec(sm, e0, e1);
+        if (k >= p.dpow_n) {
+          err = POMCP_E_ARENA;
+          phase = TP_DONE;
+        } else {
+          ret += p.dpow[k] * r;   // mcts.py:420-422
+          ++c_rollout;
+          const bool dn = ((e1 >> 15) & 3u) != 0u ||
+                          (((n0 >> 15) & 3u) != 0u && ((n1 >> 15) & 3u) != 0u);
+          if (dn) {
+            phase = TP_BACKUP;
+          } else {
+            s0 = n0;
+            s1 = n1;
+            ++t;
+            ++rdepth;
+            ++k;
+          }
+        }
+      }
+    }
+    // ------------------------------------------------------ backup
+    if (phase == TP_BACKUP) {                                // mcts.py:374-381
+      double gr = ret;
+      for (int l = plen - 1; l >= 0; --l) {
+        const uint4 e0 = path[3 * l], e1 = path[3 * l + 1], e2 = path[3 * l + 2];
+        const double r = hilo_d(e0.z, e0.w);
+        gr = (e0.x >> 31) ? r : r + p.discount * gr;
+        const int n = (int)e0.y + 1;
+        const double value0 = hilo_d(e1.x, e1.y);
+        const double total = hilo_d(e1.z, e1.w) + gr;
+        const double delta = gr - value0;
+        const double value = value0 + delta / (double)n;
+        const double agg = hilo_d(e2.x, e2.y) + delta * (gr - value);
+        uint4* sp = reinterpret_cast<uint4*>(an + (e0.x & 0x7FFFFFFFu));
+        sp[0] = make_uint4((uint32_t)n, 0u, (uint32_t)__double2loint(value),
+                           (uint32_t)__double2hiint(value));
+        sp[A] = make_uint4((uint32_t)__double2loint(total), (uint32_t)__double2hiint(total),
+                           (uint32_t)__double2loint(agg), (uint32_t)__double2hiint(agg));
+        if (value > mm_max) mm_max = value;   // utils.py:29-32
+        if (value < mm_min) mm_min = value;
+      }
+      ++root_visits;                                          // mcts.py:288
+      max_depth = depth > max_depth ? depth : max_depth;
+      ++sims;
+      phase = TP_START;
+    }
+  }
+
+  // ------------------------------------------------------------------ results
+  if (!valid) return;
+  const bool have = err == 0 && !root_abs && root_blk >= 0;
+  uint4 st[kMaxA], s1s[kMaxA];
+#pragma unroll
+  for (int a = 0; a < kMaxA; ++a) {
+    st[a] = make_uint4(0, 0, 0, 0);
+    s1s[a] = st[a];
+    if (have && a < A) {
+      st[a] = reinterpret_cast<const uint4*>(an + (int64_t)root_blk * A * 128)[a];
+      s1s[a] = reinterpret_cast<const uint4*>(an + (int64_t)root_blk * A * 128)[A + a];
+    }
+  }
+  int action = 0;
+  if (have) {   // _final_action_selection (mcts.py:565-600)
+    uint32_t ties = 0;
+    int nt = 0;
+    bool direct = false;
+    if (SEL == POMCP_SEL_PUCB) {
+      if (root_visits == 0) {
+        action = (int)d_select((uint32_t)A);
+        direct = true;
+      } else {
+        int mx = 0;
+#pragma unroll
+        for (int a = 0; a < kMaxA; ++a) {
+          if (a >= A) continue;
+          const int na = (int)st[a].x;
+          if (na == mx) {
+            ties |= 1u << a;
+            ++nt;
+          } else if (na > mx) {
+            mx = na;
+            ties = 1u << a;
+            nt = 1;
+          }
+        }
+      }
+    } else {
+      double mx = -__builtin_inf();
+#pragma unroll
+      for (int a = 0; a < kMaxA; ++a) {
+        if (a >= A) continue;
+        const double va = hilo_d(st[a].z, st[a].w);
+        if (va == mx) {
+          ties |= 1u << a;
+          ++nt;
+        } else if (va > mx) {
+          mx = va;
+          ties = 1u << a;
+          nt = 1;
+        }
+      }
+    }
+    if (!direct) action = kth_bit(ties, d_select((uint32_t)nt));
+  }
+  TreeHdr* const hw = p.hdr + tree;
+  hw->n_blocks = n_blocks;
+  hw->n_log = n_log;
+  hw->n_nodes = n_nodes;
+  hw->error = err;
+  hw->root_blk = root_blk;
+  hw->root_visits = root_visits;
+  hw->mm_min = mm_min;
+  hw->mm_max = mm_max;
+  hw->ctr[0] = c_bel;
+  hw->ctr[1] = c_sel;
+  hw->ctr[2] = c_mod;
+  hw->ctr[3] = c_a0;
+  hw->ctr[4] = c_a1;
+  pomcp_root_stats* const so = p.stats + tree;
+#pragma unroll
+  for (int a = 0; a < kMaxA; ++a) {
+    if (a >= A) continue;
+    const double va = hilo_d(st[a].z, st[a].w), tot = hilo_d(s1s[a].x, s1s[a].y);
+    so->child_visits[a] = (int)st[a].x;
+    so->child_values[a] = va;
+    so->child_totals[a] = tot;
+    p.merge[((int64_t)tree * A + a) * 2] = (double)st[a].x;
+    p.merge[((int64_t)tree * A + a) * 2 + 1] = tot;
+  }
+  so->action = action;
+  so->num_sims = sims;
+  so->search_depth = max_depth;
+  so->root_visits = root_visits;
+  so->root_absorbing = root_abs;
+  so->belief_size = bsize;
+  so->error = err;
+  so->num_children = have ? A : 0;
+  so->min_value = mm_min;
+  so->max_value = mm_max;
+  so->n_levels = n_log - log0;
+  so->n_expansions = n_blocks - blocks0;
+  so->n_new_nodes = n_nodes - nodes0;
+  so->n_rollout_steps = c_rollout;
+  so->n_probes = c_probes;
+  so->n_obs_nodes = n_nodes;
+  so->n_blocks = n_blocks;
+  so->n_log = n_log;
+  so->pad = 0;
+}
+
+template __global__ void k_search_t<POMCP_SEL_PUCB>(DevParams, int);
+template __global__ void k_search_t<POMCP_SEL_UCB>(DevParams, int);
+template __global__ void k_search_t<POMCP_SEL_UNIFORM>(DevParams, int);
+
+}  // namespace pb
