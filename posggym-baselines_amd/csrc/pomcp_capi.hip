@@ -15,13 +15,12 @@
 // Single translation unit: the kernels are compiled together with their launchers.
 #include "pomcp_kernels.hip"
 #include "pomcp_search.hip"
-#include "pomcp_search_t.hip"
 #include "../../include/pomcp_debug.h"
 
 using namespace pb;
 
 static_assert(sizeof(pomcp_grid) == sizeof(DrvGrid), "grid layout");
-static_assert(sizeof(ActNode) == 128, "action node layout");
+static_assert(sizeof(Line) == 128, "block line layout");
 static_assert(sizeof(OvfSlot) == 32, "overflow slot layout");
 
 struct pomcp_ctx {
@@ -71,15 +70,7 @@ static int dev_alloc(pomcp_ctx* ctx, void** out, size_t bytes) {
 }
 
 static unsigned grid_blocks(int B) { return (unsigned)((B + kTreesPerBlock - 1) / kTreesPerBlock); }
-static unsigned search_blocks(int B) {
-  return (unsigned)((B + kGroupsPerBlock - 1) / kGroupsPerBlock);
-}
-static unsigned search_t_blocks(int B) { return (unsigned)((B + kTPB - 1) / kTPB); }
-// POMCP_SEARCH_KERNEL=g4 selects the 16-lanes-per-tree kernel (A/B measurements)
-static bool use_g4_kernel() {
-  const char* e = std::getenv("POMCP_SEARCH_KERNEL");
-  return e && std::strcmp(e, "g4") == 0;
-}
+static unsigned search_blocks(int B) { return (unsigned)((B + kTPB - 1) / kTPB); }
 
 extern "C" {
 
@@ -116,7 +107,7 @@ static int validate(const pomcp_config* c, std::string* why) {
   if (c->depth_limit < 0 || c->step_limit < 0) return bad("depth/step limit");
   if (c->num_particles < 1 || c->extra_particles < 0) return bad("num_particles");
   if (c->num_trees < 1) return bad("num_trees >= 1");
-  if (c->max_blocks < 1 || c->max_blocks * c->num_actions * 128 > INT32_MAX) return bad("max_blocks");
+  if (c->max_blocks < 1 || c->max_blocks * (c->num_actions + 1) * 128 > INT32_MAX) return bad("max_blocks");
   if (c->num_actions > 6) { *why = "the search kernel supports at most 6 actions"; return POMCP_E_UNSUPPORTED; }
   if (c->max_particles < 1 || c->max_particles > INT32_MAX) return bad("max_particles");
   if (c->max_belief < 2 * (c->num_particles + c->extra_particles)) return bad("max_belief too small");
@@ -201,7 +192,7 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
     d.field = reinterpret_cast<decltype(d.field)>(p);                           \
   } while (0)
   ALLOC(hdr, TreeHdr, B);
-  ALLOC(an, ActNode, B * d.Nb * d.A);
+  ALLOC(an, Line, B * d.Nb * blk_lines(d.A));
   ALLOC(ovf, OvfSlot, B * d.H);
   ALLOC(plog, uint4, B * d.Np);
   ALLOC(belief, uint4, B * 2 * d.Nr);
@@ -324,32 +315,17 @@ int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_key
 int pomcp_search(pomcp_ctx* ctx, int32_t num_sims, int32_t* actions_out) {
   if (!ctx || num_sims < 0) return POMCP_E_INVALID;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
-  if (use_g4_kernel()) {
-    const dim3 grid(search_blocks(ctx->dp.B)), block(256);
-    switch (ctx->dp.sel) {
-      case POMCP_SEL_PUCB:
-        hipLaunchKernelGGL(k_search<POMCP_SEL_PUCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims);
-        break;
-      case POMCP_SEL_UCB:
-        hipLaunchKernelGGL(k_search<POMCP_SEL_UCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims);
-        break;
-      default:
-        hipLaunchKernelGGL(k_search<POMCP_SEL_UNIFORM>, grid, block, 0, ctx->stream, ctx->dp,
-                           (int)num_sims);
-    }
-  } else {
-    const dim3 grid(search_t_blocks(ctx->dp.B)), block(kTPB);
-    switch (ctx->dp.sel) {
-      case POMCP_SEL_PUCB:
-        hipLaunchKernelGGL(k_search_t<POMCP_SEL_PUCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims);
-        break;
-      case POMCP_SEL_UCB:
-        hipLaunchKernelGGL(k_search_t<POMCP_SEL_UCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims);
-        break;
-      default:
-        hipLaunchKernelGGL(k_search_t<POMCP_SEL_UNIFORM>, grid, block, 0, ctx->stream, ctx->dp,
-                           (int)num_sims);
-    }
+  const dim3 grid(search_blocks(ctx->dp.B)), block(kTPB);
+  switch (ctx->dp.sel) {
+    case POMCP_SEL_PUCB:
+      hipLaunchKernelGGL(k_search<POMCP_SEL_PUCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims);
+      break;
+    case POMCP_SEL_UCB:
+      hipLaunchKernelGGL(k_search<POMCP_SEL_UCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims);
+      break;
+    default:
+      hipLaunchKernelGGL(k_search<POMCP_SEL_UNIFORM>, grid, block, 0, ctx->stream, ctx->dp,
+                         (int)num_sims);
   }
   HIP_TRY(ctx, hipGetLastError());
   if (!actions_out) return POMCP_OK;

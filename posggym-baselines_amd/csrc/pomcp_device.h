@@ -1,16 +1,14 @@
 // Device-side data layout and wave-level helpers of the POMCP engine.
 //
-// One 64-lane wavefront owns one search tree (one planner).  Serial parts of
-// the reference's per-simulation loop run wave-uniform (scalar registers where
-// the compiler can keep them), the data-parallel parts are spread over lanes:
-//   * one tree level = one coalesced 640 B load of an action block
-//     (5 action nodes x 128 B, lane l holds bytes [16 l, 16 l + 16))
-//   * UCB / PUCB scores of the A children     -> lanes 8a (stats part 0)
-//   * obs-child lookup among 6 inline slots    -> lanes 8a+2 .. 8a+7, 1 ballot
-//   * the ego observation window (15 cells)   -> lanes 0..14, 2 ballots
-//   * belief extraction at re-root            -> 64 log records / step
-//   * RNG: each lane computes one Philox block, a draw is a readlane
-// A tree is touched by exactly one wave, so no atomics are needed.
+// The search (k_search, pomcp_search.hip) runs one tree per lane.  The
+// re-root / reset kernels (pomcp_kernels.hip) run one tree per wavefront and
+// spread the data-parallel parts over lanes:
+//   * a block load = one coalesced (A + 1) x 128 B load, lane l holds part l
+//   * obs-child lookup among the 6 inline slots -> 6 lanes, 1 ballot
+//   * the ego observation window (15 cells)    -> lanes 0..14, 2 ballots
+//   * belief extraction at re-root             -> 64 log records / step
+//   * RNG: an LDS page of Philox blocks, one per lane, a draw is a broadcast read
+// A tree is touched by exactly one wave (or lane), so no atomics are needed.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -21,14 +19,10 @@
 
 namespace pb {
 
-#ifndef POMCP_SEARCH_WAVES_PER_SIMD
-#define POMCP_SEARCH_WAVES_PER_SIMD 1
-#endif
-
 constexpr int kWave = 64;
 constexpr int kTreesPerBlock = 4;      // 256-thread workgroups, one tree per wave
 constexpr int kSlots = 6;              // inline obs children per action node
-constexpr int kLanesPerAct = 8;        // 128 B action node = 8 x 16 B
+constexpr int kLine = 8;               // 16 B parts per 128 B line
 constexpr int kBucket = 16;            // overflow map bucket (16 x 32 B)
 constexpr int kEpochShift = 50;        // obs keys use bits 0..49
 constexpr uint32_t kEpochMask = 0x3FFF;
@@ -39,23 +33,24 @@ constexpr int kMaxPath = 64;           // tree levels per simulation (one lane e
 constexpr uint32_t kRootId = 0;        // obs node id of a root created by the initial update
 
 // Action nodes (node.py:120-178) with their obs children inline (node.py:144-160).
-// An expanded obs node owns a block of A x 128 B, laid out in 16 B parts:
-//   part a: {visits, pad, value} of action a; part A + a: {total, agg};
-//   part 2A + 6a + k: child slot k of action a.
-// `ActNode` is the 128 B allocation unit (its fields describe the sizes only).
+// An expanded obs node owns a block of (A + 1) x 128 B lines, in 16 B parts:
+//   line 0     : part a = stats0 of action a {visits, pad, value}     (A <= 6)
+//   line 1 + a : part 0 = stats1 of action a {total, agg},
+//                parts 1..6 = child slots k of action a (ChildSlot)
+// so one tree level of a simulation touches two lines: the node's action
+// statistics (selection) and the chosen action's line (obs child lookup).
 struct ChildSlot {
   uint64_t key;     // obs key | valid << 62 | is_absorbing << 63
   int32_t block;    // action block of the child obs node (-1 = leaf)
   int32_t visits;   // ObsNode.visits
 };
-struct ActNode {
-  int32_t visits;
-  int32_t pad;
-  double value;
-  double total;
-  double agg;
-  ChildSlot child[kSlots];
+struct alignas(16) Line {   // allocation unit of the block arena
+  uint4 part[kLine];
 };
+__host__ __device__ constexpr int blk_lines(int A) { return A + 1; }
+__host__ __device__ constexpr int blk_parts(int A) { return kLine * (A + 1); }
+__host__ __device__ constexpr int part_stats1(int a) { return kLine * (1 + a); }
+__host__ __device__ constexpr int part_slot(int a, int k) { return kLine * (1 + a) + 1 + k; }
 
 // Overflow children (> kSlots per action node): open-addressing map keyed by
 // (action node, obs).  32 B entries; valid when key's epoch matches.
@@ -88,7 +83,7 @@ struct DevParams {
   uint32_t bucket_mask;
   uint32_t ovf_base;    // node ids >= ovf_base are overflow entries
   TreeHdr* hdr;
-  ActNode* an;          // [B][Nb][A]
+  Line* an;             // [B][Nb][A + 1] action blocks
   OvfSlot* ovf;         // [B][H]
   uint4* plog;          // [B][Np] {obs node id, t, v0, v1}
   uint4* belief;        // [B][2][Nr] {t, v0, v1, 0}

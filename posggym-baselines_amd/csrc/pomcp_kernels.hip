@@ -52,7 +52,7 @@ struct Tree {
   const DrvModel& m;
   const DrvGrid& g;
   int tree, lane;
-  ActNode* an;
+  Line* an;
   OvfSlot* ovf;
   uint4* plog;
   uint4* bel;
@@ -68,7 +68,7 @@ struct Tree {
 
   __device__ Tree(const DevParams& pp, const DrvModel& mm, int t) : p(pp), m(mm), g(mm.g), tree(t) {
     lane = lane_id();
-    an = p.an + (int64_t)t * p.Nb * p.A;
+    an = p.an + (int64_t)t * p.Nb * blk_lines(p.A);
     ovf = p.ovf + (int64_t)t * p.H;
     plog = p.plog + (int64_t)t * p.Np;
     bel = p.belief + (int64_t)t * 2 * p.Nr;
@@ -160,7 +160,7 @@ struct Tree {
 
   __device__ uint4 load_block(int blk) const {
     uint4 q = make_uint4(0, 0, 0, 0);
-    if (lane < kLanesPerAct * p.A) q = reinterpret_cast<const uint4*>(an + (int64_t)blk * p.A)[lane];
+    if (lane < blk_parts(p.A)) q = reinterpret_cast<const uint4*>(an + (int64_t)blk * blk_lines(p.A))[lane];
     return q;
   }
 
@@ -171,8 +171,8 @@ struct Tree {
       return -1;
     }
     const int b = n_blocks++;
-    if (lane < kLanesPerAct * p.A)
-      reinterpret_cast<uint4*>(an + (int64_t)b * p.A)[lane] = make_uint4(0, 0, 0, 0);
+    if (lane < blk_parts(p.A))
+      reinterpret_cast<uint4*>(an + (int64_t)b * blk_lines(p.A))[lane] = make_uint4(0, 0, 0, 0);
     ++c_expand;
     return b;
   }
@@ -258,12 +258,12 @@ struct Tree {
   __device__ bool child_ref(uint4& q, int blk, int a, uint64_t okey, bool visit, int done,
                             ChildRef* c) {
     const uint32_t ani = (uint32_t)(blk * p.A + a);
-    const int lo = 2 * p.A + kSlots * a;   // block layout: see pomcp_search.hip
+    const int lo = part_slot(a, 0);   // block layout: pomcp_device.h
     const bool cl = lane >= lo && lane < lo + kSlots;
     const uint64_t skey = (uint64_t)q.x | ((uint64_t)q.y << 32);
     const bool valid = cl && (skey & kValidBit) != 0;
     const uint64_t m = __ballot(valid && (skey & kObsMask) == okey);
-    uint4* slots = reinterpret_cast<uint4*>(an + (int64_t)blk * p.A) + lo;
+    uint4* slots = reinterpret_cast<uint4*>(an + (int64_t)blk * blk_lines(p.A)) + lo;
     int L;
     bool is_new = false;
     if (m) {

@@ -1,286 +1,461 @@
-// k_search: the POMCP simulation loop with FOUR trees per wavefront.
+// k_search: the POMCP simulation loop with ONE tree per lane.
 //
 // Replaces posggym_baselines/planning/mcts.py:269-452 (get_action, _simulate,
 // _rollout, the three selection rules, the final action choice) and the
 // search-side parts of node.py / belief.py / utils.py:15-42.
 //
-// Why 4 trees per wave: a simulation is a long chain of dependent scalar-ish
-// operations (select -> step -> observe -> descend -> back up); with one tree
-// per wave every instruction of the chain served one tree and the kernel was
-// bound by per-wave issue latency.  Here each 16-lane group owns one tree and
-// holds that tree's scalars as group-uniform VGPRs, so every instruction of
-// the chain advances four independent trees.  Trees that are in different
-// phases of a simulation (descending, rolling out, backing up, starting the
-// next one) run under exec masks: one loop iteration executes each phase
-// block once for the groups that are in it.
+// Why one tree per lane: the per-simulation work of a tree is a serial chain
+// (select -> step -> observe -> descend -> back up) with almost no data
+// parallelism inside one tree (A = 5 children).  Spreading one tree over 16
+// lanes (the previous design) made every instruction of the chain do
+// the same group-uniform work 16 times; here each lane runs its own tree and
+// every VALU instruction advances 64 trees.  The kernel is then bound by the
+// dependent memory round trips of a simulation (two per tree level: the
+// node's action statistics, then the chosen action's child slots), which the
+// other 63 lanes' trees and the other waves on the SIMD hide.
 //
-// Block layout (one expanded obs node, A action nodes, A x 128 B):
-//   part a            : stats0 of action a {visits, pad, value}
-//   part A + a        : stats1 of action a {total, agg}
-//   part 2A + 6a + k  : child slot k of action a {obs key|valid|absorbing, block, visits}
-// Lane i of a group holds parts i, 16 + i, 32 + i of the block being visited.
+// Each loop iteration runs one step of every phase (start a simulation and
+// select at the root, one tree level, one rollout step, the backup) for the
+// lanes in it, so a depth-2 simulation takes three iterations.
+//
+// Block layout: pomcp_device.h ((A + 1) x 128 B lines; a tree level reads the
+// node's statistics line and the chosen action's line).
+// The path of the running simulation (PathEntry: the level's statistics are
+// captured on the way down -- a node appears once per path and only this lane
+// writes this tree -- so the backup reads no tree memory) is held in registers
+// for the first kRegPath levels and in p.path below them.
 #pragma clang fp contract(off)
 
 namespace pb {
 
-constexpr int kG = 4;             // trees per wavefront
-constexpr int kL = 16;            // lanes per tree
-constexpr int kGroupsPerBlock = kG * (256 / kWave);   // 16 trees per 256-thread workgroup
-constexpr uint32_t kGPage = 32;   // RNG page per stream: 8 Philox blocks
-constexpr int kPathMax = 64;
+constexpr int kMaxA = 6;
+constexpr int kTPB = 256;   // trees (lanes) per workgroup
 
-enum : int { PH_LEVEL = 0, PH_ROLL = 1, PH_BACKUP = 2, PH_START = 3, PH_DONE = 4 };
+constexpr int kRegPath = 4;  // path levels held in registers (deeper ones in p.path)
 
-__device__ __forceinline__ int glane() { return lane_id() & (kL - 1); }
-__device__ __forceinline__ int gbase() { return lane_id() & ~(kL - 1); }
+// One level of the running simulation's path: {stats0 byte offset | done << 31,
+// visits before, r}, {value before, total before}, {agg before, stats1 byte
+// offset, -}.
+struct PathEntry {
+  uint4 e0, e1, e2;
+};
 
-// value of `v` on lane `src` (0..15) of this lane's group
-__device__ __forceinline__ uint32_t gshfl(uint32_t v, int src) {
-  return (uint32_t)__builtin_amdgcn_ds_bpermute((gbase() + src) << 2, (int)v);
-}
-__device__ __forceinline__ double gshfl_d(double v, int src) {
-  const int a = (gbase() + src) << 2;
-  const int lo = __builtin_amdgcn_ds_bpermute(a, __double2loint(v));
-  const int hi = __builtin_amdgcn_ds_bpermute(a, __double2hiint(v));
-  return __hiloint2double(hi, lo);
-}
-// this group's 16 bits of a wave ballot
-__device__ __forceinline__ uint32_t gballot(bool pred) {
-  const uint64_t m = __ballot(pred);
-  return (uint32_t)(m >> gbase()) & 0xFFFFu;
-}
-__device__ __forceinline__ int ffs16(uint32_t m) { return m ? __ffs((int)m) - 1 : -1; }
+enum : int { TP_LEVEL = 0, TP_ROLL = 1, TP_BACKUP = 2, TP_START = 3, TP_DONE = 4 };
 
-__device__ __forceinline__ uint4 sel_part(const uint4& q0, const uint4& q1, const uint4& q2, int r) {
-  return r == 0 ? q0 : (r == 1 ? q1 : q2);
-}
-// part p (group-uniform) of the block held in q0..q2
-__device__ __forceinline__ uint4 get_part(const uint4& q0, const uint4& q1, const uint4& q2, int p) {
-  const uint4 v = sel_part(q0, q1, q2, p >> 4);
-  const int s = p & 15;
-  return make_uint4(gshfl(v.x, s), gshfl(v.y, s), gshfl(v.z, s), gshfl(v.w, s));
-}
+template <int SEL>
+__global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
+  __shared__ DrvModel sm;
+  stage_model(p.model, sm);
+  const int tree = blockIdx.x * kTPB + threadIdx.x;
+  const bool valid = tree < p.B;
+  const int tt = valid ? tree : 0;
+  const int A = p.A;
+  char* const an = reinterpret_cast<char*>(p.an + (int64_t)tt * p.Nb * blk_lines(A));
+  const int blk_bytes = blk_lines(A) * 128;
+  uint4* const plog = p.plog + (int64_t)tt * p.Np;
+  OvfSlot* const ovf = p.ovf + (int64_t)tt * p.H;
+  PathEntry* const path = reinterpret_cast<PathEntry*>(p.path) + (int64_t)tt * kMaxPath;
+  const TreeHdr* const h = p.hdr + tt;
+  const uint4* const rbel = p.belief + (int64_t)tt * 2 * p.Nr + (int64_t)h->belief_sel * p.Nr;
+  int root_blk = h->root_blk, root_visits = h->root_visits;
+  int n_blocks = h->n_blocks, n_log = h->n_log, n_nodes = h->n_nodes;
+  const int bsize = h->belief_size, epoch = h->epoch, root_abs = h->root_abs;
+  int err = h->error;
+  double mm_min = h->mm_min, mm_max = h->mm_max;
+  const uint64_t seed = h->seed;
+  const uint32_t tkey = h->tree_key;
+  uint32_t c_bel = h->ctr[0], c_sel = h->ctr[1], c_mod = h->ctr[2], c_a0 = h->ctr[3],
+           c_a1 = h->ctr[4];
+  const int log0 = n_log, blocks0 = n_blocks, nodes0 = n_nodes;
+  int c_rollout = 0, c_probes = 0;
 
-struct GTree {
-  const DevParams& p;
-  const DrvModel& m;
-  int tree;
-  bool valid;
-  ActNode* an;
-  uint4* plog;
-  uint4* rbel;
-  OvfSlot* ovf;
-  uint32_t* rng;     // LDS: 4 pages of kGPage words (belief, model, act0, act1)
-  uint32_t* path;    // LDS: kPathMax x {stats byte offset | done << 31, r lo, r hi}
-  int root_blk, root_visits, n_blocks, n_log, n_nodes, bsize, err;
-  double mm_min, mm_max;
-  uint64_t seed;
-  uint32_t tkey;
-  uint32_t c_bel, c_sel, c_mod, c_a0, c_a1;
-  int32_t c_rollout, c_probes;
-
-  __device__ GTree(const DevParams& pp, const DrvModel& mm, int t, uint32_t* rng_lds,
-                   uint32_t* path_lds)
-      : p(pp), m(mm), tree(t), rng(rng_lds), path(path_lds) {
-    valid = t < p.B;
-    const int tt = valid ? t : 0;
-    an = p.an + (int64_t)tt * p.Nb * p.A;
-    plog = p.plog + (int64_t)tt * p.Np;
-    ovf = p.ovf + (int64_t)tt * p.H;
-    const TreeHdr* h = p.hdr + tt;
-    rbel = p.belief + (int64_t)tt * 2 * p.Nr + (int64_t)h->belief_sel * p.Nr;
-    root_blk = h->root_blk;
-    root_visits = h->root_visits;
-    n_blocks = h->n_blocks;
-    n_log = h->n_log;
-    n_nodes = h->n_nodes;
-    bsize = h->belief_size;
-    err = h->error;
-    mm_min = h->mm_min;
-    mm_max = h->mm_max;
-    seed = h->seed;
-    tkey = h->tree_key;
-    c_bel = h->ctr[0];
-    c_sel = h->ctr[1];
-    c_mod = h->ctr[2];
-    c_a0 = h->ctr[3];
-    c_a1 = h->ctr[4];
-    c_rollout = c_probes = 0;
-  }
-
-  // fields the search changes (field stores: no header copy is kept live)
-  __device__ void store_header() {
-    if (glane() != 0 || !valid) return;
-    TreeHdr* h = p.hdr + tree;
-    h->n_blocks = n_blocks;
-    h->n_log = n_log;
-    h->n_nodes = n_nodes;
-    h->error = err;
-    h->root_blk = root_blk;
-    h->root_visits = root_visits;
-    h->mm_min = mm_min;
-    h->mm_max = mm_max;
-    h->ctr[0] = c_bel;
-    h->ctr[1] = c_sel;
-    h->ctr[2] = c_mod;
-    h->ctr[3] = c_a0;
-    h->ctr[4] = c_a1;
-  }
-
-  // ---- RNG: per tree and stream a kGPage-word LDS page, lanes 0..7 refill it
-  __device__ void refill(int slot, uint32_t stream, uint32_t pg) {
-    const int i = glane();
-    if (i < (int)(kGPage / 4)) {
-      uint32_t c[4] = {pg * (kGPage / 4) + (uint32_t)i, 0u, stream, (uint32_t)(seed >> 32)};
-      philox4x32_10(c, (uint32_t)seed, tkey);
-      reinterpret_cast<uint4*>(rng + slot * kGPage)[i] = make_uint4(c[0], c[1], c[2], c[3]);
-    }
-  }
-  __device__ void warm_rng() {
-    refill(0, S_BELIEF, c_bel / kGPage);
-    refill(1, S_MODEL, c_mod / kGPage);
-    refill(2, S_ACT_BASE, c_a0 / kGPage);
-    refill(3, S_ACT_BASE + 1, c_a1 / kGPage);
-  }
-  __device__ uint32_t draw(int slot, uint32_t& ctr, uint32_t stream) {
-    const uint32_t j = ctr++;
-    if ((j & (kGPage - 1)) == 0u) refill(slot, stream, j / kGPage);
-    return rng[slot * kGPage + (j & (kGPage - 1))];
-  }
-  __device__ uint32_t d_belief(uint32_t n) { return uniform_int(draw(0, c_bel, S_BELIEF), n); }
-  __device__ uint32_t d_model(uint32_t n) { return uniform_int(draw(1, c_mod, S_MODEL), n); }
-  __device__ uint32_t d_act(int agent, uint32_t n) {
-    return agent == 0 ? uniform_int(draw(2, c_a0, S_ACT_BASE), n)
-                      : uniform_int(draw(3, c_a1, S_ACT_BASE + 1), n);
-  }
-  __device__ uint32_t d_select(uint32_t n) {
-    return uniform_int(philox_word(seed, tkey, S_SELECT, c_sel++), n);
-  }
-  __device__ double d_select_float() {
-    return uniform_float(philox_word(seed, tkey, S_SELECT, c_sel++));
-  }
-
-  __device__ void load_block(int blk, uint4* q0, uint4* q1, uint4* q2) const {
-    const uint4* b = reinterpret_cast<const uint4*>(an + (int64_t)blk * p.A);
-    const int i = glane(), np = kLanesPerAct * p.A;
-    *q0 = i < np ? b[i] : make_uint4(0, 0, 0, 0);
-    *q1 = 16 + i < np ? b[16 + i] : make_uint4(0, 0, 0, 0);
-    *q2 = 32 + i < np ? b[32 + i] : make_uint4(0, 0, 0, 0);
-  }
-
-  // ObsNode.add_child for every action (mcts.py:279-281, 318-321): zeroed block.
-  __device__ int alloc_block() {
+  // ---- RNG streams (philox.h): one stateless Philox block per draw
+  auto d_belief = [&](uint32_t n) { return uniform_int(philox_word(seed, tkey, S_BELIEF, c_bel++), n); };
+  auto d_model = [&](uint32_t n) { return uniform_int(philox_word(seed, tkey, S_MODEL, c_mod++), n); };
+  auto d_select = [&](uint32_t n) { return uniform_int(philox_word(seed, tkey, S_SELECT, c_sel++), n); };
+  auto d_act = [&](int agent, uint32_t n) {
+    return agent == 0 ? uniform_int(philox_word(seed, tkey, S_ACT_BASE, c_a0++), n)
+                      : uniform_int(philox_word(seed, tkey, S_ACT_BASE + 1, c_a1++), n);
+  };
+  // ObsNode.add_child for every action (mcts.py:279-281, 318-321): zeroed block
+  auto alloc_block = [&]() -> int {
     if (n_blocks >= p.Nb) {
       err = POMCP_E_ARENA;
       return -1;
     }
     const int b = n_blocks++;
-    uint4* d = reinterpret_cast<uint4*>(an + (int64_t)b * p.A);
-    const int i = glane(), np = kLanesPerAct * p.A;
-    for (int k = i; k < np; k += kL) d[k] = make_uint4(0, 0, 0, 0);
+    uint4* d = reinterpret_cast<uint4*>(an + (int64_t)b * blk_bytes);
+    for (int q = 0; q < blk_parts(A); ++q) d[q] = make_uint4(0, 0, 0, 0);
     return b;
-  }
-
-  __device__ void mm_update(double v) {   // utils.py:29-32
-    if (v > mm_max) mm_max = v;
-    if (v < mm_min) mm_min = v;
-  }
-  __device__ double normalize(double v) const {   // utils.py:34-39
+  };
+  auto normalize = [&](double v) {   // utils.py:34-39
     return mm_max > mm_min ? (v - mm_min) / (mm_max - mm_min) : v;
-  }
+  };
 
-  // PUCB with N == 0 (mcts.py:494-500): random.choices over the uniform prior.
-  __device__ int pucb_prior_draw() {
-    const int A = p.A;
-    const double w = 1.0 / (double)A;
-    double total = w;
-    for (int k = 1; k < A; ++k) total = total + w;
-    const double x = d_select_float() * (total + 0.0);
-    double acc = w;
-    int r = A - 1;
-    bool found = false;
-    for (int k = 0; k < A - 1; ++k) {
-      if (!found && x < acc) {
-        r = k;
-        found = true;
-      }
-      acc = acc + w;
+  int phase = TP_START, sims = 0, max_depth = 0;
+  int t = 0, depth = 0, plen = 0, blk = 0, nvis = 0, k = 0, rdepth = 0;
+  uint32_t s0 = 0, s1 = 0;
+  int32_t* leaf_ptr = nullptr;
+  double ret = 0.0;
+  PathEntry rpath[kRegPath];   // levels 0..kRegPath-1 of the running simulation
+
+  if (!valid || err != 0 || root_abs) phase = TP_DONE;   // mcts.py:270-272
+  if (phase != TP_DONE && h->root_t == 0) {
+    err = POMCP_E_STATE;
+    phase = TP_DONE;
+  }
+  if (phase != TP_DONE) {
+    if (root_blk < 0) root_blk = alloc_block();   // mcts.py:279-281
+    if (root_blk < 0 || bsize <= 0) {
+      if (err == 0) err = POMCP_E_STATE;
+      phase = TP_DONE;
     }
-    return r;
   }
+  if (num_sims <= 0) phase = TP_DONE;
 
-  // _search_action_selection (mcts.py:492-563).  Parts 0..A-1 (lanes 0..A-1 of
-  // q0) hold {visits, value} of the A children.
-  template <int SEL>
-  __device__ int choose(const uint4& q0, int visits) {
-    const int A = p.A, i = glane();
-    if (SEL == POMCP_SEL_PUCB && visits == 0) return pucb_prior_draw();
-    if (visits == 0) return (int)d_select((uint32_t)A);
-    const bool head = i < A;
-    const int n = head ? (int)q0.x : 0;
-    const double v = hilo_d(q0.z, q0.w);
-    if (SEL == POMCP_SEL_UNIFORM) {   // min_visit_action_selection
-      int min_n = visits + 1, best = 0;
-      for (int a = 0; a < A; ++a) {
-        const int na = (int)gshfl((uint32_t)n, a);
-        if (na < min_n) {
-          min_n = na;
-          best = a;
+  // Arrival at an obs node (start of _simulate, mcts.py:315-328): depth/step
+  // cutoff -> back up 0; unexpanded -> expand and roll out; else select there.
+  auto arrive = [&]() {
+    if (depth > p.depth_limit || t > p.step_limit) {   // mcts.py:315
+      ret = 0.0;
+      phase = TP_BACKUP;
+    } else if (blk < 0) {                               // mcts.py:318-328
+      const int b = alloc_block();
+      if (b < 0) {
+        phase = TP_DONE;
+      } else {
+        *leaf_ptr = b;
+        ret = 0.0;
+        k = 0;
+        rdepth = depth;   // the rollout's own depth counter (mcts.py:449)
+        phase = TP_ROLL;
+      }
+    }
+  };
+
+  while (phase != TP_DONE) {
+    // ------------------------------------------------------ start a simulation
+    if (phase == TP_START) {
+      if (sims >= num_sims) {
+        phase = TP_DONE;
+      } else {
+        const uint4 pr = rbel[d_belief((uint32_t)bsize)];   // belief.py:55
+        t = (int)pr.x;
+        s0 = pr.y;
+        s1 = pr.z;
+        blk = root_blk;
+        nvis = root_visits;
+        depth = 0;
+        plen = 0;
+        phase = TP_LEVEL;
+        arrive();
+      }
+    }
+    // ------------------------------------------------------ one tree level
+    if (phase == TP_LEVEL) {
+      char* const bp = an + (int64_t)blk * blk_bytes;
+      uint4 st[kMaxA];
+#pragma unroll
+      for (int a = 0; a < kMaxA; ++a)
+        st[a] = a < A ? reinterpret_cast<const uint4*>(bp)[a] : make_uint4(0, 0, 0, 0);
+      // _search_action_selection (mcts.py:492-563)
+      int a = 0;
+      if (SEL == POMCP_SEL_PUCB && nvis == 0) {   // random.choices over the uniform prior
+        const double w = 1.0 / (double)A;
+        double total = w;
+        for (int q = 1; q < A; ++q) total = total + w;
+        const double x = uniform_float(philox_word(seed, tkey, S_SELECT, c_sel++)) * (total + 0.0);
+        double acc = w;
+        a = A - 1;
+        for (int q = 0; q < A - 1; ++q) {
+          if (x < acc) {
+            a = q;
+            break;
+          }
+          acc = acc + w;
+        }
+      } else if (nvis == 0) {
+        a = (int)d_select((uint32_t)A);
+      } else if (SEL == POMCP_SEL_UNIFORM) {   // min_visit_action_selection
+        int min_n = nvis + 1;
+#pragma unroll
+        for (int q = 0; q < kMaxA; ++q) {
+          if (q < A && (int)st[q].x < min_n) {
+            min_n = (int)st[q].x;
+            a = q;
+          }
+        }
+      } else if (SEL == POMCP_SEL_UCB) {
+        int unv = -1;   // mcts.py:539-540: first unvisited child
+#pragma unroll
+        for (int q = kMaxA - 1; q >= 0; --q)
+          if (q < A && st[q].x == 0u) unv = q;
+        if (unv >= 0) {
+          a = unv;
+        } else {
+          const double log_n = p.logtab[nvis < p.logtab_n ? nvis : 0];
+          if (nvis >= p.logtab_n) err = POMCP_E_ARENA;
+          double best = -__builtin_inf();
+#pragma unroll
+          for (int q = 0; q < kMaxA; ++q) {
+            if (q < A) {   // mcts.py:541-542, strict '>' in action order
+              const double s = normalize(hilo_d(st[q].z, st[q].w)) +
+                               p.c * sqrt(log_n / (double)(int)st[q].x);
+              if (s > best) {
+                best = s;
+                a = q;
+              }
+            }
+          }
+        }
+      } else {   // PUCB, mcts.py:502-527
+        const double noise = 1.0 / (double)A;
+        const double prior = (1.0 / (double)A) * (1.0 - p.pucb_f) + p.pucb_f * noise;
+        const double sqrt_n = sqrt((double)nvis);
+        double best = -__builtin_inf();
+#pragma unroll
+        for (int q = 0; q < kMaxA; ++q) {
+          if (q < A) {
+            const int n = (int)st[q].x;
+            const double s = (n > 0 ? normalize(hilo_d(st[q].z, st[q].w)) : 0.0) +
+                             p.c * prior * (sqrt_n / (double)(1 + n));
+            if (s > best) {
+              best = s;
+              a = q;
+            }
+          }
         }
       }
-      return best;
-    }
-    double score = -__builtin_inf();
-    if (SEL == POMCP_SEL_UCB) {
-      const uint32_t unv = gballot(head && n == 0);   // mcts.py:539-540
-      if (unv) return ffs16(unv);
-      const double log_n = p.logtab[visits < p.logtab_n ? visits : 0];
-      if (visits >= p.logtab_n) err = POMCP_E_ARENA;
-      if (head) score = normalize(v) + p.c * sqrt(log_n / (double)n);   // mcts.py:541-542
-    } else {   // PUCB, mcts.py:502-527
-      const double noise = 1.0 / (double)A;
-      const double prior = (1.0 / (double)A) * (1.0 - p.pucb_f) + p.pucb_f * noise;
-      const double sqrt_n = sqrt((double)visits);
-      if (head) score = (n > 0 ? normalize(v) : 0.0) + p.c * prior * (sqrt_n / (double)(1 + n));
-    }
-    double best_v = -__builtin_inf();
-    int best = 0;
-    for (int a = 0; a < A; ++a) {   // strict '>' in action order
-      const double sa = gshfl_d(score, a);
-      if (sa > best_v) {
-        best_v = sa;
-        best = a;
+      uint4 sa = st[0];
+#pragma unroll
+      for (int q = 1; q < kMaxA; ++q)
+        if (q == a) sa = st[q];
+      // the chosen action's stats1 and child slots (second round trip)
+      const uint4* const ap = reinterpret_cast<const uint4*>(bp);
+      const uint4 s1a = ap[part_stats1(a)];
+      uint4 sl[kSlots];
+#pragma unroll
+      for (int q = 0; q < kSlots; ++q) sl[q] = ap[part_slot(a, q)];
+      const uint32_t ao = d_act(p.other, (uint32_t)A);   // mcts.py:331
+      const uint32_t j = d_model(2);                     // exec-order shuffle
+      uint32_t n0, n1;
+      drv_step2_vec(sm, s0, s1, p.ego == 0 ? (uint32_t)a : ao, p.ego == 0 ? ao : (uint32_t)a, j,
+                    &n0, &n1);
+      const uint32_t e0 = p.ego == 0 ? s0 : s1;
+      const uint32_t e1 = p.ego == 0 ? n0 : n1;
+      const uint32_t o1 = p.ego == 0 ? n1 : n0;
+      const double r = drv_reward_vec(sm, e0, e1);
+      const int done = (((e1 >> 15) & 3u) != 0u ||
+                        (((n0 >> 15) & 3u) != 0u && ((n1 >> 15) & 3u) != 0u)) ? 1 : 0;
+      const uint64_t okey = obs_key_vec(sm, e1, o1);
+      // ActionNode.children[obs] among the inline slots (mcts.py:356-370):
+      // filled in order, so the first invalid slot is the insertion point
+      int ks = -1;
+      bool match = false;
+#pragma unroll
+      for (int q = kSlots - 1; q >= 0; --q) {
+        const uint64_t sk = (uint64_t)sl[q].x | ((uint64_t)sl[q].y << 32);
+        const bool vb = (sk & kValidBit) != 0;
+        if (!vb || (sk & kObsMask) == okey) {
+          ks = q;
+          match = vb;
+        }
+      }
+      const uint32_t ani = (uint32_t)(blk * A + a);
+      uint32_t cid = 0;
+      int cblk = -1, cvis = 1;
+      int32_t* cptr = nullptr;
+      if (ks >= 0) {
+        uint4 sk = sl[0];
+#pragma unroll
+        for (int q = 1; q < kSlots; ++q)
+          if (q == ks) sk = sl[q];
+        if (match) {
+          cblk = (int)sk.z;
+          cvis = (int)sk.w + 1;
+        } else {
+          ++n_nodes;
+        }
+        const uint64_t nk = okey | kValidBit | ((uint64_t)done << 63);
+        uint4* slot = const_cast<uint4*>(ap) + part_slot(a, ks);
+        *slot = make_uint4((uint32_t)nk, (uint32_t)(nk >> 32), (uint32_t)cblk, (uint32_t)cvis);
+        cid = ani * kSlots + (uint32_t)ks + 1u;
+        cptr = reinterpret_cast<int32_t*>(slot) + 2;
+      } else {
+        // overflow map: open addressing over 16-entry buckets
+        const uint64_t key = okey | ((uint64_t)epoch << kEpochShift);
+        uint32_t b = ovf_hash(ani, okey) & p.bucket_mask;
+        bool found = false;
+        for (uint32_t probe = 0; probe <= p.bucket_mask && !found; ++probe) {
+          ++c_probes;
+          for (int e = 0; e < kBucket; ++e) {
+            OvfSlot* ep = ovf + (int64_t)b * kBucket + e;
+            const uint4 w0 = reinterpret_cast<const uint4*>(ep)[0];
+            const uint64_t skey = (uint64_t)w0.x | ((uint64_t)w0.y << 32);
+            const bool live = (uint32_t)(skey >> kEpochShift) == (uint32_t)epoch;
+            if (!live || (skey == key && w0.z == ani)) {
+              if (live) {
+                const uint4 w1 = reinterpret_cast<const uint4*>(ep)[1];
+                cblk = (int)w1.x;
+                cvis = (int)w1.y + 1;
+              } else {
+                ++n_nodes;
+              }
+              reinterpret_cast<uint4*>(ep)[0] =
+                  make_uint4((uint32_t)key, (uint32_t)(key >> 32), ani, (uint32_t)done);
+              reinterpret_cast<uint4*>(ep)[1] = make_uint4((uint32_t)cblk, (uint32_t)cvis, 0u, 0u);
+              cid = p.ovf_base + b * kBucket + (uint32_t)e;
+              cptr = &ep->block;
+              found = true;
+              break;
+            }
+          }
+          b = (b + 1) & p.bucket_mask;
+        }
+        if (!found) err = POMCP_E_ARENA;
+      }
+      if (err != 0 || n_log >= p.Np || plen >= kMaxPath) {
+        if (err == 0) err = POMCP_E_ARENA;
+        phase = TP_DONE;
+      } else {
+        plog[n_log++] = make_uint4(cid, (uint32_t)(t + 1), n0, n1);   // mcts.py:371
+        const uint32_t off = (uint32_t)(blk * blk_bytes + a * 16);
+        const PathEntry pe = {
+            make_uint4(off | ((uint32_t)done << 31), sa.x, (uint32_t)__double2loint(r),
+                       (uint32_t)__double2hiint(r)),
+            make_uint4(sa.z, sa.w, s1a.x, s1a.y),
+            make_uint4(s1a.z, s1a.w, (uint32_t)(blk * blk_bytes + part_stats1(a) * 16), 0u)};
+        if (plen < kRegPath) {
+#pragma unroll
+          for (int l = 0; l < kRegPath; ++l)
+            if (plen == l) rpath[l] = pe;
+        } else {
+          path[plen] = pe;
+        }
+        ++plen;
+        if (done) {
+          ret = 0.0;
+          phase = TP_BACKUP;
+        } else {
+          blk = cblk;
+          nvis = cvis;
+          leaf_ptr = cptr;
+          s0 = n0;
+          s1 = n1;
+          ++t;
+          ++depth;
+          arrive();
+        }
       }
     }
-    return best;
+    // ------------------------------------------------------ one rollout step
+    if (phase == TP_ROLL) {                                  // mcts.py:414-450
+      if (!(rdepth <= p.depth_limit && t <= p.step_limit)) {
+        phase = TP_BACKUP;
+      } else {
+        const uint32_t ae = d_act(p.ego, (uint32_t)A);       // search_policy.py:177
+        const uint32_t ao = d_act(p.other, (uint32_t)A);     // other_policy.py:151
+        const uint32_t j = d_model(2);
+        uint32_t n0, n1;
+        drv_step2_vec(sm, s0, s1, p.ego == 0 ? ae : ao, p.ego == 0 ? ao : ae, j, &n0, &n1);
+        const uint32_t e0 = p.ego == 0 ? s0 : s1, e1 = p.ego == 0 ? n0 : n1;
+        const double r = drv_reward_vec(sm, e0, e1);
+        if (k >= p.dpow_n) {
+          err = POMCP_E_ARENA;
+          phase = TP_DONE;
+        } else {
+          ret += p.dpow[k] * r;   // mcts.py:420-422
+          ++c_rollout;
+          const bool dn = ((e1 >> 15) & 3u) != 0u ||
+                          (((n0 >> 15) & 3u) != 0u && ((n1 >> 15) & 3u) != 0u);
+          if (dn) {
+            phase = TP_BACKUP;
+          } else {
+            s0 = n0;
+            s1 = n1;
+            ++t;
+            ++rdepth;
+            ++k;
+          }
+        }
+      }
+    }
+    // ------------------------------------------------------ backup
+    if (phase == TP_BACKUP) {                                // mcts.py:374-381
+      double gr = ret;
+      auto level = [&](const PathEntry& pe) {
+        const uint4 e0 = pe.e0, e1 = pe.e1, e2 = pe.e2;
+        const double r = hilo_d(e0.z, e0.w);
+        gr = (e0.x >> 31) ? r : r + p.discount * gr;
+        const int n = (int)e0.y + 1;
+        const double value0 = hilo_d(e1.x, e1.y);
+        const double total = hilo_d(e1.z, e1.w) + gr;
+        const double delta = gr - value0;
+        const double value = value0 + delta / (double)n;
+        const double agg = hilo_d(e2.x, e2.y) + delta * (gr - value);
+        *reinterpret_cast<uint4*>(an + (e0.x & 0x7FFFFFFFu)) =
+            make_uint4((uint32_t)n, 0u, (uint32_t)__double2loint(value),
+                       (uint32_t)__double2hiint(value));
+        *reinterpret_cast<uint4*>(an + e2.z) = make_uint4((uint32_t)__double2loint(total), (uint32_t)__double2hiint(total),
+                           (uint32_t)__double2loint(agg), (uint32_t)__double2hiint(agg));
+        if (value > mm_max) mm_max = value;   // utils.py:29-32
+        if (value < mm_min) mm_min = value;
+      };
+      for (int l = plen - 1; l >= kRegPath; --l) level(path[l]);
+#pragma unroll
+      for (int l = kRegPath - 1; l >= 0; --l)
+        if (l < plen) level(rpath[l]);
+      ++root_visits;                                          // mcts.py:288
+      max_depth = depth > max_depth ? depth : max_depth;
+      ++sims;
+      phase = TP_START;
+    }
   }
 
-  // _final_action_selection (mcts.py:565-600) on the root block.
-  template <int SEL>
-  __device__ int final_action() {
-    const int A = p.A;
-    uint4 q0, q1, q2;
-    load_block(root_blk, &q0, &q1, &q2);
+  // ------------------------------------------------------------------ results
+  if (!valid) return;
+  const bool have = err == 0 && !root_abs && root_blk >= 0;
+  uint4 st[kMaxA], s1s[kMaxA];
+#pragma unroll
+  for (int a = 0; a < kMaxA; ++a) {
+    st[a] = make_uint4(0, 0, 0, 0);
+    s1s[a] = st[a];
+    if (have && a < A) {
+      st[a] = reinterpret_cast<const uint4*>(an + (int64_t)root_blk * blk_bytes)[a];
+      s1s[a] = reinterpret_cast<const uint4*>(an + (int64_t)root_blk * blk_bytes)[part_stats1(a)];
+    }
+  }
+  int action = 0;
+  if (have) {   // _final_action_selection (mcts.py:565-600)
     uint32_t ties = 0;
     int nt = 0;
+    bool direct = false;
     if (SEL == POMCP_SEL_PUCB) {
-      if (root_visits == 0) return (int)d_select((uint32_t)A);
-      int mx = 0;
-      for (int a = 0; a < A; ++a) {
-        const int na = (int)gshfl(q0.x, a);
-        if (na == mx) {
-          ties |= 1u << a;
-          ++nt;
-        } else if (na > mx) {
-          mx = na;
-          ties = 1u << a;
-          nt = 1;
+      if (root_visits == 0) {
+        action = (int)d_select((uint32_t)A);
+        direct = true;
+      } else {
+        int mx = 0;
+#pragma unroll
+        for (int a = 0; a < kMaxA; ++a) {
+          if (a >= A) continue;
+          const int na = (int)st[a].x;
+          if (na == mx) {
+            ties |= 1u << a;
+            ++nt;
+          } else if (na > mx) {
+            mx = na;
+            ties = 1u << a;
+            nt = 1;
+          }
         }
       }
     } else {
       double mx = -__builtin_inf();
-      for (int a = 0; a < A; ++a) {
-        const double va = hilo_d(gshfl(q0.z, a), gshfl(q0.w, a));
+#pragma unroll
+      for (int a = 0; a < kMaxA; ++a) {
+        if (a >= A) continue;
+        const double va = hilo_d(st[a].z, st[a].w);
         if (va == mx) {
           ties |= 1u << a;
           ++nt;
@@ -291,348 +466,52 @@ struct GTree {
         }
       }
     }
-    return kth_bit(ties, d_select((uint32_t)nt));
+    if (!direct) action = kth_bit(ties, d_select((uint32_t)nt));
   }
-
-  // overflow map (children beyond the 6 inline slots), 16 lanes per probe
-  __device__ bool ovf_ref(uint32_t ani, uint64_t okey, int done, uint32_t* id, int* cblk,
-                          int* cvis, int32_t** blk_ptr) {
-    const int epoch = p.hdr[tree].epoch;
-    const uint64_t key = okey | ((uint64_t)epoch << kEpochShift);
-    uint32_t b = ovf_hash(ani, okey) & p.bucket_mask;
-    const int i = glane();
-    for (uint32_t probe = 0; probe <= p.bucket_mask; ++probe) {
-      ++c_probes;
-      OvfSlot* e = ovf + (int64_t)b * kBucket + i;
-      const uint4 s = reinterpret_cast<const uint4*>(e)[0];
-      const uint4 s2 = reinterpret_cast<const uint4*>(e)[1];
-      const uint64_t skey = (uint64_t)s.x | ((uint64_t)s.y << 32);
-      const bool ok = (uint32_t)(skey >> kEpochShift) == (uint32_t)epoch;
-      const uint32_t mm = gballot(ok && skey == key && s.z == ani);
-      const uint32_t em = gballot(!ok);
-      const int L = mm ? ffs16(mm) : ffs16(em);
-      if (mm || em) {
-        OvfSlot* t = ovf + (int64_t)b * kBucket + L;
-        *id = p.ovf_base + b * kBucket + (uint32_t)L;
-        *blk_ptr = &t->block;
-        if (mm) {
-          *cblk = (int)gshfl(s2.x, L);
-          *cvis = (int)gshfl(s2.y, L) + 1;
-        } else {
-          *cblk = -1;
-          *cvis = 1;
-          ++n_nodes;
-        }
-        if (i == 0) {
-          reinterpret_cast<uint4*>(t)[0] =
-              make_uint4((uint32_t)key, (uint32_t)(key >> 32), ani, (uint32_t)done);
-          reinterpret_cast<uint4*>(t)[1] = make_uint4((uint32_t)*cblk, (uint32_t)*cvis, 0u, 0u);
-        }
-        return true;
-      }
-      b = (b + 1) & p.bucket_mask;
-    }
-    err = POMCP_E_ARENA;
-    return false;
+  TreeHdr* const hw = p.hdr + tree;
+  hw->n_blocks = n_blocks;
+  hw->n_log = n_log;
+  hw->n_nodes = n_nodes;
+  hw->error = err;
+  hw->root_blk = root_blk;
+  hw->root_visits = root_visits;
+  hw->mm_min = mm_min;
+  hw->mm_max = mm_max;
+  hw->ctr[0] = c_bel;
+  hw->ctr[1] = c_sel;
+  hw->ctr[2] = c_mod;
+  hw->ctr[3] = c_a0;
+  hw->ctr[4] = c_a1;
+  pomcp_root_stats* const so = p.stats + tree;
+#pragma unroll
+  for (int a = 0; a < kMaxA; ++a) {
+    if (a >= A) continue;
+    const double va = hilo_d(st[a].z, st[a].w), tot = hilo_d(s1s[a].x, s1s[a].y);
+    so->child_visits[a] = (int)st[a].x;
+    so->child_values[a] = va;
+    so->child_totals[a] = tot;
+    p.merge[((int64_t)tree * A + a) * 2] = (double)st[a].x;
+    p.merge[((int64_t)tree * A + a) * 2 + 1] = tot;
   }
-};
-
-// simulation state of one tree (group-uniform registers)
-struct Sim {
-  int phase, t, depth, plen, blk, nvis, k, sims, max_depth, rdepth;
-  uint32_t s0, s1;
-  int32_t* leaf_ptr;
-  double ret;
-};
-
-template <int SEL>
-__global__ __launch_bounds__(256, POMCP_SEARCH_WAVES_PER_SIMD) void k_search(DevParams p,
-                                                                            int num_sims) {
-  __shared__ DrvModel sm;
-  __shared__ uint32_t rng_lds[kGroupsPerBlock][4 * kGPage];
-  __shared__ uint32_t path_lds[kGroupsPerBlock][kPathMax * 3];
-  stage_model(p.model, sm);
-  const int g_in_block = threadIdx.x / kL;
-  const int tree = blockIdx.x * kGroupsPerBlock + g_in_block;
-  GTree T(p, sm, tree, rng_lds[g_in_block], path_lds[g_in_block]);
-  const int i = glane();
-  // counters derived from arena growth: one particle per tree level stepped,
-  // one block per expansion, one node per new obs child
-  const int log0 = T.n_log, blocks0 = T.n_blocks, nodes0 = T.n_nodes;
-  const int A = p.A;
-  Sim S;
-  S.phase = PH_START;
-  S.sims = 0;
-  S.max_depth = 0;
-  S.t = S.depth = S.plen = S.blk = S.nvis = S.k = S.rdepth = 0;
-  S.s0 = S.s1 = 0;
-  S.leaf_ptr = nullptr;
-  S.ret = 0.0;
-  const int root_abs = T.valid ? p.hdr[tree].root_abs : 0;
-  if (!T.valid || T.err != 0 || root_abs) S.phase = PH_DONE;   // mcts.py:270-272
-  if (S.phase != PH_DONE && p.hdr[tree].root_t == 0) {
-    T.err = POMCP_E_STATE;
-    S.phase = PH_DONE;
-  }
-  if (S.phase != PH_DONE) {
-    if (T.root_blk < 0) T.root_blk = T.alloc_block();   // mcts.py:279-281
-    if (T.root_blk < 0 || T.bsize <= 0) {
-      if (T.err == 0) T.err = POMCP_E_STATE;
-      S.phase = PH_DONE;
-    }
-  }
-  T.warm_rng();
-  const bool any_sims = num_sims > 0;
-  if (!any_sims && S.phase != PH_DONE) S.phase = PH_DONE;
-  // Arrival at an obs node (start of _simulate, mcts.py:315-328): depth/step
-  // cutoff -> back up 0; unexpanded -> expand and roll out; else select there.
-  auto arrive = [&]() {
-    if (S.depth > p.depth_limit || S.t > p.step_limit) {     // mcts.py:315
-      S.ret = 0.0;
-      S.phase = PH_BACKUP;
-    } else if (S.blk < 0) {                                   // mcts.py:318-328
-      const int b = T.alloc_block();
-      if (b < 0) {
-        S.phase = PH_DONE;
-      } else {
-        if (i == 0) *S.leaf_ptr = b;
-        S.ret = 0.0;
-        S.k = 0;
-        S.rdepth = S.depth;   // the rollout's own depth counter (mcts.py:449)
-        S.phase = PH_ROLL;
-      }
-    }
-  };
-  // Loop iteration = one step of every tree: start a simulation (and select at
-  // the root), one tree level, one rollout step, the backup (in this order, so a
-  // depth-2 search takes 3 iterations per simulation).
-  while (__ballot(S.phase != PH_DONE)) {
-    // ---------------------------------------------------------- start a simulation
-    if (S.phase == PH_START) {
-      if (S.sims >= num_sims) {
-        S.phase = PH_DONE;
-      } else {
-        const uint32_t k = T.d_belief((uint32_t)T.bsize);   // belief.py:55
-        const uint4 pr = T.rbel[k];
-        S.t = (int)pr.x;
-        S.s0 = pr.y;
-        S.s1 = pr.z;
-        S.blk = T.root_blk;
-        S.nvis = T.root_visits;
-        S.depth = 0;
-        S.plen = 0;
-        S.phase = PH_LEVEL;
-        arrive();
-      }
-    }
-    // ---------------------------------------------------------- one tree level
-    if (S.phase == PH_LEVEL) {
-      {
-        uint4 q0, q1, q2;
-        T.load_block(S.blk, &q0, &q1, &q2);
-        const int a = T.choose<SEL>(q0, S.nvis);                      // mcts.py:330
-        const uint32_t ao = T.d_act(p.other, (uint32_t)A);            // mcts.py:331
-        const uint32_t j = T.d_model(2);                              // exec-order shuffle
-        uint32_t n0, n1;
-        const uint32_t ea = (uint32_t)a;
-        drv_step2_vec(sm, S.s0, S.s1, p.ego == 0 ? ea : ao, p.ego == 0 ? ao : ea, j, &n0, &n1);
-        const uint32_t e0 = p.ego == 0 ? S.s0 : S.s1;
-        const uint32_t e1 = p.ego == 0 ? n0 : n1;
-        const uint32_t o1 = p.ego == 0 ? n1 : n0;
-        const double r = drv_reward_vec(sm, e0, e1);
-        const int done = (((e1 >> 15) & 3u) != 0u ||
-                          (((n0 >> 15) & 3u) != 0u && ((n1 >> 15) & 3u) != 0u)) ? 1 : 0;
-        const uint64_t okey = obs_key_vec(sm, e1, o1);
-        // ActionNode.children[obs] among the 6 inline slots (mcts.py:356-370)
-        const int lo = 2 * A + kSlots * a;
-#define POMCP_SLOT_TEST(Q, R, MT, EM)                                              \
-  bool MT, EM;                                                                     \
-  {                                                                                \
-    const int part = 16 * (R) + i;                                                 \
-    const bool in = part >= lo && part < lo + kSlots;                              \
-    const uint64_t sk = (uint64_t)(Q).x | ((uint64_t)(Q).y << 32);                 \
-    const bool vb = (sk & kValidBit) != 0;                                         \
-    MT = in && vb && (sk & kObsMask) == okey;                                      \
-    EM = in && !vb;                                                                \
-  }
-        POMCP_SLOT_TEST(q0, 0, mt0, em0)
-        POMCP_SLOT_TEST(q1, 1, mt1, em1)
-        POMCP_SLOT_TEST(q2, 2, mt2, em2)
-#undef POMCP_SLOT_TEST
-        const uint64_t mm = (uint64_t)gballot(mt0) | ((uint64_t)gballot(mt1) << 16) |
-                            ((uint64_t)gballot(mt2) << 32);
-        const uint64_t ee = (uint64_t)gballot(em0) | ((uint64_t)gballot(em1) << 16) |
-                            ((uint64_t)gballot(em2) << 32);
-        const uint32_t ani = (uint32_t)(S.blk * A + a);
-        uint32_t cid = 0;
-        int cblk = -1, cvis = 1;
-        int32_t* cptr = nullptr;
-        bool ok = true;
-        if (mm || ee) {
-          const int P = mm ? (int)__builtin_ctzll(mm) : (int)__builtin_ctzll(ee);
-          const uint4 sl = get_part(q0, q1, q2, P);
-          const int ks = P - lo;
-          if (mm) {
-            cblk = (int)sl.z;
-            cvis = (int)sl.w + 1;
-          } else {
-            ++T.n_nodes;
-          }
-          const uint64_t nk = okey | kValidBit | ((uint64_t)done << 63);
-          uint4* slot = reinterpret_cast<uint4*>(T.an + (int64_t)S.blk * A) + P;
-          if (i == 0)
-            *slot = make_uint4((uint32_t)nk, (uint32_t)(nk >> 32), (uint32_t)cblk, (uint32_t)cvis);
-          cid = ani * kSlots + (uint32_t)ks + 1u;
-          cptr = reinterpret_cast<int32_t*>(slot) + 2;
-        } else {
-          ok = T.ovf_ref(ani, okey, done, &cid, &cblk, &cvis, &cptr);
-        }
-        if (!ok || T.err != 0 || T.n_log >= p.Np || S.plen >= kPathMax) {
-          if (T.err == 0) T.err = POMCP_E_ARENA;
-          S.phase = PH_DONE;
-        } else {
-          if (i == 0) T.plog[T.n_log] = make_uint4(cid, (uint32_t)(S.t + 1), n0, n1);   // mcts.py:371
-          ++T.n_log;
-          // path entry: byte offset of the action node's stats0 | done, reward
-          const uint32_t off = (uint32_t)((S.blk * A) * 128 + a * 16);
-          if (i == 0) {
-            uint32_t* pe = T.path + 3 * S.plen;
-            pe[0] = off | ((uint32_t)done << 31);
-            pe[1] = (uint32_t)__double2loint(r);
-            pe[2] = (uint32_t)__double2hiint(r);
-          }
-          ++S.plen;
-          if (done) {
-            S.ret = 0.0;
-            S.phase = PH_BACKUP;
-          } else {
-            S.blk = cblk;
-            S.nvis = cvis;
-            S.leaf_ptr = cptr;
-            S.s0 = n0;
-            S.s1 = n1;
-            ++S.t;
-            ++S.depth;
-            arrive();
-          }
-        }
-      }
-    }
-    // ---------------------------------------------------------- one rollout step
-    if (S.phase == PH_ROLL) {                                  // mcts.py:414-450
-      if (!(S.rdepth <= p.depth_limit && S.t <= p.step_limit)) {
-        S.phase = PH_BACKUP;
-      } else {
-        const uint32_t ae = T.d_act(p.ego, (uint32_t)A);       // search_policy.py:177
-        const uint32_t ao = T.d_act(p.other, (uint32_t)A);     // other_policy.py:151
-        const uint32_t j = T.d_model(2);
-        uint32_t n0, n1;
-        drv_step2_vec(sm, S.s0, S.s1, p.ego == 0 ? ae : ao, p.ego == 0 ? ao : ae, j, &n0, &n1);
-        const uint32_t e0 = p.ego == 0 ? S.s0 : S.s1, e1 = p.ego == 0 ? n0 : n1;
-        const double r = drv_reward_vec(sm, e0, e1);
-        if (S.k >= p.dpow_n) {
-          T.err = POMCP_E_ARENA;
-          S.phase = PH_DONE;
-        } else {
-          S.ret += p.dpow[S.k] * r;   // mcts.py:420-422
-          ++T.c_rollout;
-          const bool done = ((e1 >> 15) & 3u) != 0u ||
-                            (((n0 >> 15) & 3u) != 0u && ((n1 >> 15) & 3u) != 0u);
-          if (done) {
-            S.phase = PH_BACKUP;
-          } else {
-            S.s0 = n0;
-            S.s1 = n1;
-            ++S.t;
-            ++S.rdepth;
-            ++S.k;
-          }
-        }
-      }
-    }
-    // ---------------------------------------------------------- backup
-    if (S.phase == PH_BACKUP) {                                // mcts.py:374-381
-      double gr = S.ret;
-      const char* base = reinterpret_cast<const char*>(T.an);
-      for (int c0 = ((S.plen - 1) / kL) * kL; c0 >= 0; c0 -= kL) {
-        // statistics of the levels of this chunk, lane i -> level c0 + i
-        uint4 st0 = make_uint4(0, 0, 0, 0), st1 = make_uint4(0, 0, 0, 0);
-        if (c0 + i < S.plen) {
-          const uint32_t off = T.path[3 * (c0 + i)] & 0x7FFFFFFFu;
-          st0 = *reinterpret_cast<const uint4*>(base + off);
-          st1 = *reinterpret_cast<const uint4*>(base + off + 16 * A);
-        }
-        const int top = (S.plen - 1 - c0) < (kL - 1) ? (S.plen - 1 - c0) : (kL - 1);
-        for (int li = top; li >= 0; --li) {
-          const uint32_t* pe = T.path + 3 * (c0 + li);
-          const uint32_t w0 = pe[0];
-          const double r = hilo_d(pe[1], pe[2]);
-          gr = (w0 >> 31) ? r : r + p.discount * gr;
-          const int n = (int)gshfl(st0.x, li) + 1;
-          const double value0 = hilo_d(gshfl(st0.z, li), gshfl(st0.w, li));
-          const double total = hilo_d(gshfl(st1.x, li), gshfl(st1.y, li)) + gr;
-          const double delta = gr - value0;
-          const double value = value0 + delta / (double)n;
-          const double agg = hilo_d(gshfl(st1.z, li), gshfl(st1.w, li)) + delta * (gr - value);
-          const uint32_t off = w0 & 0x7FFFFFFFu;
-          if (i == 0)
-            *reinterpret_cast<uint4*>(const_cast<char*>(base) + off) = make_uint4(
-                (uint32_t)n, 0u, (uint32_t)__double2loint(value), (uint32_t)__double2hiint(value));
-          if (i == 1)
-            *reinterpret_cast<uint4*>(const_cast<char*>(base) + off + 16 * A) =
-                make_uint4((uint32_t)__double2loint(total), (uint32_t)__double2hiint(total),
-                           (uint32_t)__double2loint(agg), (uint32_t)__double2hiint(agg));
-          T.mm_update(value);
-        }
-      }
-      ++T.root_visits;                                          // mcts.py:288
-      S.max_depth = S.depth > S.max_depth ? S.depth : S.max_depth;
-      ++S.sims;
-      S.phase = PH_START;
-    }
-  }
-  // ------------------------------------------------------------------ results
-  int action = 0;
-  const bool have = T.valid && T.err == 0 && !root_abs && T.root_blk >= 0;
-  if (have) action = T.final_action<SEL>();
-  T.store_header();
-  if (!T.valid) return;
-  pomcp_root_stats* st = p.stats + tree;
-  uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0, q2 = q0;
-  if (have) T.load_block(T.root_blk, &q0, &q1, &q2);
-  for (int a = 0; a < A; ++a) {
-    const uint4 a0 = get_part(q0, q1, q2, a);
-    const uint4 a1 = get_part(q0, q1, q2, A + a);
-    if (i == a) {
-      const double va = hilo_d(a0.z, a0.w), tot = hilo_d(a1.x, a1.y);
-      st->child_visits[a] = (int)a0.x;
-      st->child_values[a] = va;
-      st->child_totals[a] = tot;
-      p.merge[((int64_t)tree * A + a) * 2] = (double)a0.x;
-      p.merge[((int64_t)tree * A + a) * 2 + 1] = tot;
-    }
-  }
-  if (i == 0) {
-    st->action = action;
-    st->num_sims = S.sims;
-    st->search_depth = S.max_depth;
-    st->root_visits = T.root_visits;
-    st->root_absorbing = root_abs;
-    st->belief_size = T.bsize;
-    st->error = T.err;
-    st->num_children = have ? A : 0;
-    st->min_value = T.mm_min;
-    st->max_value = T.mm_max;
-    st->n_levels = T.n_log - log0;
-    st->n_expansions = T.n_blocks - blocks0;
-    st->n_new_nodes = T.n_nodes - nodes0;
-    st->n_rollout_steps = T.c_rollout;
-    st->n_probes = T.c_probes;
-    st->n_obs_nodes = T.n_nodes;
-    st->n_blocks = T.n_blocks;
-    st->n_log = T.n_log;
-    st->pad = 0;
-  }
+  so->action = action;
+  so->num_sims = sims;
+  so->search_depth = max_depth;
+  so->root_visits = root_visits;
+  so->root_absorbing = root_abs;
+  so->belief_size = bsize;
+  so->error = err;
+  so->num_children = have ? A : 0;
+  so->min_value = mm_min;
+  so->max_value = mm_max;
+  so->n_levels = n_log - log0;
+  so->n_expansions = n_blocks - blocks0;
+  so->n_new_nodes = n_nodes - nodes0;
+  so->n_rollout_steps = c_rollout;
+  so->n_probes = c_probes;
+  so->n_obs_nodes = n_nodes;
+  so->n_blocks = n_blocks;
+  so->n_log = n_log;
+  so->pad = 0;
 }
 
 template __global__ void k_search<POMCP_SEL_PUCB>(DevParams, int);
