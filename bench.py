@@ -36,11 +36,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--trees", type=int, default=8192)
+    ap.add_argument("--trees", type=int, default=65536)
     ap.add_argument("--sims", type=int, default=65536)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--max-blocks", type=int, default=None,
-                    help="per-tree action-block arena (default min(sims + 64, 4096))")
+    ap.add_argument("--max-blocks", type=int, default=512,
+                    help="per-tree action-block arena; a depth-2 Driving-v1 tree uses ~170 "
+                         "(overflow is detected and fails the run)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-sims", type=int, default=16384)
     ap.add_argument("--cpu-sample-trees", type=int, default=4)
@@ -105,7 +106,7 @@ def main():
     cfg = MCTSConfig(seed=args.seed, num_sims=S, **TEST_CFG)
     model = DrivingModel()
     caps = plan_capacities(cfg, model.spec.max_episode_steps, S, 1, reroot=False,
-                           max_blocks=args.max_blocks or min(S + 64, 4096),
+                           max_blocks=min(args.max_blocks, S + 64),
                            overflow_slots=1024)
     stream = torch.cuda.Stream(device=dev)
     bp = BatchedPOMCP(model, "0", cfg, B, S, capacities=caps, stream=stream.cuda_stream,

@@ -194,7 +194,7 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
   ALLOC(hdr, TreeHdr, B);
   ALLOC(an, Line, B * d.Nb * blk_lines(d.A));
   ALLOC(ovf, OvfSlot, B * d.H);
-  ALLOC(plog, uint4, B * d.Np);
+  ALLOC(plog, LogRec, B * d.Np);
   ALLOC(belief, uint4, B * 2 * d.Nr);
   ALLOC(path, uint4, B * 3 * kMaxPath);
   ALLOC(logtab, double, c.log_table_size);

@@ -44,6 +44,14 @@ struct ChildSlot {
   int32_t block;    // action block of the child obs node (-1 = leaf)
   int32_t visits;   // ObsNode.visits
 };
+// Particle log record (ObsNode.belief.add_particle, mcts.py:371): the particle
+// (v0, v1) entered obs node `id`.  Its time step is not stored: every particle
+// of a node has the same t (the root's particles have t = root_t, a node at
+// depth d below it t = root_t + d), so re-rooting restores it as root_t + 1.
+struct LogRec {
+  uint32_t id, v0, v1;
+};
+
 struct alignas(16) Line {   // allocation unit of the block arena
   uint4 part[kLine];
 };
@@ -85,7 +93,7 @@ struct DevParams {
   TreeHdr* hdr;
   Line* an;             // [B][Nb][A + 1] action blocks
   OvfSlot* ovf;         // [B][H]
-  uint4* plog;          // [B][Np] {obs node id, t, v0, v1}
+  LogRec* plog;         // [B][Np] particle log {obs node id, v0, v1}
   uint4* belief;        // [B][2][Nr] {t, v0, v1, 0}
   uint4* path;          // [B][3 * kMaxPath] search path of the running simulation
   const double* logtab;

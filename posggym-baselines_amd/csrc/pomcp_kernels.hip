@@ -54,7 +54,7 @@ struct Tree {
   int tree, lane;
   Line* an;
   OvfSlot* ovf;
-  uint4* plog;
+  LogRec* plog;
   uint4* bel;
   int n_blocks, n_log, n_nodes, err, bsize, bsel, epoch, root_t;
   uint32_t root_id;
@@ -423,12 +423,12 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
           int n = 0;
           for (int base = 0; base < T.n_log; base += kWave) {
             const int i = base + lane;
-            uint4 rec = make_uint4(0xFFFFFFFFu, 0, 0, 0);
+            LogRec rec = {0xFFFFFFFFu, 0u, 0u};
             if (i < T.n_log) rec = T.plog[i];
-            const bool m = i < T.n_log && rec.x == c.id;
+            const bool m = i < T.n_log && rec.id == c.id;
             const uint64_t mask = __ballot(m);
             const int pos = n + (int)__popcll(mask & ((1ull << lane) - 1ull));
-            if (m && pos < p.Nr) nb[pos] = make_uint4(rec.y, rec.z, rec.w, 0u);
+            if (m && pos < p.Nr) nb[pos] = make_uint4((uint32_t)T.root_t + 1u, rec.v0, rec.v1, 0u);
             n += (int)__popcll(mask);
           }
           if (n > p.Nr) T.err = POMCP_E_ARENA;

@@ -52,7 +52,7 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
   const int A = p.A;
   char* const an = reinterpret_cast<char*>(p.an + (int64_t)tt * p.Nb * blk_lines(A));
   const int blk_bytes = blk_lines(A) * 128;
-  uint4* const plog = p.plog + (int64_t)tt * p.Np;
+  LogRec* const plog = p.plog + (int64_t)tt * p.Np;
   OvfSlot* const ovf = p.ovf + (int64_t)tt * p.H;
   PathEntry* const path = reinterpret_cast<PathEntry*>(p.path) + (int64_t)tt * kMaxPath;
   const TreeHdr* const h = p.hdr + tt;
@@ -318,7 +318,7 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
         if (err == 0) err = POMCP_E_ARENA;
         phase = TP_DONE;
       } else {
-        plog[n_log++] = make_uint4(cid, (uint32_t)(t + 1), n0, n1);   // mcts.py:371
+        plog[n_log++] = LogRec{cid, n0, n1};   // mcts.py:371 (t + 1: see LogRec)
         const uint32_t off = (uint32_t)(blk * blk_bytes + a * 16);
         const PathEntry pe = {
             make_uint4(off | ((uint32_t)done << 31), sa.x, (uint32_t)__double2loint(r),
