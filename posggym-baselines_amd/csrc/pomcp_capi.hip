@@ -70,7 +70,17 @@ static int dev_alloc(pomcp_ctx* ctx, void** out, size_t bytes) {
 }
 
 static unsigned grid_blocks(int B) { return (unsigned)((B + kTreesPerBlock - 1) / kTreesPerBlock); }
-static unsigned search_blocks(int B) { return (unsigned)((B + kTPB - 1) / kTPB); }
+// Trees per wavefront of k_search (64 = one tree per lane; POMCP_TREES_PER_WAVE
+// = 32 / 16 leave lanes idle so that more waves share each SIMD).
+static int search_tpw() {
+  const char* e = std::getenv("POMCP_TREES_PER_WAVE");
+  const int v = e ? std::atoi(e) : 64;
+  return (v == 16 || v == 32) ? v : 64;
+}
+static unsigned search_blocks(int B, int tpw) {
+  const int per_block = tpw * (kTPB / kWave);
+  return (unsigned)((B + per_block - 1) / per_block);
+}
 
 extern "C" {
 
@@ -108,7 +118,7 @@ static int validate(const pomcp_config* c, std::string* why) {
   if (c->num_particles < 1 || c->extra_particles < 0) return bad("num_particles");
   if (c->num_trees < 1) return bad("num_trees >= 1");
   if (c->max_blocks < 1 || c->max_blocks * (c->num_actions + 1) * 128 > INT32_MAX) return bad("max_blocks");
-  if (c->num_actions > 6) { *why = "the search kernel supports at most 6 actions"; return POMCP_E_UNSUPPORTED; }
+  if (c->num_actions > kMaxA) { *why = "the search kernel supports at most 5 actions"; return POMCP_E_UNSUPPORTED; }
   if (c->max_particles < 1 || c->max_particles > INT32_MAX) return bad("max_particles");
   if (c->max_belief < 2 * (c->num_particles + c->extra_particles)) return bad("max_belief too small");
   if (c->overflow_slots < kBucket || (c->overflow_slots & (c->overflow_slots - 1)) != 0 ||
@@ -315,17 +325,18 @@ int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_key
 int pomcp_search(pomcp_ctx* ctx, int32_t num_sims, int32_t* actions_out) {
   if (!ctx || num_sims < 0) return POMCP_E_INVALID;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
-  const dim3 grid(search_blocks(ctx->dp.B)), block(kTPB);
+  const int tpw = search_tpw();
+  const dim3 grid(search_blocks(ctx->dp.B, tpw)), block(kTPB);
   switch (ctx->dp.sel) {
     case POMCP_SEL_PUCB:
-      hipLaunchKernelGGL(k_search<POMCP_SEL_PUCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims);
+      hipLaunchKernelGGL(k_search<POMCP_SEL_PUCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims, tpw);
       break;
     case POMCP_SEL_UCB:
-      hipLaunchKernelGGL(k_search<POMCP_SEL_UCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims);
+      hipLaunchKernelGGL(k_search<POMCP_SEL_UCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims, tpw);
       break;
     default:
       hipLaunchKernelGGL(k_search<POMCP_SEL_UNIFORM>, grid, block, 0, ctx->stream, ctx->dp,
-                         (int)num_sims);
+                         (int)num_sims, tpw);
   }
   HIP_TRY(ctx, hipGetLastError());
   if (!actions_out) return POMCP_OK;

@@ -7,35 +7,47 @@
 // Why one tree per lane: the per-simulation work of a tree is a serial chain
 // (select -> step -> observe -> descend -> back up) with almost no data
 // parallelism inside one tree (A = 5 children).  Spreading one tree over 16
-// lanes (the previous design) made every instruction of the chain do
-// the same group-uniform work 16 times; here each lane runs its own tree and
-// every VALU instruction advances 64 trees.  The kernel is then bound by the
-// dependent memory round trips of a simulation (two per tree level: the
-// node's action statistics, then the chosen action's child slots), which the
-// other 63 lanes' trees and the other waves on the SIMD hide.
+// lanes (an earlier design) made every instruction of the chain do the same
+// group-uniform work 16 times; here each lane runs its own tree and every
+// VALU instruction advances 64 trees.
 //
-// Each loop iteration runs one step of every phase (start a simulation and
-// select at the root, one tree level, one rollout step, the backup) for the
-// lanes in it, so a depth-2 simulation takes three iterations.
+// What bounds it: a wave waits for the slowest of its 64 lanes at every
+// dependent memory access, so the cost of an iteration of the phase loop is
+// the number of memory waits in it, whatever the lanes' phases are.  Hence:
+//   * the ROOT's action statistics and inline child slots live in LDS for the
+//     whole launch (35 x 16 B per tree, lane-interleaved: conflict-free), so
+//     the root level of every simulation costs no HBM round trip; the root's
+//     {total, agg} stay in HBM and are loaded without waiting (they are only
+//     needed by the backup);
+//   * the belief particle of the NEXT simulation is prefetched when a
+//     simulation starts (belief.py:55: its index only depends on the belief
+//     stream's counter);
+//   * one loop iteration = start + root level (LDS) + one deeper level (two
+//     dependent HBM lines: the node's statistics, then the chosen action's
+//     child slots) + a whole rollout + the backup, so a depth-2 simulation
+//     takes two iterations and four HBM waits.
+// The root block is written back to HBM at the end of the launch.
 //
-// Block layout: pomcp_device.h ((A + 1) x 128 B lines; a tree level reads the
-// node's statistics line and the chosen action's line).
+// Block layout: pomcp_device.h ((A + 1) x 128 B lines).
 // The path of the running simulation (PathEntry: the level's statistics are
 // captured on the way down -- a node appears once per path and only this lane
 // writes this tree -- so the backup reads no tree memory) is held in registers
-// for the first kRegPath levels and in p.path below them.
+// for the root and the next kRegPath levels and in p.path below them.
 #pragma clang fp contract(off)
 
 namespace pb {
 
-constexpr int kMaxA = 6;
-constexpr int kTPB = 256;   // trees (lanes) per workgroup
+constexpr int kMaxA = 5;     // LDS root cache: A <= 5 (Driving-v1 5, PursuitEvasion-v1 4)
+constexpr int kTPB = 256;    // lanes per workgroup
+constexpr int kRootParts = kMaxA * (1 + kSlots);   // stats0[a], then slots[a][k]
+__host__ __device__ constexpr int rc_stats(int a) { return a; }
+__host__ __device__ constexpr int rc_slot(int a, int k) { return kMaxA + a * kSlots + k; }
 
-constexpr int kRegPath = 4;  // path levels held in registers (deeper ones in p.path)
+constexpr int kRegPath = 3;  // levels 1..kRegPath held in registers (deeper ones in p.path)
 
-// One level of the running simulation's path: {stats0 byte offset | done << 31,
-// visits before, r}, {value before, total before}, {agg before, stats1 byte
-// offset, -}.
+// One level (depth >= 1) of the running simulation's path: {stats0 byte
+// offset | done << 31, visits before, r}, {value before, total before},
+// {agg before, stats1 byte offset, -}.
 struct PathEntry {
   uint4 e0, e1, e2;
 };
@@ -43,11 +55,15 @@ struct PathEntry {
 enum : int { TP_LEVEL = 0, TP_ROLL = 1, TP_BACKUP = 2, TP_START = 3, TP_DONE = 4 };
 
 template <int SEL>
-__global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
+__global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims, int tpw) {
   __shared__ DrvModel sm;
+  __shared__ uint4 rc[kRootParts][kTPB];   // the root block of every lane's tree
   stage_model(p.model, sm);
-  const int tree = blockIdx.x * kTPB + threadIdx.x;
-  const bool valid = tree < p.B;
+  // tpw trees per wavefront (lanes >= tpw idle)
+  const int lid = (int)threadIdx.x;
+  const int lane = lid & (kWave - 1);
+  const int tree = (int)(blockIdx.x * (kTPB / kWave) + (threadIdx.x >> 6)) * tpw + lane;
+  const bool valid = lane < tpw && tree < p.B;
   const int tt = valid ? tree : 0;
   const int A = p.A;
   char* const an = reinterpret_cast<char*>(p.an + (int64_t)tt * p.Nb * blk_lines(A));
@@ -92,12 +108,93 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
     return mm_max > mm_min ? (v - mm_min) / (mm_max - mm_min) : v;
   };
 
+  // _search_action_selection (mcts.py:492-563) over the statistics st[] of a
+  // node with nv visits
+  auto select_action = [&](const uint4 (&st)[kMaxA], int nv) -> int {
+    int a = 0;
+    if (SEL == POMCP_SEL_PUCB && nv == 0) {   // random.choices over the uniform prior
+      const double w = 1.0 / (double)A;
+      double total = w;
+      for (int q = 1; q < A; ++q) total = total + w;
+      const double x = uniform_float(philox_word(seed, tkey, S_SELECT, c_sel++)) * (total + 0.0);
+      double acc = w;
+      a = A - 1;
+      for (int q = 0; q < A - 1; ++q) {
+        if (x < acc) {
+          a = q;
+          break;
+        }
+        acc = acc + w;
+      }
+    } else if (nv == 0) {
+      a = (int)d_select((uint32_t)A);
+    } else if (SEL == POMCP_SEL_UNIFORM) {   // min_visit_action_selection
+      int min_n = nv + 1;
+#pragma unroll
+      for (int q = 0; q < kMaxA; ++q) {
+        if (q < A && (int)st[q].x < min_n) {
+          min_n = (int)st[q].x;
+          a = q;
+        }
+      }
+    } else if (SEL == POMCP_SEL_UCB) {
+      int unv = -1;   // mcts.py:539-540: first unvisited child
+#pragma unroll
+      for (int q = kMaxA - 1; q >= 0; --q)
+        if (q < A && st[q].x == 0u) unv = q;
+      if (unv >= 0) {
+        a = unv;
+      } else {
+        const double log_n = p.logtab[nv < p.logtab_n ? nv : 0];
+        if (nv >= p.logtab_n) err = POMCP_E_ARENA;
+        double best = -__builtin_inf();
+#pragma unroll
+        for (int q = 0; q < kMaxA; ++q) {
+          if (q < A) {   // mcts.py:541-542, strict '>' in action order
+            const double s = normalize(hilo_d(st[q].z, st[q].w)) +
+                             p.c * sqrt(log_n / (double)(int)st[q].x);
+            if (s > best) {
+              best = s;
+              a = q;
+            }
+          }
+        }
+      }
+    } else {   // PUCB, mcts.py:502-527
+      const double noise = 1.0 / (double)A;
+      const double prior = (1.0 / (double)A) * (1.0 - p.pucb_f) + p.pucb_f * noise;
+      const double sqrt_n = sqrt((double)nv);
+      double best = -__builtin_inf();
+#pragma unroll
+      for (int q = 0; q < kMaxA; ++q) {
+        if (q < A) {
+          const int n = (int)st[q].x;
+          const double s = (n > 0 ? normalize(hilo_d(st[q].z, st[q].w)) : 0.0) +
+                           p.c * prior * (sqrt_n / (double)(1 + n));
+          if (s > best) {
+            best = s;
+            a = q;
+          }
+        }
+      }
+    }
+    return a;
+  };
+
   int phase = TP_START, sims = 0, max_depth = 0;
   int t = 0, depth = 0, plen = 0, blk = 0, nvis = 0, k = 0, rdepth = 0;
   uint32_t s0 = 0, s1 = 0;
-  int32_t* leaf_ptr = nullptr;
+  int32_t* leaf_ptr = nullptr;   // where a leaf child's block index goes (HBM) ...
+  int leaf_rc = -1;              // ... or its root-cache slot part (LDS)
   double ret = 0.0;
-  PathEntry rpath[kRegPath];   // levels 0..kRegPath-1 of the running simulation
+  uint4 pf = make_uint4(0, 0, 0, 0);   // belief particle of the next simulation
+  // the root level of the running simulation: {a | done << 31, visits before},
+  // r, value before; {total, agg} before (HBM load, consumed by the backup)
+  int r0_on = 0;
+  uint32_t r0_a = 0, r0_vis = 0;
+  double r0_r = 0.0, r0_val = 0.0;
+  uint4 r0_s1 = make_uint4(0, 0, 0, 0);
+  PathEntry rpath[kRegPath];     // levels 1..kRegPath
 
   if (!valid || err != 0 || root_abs) phase = TP_DONE;   // mcts.py:270-272
   if (phase != TP_DONE && h->root_t == 0) {
@@ -112,10 +209,102 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
     }
   }
   if (num_sims <= 0) phase = TP_DONE;
+  const bool cached = phase != TP_DONE;   // this lane's root block is in rc[][lid]
+  const uint4* const rb = reinterpret_cast<const uint4*>(an + (int64_t)(cached ? root_blk : 0) * blk_bytes);
+  if (cached) {
+#pragma unroll
+    for (int a = 0; a < kMaxA; ++a) {
+      if (a < A) {
+        rc[rc_stats(a)][lid] = rb[a];
+#pragma unroll
+        for (int q = 0; q < kSlots; ++q) rc[rc_slot(a, q)][lid] = rb[part_slot(a, q)];
+      }
+    }
+    pf = rbel[d_belief((uint32_t)bsize)];   // the first simulation's particle
+  }
 
-  // Arrival at an obs node (start of _simulate, mcts.py:315-328): depth/step
-  // cutoff -> back up 0; unexpanded -> expand and roll out; else select there.
-  auto arrive = [&]() {
+  // Overflow children (beyond the kSlots inline ones) of action node ani.
+  auto ovf_child = [&](uint32_t ani, uint64_t okey, int done, uint32_t* cid, int* cblk, int* cvis,
+                       int32_t** cptr) {
+    const uint64_t key = okey | ((uint64_t)epoch << kEpochShift);
+    uint32_t b = ovf_hash(ani, okey) & p.bucket_mask;
+    bool found = false;
+    for (uint32_t probe = 0; probe <= p.bucket_mask && !found; ++probe) {
+      ++c_probes;
+      for (int e = 0; e < kBucket; ++e) {
+        OvfSlot* ep = ovf + (int64_t)b * kBucket + e;
+        const uint4 w0 = reinterpret_cast<const uint4*>(ep)[0];
+        const uint64_t skey = (uint64_t)w0.x | ((uint64_t)w0.y << 32);
+        const bool live = (uint32_t)(skey >> kEpochShift) == (uint32_t)epoch;
+        if (!live || (skey == key && w0.z == ani)) {
+          if (live) {
+            const uint4 w1 = reinterpret_cast<const uint4*>(ep)[1];
+            *cblk = (int)w1.x;
+            *cvis = (int)w1.y + 1;
+          } else {
+            ++n_nodes;
+          }
+          reinterpret_cast<uint4*>(ep)[0] =
+              make_uint4((uint32_t)key, (uint32_t)(key >> 32), ani, (uint32_t)done);
+          reinterpret_cast<uint4*>(ep)[1] = make_uint4((uint32_t)*cblk, (uint32_t)*cvis, 0u, 0u);
+          *cid = p.ovf_base + b * kBucket + (uint32_t)e;
+          *cptr = &ep->block;
+          found = true;
+          break;
+        }
+      }
+      b = (b + 1) & p.bucket_mask;
+    }
+    if (!found) err = POMCP_E_ARENA;
+  };
+
+  // The generative step of one tree level (mcts.py:331-352) for ego action a.
+  auto tree_step = [&](int a, uint32_t* n0, uint32_t* n1, double* r, int* done, uint64_t* okey) {
+    const uint32_t ao = d_act(p.other, (uint32_t)A);   // mcts.py:331
+    const uint32_t j = d_model(2);                     // exec-order shuffle
+    drv_step2_vec(sm, s0, s1, p.ego == 0 ? (uint32_t)a : ao, p.ego == 0 ? ao : (uint32_t)a, j,
+                  n0, n1);
+    const uint32_t e0 = p.ego == 0 ? s0 : s1;
+    const uint32_t e1 = p.ego == 0 ? *n0 : *n1;
+    const uint32_t o1 = p.ego == 0 ? *n1 : *n0;
+    *r = drv_reward_vec(sm, e0, e1);
+    *done = (((e1 >> 15) & 3u) != 0u ||
+             (((*n0 >> 15) & 3u) != 0u && ((*n1 >> 15) & 3u) != 0u)) ? 1 : 0;
+    *okey = obs_key_vec(sm, e1, o1);
+  };
+
+  // ActionNode.children[obs] among the inline slots (mcts.py:356-370): filled
+  // in order, so the first invalid slot is the insertion point.  -1: all taken.
+  auto find_slot = [&](const uint4 (&sl)[kSlots], uint64_t okey, bool* match) -> int {
+    int ks = -1;
+    *match = false;
+#pragma unroll
+    for (int q = kSlots - 1; q >= 0; --q) {
+      const uint64_t sk = (uint64_t)sl[q].x | ((uint64_t)sl[q].y << 32);
+      const bool vb = (sk & kValidBit) != 0;
+      if (!vb || (sk & kObsMask) == okey) {
+        ks = q;
+        *match = vb;
+      }
+    }
+    return ks;
+  };
+
+  // Descend into the child (mcts.py:371-376): arrival at an obs node (start of
+  // _simulate, mcts.py:315-328): depth/step cutoff -> back up 0; unexpanded ->
+  // expand and roll out; else select there (next LEVEL).
+  auto descend = [&](int done, int cblk, int cvis, uint32_t n0, uint32_t n1) {
+    if (done) {
+      ret = 0.0;
+      phase = TP_BACKUP;
+      return;
+    }
+    blk = cblk;
+    nvis = cvis;
+    s0 = n0;
+    s1 = n1;
+    ++t;
+    ++depth;
     if (depth > p.depth_limit || t > p.step_limit) {   // mcts.py:315
       ret = 0.0;
       phase = TP_BACKUP;
@@ -124,147 +313,119 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
       if (b < 0) {
         phase = TP_DONE;
       } else {
-        *leaf_ptr = b;
+        if (leaf_rc >= 0) rc[leaf_rc][lid].z = (uint32_t)b;
+        else *leaf_ptr = b;
         ret = 0.0;
         k = 0;
         rdepth = depth;   // the rollout's own depth counter (mcts.py:449)
         phase = TP_ROLL;
       }
+    } else {
+      phase = TP_LEVEL;
     }
   };
 
   while (phase != TP_DONE) {
-    // ------------------------------------------------------ start a simulation
+    // ------------------------------------- start a simulation + the root level
     if (phase == TP_START) {
       if (sims >= num_sims) {
         phase = TP_DONE;
       } else {
-        const uint4 pr = rbel[d_belief((uint32_t)bsize)];   // belief.py:55
+        const uint4 pr = pf;                                     // belief.py:55
+        if (sims + 1 < num_sims) pf = rbel[d_belief((uint32_t)bsize)];
         t = (int)pr.x;
         s0 = pr.y;
         s1 = pr.z;
-        blk = root_blk;
-        nvis = root_visits;
         depth = 0;
         plen = 0;
-        phase = TP_LEVEL;
-        arrive();
+        r0_on = 0;
+        if (0 > p.depth_limit || t > p.step_limit) {            // mcts.py:315
+          ret = 0.0;
+          phase = TP_BACKUP;
+        } else {
+          uint4 st[kMaxA];
+#pragma unroll
+          for (int q = 0; q < kMaxA; ++q) st[q] = q < A ? rc[rc_stats(q)][lid] : make_uint4(0, 0, 0, 0);
+          const int a = select_action(st, root_visits);
+          uint4 sa = st[0];
+          uint4 sl[kSlots];
+#pragma unroll
+          for (int q = 1; q < kMaxA; ++q)
+            if (q == a) sa = st[q];
+#pragma unroll
+          for (int q = 0; q < kSlots; ++q) sl[q] = rc[rc_slot(a, q)][lid];
+          r0_s1 = rb[part_stats1(a)];   // no wait: consumed by the backup
+          uint32_t n0, n1;
+          double r;
+          int done;
+          uint64_t okey;
+          tree_step(a, &n0, &n1, &r, &done, &okey);
+          bool match;
+          const int ks = find_slot(sl, okey, &match);
+          const uint32_t ani = (uint32_t)(root_blk * A + a);
+          uint32_t cid = 0;
+          int cblk = -1, cvis = 1;
+          if (ks >= 0) {
+            uint4 sk = sl[0];
+#pragma unroll
+            for (int q = 1; q < kSlots; ++q)
+              if (q == ks) sk = sl[q];
+            if (match) {
+              cblk = (int)sk.z;
+              cvis = (int)sk.w + 1;
+            } else {
+              ++n_nodes;
+            }
+            const uint64_t nk = okey | kValidBit | ((uint64_t)done << 63);
+            rc[rc_slot(a, ks)][lid] = make_uint4((uint32_t)nk, (uint32_t)(nk >> 32), (uint32_t)cblk, (uint32_t)cvis);
+            cid = ani * kSlots + (uint32_t)ks + 1u;
+            leaf_rc = rc_slot(a, ks);
+          } else {
+            ovf_child(ani, okey, done, &cid, &cblk, &cvis, &leaf_ptr);
+            leaf_rc = -1;
+          }
+          if (err != 0 || n_log >= p.Np) {
+            if (err == 0) err = POMCP_E_ARENA;
+            phase = TP_DONE;
+          } else {
+            plog[n_log++] = LogRec{cid, n0, n1};   // mcts.py:371 (t + 1: see LogRec)
+            r0_on = 1;
+            r0_a = (uint32_t)a | ((uint32_t)done << 31);
+            r0_vis = sa.x;
+            r0_r = r;
+            r0_val = hilo_d(sa.z, sa.w);
+            descend(done, cblk, cvis, n0, n1);
+          }
+        }
       }
     }
-    // ------------------------------------------------------ one tree level
+    // ------------------------------------------------- one level below the root
     if (phase == TP_LEVEL) {
-      char* const bp = an + (int64_t)blk * blk_bytes;
+      const uint4* const ap = reinterpret_cast<const uint4*>(an + (int64_t)blk * blk_bytes);
       uint4 st[kMaxA];
 #pragma unroll
-      for (int a = 0; a < kMaxA; ++a)
-        st[a] = a < A ? reinterpret_cast<const uint4*>(bp)[a] : make_uint4(0, 0, 0, 0);
-      // _search_action_selection (mcts.py:492-563)
-      int a = 0;
-      if (SEL == POMCP_SEL_PUCB && nvis == 0) {   // random.choices over the uniform prior
-        const double w = 1.0 / (double)A;
-        double total = w;
-        for (int q = 1; q < A; ++q) total = total + w;
-        const double x = uniform_float(philox_word(seed, tkey, S_SELECT, c_sel++)) * (total + 0.0);
-        double acc = w;
-        a = A - 1;
-        for (int q = 0; q < A - 1; ++q) {
-          if (x < acc) {
-            a = q;
-            break;
-          }
-          acc = acc + w;
-        }
-      } else if (nvis == 0) {
-        a = (int)d_select((uint32_t)A);
-      } else if (SEL == POMCP_SEL_UNIFORM) {   // min_visit_action_selection
-        int min_n = nvis + 1;
-#pragma unroll
-        for (int q = 0; q < kMaxA; ++q) {
-          if (q < A && (int)st[q].x < min_n) {
-            min_n = (int)st[q].x;
-            a = q;
-          }
-        }
-      } else if (SEL == POMCP_SEL_UCB) {
-        int unv = -1;   // mcts.py:539-540: first unvisited child
-#pragma unroll
-        for (int q = kMaxA - 1; q >= 0; --q)
-          if (q < A && st[q].x == 0u) unv = q;
-        if (unv >= 0) {
-          a = unv;
-        } else {
-          const double log_n = p.logtab[nvis < p.logtab_n ? nvis : 0];
-          if (nvis >= p.logtab_n) err = POMCP_E_ARENA;
-          double best = -__builtin_inf();
-#pragma unroll
-          for (int q = 0; q < kMaxA; ++q) {
-            if (q < A) {   // mcts.py:541-542, strict '>' in action order
-              const double s = normalize(hilo_d(st[q].z, st[q].w)) +
-                               p.c * sqrt(log_n / (double)(int)st[q].x);
-              if (s > best) {
-                best = s;
-                a = q;
-              }
-            }
-          }
-        }
-      } else {   // PUCB, mcts.py:502-527
-        const double noise = 1.0 / (double)A;
-        const double prior = (1.0 / (double)A) * (1.0 - p.pucb_f) + p.pucb_f * noise;
-        const double sqrt_n = sqrt((double)nvis);
-        double best = -__builtin_inf();
-#pragma unroll
-        for (int q = 0; q < kMaxA; ++q) {
-          if (q < A) {
-            const int n = (int)st[q].x;
-            const double s = (n > 0 ? normalize(hilo_d(st[q].z, st[q].w)) : 0.0) +
-                             p.c * prior * (sqrt_n / (double)(1 + n));
-            if (s > best) {
-              best = s;
-              a = q;
-            }
-          }
-        }
-      }
+      for (int q = 0; q < kMaxA; ++q) st[q] = q < A ? ap[q] : make_uint4(0, 0, 0, 0);
+      const int a = select_action(st, nvis);
       uint4 sa = st[0];
 #pragma unroll
       for (int q = 1; q < kMaxA; ++q)
         if (q == a) sa = st[q];
       // the chosen action's stats1 and child slots (second round trip)
-      const uint4* const ap = reinterpret_cast<const uint4*>(bp);
       const uint4 s1a = ap[part_stats1(a)];
       uint4 sl[kSlots];
 #pragma unroll
       for (int q = 0; q < kSlots; ++q) sl[q] = ap[part_slot(a, q)];
-      const uint32_t ao = d_act(p.other, (uint32_t)A);   // mcts.py:331
-      const uint32_t j = d_model(2);                     // exec-order shuffle
       uint32_t n0, n1;
-      drv_step2_vec(sm, s0, s1, p.ego == 0 ? (uint32_t)a : ao, p.ego == 0 ? ao : (uint32_t)a, j,
-                    &n0, &n1);
-      const uint32_t e0 = p.ego == 0 ? s0 : s1;
-      const uint32_t e1 = p.ego == 0 ? n0 : n1;
-      const uint32_t o1 = p.ego == 0 ? n1 : n0;
-      const double r = drv_reward_vec(sm, e0, e1);
-      const int done = (((e1 >> 15) & 3u) != 0u ||
-                        (((n0 >> 15) & 3u) != 0u && ((n1 >> 15) & 3u) != 0u)) ? 1 : 0;
-      const uint64_t okey = obs_key_vec(sm, e1, o1);
-      // ActionNode.children[obs] among the inline slots (mcts.py:356-370):
-      // filled in order, so the first invalid slot is the insertion point
-      int ks = -1;
-      bool match = false;
-#pragma unroll
-      for (int q = kSlots - 1; q >= 0; --q) {
-        const uint64_t sk = (uint64_t)sl[q].x | ((uint64_t)sl[q].y << 32);
-        const bool vb = (sk & kValidBit) != 0;
-        if (!vb || (sk & kObsMask) == okey) {
-          ks = q;
-          match = vb;
-        }
-      }
+      double r;
+      int done;
+      uint64_t okey;
+      tree_step(a, &n0, &n1, &r, &done, &okey);
+      bool match;
+      const int ks = find_slot(sl, okey, &match);
       const uint32_t ani = (uint32_t)(blk * A + a);
       uint32_t cid = 0;
       int cblk = -1, cvis = 1;
-      int32_t* cptr = nullptr;
+      leaf_rc = -1;
       if (ks >= 0) {
         uint4 sk = sl[0];
 #pragma unroll
@@ -280,39 +441,9 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
         uint4* slot = const_cast<uint4*>(ap) + part_slot(a, ks);
         *slot = make_uint4((uint32_t)nk, (uint32_t)(nk >> 32), (uint32_t)cblk, (uint32_t)cvis);
         cid = ani * kSlots + (uint32_t)ks + 1u;
-        cptr = reinterpret_cast<int32_t*>(slot) + 2;
+        leaf_ptr = reinterpret_cast<int32_t*>(slot) + 2;
       } else {
-        // overflow map: open addressing over 16-entry buckets
-        const uint64_t key = okey | ((uint64_t)epoch << kEpochShift);
-        uint32_t b = ovf_hash(ani, okey) & p.bucket_mask;
-        bool found = false;
-        for (uint32_t probe = 0; probe <= p.bucket_mask && !found; ++probe) {
-          ++c_probes;
-          for (int e = 0; e < kBucket; ++e) {
-            OvfSlot* ep = ovf + (int64_t)b * kBucket + e;
-            const uint4 w0 = reinterpret_cast<const uint4*>(ep)[0];
-            const uint64_t skey = (uint64_t)w0.x | ((uint64_t)w0.y << 32);
-            const bool live = (uint32_t)(skey >> kEpochShift) == (uint32_t)epoch;
-            if (!live || (skey == key && w0.z == ani)) {
-              if (live) {
-                const uint4 w1 = reinterpret_cast<const uint4*>(ep)[1];
-                cblk = (int)w1.x;
-                cvis = (int)w1.y + 1;
-              } else {
-                ++n_nodes;
-              }
-              reinterpret_cast<uint4*>(ep)[0] =
-                  make_uint4((uint32_t)key, (uint32_t)(key >> 32), ani, (uint32_t)done);
-              reinterpret_cast<uint4*>(ep)[1] = make_uint4((uint32_t)cblk, (uint32_t)cvis, 0u, 0u);
-              cid = p.ovf_base + b * kBucket + (uint32_t)e;
-              cptr = &ep->block;
-              found = true;
-              break;
-            }
-          }
-          b = (b + 1) & p.bucket_mask;
-        }
-        if (!found) err = POMCP_E_ARENA;
+        ovf_child(ani, okey, done, &cid, &cblk, &cvis, &leaf_ptr);
       }
       if (err != 0 || n_log >= p.Np || plen >= kMaxPath) {
         if (err == 0) err = POMCP_E_ARENA;
@@ -333,23 +464,11 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
           path[plen] = pe;
         }
         ++plen;
-        if (done) {
-          ret = 0.0;
-          phase = TP_BACKUP;
-        } else {
-          blk = cblk;
-          nvis = cvis;
-          leaf_ptr = cptr;
-          s0 = n0;
-          s1 = n1;
-          ++t;
-          ++depth;
-          arrive();
-        }
+        descend(done, cblk, cvis, n0, n1);
       }
     }
-    // ------------------------------------------------------ one rollout step
-    if (phase == TP_ROLL) {                                  // mcts.py:414-450
+    // ------------------------------------------------------ the rollout
+    while (phase == TP_ROLL) {                               // mcts.py:414-450
       if (!(rdepth <= p.depth_limit && t <= p.step_limit)) {
         phase = TP_BACKUP;
       } else {
@@ -396,8 +515,9 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
         *reinterpret_cast<uint4*>(an + (e0.x & 0x7FFFFFFFu)) =
             make_uint4((uint32_t)n, 0u, (uint32_t)__double2loint(value),
                        (uint32_t)__double2hiint(value));
-        *reinterpret_cast<uint4*>(an + e2.z) = make_uint4((uint32_t)__double2loint(total), (uint32_t)__double2hiint(total),
-                           (uint32_t)__double2loint(agg), (uint32_t)__double2hiint(agg));
+        *reinterpret_cast<uint4*>(an + e2.z) = make_uint4(
+            (uint32_t)__double2loint(total), (uint32_t)__double2hiint(total),
+            (uint32_t)__double2loint(agg), (uint32_t)__double2hiint(agg));
         if (value > mm_max) mm_max = value;   // utils.py:29-32
         if (value < mm_min) mm_min = value;
       };
@@ -405,6 +525,22 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
 #pragma unroll
       for (int l = kRegPath - 1; l >= 0; --l)
         if (l < plen) level(rpath[l]);
+      if (r0_on) {   // the root level: stats0 in LDS, stats1 in HBM
+        const int a = (int)(r0_a & 0x7FFFFFFFu);
+        gr = (r0_a >> 31) ? r0_r : r0_r + p.discount * gr;
+        const int n = (int)r0_vis + 1;
+        const double total = hilo_d(r0_s1.x, r0_s1.y) + gr;
+        const double delta = gr - r0_val;
+        const double value = r0_val + delta / (double)n;
+        const double agg = hilo_d(r0_s1.z, r0_s1.w) + delta * (gr - value);
+        rc[rc_stats(a)][lid] = make_uint4((uint32_t)n, 0u, (uint32_t)__double2loint(value),
+                                          (uint32_t)__double2hiint(value));
+        const_cast<uint4*>(rb)[part_stats1(a)] = make_uint4(
+            (uint32_t)__double2loint(total), (uint32_t)__double2hiint(total),
+            (uint32_t)__double2loint(agg), (uint32_t)__double2hiint(agg));
+        if (value > mm_max) mm_max = value;
+        if (value < mm_min) mm_min = value;
+      }
       ++root_visits;                                          // mcts.py:288
       max_depth = depth > max_depth ? depth : max_depth;
       ++sims;
@@ -414,6 +550,16 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
 
   // ------------------------------------------------------------------ results
   if (!valid) return;
+  if (cached) {   // write the root block back
+#pragma unroll
+    for (int a = 0; a < kMaxA; ++a) {
+      if (a < A) {
+        const_cast<uint4*>(rb)[a] = rc[rc_stats(a)][lid];
+#pragma unroll
+        for (int q = 0; q < kSlots; ++q) const_cast<uint4*>(rb)[part_slot(a, q)] = rc[rc_slot(a, q)][lid];
+      }
+    }
+  }
   const bool have = err == 0 && !root_abs && root_blk >= 0;
   uint4 st[kMaxA], s1s[kMaxA];
 #pragma unroll
@@ -421,7 +567,8 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
     st[a] = make_uint4(0, 0, 0, 0);
     s1s[a] = st[a];
     if (have && a < A) {
-      st[a] = reinterpret_cast<const uint4*>(an + (int64_t)root_blk * blk_bytes)[a];
+      st[a] = cached ? rc[rc_stats(a)][lid]
+                     : reinterpret_cast<const uint4*>(an + (int64_t)root_blk * blk_bytes)[a];
       s1s[a] = reinterpret_cast<const uint4*>(an + (int64_t)root_blk * blk_bytes)[part_stats1(a)];
     }
   }
@@ -514,8 +661,8 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
   so->pad = 0;
 }
 
-template __global__ void k_search<POMCP_SEL_PUCB>(DevParams, int);
-template __global__ void k_search<POMCP_SEL_UCB>(DevParams, int);
-template __global__ void k_search<POMCP_SEL_UNIFORM>(DevParams, int);
+template __global__ void k_search<POMCP_SEL_PUCB>(DevParams, int, int);
+template __global__ void k_search<POMCP_SEL_UCB>(DevParams, int, int);
+template __global__ void k_search<POMCP_SEL_UNIFORM>(DevParams, int, int);
 
 }  // namespace pb
