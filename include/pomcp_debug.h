@@ -8,6 +8,12 @@ extern "C" {
 /* out[4*i + k] = {sqrt(a), a / b, a + 0.95 * b, (a - b) / (a + b)} computed on
  * device 0 in FP64 (checks the device FP64 path is correctly rounded). */
 int pomcp_debug_fp_selftest(const double* a, const double* b, int32_t n, double* out);
+/* k_search phase cycles per wave, [waves][8] (libpomcp_hip built with
+ * -DPOMCP_PHASE_TIMING; POMCP_E_UNSUPPORTED otherwise).  The first call
+ * enables collection (count = 0); later calls copy the last search's values
+ * when capacity >= count. */
+typedef struct pomcp_ctx pomcp_ctx;
+int pomcp_debug_phase_timing(pomcp_ctx* ctx, uint64_t* out, int32_t capacity, int32_t* count);
 #ifdef __cplusplus
 }
 #endif

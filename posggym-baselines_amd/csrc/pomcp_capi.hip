@@ -70,17 +70,8 @@ static int dev_alloc(pomcp_ctx* ctx, void** out, size_t bytes) {
 }
 
 static unsigned grid_blocks(int B) { return (unsigned)((B + kTreesPerBlock - 1) / kTreesPerBlock); }
-// Trees per wavefront of k_search (64 = one tree per lane; POMCP_TREES_PER_WAVE
-// = 32 / 16 leave lanes idle so that more waves share each SIMD).
-static int search_tpw() {
-  const char* e = std::getenv("POMCP_TREES_PER_WAVE");
-  const int v = e ? std::atoi(e) : 64;
-  return (v == 16 || v == 32) ? v : 64;
-}
-static unsigned search_blocks(int B, int tpw) {
-  const int per_block = tpw * (kTPB / kWave);
-  return (unsigned)((B + per_block - 1) / per_block);
-}
+static unsigned search_blocks(int B) { return (unsigned)((B + kTPB - 1) / kTPB); }
+static int search_waves(int B) { return (B + kWave - 1) / kWave; }
 
 extern "C" {
 
@@ -119,7 +110,9 @@ static int validate(const pomcp_config* c, std::string* why) {
   if (c->num_trees < 1) return bad("num_trees >= 1");
   if (c->max_blocks < 1 || c->max_blocks * (c->num_actions + 1) * 128 > INT32_MAX) return bad("max_blocks");
   if (c->num_actions > kMaxA) { *why = "the search kernel supports at most 5 actions"; return POMCP_E_UNSUPPORTED; }
-  if (c->max_particles < 1 || c->max_particles > INT32_MAX) return bad("max_particles");
+  if (c->max_particles < 1 || c->max_particles * kWave > UINT32_MAX) return bad("max_particles");
+  if (c->max_blocks * c->num_actions * kSlots + 1 + c->overflow_slots >= (int64_t)kIdMask)
+    return bad("obs node ids exceed 2^26 (max_blocks * A * 6 + overflow_slots)");
   if (c->max_belief < 2 * (c->num_particles + c->extra_particles)) return bad("max_belief too small");
   if (c->overflow_slots < kBucket || (c->overflow_slots & (c->overflow_slots - 1)) != 0 ||
       c->overflow_slots > (1ll << 28))
@@ -204,7 +197,10 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
   ALLOC(hdr, TreeHdr, B);
   ALLOC(an, Line, B * d.Nb * blk_lines(d.A));
   ALLOC(ovf, OvfSlot, B * d.H);
-  ALLOC(plog, LogRec, B * d.Np);
+  ALLOC(plog, LogRec, (int64_t)search_waves((int)B) * kWave * d.Np);
+  ALLOC(wlog, uint32_t, search_waves((int)B));
+  ALLOC(want, uint32_t, B);
+  ALLOC(cnt, int32_t, B);
   ALLOC(belief, uint4, B * 2 * d.Nr);
   ALLOC(path, uint4, B * 3 * kMaxPath);
   ALLOC(logtab, double, c.log_table_size);
@@ -312,6 +308,13 @@ int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_key
                               hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(ctx, hipMemcpyAsync((void*)ctx->dp.in_obs, obs_keys, sizeof(uint64_t) * B,
                               hipMemcpyHostToDevice, ctx->stream));
+  // re-root: child lookup per tree, one ordered scan of each search wave's log,
+  // then the per-tree update (initial belief / re-root + reinvigoration)
+  hipLaunchKernelGGL(k_reroot_child, dim3(grid_blocks(B)), dim3(256), 0, ctx->stream, ctx->dp);
+  HIP_TRY(ctx, hipGetLastError());
+  hipLaunchKernelGGL(k_extract, dim3(grid_blocks(search_waves(B))), dim3(256), 0, ctx->stream,
+                     ctx->dp);
+  HIP_TRY(ctx, hipGetLastError());
   hipLaunchKernelGGL(k_update, dim3(grid_blocks(B)), dim3(256), 0, ctx->stream, ctx->dp);
   HIP_TRY(ctx, hipGetLastError());
   HIP_TRY(ctx, hipMemcpyAsync(ctx->host_upd.data(), ctx->dp.upd_out, sizeof(int32_t) * 2 * B,
@@ -325,18 +328,17 @@ int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_key
 int pomcp_search(pomcp_ctx* ctx, int32_t num_sims, int32_t* actions_out) {
   if (!ctx || num_sims < 0) return POMCP_E_INVALID;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
-  const int tpw = search_tpw();
-  const dim3 grid(search_blocks(ctx->dp.B, tpw)), block(kTPB);
+  const dim3 grid(search_blocks(ctx->dp.B)), block(kTPB);
   switch (ctx->dp.sel) {
     case POMCP_SEL_PUCB:
-      hipLaunchKernelGGL(k_search<POMCP_SEL_PUCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims, tpw);
+      hipLaunchKernelGGL(k_search<POMCP_SEL_PUCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims);
       break;
     case POMCP_SEL_UCB:
-      hipLaunchKernelGGL(k_search<POMCP_SEL_UCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims, tpw);
+      hipLaunchKernelGGL(k_search<POMCP_SEL_UCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims);
       break;
     default:
       hipLaunchKernelGGL(k_search<POMCP_SEL_UNIFORM>, grid, block, 0, ctx->stream, ctx->dp,
-                         (int)num_sims, tpw);
+                         (int)num_sims);
   }
   HIP_TRY(ctx, hipGetLastError());
   if (!actions_out) return POMCP_OK;
@@ -521,6 +523,35 @@ int pomcp_debug_fp_selftest(const double* a, const double* b, int32_t n, double*
   (void)hipFree(db);
   (void)hipFree(dout);
   return e == hipSuccess ? POMCP_OK : POMCP_E_HIP;
+}
+
+// Debug: per-wave phase cycles of k_search (diagnostics build only).
+int pomcp_debug_phase_timing(pomcp_ctx* ctx, uint64_t* out, int32_t capacity, int32_t* count) {
+  if (!ctx || !count) return POMCP_E_INVALID;
+#ifndef POMCP_PHASE_TIMING
+  (void)out;
+  (void)capacity;
+  *count = 0;
+  return POMCP_E_UNSUPPORTED;
+#else
+  const int per_block = kTPB / kWave;
+  const int64_t waves = (int64_t)search_blocks(ctx->dp.B) * per_block;
+  if (ctx->dp.timing == nullptr) {   // first call: allocate; the next search fills it
+    void* p = nullptr;
+    if (dev_alloc(ctx, &p, sizeof(uint64_t) * 8 * (size_t)waves) != POMCP_OK) return POMCP_E_HIP;
+    HIP_TRY(ctx, hipMemset(p, 0, sizeof(uint64_t) * 8 * (size_t)waves));
+    ctx->dp.timing = reinterpret_cast<uint64_t*>(p);
+    *count = 0;
+    return POMCP_OK;
+  }
+  *count = (int32_t)(8 * waves);
+  if (out && capacity >= *count) {
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipMemcpy(out, ctx->dp.timing, sizeof(uint64_t) * 8 * (size_t)waves,
+                           hipMemcpyDeviceToHost));
+  }
+  return POMCP_OK;
+#endif
 }
 
 }  // extern "C"

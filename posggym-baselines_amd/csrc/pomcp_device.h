@@ -45,11 +45,19 @@ struct ChildSlot {
   int32_t visits;   // ObsNode.visits
 };
 // Particle log record (ObsNode.belief.add_particle, mcts.py:371): the particle
-// (v0, v1) entered obs node `id`.  Its time step is not stored: every particle
-// of a node has the same t (the root's particles have t = root_t, a node at
-// depth d below it t = root_t + d), so re-rooting restores it as root_t + 1.
+// (v0, v1) entered obs node `id` of the tree in lane `lane` of the search wave.
+// Its time step is not stored: every particle of a node has the same t (the
+// root's particles have t = root_t, a node at depth d below it t = root_t + d),
+// so re-rooting restores it as root_t + 1.
+// The log is shared by the 64 trees of a search wavefront (one tree per lane):
+// the lanes appending in one step write consecutive records, so one store
+// instruction writes whole lines instead of 64 scattered 12 B pieces.  A
+// tree's records keep their insertion order; k_extract separates them again.
+constexpr int kIdBits = 26;                       // obs node ids < 2^26 (pomcp_create checks)
+constexpr uint32_t kIdMask = (1u << kIdBits) - 1u;
 struct LogRec {
-  uint32_t id, v0, v1;
+  uint32_t id;      // obs node id | lane << kIdBits
+  uint32_t v0, v1;
 };
 
 struct alignas(16) Line {   // allocation unit of the block arena
@@ -93,7 +101,10 @@ struct DevParams {
   TreeHdr* hdr;
   Line* an;             // [B][Nb][A + 1] action blocks
   OvfSlot* ovf;         // [B][H]
-  LogRec* plog;         // [B][Np] particle log {obs node id, v0, v1}
+  LogRec* plog;         // [waves][64 * Np] per-search-wave particle log
+  uint32_t* wlog;       // [waves] records in each wave's log
+  uint32_t* want;       // [B] re-root: log id of the child to extract (0xFFFFFFFF: none)
+  int32_t* cnt;         // [B] re-root: particles extracted into the new root belief
   uint4* belief;        // [B][2][Nr] {t, v0, v1, 0}
   uint4* path;          // [B][3 * kMaxPath] search path of the running simulation
   const double* logtab;
@@ -107,6 +118,7 @@ struct DevParams {
   const int32_t* in_actions;
   const uint64_t* in_obs;
   uint64_t* out_obs;
+  uint64_t* timing;     // [waves][8] phase cycles (diagnostics build only), may be null
 };
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }

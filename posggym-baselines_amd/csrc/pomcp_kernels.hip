@@ -54,7 +54,6 @@ struct Tree {
   int tree, lane;
   Line* an;
   OvfSlot* ovf;
-  LogRec* plog;
   uint4* bel;
   int n_blocks, n_log, n_nodes, err, bsize, bsel, epoch, root_t;
   uint32_t root_id;
@@ -70,7 +69,6 @@ struct Tree {
     lane = lane_id();
     an = p.an + (int64_t)t * p.Nb * blk_lines(p.A);
     ovf = p.ovf + (int64_t)t * p.H;
-    plog = p.plog + (int64_t)t * p.Np;
     bel = p.belief + (int64_t)t * 2 * p.Nr;
     const TreeHdr h = p.hdr[t];
     n_blocks = uni(h.n_blocks);
@@ -355,6 +353,7 @@ __global__ __launch_bounds__(256) void k_reset(DevParams p) {
     clear_ovf(p, tree, lane);
     epoch = 1;
   }
+  if (lane == 0 && (tree & (kWave - 1)) == 0) p.wlog[tree / kWave] = 0u;
   if (lane == 0) {
     h.n_blocks = 0;
     h.n_log = 0;
@@ -371,6 +370,73 @@ __global__ __launch_bounds__(256) void k_reset(DevParams p) {
     h.mm_min = p.has_kb ? p.kb_min : __builtin_inf();
     p.hdr[tree] = h;
   }
+}
+
+// Re-root, step 1 (MCTS._update, mcts.py:236-247): find or create the root's
+// child (action, obs) and publish its log id for k_extract.
+__global__ __launch_bounds__(256) void k_reroot_child(DevParams p) {
+  __shared__ DrvModel sm;
+  stage_model(p.model, sm);
+  const int tree = blockIdx.x * kTreesPerBlock + (threadIdx.x >> 6);
+  if (tree >= p.B) return;
+  Tree T(p, sm, tree);
+  uint32_t want = 0xFFFFFFFFu;
+  if (T.err == 0 && !T.root_abs && T.root_t > 0) {
+    const int action = uni(p.in_actions[tree]);
+    if (T.root_blk >= 0 && action >= 0 && action < p.A) {
+      uint4 q = T.load_block(T.root_blk);
+      ChildRef c;
+      if (T.child_ref(q, T.root_blk, action, uni64(p.in_obs[tree]), false, T.root_abs, &c))
+        want = c.id | ((uint32_t)(tree & (kWave - 1)) << kIdBits);
+    }
+  }
+  T.store_header();   // child_ref may have created the child (n_nodes)
+  if (T.lane == 0) p.want[tree] = want;
+}
+
+// Re-root, step 2: one wavefront per SEARCH wave scans that wave's shared log
+// once, in order, and appends each record of a wanted child to its tree's new
+// root belief ({root_t + 1, v0, v1}), preserving insertion order per tree.
+__global__ __launch_bounds__(256) void k_extract(DevParams p) {
+  const int sw = blockIdx.x * kTreesPerBlock + (threadIdx.x >> 6);   // search wave
+  const int lane = lane_id();
+  __shared__ uint32_t want[kTreesPerBlock][kWave];
+  __shared__ int32_t cnt[kTreesPerBlock][kWave];
+  __shared__ uint32_t tval[kTreesPerBlock][kWave];
+  __shared__ int64_t dst[kTreesPerBlock][kWave];
+  const int wi = threadIdx.x >> 6;
+  const int nwaves = (p.B + kWave - 1) / kWave;
+  if (sw >= nwaves) return;
+  const int tree = sw * kWave + lane;
+  const bool valid = tree < p.B;
+  const TreeHdr h = p.hdr[valid ? tree : 0];
+  want[wi][lane] = valid ? p.want[tree] : 0xFFFFFFFFu;
+  cnt[wi][lane] = 0;
+  tval[wi][lane] = (uint32_t)h.root_t + 1u;
+  dst[wi][lane] = ((int64_t)tree * 2 + (h.belief_sel ^ 1)) * p.Nr;
+  __builtin_amdgcn_wave_barrier();
+  const LogRec* const wl = p.plog + (int64_t)sw * kWave * p.Np;
+  const uint32_t n = p.wlog[sw];
+  for (uint32_t base = 0; base < n; base += kWave) {
+    const uint32_t i = base + (uint32_t)lane;
+    LogRec r = {0xFFFFFFFFu, 0u, 0u};
+    if (i < n) r = wl[i];
+    const uint32_t l = r.id >> kIdBits;
+    const bool m = i < n && want[wi][l] == r.id;
+    uint64_t mask = __ballot(m);
+    while (mask) {   // matches of this chunk in log order
+      const int j = __ffsll((long long)mask) - 1;
+      mask &= mask - 1ull;
+      const int lj = __builtin_amdgcn_readlane((int)l, j);
+      const int pos = cnt[wi][lj];
+      if (lane == j) {
+        if (pos < p.Nr) p.belief[dst[wi][lj] + pos] = make_uint4(tval[wi][lj], r.v0, r.v1, 0u);
+        cnt[wi][lj] = pos + 1;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  if (valid) p.cnt[tree] = cnt[wi][lane];
 }
 
 __global__ __launch_bounds__(256) void k_update(DevParams p) {
@@ -418,19 +484,10 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
         uint4 q = T.load_block(T.root_blk);
         ChildRef c;
         if (T.child_ref(q, T.root_blk, action, obs, false, T.root_abs, &c)) {
-          // the child's belief: its particles from the log, insertion order
+          // the child's belief: its particles from the log in insertion order,
+          // already gathered into the other belief buffer by k_extract
           uint4* nb = T.other_belief();
-          int n = 0;
-          for (int base = 0; base < T.n_log; base += kWave) {
-            const int i = base + lane;
-            LogRec rec = {0xFFFFFFFFu, 0u, 0u};
-            if (i < T.n_log) rec = T.plog[i];
-            const bool m = i < T.n_log && rec.id == c.id;
-            const uint64_t mask = __ballot(m);
-            const int pos = n + (int)__popcll(mask & ((1ull << lane) - 1ull));
-            if (m && pos < p.Nr) nb[pos] = make_uint4((uint32_t)T.root_t + 1u, rec.v0, rec.v1, 0u);
-            n += (int)__popcll(mask);
-          }
+          int n = uni(p.cnt[tree]);
           if (n > p.Nr) T.err = POMCP_E_ARENA;
           // _reinvigorate (mcts.py:651-700) -> BeliefRejectionSampler (belief.py:145-194)
           const int need = p.n_target - n;
@@ -513,6 +570,7 @@ __global__ __launch_bounds__(256) void k_restore(DevParams p, const TreeHdr* sna
     clear_ovf(p, tree, lane);
     epoch = 1;
   }
+  if (lane == 0 && (tree & (kWave - 1)) == 0) p.wlog[tree / kWave] = 0u;   // snapshot: empty logs
   if (lane == 0) {
     TreeHdr h = snap[tree];
     h.epoch = epoch;

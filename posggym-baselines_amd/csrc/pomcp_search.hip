@@ -52,23 +52,54 @@ struct PathEntry {
   uint4 e0, e1, e2;
 };
 
+// Phase timing (diagnostics build, -DPOMCP_PHASE_TIMING): per-wave s_memtime
+// deltas per loop section into p.timing[wave][8]; each mark first drains every
+// outstanding memory operation, so a section is charged the waits it issued.
+#ifdef POMCP_PHASE_TIMING
+#define PT_MARK(slot)                                          \
+  do {                                                         \
+    __builtin_amdgcn_s_waitcnt(0);                             \
+    const uint64_t pt_now_ = __builtin_amdgcn_s_memtime();     \
+    pt[slot] += pt_now_ - pt_last;                             \
+    pt_last = pt_now_;                                         \
+  } while (0)
+#else
+#define PT_MARK(slot) \
+  do {                \
+  } while (0)
+#endif
+
 enum : int { TP_LEVEL = 0, TP_ROLL = 1, TP_BACKUP = 2, TP_START = 3, TP_DONE = 4 };
 
 template <int SEL>
-__global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims, int tpw) {
+__global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
   __shared__ DrvModel sm;
   __shared__ uint4 rc[kRootParts][kTPB];   // the root block of every lane's tree
   stage_model(p.model, sm);
-  // tpw trees per wavefront (lanes >= tpw idle)
   const int lid = (int)threadIdx.x;
   const int lane = lid & (kWave - 1);
-  const int tree = (int)(blockIdx.x * (kTPB / kWave) + (threadIdx.x >> 6)) * tpw + lane;
-  const bool valid = lane < tpw && tree < p.B;
+  const int wave = (int)(blockIdx.x * (kTPB / kWave) + (threadIdx.x >> 6));
+  const int tree = wave * kWave + lane;
+  const bool valid = tree < p.B;
   const int tt = valid ? tree : 0;
   const int A = p.A;
   char* const an = reinterpret_cast<char*>(p.an + (int64_t)tt * p.Nb * blk_lines(A));
   const int blk_bytes = blk_lines(A) * 128;
-  LogRec* const plog = p.plog + (int64_t)tt * p.Np;
+  // the wave's shared particle log (pomcp_device.h LogRec); wpos is the same in
+  // every lane still in the loop (advanced by ballot at convergent points)
+  LogRec* const wl = p.plog + (int64_t)wave * kWave * p.Np;
+  const uint32_t wpos0 = p.wlog[wave];
+  uint32_t wpos = wpos0;
+  bool app = false;          // this lane has a record to append
+  LogRec rec = {0u, 0u, 0u};
+  auto append = [&]() {      // call where every lane still in the loop is active
+    const uint64_t m = __ballot(app);
+    if (m != 0ull) {
+      if (app) wl[wpos + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = rec;
+      wpos += (uint32_t)__popcll(m);
+      app = false;
+    }
+  };
   OvfSlot* const ovf = p.ovf + (int64_t)tt * p.H;
   PathEntry* const path = reinterpret_cast<PathEntry*>(p.path) + (int64_t)tt * kMaxPath;
   const TreeHdr* const h = p.hdr + tt;
@@ -325,7 +356,12 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims, int 
     }
   };
 
+#ifdef POMCP_PHASE_TIMING
+  uint64_t pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t pt_last = __builtin_amdgcn_s_memtime();
+#endif
   while (phase != TP_DONE) {
+    PT_MARK(7);
     // ------------------------------------- start a simulation + the root level
     if (phase == TP_START) {
       if (sims >= num_sims) {
@@ -388,7 +424,9 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims, int 
             if (err == 0) err = POMCP_E_ARENA;
             phase = TP_DONE;
           } else {
-            plog[n_log++] = LogRec{cid, n0, n1};   // mcts.py:371 (t + 1: see LogRec)
+            rec = LogRec{cid | ((uint32_t)lane << kIdBits), n0, n1};   // mcts.py:371
+            app = true;
+            ++n_log;
             r0_on = 1;
             r0_a = (uint32_t)a | ((uint32_t)done << 31);
             r0_vis = sa.x;
@@ -398,14 +436,18 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims, int 
           }
         }
       }
+      PT_MARK(0);
     }
+    append();
     // ------------------------------------------------- one level below the root
     if (phase == TP_LEVEL) {
       const uint4* const ap = reinterpret_cast<const uint4*>(an + (int64_t)blk * blk_bytes);
       uint4 st[kMaxA];
 #pragma unroll
       for (int q = 0; q < kMaxA; ++q) st[q] = q < A ? ap[q] : make_uint4(0, 0, 0, 0);
+      PT_MARK(1);
       const int a = select_action(st, nvis);
+      PT_MARK(2);
       uint4 sa = st[0];
 #pragma unroll
       for (int q = 1; q < kMaxA; ++q)
@@ -415,6 +457,7 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims, int 
       uint4 sl[kSlots];
 #pragma unroll
       for (int q = 0; q < kSlots; ++q) sl[q] = ap[part_slot(a, q)];
+      PT_MARK(3);
       uint32_t n0, n1;
       double r;
       int done;
@@ -449,7 +492,9 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims, int 
         if (err == 0) err = POMCP_E_ARENA;
         phase = TP_DONE;
       } else {
-        plog[n_log++] = LogRec{cid, n0, n1};   // mcts.py:371 (t + 1: see LogRec)
+        rec = LogRec{cid | ((uint32_t)lane << kIdBits), n0, n1};   // mcts.py:371
+        app = true;
+        ++n_log;
         const uint32_t off = (uint32_t)(blk * blk_bytes + a * 16);
         const PathEntry pe = {
             make_uint4(off | ((uint32_t)done << 31), sa.x, (uint32_t)__double2loint(r),
@@ -466,7 +511,9 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims, int 
         ++plen;
         descend(done, cblk, cvis, n0, n1);
       }
+      PT_MARK(4);
     }
+    append();
     // ------------------------------------------------------ the rollout
     while (phase == TP_ROLL) {                               // mcts.py:414-450
       if (!(rdepth <= p.depth_limit && t <= p.step_limit)) {
@@ -498,6 +545,7 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims, int 
           }
         }
       }
+      PT_MARK(5);
     }
     // ------------------------------------------------------ backup
     if (phase == TP_BACKUP) {                                // mcts.py:374-381
@@ -545,10 +593,22 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims, int 
       max_depth = depth > max_depth ? depth : max_depth;
       ++sims;
       phase = TP_START;
+      PT_MARK(6);
     }
   }
+#ifdef POMCP_PHASE_TIMING
+  if (p.timing != nullptr && (threadIdx.x & (kWave - 1)) == 0) {
+    for (int i = 0; i < 8; ++i) p.timing[wave * 8 + i] = pt[i];
+  }
+#endif
 
   // ------------------------------------------------------------------ results
+  {   // the wave's log length: every lane's appends of this launch
+    uint32_t mine = valid ? (uint32_t)(n_log - log0) : 0u;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) mine += (uint32_t)__shfl_xor((int)mine, o);
+    if (lane == 0) p.wlog[wave] = wpos0 + mine;
+  }
   if (!valid) return;
   if (cached) {   // write the root block back
 #pragma unroll
@@ -661,8 +721,8 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims, int 
   so->pad = 0;
 }
 
-template __global__ void k_search<POMCP_SEL_PUCB>(DevParams, int, int);
-template __global__ void k_search<POMCP_SEL_UCB>(DevParams, int, int);
-template __global__ void k_search<POMCP_SEL_UNIFORM>(DevParams, int, int);
+template __global__ void k_search<POMCP_SEL_PUCB>(DevParams, int);
+template __global__ void k_search<POMCP_SEL_UCB>(DevParams, int);
+template __global__ void k_search<POMCP_SEL_UNIFORM>(DevParams, int);
 
 }  // namespace pb

@@ -146,6 +146,8 @@ SIGNATURES = [
 ]
 DEBUG_SIGNATURES = [
     ("pomcp_debug_fp_selftest", C.c_int, [_PD, _PD, C.c_int32, _PD]),
+    ("pomcp_debug_phase_timing", C.c_int,
+     [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32, C.POINTER(C.c_int32)]),
 ]
 
 _lib = None

@@ -14,7 +14,7 @@ PROJECT = os.path.dirname(PKG)                       # posggym-baselines_amd/
 REPO = os.path.dirname(PROJECT)
 CSRC = os.path.join(PROJECT, "csrc")
 INCLUDE = os.path.join(REPO, "include")
-OUT = os.path.join(PKG, "_lib", "libpomcp_hip.so")
+OUT = os.environ.get("POMCP_LIB_PATH") or os.path.join(PKG, "_lib", "libpomcp_hip.so")
 SOURCES = [os.path.join(CSRC, "pomcp_capi.hip")]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in
                   ("pomcp_kernels.hip", "pomcp_search.hip", "pomcp_device.h", "driving.h",
@@ -25,6 +25,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("POMCP_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC",
          "-shared", f"-I{INCLUDE}", "-Wall", "-Wno-unused-function"]
+# diagnostics builds (e.g. POMCP_EXTRA_FLAGS=-DPOMCP_PHASE_TIMING with a separate
+# POMCP_LIB_PATH); never the default library
+FLAGS += os.environ.get("POMCP_EXTRA_FLAGS", "").split()
 
 
 def up_to_date() -> bool:

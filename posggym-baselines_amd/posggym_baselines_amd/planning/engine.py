@@ -31,8 +31,12 @@ def _next_pow2(n: int) -> int:
     return 1 << max(4, (int(n) - 1).bit_length())
 
 
+ID_LIMIT = (1 << 26) - 1   # obs node ids share a log word with the lane (pomcp_device.h)
+
+
 def plan_capacities(config, step_limit: int, num_sims: int, searches: int = 1,
-                    reroot: bool = True, max_blocks: int = None, overflow_slots: int = None):
+                    reroot: bool = True, max_blocks: int = None, overflow_slots: int = None,
+                    num_actions: int = 5):
     """Worst-case arena sizes for ``searches`` searches of ``num_sims`` each.
 
     Every simulation expands at most one leaf (mcts.py:318-328) and appends one
@@ -44,8 +48,13 @@ def plan_capacities(config, step_limit: int, num_sims: int, searches: int = 1,
     levels = min(config.depth_limit, step_limit) + 1
     n_target = config.num_particles + config.extra_particles
     total = num_sims * searches
-    nb = total + 2 * searches + 16 if max_blocks is None else max_blocks
     ovf = _next_pow2(max(64, total // 8)) if overflow_slots is None else overflow_slots
+    ovf = min(ovf, 1 << 24)
+    if max_blocks is None:
+        # one expansion per simulation at most, within the obs node id space
+        nb = min(total + 2 * searches + 16, (ID_LIMIT - 1 - ovf) // (num_actions * 6))
+    else:
+        nb = max_blocks
     np_ = total * min(levels, 64) + searches * 2 * n_target + 64
     nr = (np_ + 2 * n_target + 64) if reroot else (4 * n_target + 64)
     return Capacities(
@@ -81,7 +90,8 @@ class PomcpEngine:
             sims = num_sims if num_sims is not None else (config.num_sims or 4096)
             budget = searches if searches is not None else (
                 (step_limit if step_limit < INT32_MAX else 100) + 1)
-            capacities = plan_capacities(config, step_limit, sims, budget)
+            capacities = plan_capacities(config, step_limit, sims, budget,
+                                         num_actions=self.A)
         self.capacities = capacities
         c = N.PomcpConfig()
         c.abi_version = N.POMCP_ABI_VERSION

@@ -196,7 +196,8 @@ class BatchedPOMCP:
         from posggym_baselines_amd.planning.engine import plan_capacities
         if capacities is None:
             step_limit = config.step_limit or model.spec.max_episode_steps
-            capacities = plan_capacities(config, step_limit, num_sims, searches, reroot=reroot)
+            capacities = plan_capacities(config, step_limit, num_sims, searches, reroot=reroot,
+                                         num_actions=model.action_spaces[agent_id].n)
         self.num_trees = num_trees
         self.num_sims = num_sims
         self.engine = PomcpEngine(model, agent_id, config, num_trees=num_trees,

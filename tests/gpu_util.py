@@ -63,3 +63,42 @@ def gpu_episode(cfg_kwargs, num_sims, env_seed, ego="0", max_steps=50):
     trace = run_episode(step, env_seed, ego=ego, max_steps=max_steps)
     planner.close()
     return trace, records
+
+
+def batched_episodes(cfg_kwargs, num_sims, env_seeds, steps):
+    """Lockstep episodes of len(env_seeds) independent planners in ONE engine
+    (tree b = planner b, env seed env_seeds[b]), `steps` real steps each.
+    Returns per-tree record lists in the oracle format."""
+    import numpy as np
+    from oracle.driving import DrivingModel as EnvModel
+    from oracle.driving import pack_obs
+    from oracle.episode import ENV_TREE_BASE
+    from oracle.rng import S_ENV_POLICY_BASE, Streams
+    from posggym_baselines_amd.envs import DrivingModel
+    from posggym_baselines_amd.planning import BatchedPOMCP
+    model = DrivingModel()
+    B = len(env_seeds)
+    bp = BatchedPOMCP(model, "0", product_config(cfg_kwargs, num_sims), B, num_sims,
+                      searches=steps, reroot=True)
+    envs = []
+    for s in env_seeds:
+        es = Streams(s, ENV_TREE_BASE)
+        env = EnvModel(es)
+        st = env.sample_initial_state()
+        envs.append([es, env, st, env.sample_initial_obs(st)])
+    records = [[] for _ in range(B)]
+    last = np.full(B, -1, dtype=np.int32)
+    for t in range(steps):
+        keys = np.array([pack_obs(e[3]["0"]) for e in envs], dtype=np.uint64)
+        bp.engine.update(last, keys)
+        actions = bp.search()
+        stats = bp.engine.root_stats()
+        for b in range(B):
+            records[b].append(stats_record(stats[b], 5, True, actions[b], bp.engine.root_belief(b)))
+            es, env, st, obs = envs[b]
+            acts = {"0": int(actions[b]), "1": es.randint(S_ENV_POLICY_BASE + 1, 5)}
+            ts = env.step(st, acts)
+            envs[b][2], envs[b][3] = ts.state, ts.observations
+        last = actions.astype(np.int32)
+    bp.close()
+    return records

@@ -135,3 +135,22 @@ def test_many_trees_properties():
              for s in bp.engine.root_stats()]
     assert first == again
     bp.close()
+
+
+def test_batched_episodes_reroot_across_waves():
+    """70 planners (two search waves sharing particle logs) over 6 real steps:
+    re-root + log extraction + reinvigoration per tree equal the oracle."""
+    from gpu_util import batched_episodes
+    from oracle.run import oracle_episode
+    S, K = 96, 6
+    seeds, exp = [], []
+    s = 3000
+    while len(seeds) < 70:   # planners whose episodes last >= K steps
+        trace, recs = oracle_episode(TEST_CFG, S, s, tree=len(seeds), max_steps=K)
+        if trace["len"] >= K and all(r["searched"] for r in recs):
+            seeds.append(s)
+            exp.append(recs)
+        s += 1
+    got = batched_episodes(TEST_CFG, S, seeds, K)
+    for b in range(len(seeds)):
+        assert got[b] == exp[b], f"tree {b} (env seed {seeds[b]})"

@@ -1,0 +1,64 @@
+"""k_search phase breakdown (diagnostics; run on the GPU box).
+
+Builds a diagnostics copy of the engine with -DPOMCP_PHASE_TIMING into
+/tmp, runs one warm search on the bench workload and prints the share of wave
+time per loop section (each mark drains outstanding memory operations, so a
+section is charged the waits of the loads it issued).
+
+    python tools/phase_timing.py [--trees B --sims S]
+"""
+import argparse
+import ctypes as C
+import math
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = "/tmp/libpomcp_hip_timing.so"
+os.environ["POMCP_LIB_PATH"] = LIB
+sys.path[:0] = [ROOT, os.path.join(ROOT, "posggym-baselines_amd")]
+NAMES = ["start+root (LDS)", "level: stats line wait", "level: selection",
+         "level: child line wait", "level: step+slot+log", "rollout", "backup", "loop/other"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--trees", type=int, default=65536)
+    ap.add_argument("--sims", type=int, default=4096)
+    args = ap.parse_args()
+    env = dict(os.environ, POMCP_EXTRA_FLAGS="-DPOMCP_PHASE_TIMING")
+    subprocess.run([sys.executable, "-c", "from posggym_baselines_amd import build; build.build(force=True)"],
+                   check=True, env=env, cwd=os.path.join(ROOT, "posggym-baselines_amd"))
+    import numpy as np
+    from posggym_baselines_amd import _native as N
+    from posggym_baselines_amd.envs import DrivingModel
+    from posggym_baselines_amd.planning import BatchedPOMCP, MCTSConfig
+    from posggym_baselines_amd.planning.engine import plan_capacities
+    import bench
+    cfg = MCTSConfig(seed=0, num_sims=args.sims, **bench.TEST_CFG)
+    model = DrivingModel()
+    caps = plan_capacities(cfg, 50, args.sims, 1, reroot=False, max_blocks=512, overflow_slots=1024)
+    bp = BatchedPOMCP(model, "0", cfg, args.trees, args.sims, capacities=caps)
+    bp.init_synthetic(1000)
+    fn = N.load().pomcp_debug_phase_timing
+    cnt = C.c_int32()
+    assert fn(bp.engine._ctx, None, 0, C.byref(cnt)) == 0
+    bp.restore()
+    bp.search(fetch=False)
+    assert fn(bp.engine._ctx, None, 0, C.byref(cnt)) == 0
+    buf = np.zeros(cnt.value, dtype=np.uint64)
+    assert fn(bp.engine._ctx, buf.ctypes.data_as(C.POINTER(C.c_uint64)), cnt.value, C.byref(cnt)) == 0
+    per = buf.reshape(-1, 8).astype(np.float64)
+    per = per[per.sum(1) > 0]
+    tot = per.sum(0)
+    sims = args.sims
+    print(f"waves {len(per)}; s_memtime ticks per wave per simulation round:")
+    for i, n in enumerate(NAMES):
+        print(f"  {n:26s} {tot[i] / len(per) / sims:10.1f}  {100 * tot[i] / tot.sum():5.1f}%")
+    print(f"  {'total':26s} {tot.sum() / len(per) / sims:10.1f}")
+    bp.close()
+
+
+if __name__ == "__main__":
+    main()
