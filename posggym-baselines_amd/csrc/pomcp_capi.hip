@@ -109,7 +109,7 @@ static int validate(const pomcp_config* c, std::string* why) {
   if (c->num_particles < 1 || c->extra_particles < 0) return bad("num_particles");
   if (c->num_trees < 1) return bad("num_trees >= 1");
   if (c->max_blocks < 1 || c->max_blocks * (c->num_actions + 1) * 128 > INT32_MAX) return bad("max_blocks");
-  if (c->num_actions > kMaxA) { *why = "the search kernel supports at most 5 actions"; return POMCP_E_UNSUPPORTED; }
+  if (c->num_actions < 2 || c->num_actions > kMaxA) { *why = "the search kernel supports 2 to 5 actions"; return POMCP_E_UNSUPPORTED; }
   if (c->max_particles < 1 || c->max_particles * kWave > UINT32_MAX) return bad("max_particles");
   if (c->max_blocks * c->num_actions * kSlots + 1 + c->overflow_slots >= (int64_t)kIdMask)
     return bad("obs node ids exceed 2^26 (max_blocks * A * 6 + overflow_slots)");
@@ -329,17 +329,17 @@ int pomcp_search(pomcp_ctx* ctx, int32_t num_sims, int32_t* actions_out) {
   if (!ctx || num_sims < 0) return POMCP_E_INVALID;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   const dim3 grid(search_blocks(ctx->dp.B)), block(kTPB);
-  switch (ctx->dp.sel) {
-    case POMCP_SEL_PUCB:
-      hipLaunchKernelGGL(k_search<POMCP_SEL_PUCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims);
-      break;
-    case POMCP_SEL_UCB:
-      hipLaunchKernelGGL(k_search<POMCP_SEL_UCB>, grid, block, 0, ctx->stream, ctx->dp, (int)num_sims);
-      break;
-    default:
-      hipLaunchKernelGGL(k_search<POMCP_SEL_UNIFORM>, grid, block, 0, ctx->stream, ctx->dp,
-                         (int)num_sims);
-  }
+  // kernel per (selection rule, action count): the per-child loops unroll
+  using KFn = void (*)(DevParams, int);
+  static const KFn table[3][4] = {
+      {k_search<POMCP_SEL_PUCB, 2>, k_search<POMCP_SEL_PUCB, 3>, k_search<POMCP_SEL_PUCB, 4>,
+       k_search<POMCP_SEL_PUCB, 5>},
+      {k_search<POMCP_SEL_UCB, 2>, k_search<POMCP_SEL_UCB, 3>, k_search<POMCP_SEL_UCB, 4>,
+       k_search<POMCP_SEL_UCB, 5>},
+      {k_search<POMCP_SEL_UNIFORM, 2>, k_search<POMCP_SEL_UNIFORM, 3>,
+       k_search<POMCP_SEL_UNIFORM, 4>, k_search<POMCP_SEL_UNIFORM, 5>}};
+  hipLaunchKernelGGL(table[ctx->dp.sel][ctx->dp.A - 2], grid, block, 0, ctx->stream, ctx->dp,
+                     (int)num_sims);
   HIP_TRY(ctx, hipGetLastError());
   if (!actions_out) return POMCP_OK;
   const int rc = pomcp_get_root_stats(ctx, ctx->host_stats.data());
@@ -538,16 +538,16 @@ int pomcp_debug_phase_timing(pomcp_ctx* ctx, uint64_t* out, int32_t capacity, in
   const int64_t waves = (int64_t)search_blocks(ctx->dp.B) * per_block;
   if (ctx->dp.timing == nullptr) {   // first call: allocate; the next search fills it
     void* p = nullptr;
-    if (dev_alloc(ctx, &p, sizeof(uint64_t) * 8 * (size_t)waves) != POMCP_OK) return POMCP_E_HIP;
-    HIP_TRY(ctx, hipMemset(p, 0, sizeof(uint64_t) * 8 * (size_t)waves));
+    if (dev_alloc(ctx, &p, sizeof(uint64_t) * 16 * (size_t)waves) != POMCP_OK) return POMCP_E_HIP;
+    HIP_TRY(ctx, hipMemset(p, 0, sizeof(uint64_t) * 16 * (size_t)waves));
     ctx->dp.timing = reinterpret_cast<uint64_t*>(p);
     *count = 0;
     return POMCP_OK;
   }
-  *count = (int32_t)(8 * waves);
+  *count = (int32_t)(16 * waves);
   if (out && capacity >= *count) {
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    HIP_TRY(ctx, hipMemcpy(out, ctx->dp.timing, sizeof(uint64_t) * 8 * (size_t)waves,
+    HIP_TRY(ctx, hipMemcpy(out, ctx->dp.timing, sizeof(uint64_t) * 16 * (size_t)waves,
                            hipMemcpyDeviceToHost));
   }
   return POMCP_OK;

@@ -118,7 +118,7 @@ struct DevParams {
   const int32_t* in_actions;
   const uint64_t* in_obs;
   uint64_t* out_obs;
-  uint64_t* timing;     // [waves][8] phase cycles (diagnostics build only), may be null
+  uint64_t* timing;     // [waves][16] phase cycles (diagnostics build only), may be null
 };
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }

@@ -22,10 +22,13 @@
 //   * the belief particle of the NEXT simulation is prefetched when a
 //     simulation starts (belief.py:55: its index only depends on the belief
 //     stream's counter);
-//   * one loop iteration = start + root level (LDS) + one deeper level (two
-//     dependent HBM lines: the node's statistics, then the chosen action's
-//     child slots) + a whole rollout + the backup, so a depth-2 simulation
-//     takes two iterations and four HBM waits.
+//   * one loop iteration = one level below the root + a whole rollout + the
+//     backup + the start of the next simulation with its root level (LDS);
+//     whenever a lane descends into an expanded node, the node's statistics
+//     line is loaded right away and consumed by the NEXT iteration, so its
+//     latency hides behind the rest of this iteration; only the chosen
+//     action's child line is waited for.  A depth-2 simulation takes two
+//     iterations.
 // The root block is written back to HBM at the end of the launch.
 //
 // Block layout: pomcp_device.h ((A + 1) x 128 B lines).
@@ -53,7 +56,7 @@ struct PathEntry {
 };
 
 // Phase timing (diagnostics build, -DPOMCP_PHASE_TIMING): per-wave s_memtime
-// deltas per loop section into p.timing[wave][8]; each mark first drains every
+// deltas per loop section into p.timing[wave][16]; each mark first drains every
 // outstanding memory operation, so a section is charged the waits it issued.
 #ifdef POMCP_PHASE_TIMING
 #define PT_MARK(slot)                                          \
@@ -71,8 +74,9 @@ struct PathEntry {
 
 enum : int { TP_LEVEL = 0, TP_ROLL = 1, TP_BACKUP = 2, TP_START = 3, TP_DONE = 4 };
 
-template <int SEL>
+template <int SEL, int NA>
 __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
+  static_assert(NA >= 2 && NA <= kMaxA, "action count");
   __shared__ DrvModel sm;
   __shared__ uint4 rc[kRootParts][kTPB];   // the root block of every lane's tree
   stage_model(p.model, sm);
@@ -82,7 +86,7 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
   const int tree = wave * kWave + lane;
   const bool valid = tree < p.B;
   const int tt = valid ? tree : 0;
-  const int A = p.A;
+  constexpr int A = NA;   // == p.A (host dispatch)
   char* const an = reinterpret_cast<char*>(p.an + (int64_t)tt * p.Nb * blk_lines(A));
   const int blk_bytes = blk_lines(A) * 128;
   // the wave's shared particle log (pomcp_device.h LogRec); wpos is the same in
@@ -115,6 +119,11 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
            c_a1 = h->ctr[4];
   const int log0 = n_log, blocks0 = n_blocks, nodes0 = n_nodes;
   int c_rollout = 0, c_probes = 0;
+#ifdef POMCP_PHASE_TIMING
+  uint64_t pt[16];
+  for (int i = 0; i < 16; ++i) pt[i] = 0;
+  uint64_t pt_last = __builtin_amdgcn_s_memtime();
+#endif
 
   // ---- RNG streams (philox.h): one stateless Philox block per draw
   auto d_belief = [&](uint32_t n) { return uniform_int(philox_word(seed, tkey, S_BELIEF, c_bel++), n); };
@@ -135,13 +144,12 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
     for (int q = 0; q < blk_parts(A); ++q) d[q] = make_uint4(0, 0, 0, 0);
     return b;
   };
-  auto normalize = [&](double v) {   // utils.py:34-39
-    return mm_max > mm_min ? (v - mm_min) / (mm_max - mm_min) : v;
-  };
 
   // _search_action_selection (mcts.py:492-563) over the statistics st[] of a
-  // node with nv visits
-  auto select_action = [&](const uint4 (&st)[kMaxA], int nv) -> int {
+  // node with nv visits; log_n = math.log(nv) (host table, prefetched).  The
+  // children's scores are computed branch-free (independent chains the wave
+  // issues back to back); the strict '>' scan in action order is kept.
+  auto select_action = [&](const uint4 (&st)[kMaxA], int nv, double log_n) -> int {
     int a = 0;
     if (SEL == POMCP_SEL_PUCB && nv == 0) {   // random.choices over the uniform prior
       const double w = 1.0 / (double)A;
@@ -162,51 +170,51 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
     } else if (SEL == POMCP_SEL_UNIFORM) {   // min_visit_action_selection
       int min_n = nv + 1;
 #pragma unroll
-      for (int q = 0; q < kMaxA; ++q) {
-        if (q < A && (int)st[q].x < min_n) {
+      for (int q = 0; q < A; ++q) {
+        if ((int)st[q].x < min_n) {
           min_n = (int)st[q].x;
           a = q;
         }
       }
-    } else if (SEL == POMCP_SEL_UCB) {
-      int unv = -1;   // mcts.py:539-540: first unvisited child
-#pragma unroll
-      for (int q = kMaxA - 1; q >= 0; --q)
-        if (q < A && st[q].x == 0u) unv = q;
-      if (unv >= 0) {
-        a = unv;
-      } else {
-        const double log_n = p.logtab[nv < p.logtab_n ? nv : 0];
+    } else {
+      const bool nz = mm_max > mm_min;   // utils.py:34-39
+      const double range = mm_max - mm_min;
+      double sc[A];
+      if (SEL == POMCP_SEL_UCB) {          // mcts.py:529-546
         if (nv >= p.logtab_n) err = POMCP_E_ARENA;
-        double best = -__builtin_inf();
 #pragma unroll
-        for (int q = 0; q < kMaxA; ++q) {
-          if (q < A) {   // mcts.py:541-542, strict '>' in action order
-            const double s = normalize(hilo_d(st[q].z, st[q].w)) +
-                             p.c * sqrt(log_n / (double)(int)st[q].x);
-            if (s > best) {
-              best = s;
-              a = q;
-            }
-          }
+        for (int q = 0; q < A; ++q) {
+          const double v = hilo_d(st[q].z, st[q].w);
+          const double nvq = nz ? (v - mm_min) / range : v;
+          const int n = (int)st[q].x > 0 ? (int)st[q].x : 1;
+          sc[q] = nvq + p.c * sqrt(log_n / (double)n);
+        }
+      } else {                             // PUCB, mcts.py:502-527
+        const double noise = 1.0 / (double)A;
+        const double prior = (1.0 / (double)A) * (1.0 - p.pucb_f) + p.pucb_f * noise;
+        const double sqrt_n = sqrt((double)nv);
+#pragma unroll
+        for (int q = 0; q < A; ++q) {
+          const int n = (int)st[q].x;
+          const double v = hilo_d(st[q].z, st[q].w);
+          const double nvq = nz ? (v - mm_min) / range : v;
+          sc[q] = (n > 0 ? nvq : 0.0) + p.c * prior * (sqrt_n / (double)(1 + n));
         }
       }
-    } else {   // PUCB, mcts.py:502-527
-      const double noise = 1.0 / (double)A;
-      const double prior = (1.0 / (double)A) * (1.0 - p.pucb_f) + p.pucb_f * noise;
-      const double sqrt_n = sqrt((double)nv);
-      double best = -__builtin_inf();
+      double best = sc[0];
 #pragma unroll
-      for (int q = 0; q < kMaxA; ++q) {
-        if (q < A) {
-          const int n = (int)st[q].x;
-          const double s = (n > 0 ? normalize(hilo_d(st[q].z, st[q].w)) : 0.0) +
-                           p.c * prior * (sqrt_n / (double)(1 + n));
-          if (s > best) {
-            best = s;
-            a = q;
-          }
+      for (int q = 1; q < A; ++q) {
+        if (sc[q] > best) {
+          best = sc[q];
+          a = q;
         }
+      }
+      if (SEL == POMCP_SEL_UCB) {   // mcts.py:539-540: the first unvisited child wins
+        int unv = -1;
+#pragma unroll
+        for (int q = A - 1; q >= 0; --q)
+          if (st[q].x == 0u) unv = q;
+        if (unv >= 0) a = unv;
       }
     }
     return a;
@@ -226,6 +234,11 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
   double r0_r = 0.0, r0_val = 0.0;
   uint4 r0_s1 = make_uint4(0, 0, 0, 0);
   PathEntry rpath[kRegPath];     // levels 1..kRegPath
+  uint4 pre[kMaxA];              // statistics line of the next LEVEL pass's node
+#pragma unroll
+  for (int q = 0; q < kMaxA; ++q) pre[q] = make_uint4(0, 0, 0, 0);
+  double pre_logn = 0.0;         // math.log(visits) of that node
+  auto logtab = [&](int n) { return p.logtab[n < p.logtab_n ? n : 0]; };
 
   if (!valid || err != 0 || root_abs) phase = TP_DONE;   // mcts.py:270-272
   if (phase != TP_DONE && h->root_t == 0) {
@@ -241,6 +254,7 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
   }
   if (num_sims <= 0) phase = TP_DONE;
   const bool cached = phase != TP_DONE;   // this lane's root block is in rc[][lid]
+  double root_logn = logtab(root_visits); // math.log(root visits) of the next simulation
   const uint4* const rb = reinterpret_cast<const uint4*>(an + (int64_t)(cached ? root_blk : 0) * blk_bytes);
   if (cached) {
 #pragma unroll
@@ -290,18 +304,24 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
   };
 
   // The generative step of one tree level (mcts.py:331-352) for ego action a.
-  auto tree_step = [&](int a, uint32_t* n0, uint32_t* n1, double* r, int* done, uint64_t* okey) {
-    const uint32_t ao = d_act(p.other, (uint32_t)A);   // mcts.py:331
-    const uint32_t j = d_model(2);                     // exec-order shuffle
+  // ao: the other agent's action (mcts.py:331), j: the model's exec-order
+  // shuffle draw; both are drawn before the selection (their streams are
+  // independent of it) so that they overlap the statistics load.
+  auto tree_step = [&](int a, uint32_t ao, uint32_t j, uint32_t* n0, uint32_t* n1, double* r,
+                       int* done, uint64_t* okey) {
+    PT_MARK(15);
     drv_step2_vec(sm, s0, s1, p.ego == 0 ? (uint32_t)a : ao, p.ego == 0 ? ao : (uint32_t)a, j,
                   n0, n1);
+    PT_MARK(9);
     const uint32_t e0 = p.ego == 0 ? s0 : s1;
     const uint32_t e1 = p.ego == 0 ? *n0 : *n1;
     const uint32_t o1 = p.ego == 0 ? *n1 : *n0;
     *r = drv_reward_vec(sm, e0, e1);
     *done = (((e1 >> 15) & 3u) != 0u ||
              (((*n0 >> 15) & 3u) != 0u && ((*n1 >> 15) & 3u) != 0u)) ? 1 : 0;
+    PT_MARK(10);
     *okey = obs_key_vec(sm, e1, o1);
+    PT_MARK(11);
   };
 
   // ActionNode.children[obs] among the inline slots (mcts.py:356-370): filled
@@ -351,22 +371,24 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
         rdepth = depth;   // the rollout's own depth counter (mcts.py:449)
         phase = TP_ROLL;
       }
-    } else {
+    } else {   // next LEVEL pass: issue its statistics line now (no wait)
       phase = TP_LEVEL;
+      const uint4* const cp = reinterpret_cast<const uint4*>(an + (int64_t)blk * blk_bytes);
+#pragma unroll
+      for (int q = 0; q < kMaxA; ++q) pre[q] = q < A ? cp[q] : make_uint4(0, 0, 0, 0);
+      pre_logn = logtab(nvis);
     }
   };
 
-#ifdef POMCP_PHASE_TIMING
-  uint64_t pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t pt_last = __builtin_amdgcn_s_memtime();
-#endif
-  while (phase != TP_DONE) {
+  // One iteration of this uniform loop = one simulation of every lane's tree,
+  // lanes in lockstep: the start and root level, then the levels below it
+  // (one pass per depth while any lane still descends), the rollouts, the
+  // backup.  A lane that has failed (or has no search) idles, masked.
+  for (int it = 0; it < num_sims; ++it) {
     PT_MARK(7);
     // ------------------------------------- start a simulation + the root level
     if (phase == TP_START) {
-      if (sims >= num_sims) {
-        phase = TP_DONE;
-      } else {
+      {
         const uint4 pr = pf;                                     // belief.py:55
         if (sims + 1 < num_sims) pf = rbel[d_belief((uint32_t)bsize)];
         t = (int)pr.x;
@@ -379,10 +401,12 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
           ret = 0.0;
           phase = TP_BACKUP;
         } else {
+          const uint32_t ao = d_act(p.other, (uint32_t)A);
+          const uint32_t j = d_model(2);
           uint4 st[kMaxA];
 #pragma unroll
           for (int q = 0; q < kMaxA; ++q) st[q] = q < A ? rc[rc_stats(q)][lid] : make_uint4(0, 0, 0, 0);
-          const int a = select_action(st, root_visits);
+          const int a = select_action(st, root_visits, root_logn);
           uint4 sa = st[0];
           uint4 sl[kSlots];
 #pragma unroll
@@ -395,7 +419,7 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
           double r;
           int done;
           uint64_t okey;
-          tree_step(a, &n0, &n1, &r, &done, &okey);
+          tree_step(a, ao, j, &n0, &n1, &r, &done, &okey);
           bool match;
           const int ks = find_slot(sl, okey, &match);
           const uint32_t ani = (uint32_t)(root_blk * A + a);
@@ -436,84 +460,93 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
           }
         }
       }
+      root_logn = logtab(root_visits + 1);   // the next simulation's (no wait)
       PT_MARK(0);
     }
     append();
-    // ------------------------------------------------- one level below the root
-    if (phase == TP_LEVEL) {
-      const uint4* const ap = reinterpret_cast<const uint4*>(an + (int64_t)blk * blk_bytes);
-      uint4 st[kMaxA];
-#pragma unroll
-      for (int q = 0; q < kMaxA; ++q) st[q] = q < A ? ap[q] : make_uint4(0, 0, 0, 0);
-      PT_MARK(1);
-      const int a = select_action(st, nvis);
-      PT_MARK(2);
-      uint4 sa = st[0];
-#pragma unroll
-      for (int q = 1; q < kMaxA; ++q)
-        if (q == a) sa = st[q];
-      // the chosen action's stats1 and child slots (second round trip)
-      const uint4 s1a = ap[part_stats1(a)];
-      uint4 sl[kSlots];
-#pragma unroll
-      for (int q = 0; q < kSlots; ++q) sl[q] = ap[part_slot(a, q)];
-      PT_MARK(3);
-      uint32_t n0, n1;
-      double r;
-      int done;
-      uint64_t okey;
-      tree_step(a, &n0, &n1, &r, &done, &okey);
-      bool match;
-      const int ks = find_slot(sl, okey, &match);
-      const uint32_t ani = (uint32_t)(blk * A + a);
-      uint32_t cid = 0;
-      int cblk = -1, cvis = 1;
-      leaf_rc = -1;
-      if (ks >= 0) {
-        uint4 sk = sl[0];
-#pragma unroll
-        for (int q = 1; q < kSlots; ++q)
-          if (q == ks) sk = sl[q];
-        if (match) {
-          cblk = (int)sk.z;
-          cvis = (int)sk.w + 1;
+    // ------------------------------------------------- the levels below the root
+    while (__ballot(phase == TP_LEVEL) != 0ull) {
+      if (phase == TP_LEVEL) {
+        const uint4* const ap = reinterpret_cast<const uint4*>(an + (int64_t)blk * blk_bytes);
+        const uint32_t ao = d_act(p.other, (uint32_t)A);
+        const uint32_t j = d_model(2);
+        PT_MARK(8);
+        uint4 st[kMaxA];   // prefetched by descend()
+  #pragma unroll
+        for (int q = 0; q < kMaxA; ++q) st[q] = pre[q];
+        PT_MARK(1);
+        const int a = select_action(st, nvis, pre_logn);
+        PT_MARK(2);
+        uint4 sa = st[0];
+  #pragma unroll
+        for (int q = 1; q < kMaxA; ++q)
+          if (q == a) sa = st[q];
+        // the chosen action's stats1 and child slots (second round trip)
+        const uint4 s1a = ap[part_stats1(a)];
+        uint4 sl[kSlots];
+  #pragma unroll
+        for (int q = 0; q < kSlots; ++q) sl[q] = ap[part_slot(a, q)];
+        PT_MARK(3);
+        uint32_t n0, n1;
+        double r;
+        int done;
+        uint64_t okey;
+        tree_step(a, ao, j, &n0, &n1, &r, &done, &okey);
+        bool match;
+        const int ks = find_slot(sl, okey, &match);
+        PT_MARK(12);
+        const uint32_t ani = (uint32_t)(blk * A + a);
+        uint32_t cid = 0;
+        int cblk = -1, cvis = 1;
+        leaf_rc = -1;
+        if (ks >= 0) {
+          uint4 sk = sl[0];
+  #pragma unroll
+          for (int q = 1; q < kSlots; ++q)
+            if (q == ks) sk = sl[q];
+          if (match) {
+            cblk = (int)sk.z;
+            cvis = (int)sk.w + 1;
+          } else {
+            ++n_nodes;
+          }
+          const uint64_t nk = okey | kValidBit | ((uint64_t)done << 63);
+          uint4* slot = const_cast<uint4*>(ap) + part_slot(a, ks);
+          *slot = make_uint4((uint32_t)nk, (uint32_t)(nk >> 32), (uint32_t)cblk, (uint32_t)cvis);
+          cid = ani * kSlots + (uint32_t)ks + 1u;
+          leaf_ptr = reinterpret_cast<int32_t*>(slot) + 2;
         } else {
-          ++n_nodes;
+          ovf_child(ani, okey, done, &cid, &cblk, &cvis, &leaf_ptr);
         }
-        const uint64_t nk = okey | kValidBit | ((uint64_t)done << 63);
-        uint4* slot = const_cast<uint4*>(ap) + part_slot(a, ks);
-        *slot = make_uint4((uint32_t)nk, (uint32_t)(nk >> 32), (uint32_t)cblk, (uint32_t)cvis);
-        cid = ani * kSlots + (uint32_t)ks + 1u;
-        leaf_ptr = reinterpret_cast<int32_t*>(slot) + 2;
-      } else {
-        ovf_child(ani, okey, done, &cid, &cblk, &cvis, &leaf_ptr);
-      }
-      if (err != 0 || n_log >= p.Np || plen >= kMaxPath) {
-        if (err == 0) err = POMCP_E_ARENA;
-        phase = TP_DONE;
-      } else {
-        rec = LogRec{cid | ((uint32_t)lane << kIdBits), n0, n1};   // mcts.py:371
-        app = true;
-        ++n_log;
-        const uint32_t off = (uint32_t)(blk * blk_bytes + a * 16);
-        const PathEntry pe = {
-            make_uint4(off | ((uint32_t)done << 31), sa.x, (uint32_t)__double2loint(r),
-                       (uint32_t)__double2hiint(r)),
-            make_uint4(sa.z, sa.w, s1a.x, s1a.y),
-            make_uint4(s1a.z, s1a.w, (uint32_t)(blk * blk_bytes + part_stats1(a) * 16), 0u)};
-        if (plen < kRegPath) {
-#pragma unroll
-          for (int l = 0; l < kRegPath; ++l)
-            if (plen == l) rpath[l] = pe;
+        PT_MARK(13);
+        if (err != 0 || n_log >= p.Np || plen >= kMaxPath) {
+          if (err == 0) err = POMCP_E_ARENA;
+          phase = TP_DONE;
         } else {
-          path[plen] = pe;
+          rec = LogRec{cid | ((uint32_t)lane << kIdBits), n0, n1};   // mcts.py:371
+          app = true;
+          ++n_log;
+          const uint32_t off = (uint32_t)(blk * blk_bytes + a * 16);
+          const PathEntry pe = {
+              make_uint4(off | ((uint32_t)done << 31), sa.x, (uint32_t)__double2loint(r),
+                         (uint32_t)__double2hiint(r)),
+              make_uint4(sa.z, sa.w, s1a.x, s1a.y),
+              make_uint4(s1a.z, s1a.w, (uint32_t)(blk * blk_bytes + part_stats1(a) * 16), 0u)};
+          if (plen < kRegPath) {
+  #pragma unroll
+            for (int l = 0; l < kRegPath; ++l)
+              if (plen == l) rpath[l] = pe;
+          } else {
+            path[plen] = pe;
+          }
+          ++plen;
+          PT_MARK(14);
+          descend(done, cblk, cvis, n0, n1);
         }
-        ++plen;
-        descend(done, cblk, cvis, n0, n1);
+        PT_MARK(4);
       }
-      PT_MARK(4);
+      append();
     }
-    append();
     // ------------------------------------------------------ the rollout
     while (phase == TP_ROLL) {                               // mcts.py:414-450
       if (!(rdepth <= p.depth_limit && t <= p.step_limit)) {
@@ -598,7 +631,7 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
   }
 #ifdef POMCP_PHASE_TIMING
   if (p.timing != nullptr && (threadIdx.x & (kWave - 1)) == 0) {
-    for (int i = 0; i < 8; ++i) p.timing[wave * 8 + i] = pt[i];
+    for (int i = 0; i < 16; ++i) p.timing[wave * 16 + i] = pt[i];
   }
 #endif
 
@@ -721,8 +754,14 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
   so->pad = 0;
 }
 
-template __global__ void k_search<POMCP_SEL_PUCB>(DevParams, int);
-template __global__ void k_search<POMCP_SEL_UCB>(DevParams, int);
-template __global__ void k_search<POMCP_SEL_UNIFORM>(DevParams, int);
+#define PB_SEARCH_INST(NA)                                                 \
+  template __global__ void k_search<POMCP_SEL_PUCB, NA>(DevParams, int);  \
+  template __global__ void k_search<POMCP_SEL_UCB, NA>(DevParams, int);   \
+  template __global__ void k_search<POMCP_SEL_UNIFORM, NA>(DevParams, int);
+PB_SEARCH_INST(2)
+PB_SEARCH_INST(3)
+PB_SEARCH_INST(4)
+PB_SEARCH_INST(5)
+#undef PB_SEARCH_INST
 
 }  // namespace pb

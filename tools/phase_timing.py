@@ -19,7 +19,9 @@ LIB = "/tmp/libpomcp_hip_timing.so"
 os.environ["POMCP_LIB_PATH"] = LIB
 sys.path[:0] = [ROOT, os.path.join(ROOT, "posggym-baselines_amd")]
 NAMES = ["start+root (LDS)", "level: stats line wait", "level: selection",
-         "level: child line wait", "level: step+slot+log", "rollout", "backup", "loop/other"]
+         "level: child line wait", "level: rest", "rollout", "backup", "loop/other",
+         "  step: philox x2", "  step: drv_step2", "  step: reward+done", "  step: obs key",
+         "  find_slot", "  slot write / ovf", "  log+path entry", "  (before step)"]
 
 
 def main():
@@ -49,7 +51,7 @@ def main():
     assert fn(bp.engine._ctx, None, 0, C.byref(cnt)) == 0
     buf = np.zeros(cnt.value, dtype=np.uint64)
     assert fn(bp.engine._ctx, buf.ctypes.data_as(C.POINTER(C.c_uint64)), cnt.value, C.byref(cnt)) == 0
-    per = buf.reshape(-1, 8).astype(np.float64)
+    per = buf.reshape(-1, 16).astype(np.float64)
     per = per[per.sum(1) > 0]
     tot = per.sum(0)
     sims = args.sims
