@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define POMCP_ABI_VERSION 1
+#define POMCP_ABI_VERSION 2
 #define POMCP_MAX_ACTIONS 8
 
 typedef enum pomcp_status {
@@ -39,7 +39,10 @@ typedef enum pomcp_selection {
   POMCP_SEL_UNIFORM = 2   /* mcts.py:548-563 + max_value final */
 } pomcp_selection;
 
-typedef enum pomcp_env { POMCP_ENV_DRIVING = 1 } pomcp_env;
+typedef enum pomcp_env {
+  POMCP_ENV_DRIVING = 1,            /* Driving-v1: pomcp_config.grid */
+  POMCP_ENV_PURSUIT_EVASION = 2     /* PursuitEvasion-v1: pomcp_config.pe_grid */
+} pomcp_env;
 
 /* Driving-v1 grid tables (16-wide row stride). */
 typedef struct pomcp_grid {
@@ -50,6 +53,16 @@ typedef struct pomcp_grid {
   int32_t obs_front, obs_back, obs_side;
   int32_t pad[2];
 } pomcp_grid;
+
+/* PursuitEvasion-v1 grid (16-wide row stride; coordinates are (x, y)). */
+typedef struct pomcp_pe_grid {
+  uint8_t wall[256];
+  uint8_t goal_dist[4][256];      /* BFS distance to goal k (127 = unreachable) */
+  uint8_t evader_start[4][2], pursuer_start[4][2], goal[4][2];
+  int32_t width, height, n_evader_start, n_pursuer_start, n_goal, max_obs_distance;
+  int32_t use_progress_reward, pad;
+  double reward_norm;             /* R_MAX + R_PROGRESS * longest start-goal path */
+} pomcp_pe_grid;
 
 /* MCTSConfig (config.py:8-55) after __post_init__, plus engine sizing. */
 typedef struct pomcp_config {
@@ -83,7 +96,8 @@ typedef struct pomcp_config {
   int64_t log_table_size;
   const double* discount_pow;   /* discount ** k */
   int64_t discount_pow_size;
-  pomcp_grid grid;
+  pomcp_grid grid;              /* env_id == POMCP_ENV_DRIVING */
+  pomcp_pe_grid pe_grid;        /* env_id == POMCP_ENV_PURSUIT_EVASION */
 } pomcp_config;
 
 /* Per-tree result of the last search (MCTS.step_statistics + root children). */
@@ -153,7 +167,7 @@ int pomcp_rekey(pomcp_ctx* ctx, uint64_t seed);
  * the operand of the RCCL all-reduce at action-selection time. */
 int pomcp_root_merge_buffer(pomcp_ctx* ctx, void** device_ptr);
 
-/* Bench / batch helpers: synthetic Driving-v1 roots.  Tree b samples s0 from
+/* Bench / batch helpers: synthetic roots (the configured environment).  Tree b samples s0 from
  * the model's b0 under env key (env_seed_base + b, 0x40000000) and the ego's
  * initial obs is written to obs_keys_out (host, [num_trees], may be NULL). */
 int pomcp_synthetic_obs(pomcp_ctx* ctx, uint64_t env_seed_base, uint64_t* obs_keys_out);
@@ -174,6 +188,15 @@ int pomcp_driving_step(const pomcp_grid* g, uint64_t seed, uint32_t tree, uint32
                        double rewards_out[2], int32_t terminated_out[2],
                        uint64_t obs_keys_out[2]);
 int pomcp_driving_obs(const pomcp_grid* g, const uint32_t state[2], uint64_t obs_keys_out[2]);
+
+/* ---- Host (CPU) PursuitEvasion-v1 model from csrc/pursuit_evasion.h ----- */
+int pomcp_pe_sample_initial_state(const pomcp_pe_grid* g, uint64_t seed, uint32_t tree,
+                                  uint32_t* model_ctr, uint32_t state_out[2]);
+/* One joint step (deterministic: no model draw). */
+int pomcp_pe_step(const pomcp_pe_grid* g, const uint32_t state[2], const int32_t actions[2],
+                  uint32_t next_out[2], double rewards_out[2], int32_t terminated_out[2],
+                  uint64_t obs_keys_out[2]);
+int pomcp_pe_obs(const pomcp_pe_grid* g, const uint32_t state[2], uint64_t obs_keys_out[2]);
 
 #ifdef __cplusplus
 }

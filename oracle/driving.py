@@ -161,6 +161,13 @@ def pack_obs(obs) -> int:
 class DrivingModel:
     """Driving-v1 restatement, 2+ agents, ``obs_dim=(front, back, side)``."""
 
+    env_id = "Driving-v1"
+    pack_obs = staticmethod(pack_obs)
+
+    @staticmethod
+    def pack_words(state):
+        return pack_vehicle(state[0]), pack_vehicle(state[1])
+
     def __init__(self, streams: Streams, grid="14x14RoundAbout", num_agents=2,
                  obs_dim=(3, 1, 1)):
         self.grid_name = grid

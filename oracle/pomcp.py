@@ -12,7 +12,6 @@ line (citations inline).  Pinned by ``tests/golden/*.json``, which
 """
 import math
 
-from oracle.driving import pack_obs
 from oracle.rng import S_BELIEF, S_SELECT, Streams
 
 INF = float("inf")
@@ -171,7 +170,7 @@ class OraclePOMCP:
         if b < 0:                                      # node.py:58-63 AssertionError
             raise AssertionError(f"root has no child node for {action=}")
         an = b * self.A + action
-        key = (an, pack_obs(obs))
+        key = (an, self.model.pack_obs(obs))
         child = self.children.get(key)
         if child is None:                              # mcts.py:240-247
             child = self._new_obs_node(self.on_t[root] + 1, 0, self.on_abs[root])
@@ -343,7 +342,7 @@ class OraclePOMCP:
             done = (ts.terminations[self.agent_id] or ts.truncations[self.agent_id]
                     or ts.all_done)
             an = self.on_block[node] * A + a
-            key = (an, pack_obs(ts.observations[self.agent_id]))
+            key = (an, self.model.pack_obs(ts.observations[self.agent_id]))
             child = self.children.get(key)
             if child is not None:                                               # mcts.py:358-367
                 self.on_visits[child] += 1

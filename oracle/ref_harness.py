@@ -16,8 +16,8 @@ Injection:
     wrapped so that after ``num_sims`` depth-0 calls the clock jumps past
     ``search_time_limit`` and ``get_action``'s while loop (``mcts.py:285``)
     exits after exactly ``num_sims`` simulations;
-  * the model is ``oracle.driving.DrivingModel`` whose action spaces and RNG
-    draw from the same ``Streams``.
+  * the model is the build's restatement (``oracle.envs``: Driving-v1 or
+    PursuitEvasion-v1) whose action spaces and RNG draw from the same ``Streams``.
 """
 import os
 import sys
@@ -133,7 +133,7 @@ def reference_record(planner, searched, action):
     parts = [(p.state, p.t) for p in root.belief.particles]
     st = planner.step_statistics
     rec["belief_size"] = len(parts)
-    rec["belief_digest"] = belief_digest(parts)
+    rec["belief_digest"] = belief_digest(parts, planner.model.pack_words)
     rec["num_sims"] = int(st["num_sims"])
     if rec["num_sims"] > 0:
         kids = root.get_child_nodes()
@@ -147,15 +147,15 @@ def reference_record(planner, searched, action):
     return rec
 
 
-def reference_episode(cfg_kwargs, num_sims, env_seed, ego="0", grid="14x14RoundAbout",
-                      tree=0, max_steps=50):
+def reference_episode(cfg_kwargs, num_sims, env_seed, ego="0", grid=None,
+                      tree=0, max_steps=50, env="Driving-v1"):
     """One full episode with the real reference POMCP. Returns (trace, records)."""
-    from oracle.driving import DrivingModel
+    from oracle.envs import make_model
     from oracle.episode import run_episode
     from oracle.rng import Streams
 
     streams = Streams(cfg_kwargs.get("seed") or 0, tree)
-    model = DrivingModel(streams, grid=grid)
+    model = make_model(env, streams, grid=grid)
     planner = make_reference_pomcp(model, ego, cfg_kwargs, num_sims, streams)
     planner.reset()
     records = []
@@ -166,6 +166,6 @@ def reference_episode(cfg_kwargs, num_sims, env_seed, ego="0", grid="14x14RoundA
         records.append(reference_record(planner, searched, a))
         return a
 
-    trace = run_episode(step, env_seed, ego=ego, grid=grid, max_steps=max_steps)
+    trace = run_episode(step, env_seed, ego=ego, grid=grid, max_steps=max_steps, env=env)
     planner.close()
     return trace, records

@@ -2,7 +2,7 @@
 
 TEST INFRASTRUCTURE (see ``oracle/__init__.py``).
 """
-from oracle.driving import DrivingModel
+from oracle.envs import make_model
 from oracle.episode import belief_digest, fhex, run_episode
 from oracle.pomcp import OracleConfig, OraclePOMCP
 from oracle.rng import Streams
@@ -15,7 +15,7 @@ def oracle_record(p: OraclePOMCP, searched, action):
     st = p.stats
     parts = st["belief"]
     rec["belief_size"] = len(parts)
-    rec["belief_digest"] = belief_digest(parts)
+    rec["belief_digest"] = belief_digest(parts, p.model.pack_words)
     rec["num_sims"] = int(st.get("num_sims", 0))
     if rec["num_sims"] > 0:
         rec["search_depth"] = st["search_depth"]
@@ -28,16 +28,16 @@ def oracle_record(p: OraclePOMCP, searched, action):
     return rec
 
 
-def make_oracle(cfg_kwargs, num_sims, ego="0", grid="14x14RoundAbout", tree=0):
+def make_oracle(cfg_kwargs, num_sims, ego="0", grid=None, tree=0, env="Driving-v1"):
     streams = Streams(cfg_kwargs.get("seed") or 0, tree)
-    model = DrivingModel(streams, grid=grid)
+    model = make_model(env, streams, grid=grid)
     cfg = OracleConfig(num_sims=num_sims, **cfg_kwargs)
     return OraclePOMCP(model, ego, cfg, streams)
 
 
-def oracle_episode(cfg_kwargs, num_sims, env_seed, ego="0", grid="14x14RoundAbout", tree=0,
-                   max_steps=50):
-    p = make_oracle(cfg_kwargs, num_sims, ego=ego, grid=grid, tree=tree)
+def oracle_episode(cfg_kwargs, num_sims, env_seed, ego="0", grid=None, tree=0,
+                   max_steps=50, env="Driving-v1"):
+    p = make_oracle(cfg_kwargs, num_sims, ego=ego, grid=grid, tree=tree, env=env)
     records = []
 
     def step(obs):
@@ -46,14 +46,14 @@ def oracle_episode(cfg_kwargs, num_sims, env_seed, ego="0", grid="14x14RoundAbou
         records.append(oracle_record(p, searched, a))
         return a
 
-    trace = run_episode(step, env_seed, ego=ego, grid=grid, max_steps=max_steps)
+    trace = run_episode(step, env_seed, ego=ego, grid=grid, max_steps=max_steps, env=env)
     return trace, records
 
 
-def oracle_first_step(cfg_kwargs, num_sims, tree, env_seed, rekey=None):
+def oracle_first_step(cfg_kwargs, num_sims, tree, env_seed, rekey=None, env="Driving-v1"):
     """Record of the first planner step of an episode (synthetic root), optionally
     with the search streams re-keyed after the initial update (root-parallel)."""
-    p = make_oracle(cfg_kwargs, num_sims, tree=tree)
+    p = make_oracle(cfg_kwargs, num_sims, tree=tree, env=env)
     recs = []
 
     def step(obs):
@@ -65,5 +65,5 @@ def oracle_first_step(cfg_kwargs, num_sims, tree, env_seed, rekey=None):
         recs.append(oracle_record(p, True, a))
         return a
 
-    run_episode(step, env_seed, max_steps=1)
+    run_episode(step, env_seed, max_steps=1, env=env)
     return recs[0], p

@@ -20,6 +20,7 @@
 using namespace pb;
 
 static_assert(sizeof(pomcp_grid) == sizeof(DrvGrid), "grid layout");
+static_assert(sizeof(pomcp_pe_grid) == 1344, "pe grid layout");
 static_assert(sizeof(Line) == 128, "block line layout");
 static_assert(sizeof(OvfSlot) == 32, "overflow slot layout");
 
@@ -35,13 +36,25 @@ struct pomcp_ctx {
   TreeHdr* snap_hdr = nullptr;
   std::vector<int32_t> host_upd;
   std::vector<pomcp_root_stats> host_stats;
-  DrvModel host_model;
+  DrvModel host_drv;      // the configured environment's device tables
+  PeModel host_pe;
+  const void* host_model = nullptr;
+  size_t model_bytes = 0;
 };
 
 static void make_model(const pomcp_grid* g, DrvModel* m) {
   std::memcpy(&m->g, g, sizeof(DrvGrid));
   build_model_tables(m->g, m);
 }
+
+// Launch `KERNEL<Env>` for the context's environment.
+#define PB_ENV_LAUNCH(ctx, KERNEL, grid, block, ...)                                          \
+  do {                                                                                         \
+    if ((ctx)->dp.env == POMCP_ENV_PURSUIT_EVASION)                                            \
+      hipLaunchKernelGGL(KERNEL<EnvPursuitEvasion>, grid, block, 0, (ctx)->stream, __VA_ARGS__); \
+    else                                                                                       \
+      hipLaunchKernelGGL(KERNEL<EnvDriving>, grid, block, 0, (ctx)->stream, __VA_ARGS__);    \
+  } while (0)
 
 #define HIP_TRY(ctx, expr)                                                          \
   do {                                                                              \
@@ -95,8 +108,21 @@ static int validate(const pomcp_config* c, std::string* why) {
     return POMCP_E_INVALID;
   };
   if (c->abi_version != POMCP_ABI_VERSION) return bad("ABI version mismatch");
-  if (c->env_id != POMCP_ENV_DRIVING) { *why = "only Driving-v1 is implemented"; return POMCP_E_UNSUPPORTED; }
-  if (c->num_agents != 2) { *why = "Driving-v1 engine supports 2 agents"; return POMCP_E_UNSUPPORTED; }
+  if (c->env_id != POMCP_ENV_DRIVING && c->env_id != POMCP_ENV_PURSUIT_EVASION) {
+    *why = "env_id: Driving-v1 or PursuitEvasion-v1";
+    return POMCP_E_UNSUPPORTED;
+  }
+  if (c->num_agents != 2) { *why = "the engine's models are 2-agent"; return POMCP_E_UNSUPPORTED; }
+  if (c->num_actions != (c->env_id == POMCP_ENV_DRIVING ? 5 : 4)) return bad("num_actions of the model");
+  if (c->env_id == POMCP_ENV_PURSUIT_EVASION) {
+    const pomcp_pe_grid& g = c->pe_grid;
+    if (g.width < 1 || g.width > 16 || g.height < 1 || g.height > 16) return bad("pe grid size");
+    if (g.n_evader_start < 1 || g.n_evader_start > 4 || g.n_pursuer_start < 1 ||
+        g.n_pursuer_start > 4 || g.n_goal < 1 || g.n_goal > 4)
+      return bad("pe starts / goals (1..4 each)");
+    if (g.max_obs_distance < 0 || g.max_obs_distance > 15) return bad("max_obs_distance 0..15");
+    if (!(g.reward_norm > 0.0)) return bad("reward_norm > 0");
+  }
   if (c->ego_agent < 0 || c->ego_agent >= c->num_agents) return bad("ego_agent out of range");
   if (c->num_actions < 1 || c->num_actions > POMCP_MAX_ACTIONS) return bad("num_actions");
   if (c->action_selection < 0 || c->action_selection > 2) return bad("action_selection");
@@ -119,6 +145,7 @@ static int validate(const pomcp_config* c, std::string* why) {
     return bad("overflow_slots must be a power of two in [16, 2^28]");
   if (!c->log_table || c->log_table_size < 2) return bad("log_table");
   if (!c->discount_pow || c->discount_pow_size < 1) return bad("discount_pow");
+  if (c->env_id != POMCP_ENV_DRIVING) return POMCP_OK;
   const pomcp_grid& g = c->grid;
   if (g.width < 1 || g.width > 16 || g.height < 1 || g.height > 16) return bad("grid size");
   if (g.num_locs < 2 || g.num_locs > 8) return bad("grid locations");
@@ -160,8 +187,17 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
     ctx->own_stream = true;
   }
   const pomcp_config& c = *cfg;
-  make_model(&c.grid, &ctx->host_model);
   DevParams& d = ctx->dp;
+  d.env = c.env_id;
+  if (c.env_id == POMCP_ENV_PURSUIT_EVASION) {
+    build_pe_model(c.pe_grid, &ctx->host_pe);
+    ctx->host_model = &ctx->host_pe;
+    ctx->model_bytes = sizeof(PeModel);
+  } else {
+    make_model(&c.grid, &ctx->host_drv);
+    ctx->host_model = &ctx->host_drv;
+    ctx->model_bytes = sizeof(DrvModel);
+  }
   d.B = c.num_trees;
   d.A = c.num_actions;
   d.ego = c.ego_agent;
@@ -205,7 +241,7 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
   ALLOC(path, uint4, B * 3 * kMaxPath);
   ALLOC(logtab, double, c.log_table_size);
   ALLOC(dpow, double, c.discount_pow_size);
-  ALLOC(model, DrvModel, 1);
+  ALLOC(model, uint8_t, ctx->model_bytes);
   ALLOC(stats, pomcp_root_stats, B);
   ALLOC(merge, double, B * d.A * 2);
   ALLOC(upd_out, int32_t, B * 2);
@@ -224,7 +260,7 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
                      hipMemcpyHostToDevice, s) != hipSuccess ||
       hipMemcpyAsync((void*)d.dpow, c.discount_pow, sizeof(double) * c.discount_pow_size,
                      hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemcpyAsync((void*)d.model, &ctx->host_model, sizeof(DrvModel), hipMemcpyHostToDevice,
+      hipMemcpyAsync((void*)d.model, ctx->host_model, ctx->model_bytes, hipMemcpyHostToDevice,
                      s) != hipSuccess) {
     ctx->err = "initial upload failed";
     pomcp_destroy(ctx);
@@ -310,12 +346,12 @@ int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_key
                               hipMemcpyHostToDevice, ctx->stream));
   // re-root: child lookup per tree, one ordered scan of each search wave's log,
   // then the per-tree update (initial belief / re-root + reinvigoration)
-  hipLaunchKernelGGL(k_reroot_child, dim3(grid_blocks(B)), dim3(256), 0, ctx->stream, ctx->dp);
+  PB_ENV_LAUNCH(ctx, k_reroot_child, dim3(grid_blocks(B)), dim3(256), ctx->dp);
   HIP_TRY(ctx, hipGetLastError());
   hipLaunchKernelGGL(k_extract, dim3(grid_blocks(search_waves(B))), dim3(256), 0, ctx->stream,
                      ctx->dp);
   HIP_TRY(ctx, hipGetLastError());
-  hipLaunchKernelGGL(k_update, dim3(grid_blocks(B)), dim3(256), 0, ctx->stream, ctx->dp);
+  PB_ENV_LAUNCH(ctx, k_update, dim3(grid_blocks(B)), dim3(256), ctx->dp);
   HIP_TRY(ctx, hipGetLastError());
   HIP_TRY(ctx, hipMemcpyAsync(ctx->host_upd.data(), ctx->dp.upd_out, sizeof(int32_t) * 2 * B,
                               hipMemcpyDeviceToHost, ctx->stream));
@@ -329,17 +365,15 @@ int pomcp_search(pomcp_ctx* ctx, int32_t num_sims, int32_t* actions_out) {
   if (!ctx || num_sims < 0) return POMCP_E_INVALID;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   const dim3 grid(search_blocks(ctx->dp.B)), block(kTPB);
-  // kernel per (selection rule, action count): the per-child loops unroll
+  // kernel per (environment, selection rule); the action count is the model's
   using KFn = void (*)(DevParams, int);
-  static const KFn table[3][4] = {
-      {k_search<POMCP_SEL_PUCB, 2>, k_search<POMCP_SEL_PUCB, 3>, k_search<POMCP_SEL_PUCB, 4>,
-       k_search<POMCP_SEL_PUCB, 5>},
-      {k_search<POMCP_SEL_UCB, 2>, k_search<POMCP_SEL_UCB, 3>, k_search<POMCP_SEL_UCB, 4>,
-       k_search<POMCP_SEL_UCB, 5>},
-      {k_search<POMCP_SEL_UNIFORM, 2>, k_search<POMCP_SEL_UNIFORM, 3>,
-       k_search<POMCP_SEL_UNIFORM, 4>, k_search<POMCP_SEL_UNIFORM, 5>}};
-  hipLaunchKernelGGL(table[ctx->dp.sel][ctx->dp.A - 2], grid, block, 0, ctx->stream, ctx->dp,
-                     (int)num_sims);
+  static const KFn table[2][3] = {
+      {k_search<EnvDriving, POMCP_SEL_PUCB, 5>, k_search<EnvDriving, POMCP_SEL_UCB, 5>,
+       k_search<EnvDriving, POMCP_SEL_UNIFORM, 5>},
+      {k_search<EnvPursuitEvasion, POMCP_SEL_PUCB, 4>, k_search<EnvPursuitEvasion, POMCP_SEL_UCB, 4>,
+       k_search<EnvPursuitEvasion, POMCP_SEL_UNIFORM, 4>}};
+  const int e = ctx->dp.env == POMCP_ENV_PURSUIT_EVASION ? 1 : 0;
+  hipLaunchKernelGGL(table[e][ctx->dp.sel], grid, block, 0, ctx->stream, ctx->dp, (int)num_sims);
   HIP_TRY(ctx, hipGetLastError());
   if (!actions_out) return POMCP_OK;
   const int rc = pomcp_get_root_stats(ctx, ctx->host_stats.data());
@@ -412,8 +446,8 @@ int pomcp_root_merge_buffer(pomcp_ctx* ctx, void** device_ptr) {
 int pomcp_synthetic_obs(pomcp_ctx* ctx, uint64_t env_seed_base, uint64_t* obs_keys_out) {
   if (!ctx) return POMCP_E_INVALID;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
-  hipLaunchKernelGGL(k_synthetic_obs, dim3(grid_blocks(ctx->dp.B)), dim3(256), 0, ctx->stream,
-                     ctx->dp, env_seed_base);
+  PB_ENV_LAUNCH(ctx, k_synthetic_obs, dim3(grid_blocks(ctx->dp.B)), dim3(256), ctx->dp,
+                env_seed_base);
   HIP_TRY(ctx, hipGetLastError());
   if (obs_keys_out) {
     HIP_TRY(ctx, hipMemcpyAsync(obs_keys_out, ctx->dp.out_obs, sizeof(uint64_t) * ctx->dp.B,
@@ -504,6 +538,51 @@ int pomcp_driving_obs(const pomcp_grid* g, const uint32_t state[2], uint64_t obs
   make_model(g, &m);
   obs_keys_out[0] = obs_key_fast(m, state[0], state[1]);
   obs_keys_out[1] = obs_key_fast(m, state[1], state[0]);
+  return POMCP_OK;
+}
+
+// ---------------------------------------------------------- host PursuitEvasion
+
+int pomcp_pe_sample_initial_state(const pomcp_pe_grid* g, uint64_t seed, uint32_t tree,
+                                  uint32_t* model_ctr, uint32_t state_out[2]) {
+  if (!g || !model_ctr || !state_out) return POMCP_E_INVALID;
+  PeModel m;
+  build_pe_model(*g, &m);
+  Streams s;
+  s.seed = seed;
+  s.tree = tree;
+  for (int k = 0; k < 5; ++k) s.ctr[k] = 0;
+  s.ctr[2] = *model_ctr;
+  pe_sample_initial_state(m, [&](uint32_t n) { return s.model(n); }, &state_out[0], &state_out[1]);
+  *model_ctr = s.ctr[2];
+  return POMCP_OK;
+}
+
+int pomcp_pe_step(const pomcp_pe_grid* g, const uint32_t state[2], const int32_t actions[2],
+                  uint32_t next_out[2], double rewards_out[2], int32_t terminated_out[2],
+                  uint64_t obs_keys_out[2]) {
+  if (!g || !state || !actions || !next_out || !rewards_out || !terminated_out || !obs_keys_out)
+    return POMCP_E_INVALID;
+  for (int i = 0; i < 2; ++i)
+    if (actions[i] < 0 || actions[i] > 3) return POMCP_E_INVALID;
+  PeModel m;
+  build_pe_model(*g, &m);
+  uint32_t prog, outcome;
+  pe_step(m, state[0], state[1], (uint32_t)actions[0], (uint32_t)actions[1], &next_out[0],
+          &next_out[1], &prog, &outcome);
+  for (int i = 0; i < 2; ++i) {
+    rewards_out[i] = pe_reward(m, i, state[0], prog, outcome);
+    terminated_out[i] = pe_done(next_out[0]) ? 1 : 0;
+    obs_keys_out[i] = pe_obs_key(m, i, next_out[0], next_out[1]);
+  }
+  return POMCP_OK;
+}
+
+int pomcp_pe_obs(const pomcp_pe_grid* g, const uint32_t state[2], uint64_t obs_keys_out[2]) {
+  if (!g || !state || !obs_keys_out) return POMCP_E_INVALID;
+  PeModel m;
+  build_pe_model(*g, &m);
+  for (int i = 0; i < 2; ++i) obs_keys_out[i] = pe_obs_key(m, i, state[0], state[1]);
   return POMCP_OK;
 }
 

@@ -111,7 +111,8 @@ struct DevParams {
   int64_t logtab_n;
   const double* dpow;
   int32_t dpow_n;
-  const DrvModel* model;
+  const void* model;    // Env::Model (envs.h), staged in LDS by every kernel
+  int32_t env;          // pomcp_env
   pomcp_root_stats* stats;
   double* merge;        // [B][A][2]
   int32_t* upd_out;     // [B][2] {root_abs, error}

@@ -13,17 +13,9 @@
 #pragma clang fp contract(off)
 
 #include "pomcp_device.h"
-#include "driving_vec.h"
+#include "envs.h"
 
 namespace pb {
-
-__device__ __forceinline__ void stage_model(const DrvModel* src, DrvModel& dst) {
-  static_assert(sizeof(DrvModel) % 4 == 0, "model size");
-  const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
-  uint32_t* d = reinterpret_cast<uint32_t*>(&dst);
-  for (int i = threadIdx.x; i < (int)(sizeof(DrvModel) / 4); i += blockDim.x) d[i] = s[i];
-  __syncthreads();
-}
 
 __device__ __forceinline__ double hilo(uint32_t lo, uint32_t hi) {
   return __hiloint2double((int)hi, (int)lo);
@@ -47,10 +39,11 @@ struct ChildRef {
   int32_t* blk_ptr;   // where the child's block index lives (for expansion)
 };
 
+template <class Env>
 struct Tree {
+  using Model = typename Env::Model;
   const DevParams& p;
-  const DrvModel& m;
-  const DrvGrid& g;
+  const Model& m;
   int tree, lane;
   Line* an;
   OvfSlot* ovf;
@@ -65,7 +58,7 @@ struct Tree {
   LdsStream r_belief, r_model, r_act0, r_act1;
   int64_t c_levels, c_expand, c_new, c_rollout, c_probes;
 
-  __device__ Tree(const DevParams& pp, const DrvModel& mm, int t) : p(pp), m(mm), g(mm.g), tree(t) {
+  __device__ Tree(const DevParams& pp, const Model& mm, int t) : p(pp), m(mm), tree(t) {
     lane = lane_id();
     an = p.an + (int64_t)t * p.Nb * blk_lines(p.A);
     ovf = p.ovf + (int64_t)t * p.H;
@@ -185,14 +178,17 @@ struct Tree {
     return v;
   }
 
+  // model.step (belief.py:165-170): Driving draws its execution-order shuffle
+  // from the model stream first; the ego's next observation key
   __device__ void joint_step(uint32_t s0, uint32_t s1, int ego_a, int oth_a, uint32_t* n0,
-                             uint32_t* n1) {
-    const uint32_t j = d_model(2);   // Python random.shuffle of the exec order
-    const int a0 = p.ego == 0 ? ego_a : oth_a;
-    const int a1 = p.ego == 0 ? oth_a : ego_a;
-    drv_step2_fast(m, s0, s1, a0, a1, j, n0, n1);
+                             uint32_t* n1, uint64_t* okey) {
+    const uint32_t j = Env::kStepDraws ? d_model(2) : 0u;
+    double r;
+    int done;
+    Env::step(m, p.ego, s0, s1, (uint32_t)ego_a, (uint32_t)oth_a, j, n0, n1, &r, &done);
     *n0 = uniu(*n0);
     *n1 = uniu(*n1);
+    *okey = uni64(Env::obs_key(m, p.ego, *n0, *n1));
   }
 
   // Overflow map (children beyond the kSlots inline ones).
@@ -313,26 +309,13 @@ struct Tree {
     return true;
   }
 
-  // sample_agent_initial_state (oracle/driving.py): ego from its obs, the other
-  // vehicle rejected until the ego window matches (<= 64 tries).
+  // model.sample_agent_initial_state (mcts.py:179-198), model-stream draws
   __device__ bool sample_agent_initial(uint64_t obs, uint32_t* s0, uint32_t* s1) {
-    const int eloc = loc_index(g, (int)((obs >> 32) & 15), (int)((obs >> 36) & 15));
-    const int edest = loc_index(g, (int)((obs >> 40) & 15), (int)((obs >> 44) & 15));
-    if (eloc < 0 || edest < 0) return false;
-    const uint32_t all = (1u << g.num_locs) - 1u;
-    const uint32_t ev = make_vehicle(g, eloc, edest);
-    uint32_t ov = 0;
-    for (int tr = 0; tr < 64; ++tr) {
-      const uint32_t av = all & ~(1u << eloc);
-      const int s = kth_bit(av, d_model((uint32_t)popc8(av)));
-      const uint32_t avd = all & ~(1u << edest) & ~(1u << s);
-      const int d = kth_bit(avd, d_model((uint32_t)popc8(avd)));
-      ov = uniu(make_vehicle(g, s, d));
-      if (uni64(obs_key_fast(m, ev, ov)) == obs) break;
-    }
-    *s0 = p.ego == 0 ? ev : ov;
-    *s1 = p.ego == 0 ? ov : ev;
-    return true;
+    const bool ok = Env::sample_agent_initial(m, p.ego, obs,
+                                              [&](uint32_t n) { return d_model(n); }, s0, s1);
+    *s0 = uniu(*s0);
+    *s1 = uniu(*s1);
+    return ok;
   }
 };
 
@@ -374,12 +357,13 @@ __global__ __launch_bounds__(256) void k_reset(DevParams p) {
 
 // Re-root, step 1 (MCTS._update, mcts.py:236-247): find or create the root's
 // child (action, obs) and publish its log id for k_extract.
+template <class Env>
 __global__ __launch_bounds__(256) void k_reroot_child(DevParams p) {
-  __shared__ DrvModel sm;
+  __shared__ typename Env::Model sm;
   stage_model(p.model, sm);
   const int tree = blockIdx.x * kTreesPerBlock + (threadIdx.x >> 6);
   if (tree >= p.B) return;
-  Tree T(p, sm, tree);
+  Tree<Env> T(p, sm, tree);
   uint32_t want = 0xFFFFFFFFu;
   if (T.err == 0 && !T.root_abs && T.root_t > 0) {
     const int action = uni(p.in_actions[tree]);
@@ -439,13 +423,14 @@ __global__ __launch_bounds__(256) void k_extract(DevParams p) {
   if (valid) p.cnt[tree] = cnt[wi][lane];
 }
 
+template <class Env>
 __global__ __launch_bounds__(256) void k_update(DevParams p) {
-  __shared__ DrvModel sm;
+  __shared__ typename Env::Model sm;
   stage_model(p.model, sm);
   const int tree = blockIdx.x * kTreesPerBlock + (threadIdx.x >> 6);
   if (tree >= p.B) return;
   __shared__ uint32_t rng_lds[kTreesPerBlock][4 * kRngPage];
-  Tree T(p, sm, tree);
+  Tree<Env> T(p, sm, tree);
   T.warm_rng(rng_lds[threadIdx.x >> 6]);
   const int lane = T.lane;
   if (T.err == 0 && !T.root_abs) {   // mcts.py:161-162
@@ -503,9 +488,8 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
                 const uint4 hp = pbel[T.d_belief((uint32_t)T.bsize)];
                 const int ao = (int)T.d_act(p.other, (uint32_t)p.A);
                 uint32_t n0, n1;
-                T.joint_step(uniu(hp.y), uniu(hp.z), action, ao, &n0, &n1);
-                const uint32_t e1 = p.ego == 0 ? n0 : n1, o1 = p.ego == 0 ? n1 : n0;
-                const uint64_t k = uni64(obs_key_fast(sm, e1, o1));
+                uint64_t k;
+                T.joint_step(uniu(hp.y), uniu(hp.z), action, ao, &n0, &n1, &k);
                 const uint4 rec = make_uint4(uniu(hp.x) + 1u, n0, n1, 0u);
                 if (k == obs) {
                   if (lane == 0) nb[n + got] = rec;
@@ -542,10 +526,11 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
   }
 }
 
-// Synthetic Driving-v1 roots: env b0 sample for tree b under key
-// (env_seed_base + b, 0x40000000), ego's initial observation.
+// Synthetic roots: env b0 sample for tree b under key (env_seed_base + b,
+// 0x40000000), the ego's initial observation.
+template <class Env>
 __global__ __launch_bounds__(256) void k_synthetic_obs(DevParams p, uint64_t env_seed_base) {
-  __shared__ DrvModel sm;
+  __shared__ typename Env::Model sm;
   stage_model(p.model, sm);
   const int tree = blockIdx.x * kTreesPerBlock + (threadIdx.x >> 6);
   if (tree >= p.B) return;
@@ -554,9 +539,8 @@ __global__ __launch_bounds__(256) void k_synthetic_obs(DevParams p, uint64_t env
   env.tree = 0x40000000u;
   for (int k = 0; k < 5; ++k) env.ctr[k] = 0;
   uint32_t s0, s1;
-  drv_sample_initial_state2(sm.g, [&](uint32_t n) { return env.model(n); }, &s0, &s1);
-  const uint32_t e = p.ego == 0 ? s0 : s1, o = p.ego == 0 ? s1 : s0;
-  const uint64_t key = obs_key_fast(sm, e, o);
+  Env::sample_initial(sm, [&](uint32_t n) { return env.model(n); }, &s0, &s1);
+  const uint64_t key = Env::obs_key(sm, p.ego, s0, s1);
   if (lane_id() == 0) p.out_obs[tree] = key;
 }
 

@@ -74,10 +74,10 @@ struct PathEntry {
 
 enum : int { TP_LEVEL = 0, TP_ROLL = 1, TP_BACKUP = 2, TP_START = 3, TP_DONE = 4 };
 
-template <int SEL, int NA>
+template <class Env, int SEL, int NA>
 __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
   static_assert(NA >= 2 && NA <= kMaxA, "action count");
-  __shared__ DrvModel sm;
+  __shared__ typename Env::Model sm;
   __shared__ uint4 rc[kRootParts][kTPB];   // the root block of every lane's tree
   stage_model(p.model, sm);
   const int lid = (int)threadIdx.x;
@@ -310,17 +310,9 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
   auto tree_step = [&](int a, uint32_t ao, uint32_t j, uint32_t* n0, uint32_t* n1, double* r,
                        int* done, uint64_t* okey) {
     PT_MARK(15);
-    drv_step2_vec(sm, s0, s1, p.ego == 0 ? (uint32_t)a : ao, p.ego == 0 ? ao : (uint32_t)a, j,
-                  n0, n1);
+    Env::step(sm, p.ego, s0, s1, (uint32_t)a, ao, j, n0, n1, r, done);
     PT_MARK(9);
-    const uint32_t e0 = p.ego == 0 ? s0 : s1;
-    const uint32_t e1 = p.ego == 0 ? *n0 : *n1;
-    const uint32_t o1 = p.ego == 0 ? *n1 : *n0;
-    *r = drv_reward_vec(sm, e0, e1);
-    *done = (((e1 >> 15) & 3u) != 0u ||
-             (((*n0 >> 15) & 3u) != 0u && ((*n1 >> 15) & 3u) != 0u)) ? 1 : 0;
-    PT_MARK(10);
-    *okey = obs_key_vec(sm, e1, o1);
+    *okey = Env::obs_key(sm, p.ego, *n0, *n1);
     PT_MARK(11);
   };
 
@@ -402,7 +394,7 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
           phase = TP_BACKUP;
         } else {
           const uint32_t ao = d_act(p.other, (uint32_t)A);
-          const uint32_t j = d_model(2);
+          const uint32_t j = Env::kStepDraws ? d_model(2) : 0u;
           uint4 st[kMaxA];
 #pragma unroll
           for (int q = 0; q < kMaxA; ++q) st[q] = q < A ? rc[rc_stats(q)][lid] : make_uint4(0, 0, 0, 0);
@@ -469,7 +461,7 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
       if (phase == TP_LEVEL) {
         const uint4* const ap = reinterpret_cast<const uint4*>(an + (int64_t)blk * blk_bytes);
         const uint32_t ao = d_act(p.other, (uint32_t)A);
-        const uint32_t j = d_model(2);
+        const uint32_t j = Env::kStepDraws ? d_model(2) : 0u;
         PT_MARK(8);
         uint4 st[kMaxA];   // prefetched by descend()
   #pragma unroll
@@ -554,19 +546,17 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
       } else {
         const uint32_t ae = d_act(p.ego, (uint32_t)A);       // search_policy.py:177
         const uint32_t ao = d_act(p.other, (uint32_t)A);     // other_policy.py:151
-        const uint32_t j = d_model(2);
+        const uint32_t j = Env::kStepDraws ? d_model(2) : 0u;
         uint32_t n0, n1;
-        drv_step2_vec(sm, s0, s1, p.ego == 0 ? ae : ao, p.ego == 0 ? ao : ae, j, &n0, &n1);
-        const uint32_t e0 = p.ego == 0 ? s0 : s1, e1 = p.ego == 0 ? n0 : n1;
-        const double r = drv_reward_vec(sm, e0, e1);
+        double r;
+        int dn;
+        Env::step(sm, p.ego, s0, s1, ae, ao, j, &n0, &n1, &r, &dn);
         if (k >= p.dpow_n) {
           err = POMCP_E_ARENA;
           phase = TP_DONE;
         } else {
           ret += p.dpow[k] * r;   // mcts.py:420-422
           ++c_rollout;
-          const bool dn = ((e1 >> 15) & 3u) != 0u ||
-                          (((n0 >> 15) & 3u) != 0u && ((n1 >> 15) & 3u) != 0u);
           if (dn) {
             phase = TP_BACKUP;
           } else {
@@ -754,14 +744,12 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
   so->pad = 0;
 }
 
-#define PB_SEARCH_INST(NA)                                                 \
-  template __global__ void k_search<POMCP_SEL_PUCB, NA>(DevParams, int);  \
-  template __global__ void k_search<POMCP_SEL_UCB, NA>(DevParams, int);   \
-  template __global__ void k_search<POMCP_SEL_UNIFORM, NA>(DevParams, int);
-PB_SEARCH_INST(2)
-PB_SEARCH_INST(3)
-PB_SEARCH_INST(4)
-PB_SEARCH_INST(5)
+#define PB_SEARCH_INST(E, NA)                                                 \
+  template __global__ void k_search<E, POMCP_SEL_PUCB, NA>(DevParams, int);  \
+  template __global__ void k_search<E, POMCP_SEL_UCB, NA>(DevParams, int);   \
+  template __global__ void k_search<E, POMCP_SEL_UNIFORM, NA>(DevParams, int);
+PB_SEARCH_INST(EnvDriving, 5)
+PB_SEARCH_INST(EnvPursuitEvasion, 4)
 #undef PB_SEARCH_INST
 
 }  // namespace pb

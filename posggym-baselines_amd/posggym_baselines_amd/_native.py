@@ -11,7 +11,7 @@ import os
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.environ.get("POMCP_LIB_PATH") or os.path.join(LIB_DIR, "libpomcp_hip.so")
 
-POMCP_ABI_VERSION = 1
+POMCP_ABI_VERSION = 2
 POMCP_MAX_ACTIONS = 8
 
 POMCP_OK = 0
@@ -25,6 +25,7 @@ POMCP_E_NO_DEVICE = -7
 
 SEL_PUCB, SEL_UCB, SEL_UNIFORM = 0, 1, 2
 ENV_DRIVING = 1
+ENV_PURSUIT_EVASION = 2
 
 STATUS_NAMES = {
     POMCP_E_INVALID: "POMCP_E_INVALID",
@@ -51,6 +52,25 @@ class PomcpGrid(C.Structure):
         ("obs_back", C.c_int32),
         ("obs_side", C.c_int32),
         ("pad", C.c_int32 * 2),
+    ]
+
+
+class PomcpPeGrid(C.Structure):
+    _fields_ = [
+        ("wall", C.c_uint8 * 256),
+        ("goal_dist", (C.c_uint8 * 256) * 4),
+        ("evader_start", (C.c_uint8 * 2) * 4),
+        ("pursuer_start", (C.c_uint8 * 2) * 4),
+        ("goal", (C.c_uint8 * 2) * 4),
+        ("width", C.c_int32),
+        ("height", C.c_int32),
+        ("n_evader_start", C.c_int32),
+        ("n_pursuer_start", C.c_int32),
+        ("n_goal", C.c_int32),
+        ("max_obs_distance", C.c_int32),
+        ("use_progress_reward", C.c_int32),
+        ("pad", C.c_int32),
+        ("reward_norm", C.c_double),
     ]
 
 
@@ -86,6 +106,7 @@ class PomcpConfig(C.Structure):
         ("discount_pow", C.POINTER(C.c_double)),
         ("discount_pow_size", C.c_int64),
         ("grid", PomcpGrid),
+        ("pe_grid", PomcpPeGrid),
     ]
 
 
@@ -143,6 +164,10 @@ SIGNATURES = [
     ("pomcp_driving_step", C.c_int,
      [C.POINTER(PomcpGrid), C.c_uint64, C.c_uint32, _PU32, _PU32, _P32, _PU32, _PD, _P32, _PU64]),
     ("pomcp_driving_obs", C.c_int, [C.POINTER(PomcpGrid), _PU32, _PU64]),
+    ("pomcp_pe_sample_initial_state", C.c_int,
+     [C.POINTER(PomcpPeGrid), C.c_uint64, C.c_uint32, _PU32, _PU32]),
+    ("pomcp_pe_step", C.c_int, [C.POINTER(PomcpPeGrid), _PU32, _P32, _PU32, _PD, _P32, _PU64]),
+    ("pomcp_pe_obs", C.c_int, [C.POINTER(PomcpPeGrid), _PU32, _PU64]),
 ]
 DEBUG_SIGNATURES = [
     ("pomcp_debug_fp_selftest", C.c_int, [_PD, _PD, C.c_int32, _PD]),

@@ -163,6 +163,12 @@ class DrivingModel:
             self._grid = g
         return self._grid
 
+    def configure_engine(self, cfg):
+        """Fill the environment part of a ``pomcp_config``."""
+        from posggym_baselines_amd._native import ENV_DRIVING
+        cfg.env_id = ENV_DRIVING
+        cfg.grid = self.pomcp_grid()
+
     def obs_key(self, obs) -> int:
         return obs if isinstance(obs, (int, np.integer)) else pack_obs(obs)
 

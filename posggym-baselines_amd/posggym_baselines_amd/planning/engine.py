@@ -68,10 +68,10 @@ class PomcpEngine:
     def __init__(self, model, agent_id, config, num_trees=1, capacities=None, num_sims=None,
                  searches=None, device=None, stream=None, tree_key_base=0, seed=None):
         lib = N.load()
-        if not hasattr(model, "pomcp_grid"):
+        if not hasattr(model, "configure_engine"):
             raise NotImplementedError(
                 f"{type(model).__name__} has no GPU generative model; the engine implements "
-                "Driving-v1 (posggym_baselines_amd.envs.DrivingModel)")
+                "Driving-v1 and PursuitEvasion-v1 (posggym_baselines_amd.envs)")
         if config.truncated and not config.use_rollout_if_no_value:
             raise NotImplementedError("truncated search needs a value function (none on GPU)")
         self.model = model
@@ -95,7 +95,6 @@ class PomcpEngine:
         self.capacities = capacities
         c = N.PomcpConfig()
         c.abi_version = N.POMCP_ABI_VERSION
-        c.env_id = N.ENV_DRIVING
         c.num_agents = len(model.possible_agents)
         c.ego_agent = self.ego
         c.num_actions = self.A
@@ -132,7 +131,7 @@ class PomcpEngine:
         c.log_table_size = len(self._logtab)
         c.discount_pow = self._dpow.ctypes.data_as(C.POINTER(C.c_double))
         c.discount_pow_size = len(self._dpow)
-        c.grid = model.pomcp_grid()
+        model.configure_engine(c)
         self._cfg = c
         dev = config.device if device is None else device
         ctx = C.c_void_p()

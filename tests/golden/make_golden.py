@@ -26,7 +26,7 @@ TEST_CFG = dict(discount=0.95, search_time_limit=0.1, c=SQRT2, truncated=False,
                 step_limit=None, epsilon=0.92, seed=0, state_belief_only=True)
 
 CASES = {
-    # name: (cfg overrides, num_sims, [(planner seed, env seed)], ego, max_steps)
+    # name: (cfg overrides, num_sims, [(planner seed, env seed)], ego, max_steps[, env])
     "c1_ucb": ({}, 128, [(0, 0), (1, 1), (2, 2)], "0", 50),
     "c1_pucb": ({"action_selection": "pucb"}, 128, [(0, 3), (4, 4)], "0", 50),
     "uniform": ({"action_selection": "uniform"}, 64, [(5, 5)], "0", 50),
@@ -34,18 +34,23 @@ CASES = {
     "known_bounds": ({"known_bounds": (-1.0, 1.0)}, 96, [(7, 7)], "0", 50),
     "ego1_ucb": ({}, 96, [(8, 8)], "1", 50),
     "large_first_step": ({}, 2048, [(9, 9), (10, 10)], "0", 1),
+    # BASELINE config 3: PursuitEvasion-v1 (16x16, max_obs_distance 12, progress reward)
+    "pe_evader_ucb": ({}, 128, [(11, 11), (12, 12)], "0", 100, "PursuitEvasion-v1"),
+    "pe_pursuer_pucb": ({"action_selection": "pucb"}, 96, [(13, 13)], "1", 100,
+                        "PursuitEvasion-v1"),
 }
 
 
 def run_case(name):
-    over, num_sims, pairs, ego, max_steps = CASES[name]
-    out = {"case": name, "num_sims": num_sims, "ego": ego, "episodes": []}
+    over, num_sims, pairs, ego, max_steps = CASES[name][:5]
+    env = CASES[name][5] if len(CASES[name]) > 5 else "Driving-v1"
+    out = {"case": name, "env": env, "num_sims": num_sims, "ego": ego, "episodes": []}
     for seed, env_seed in pairs:
         cfg = dict(TEST_CFG)
         cfg.update(over)
         cfg["seed"] = seed
-        tr, rr = reference_episode(cfg, num_sims, env_seed, ego=ego, max_steps=max_steps)
-        to, ro = oracle_episode(cfg, num_sims, env_seed, ego=ego, max_steps=max_steps)
+        tr, rr = reference_episode(cfg, num_sims, env_seed, ego=ego, max_steps=max_steps, env=env)
+        to, ro = oracle_episode(cfg, num_sims, env_seed, ego=ego, max_steps=max_steps, env=env)
         if tr != to or rr != ro:
             raise SystemExit(f"oracle disagrees with reference in case {name} seed {seed}")
         cfg_json = dict(cfg)

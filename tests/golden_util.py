@@ -4,7 +4,17 @@ import os
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 EPISODE_CASES = ["c1_ucb", "c1_pucb", "uniform", "deep_ucb", "known_bounds", "ego1_ucb",
-                 "large_first_step"]
+                 "large_first_step", "pe_evader_ucb", "pe_pursuer_pucb"]
+
+
+def case_env(data):
+    return data.get("env", "Driving-v1")
+
+
+def case_max_steps(case, data):
+    if case == "large_first_step":
+        return 1
+    return 100 if case_env(data) == "PursuitEvasion-v1" else 50
 
 
 def load(name):

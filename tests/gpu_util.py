@@ -1,6 +1,8 @@
 """Drive the product (GPU) planner in the oracle's record format."""
-from oracle.episode import belief_digest, fhex, run_episode
-from oracle.driving import unpack_vehicle
+import hashlib
+import struct
+
+from oracle.episode import fhex, run_episode
 
 
 def product_config(cfg_kwargs, num_sims):
@@ -12,8 +14,17 @@ def product_config(cfg_kwargs, num_sims):
 
 
 def rows_digest(rows):
-    parts = [((unpack_vehicle(int(v0)), unpack_vehicle(int(v1))), int(t)) for t, v0, v1 in rows]
-    return len(parts), belief_digest(parts)
+    """(size, sha1 over (t, v0, v1) u32 triples): oracle.episode.belief_digest of
+    the packed particle words."""
+    h = hashlib.sha1()
+    for t, v0, v1 in rows:
+        h.update(struct.pack("<III", int(t), int(v0), int(v1)))
+    return len(rows), h.hexdigest()
+
+
+def product_model(env):
+    from posggym_baselines_amd.envs import DrivingModel, PursuitEvasionModel
+    return PursuitEvasionModel() if env == "PursuitEvasion-v1" else DrivingModel()
 
 
 def stats_record(st, A, searched, action, rows):
@@ -33,10 +44,9 @@ def stats_record(st, A, searched, action, rows):
     return rec
 
 
-def gpu_episode(cfg_kwargs, num_sims, env_seed, ego="0", max_steps=50):
-    from posggym_baselines_amd.envs import DrivingModel
+def gpu_episode(cfg_kwargs, num_sims, env_seed, ego="0", max_steps=50, env="Driving-v1"):
     from posggym_baselines_amd.planning import POMCP, RandomSearchPolicy
-    model = DrivingModel()
+    model = product_model(env)
     planner = POMCP(model, ego, product_config(cfg_kwargs, num_sims),
                     RandomSearchPolicy(model, ego))
     planner.reset()
@@ -60,7 +70,7 @@ def gpu_episode(cfg_kwargs, num_sims, env_seed, ego="0", max_steps=50):
         records.append(rec)
         return a
 
-    trace = run_episode(step, env_seed, ego=ego, max_steps=max_steps)
+    trace = run_episode(step, env_seed, ego=ego, max_steps=max_steps, env=env)
     planner.close()
     return trace, records
 

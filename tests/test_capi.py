@@ -39,6 +39,7 @@ def test_struct_layout_matches_header(tmp_path):
         "pomcp_config": [f[0] for f in N.PomcpConfig._fields_],
         "pomcp_root_stats": [f[0] for f in N.PomcpRootStats._fields_],
         "pomcp_grid": [f[0] for f in N.PomcpGrid._fields_],
+        "pomcp_pe_grid": [f[0] for f in N.PomcpPeGrid._fields_],
     }
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "pomcp.h"', "int main(void){"]
     for st, fs in fields.items():
@@ -53,7 +54,7 @@ def test_struct_layout_matches_header(tmp_path):
     out = dict(line.rsplit(" ", 1) for line in subprocess.run(
         [str(exe)], check=True, capture_output=True, text=True).stdout.split("\n") if line)
     for st, cls in (("pomcp_config", N.PomcpConfig), ("pomcp_root_stats", N.PomcpRootStats),
-                    ("pomcp_grid", N.PomcpGrid)):
+                    ("pomcp_grid", N.PomcpGrid), ("pomcp_pe_grid", N.PomcpPeGrid)):
         assert int(out[st]) == ctypes.sizeof(cls), st
         for f in fields[st]:
             assert int(out[f"{st}.{f}"]) == getattr(cls, f).offset, f"{st}.{f}"

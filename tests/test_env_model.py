@@ -47,3 +47,52 @@ def test_grid_tables_match_oracle():
         g = Grid(rows)
         assert (w, h, locs, dirs) == (g.width, g.height, g.locs, g.init_dir)
         assert dist == g.dist
+
+
+@pytest.mark.parametrize("grid", ["16x16", "8x8"])
+def test_host_pursuit_evasion_matches_oracle(grid):
+    """Host build of csrc/pursuit_evasion.h against oracle/pursuit_evasion.py:
+    states, rewards (bit-exact FP64), terminations and both agents' obs."""
+    from oracle.pursuit_evasion import PursuitEvasionModel as OraclePE
+    from oracle.pursuit_evasion import pack_obs as pe_pack_obs, pack_state_words
+    from posggym_baselines_amd.envs import PursuitEvasionModel
+    from posggym_baselines_amd.envs.pursuit_evasion import pack_obs as product_pe_pack
+    n_done = 0
+    for seed in range(60):
+        om = OraclePE(Streams(seed, ENV_TREE_BASE), grid=grid)
+        pm = PursuitEvasionModel(grid=grid, seed=seed)
+        assert pm.reward_norm == om.reward_norm
+        os_ = om.sample_initial_state()
+        ps = pm.sample_initial_state()
+        assert ps == pack_state_words(os_)
+        oo, po = om.sample_initial_obs(os_), pm.sample_initial_obs(ps)
+        assert {k: pe_pack_obs(v) for k, v in oo.items()} == {k: product_pe_pack(v) for k, v in po.items()}
+        act = Streams(seed + 999, 5)
+        for t in range(100):
+            acts = {"0": act.randint(8, 4), "1": act.randint(9, 4)}
+            ots, pts = om.step(os_, acts), pm.step(ps, acts)
+            assert pts.state == pack_state_words(ots.state), (seed, t)
+            assert [x.hex() for x in pts.rewards.values()] == [x.hex() for x in ots.rewards.values()]
+            assert pts.terminations == ots.terminations and pts.all_done == ots.all_done
+            for a in ("0", "1"):
+                assert pts.observations[a] == ots.observations[a], (seed, t, a)
+            os_, ps = ots.state, pts.state
+            if ots.all_done:
+                n_done += 1
+                break
+    assert n_done > 0
+
+
+def test_pursuit_evasion_agent_initial_state_consistent():
+    """sample_agent_initial_state returns states whose ego obs equals the given
+    obs whenever the draws allow (rejection bound 64)."""
+    from oracle.pursuit_evasion import PursuitEvasionModel as OraclePE
+    for ego in ("0", "1"):
+        hits = 0
+        for seed in range(40):
+            m = OraclePE(Streams(seed, 3))
+            st = m.sample_initial_state()
+            obs = m.sample_initial_obs(st)[ego]
+            s2 = m.sample_agent_initial_state(ego, obs)
+            hits += m.sample_initial_obs(s2)[ego] == obs
+        assert hits >= 38

@@ -1,7 +1,7 @@
 """Oracle pinning: the CPU restatement against the reference's golden vectors."""
 import pytest
 
-from golden_util import EPISODE_CASES, cfg_kwargs, load
+from golden_util import EPISODE_CASES, case_env, case_max_steps, cfg_kwargs, load
 from oracle.pomcp import OracleConfig
 from oracle.rng import Streams, StreamRandom, philox4x32_10
 from oracle.run import oracle_episode
@@ -61,9 +61,9 @@ def test_oracle_matches_reference_goldens(case):
     data = load(case)
     for ep in data["episodes"]:
         kw = cfg_kwargs(ep["config"])
-        max_steps = 1 if case == "large_first_step" else 50
         trace, records = oracle_episode(kw, data["num_sims"], ep["env_seed"], ego=data["ego"],
-                                        max_steps=max_steps)
+                                        max_steps=case_max_steps(case, data),
+                                        env=case_env(data))
         assert trace == ep["trace"]
         assert len(records) == len(ep["records"])
         for t, (got, exp) in enumerate(zip(records, ep["records"])):
