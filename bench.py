@@ -26,8 +26,17 @@ for _p in (ROOT, os.path.join(ROOT, "posggym-baselines_amd")):
         sys.path.insert(0, _p)
 
 # algorithmic HBM bytes (DESIGN.md "Algorithmic bytes"): per simulation, per
-# tree level stepped, per leaf expansion, per obs node created
-B_SIM, B_LEVEL, B_EXPAND, B_NEW_NODE = 16, 168, 144, 28
+# tree level stepped (node 8 + A x 12 child statistics + 100), per leaf expansion
+# (A x 28 + 4), per obs node created
+B_SIM, B_NEW_NODE = 16, 28
+
+
+def b_level(A):
+    return 8 + 12 * A + 100
+
+
+def b_expand(A):
+    return 28 * A + 4
 HBM_PEAK_GBS = 8000.0
 
 
@@ -42,6 +51,8 @@ def parse():
     ap.add_argument("--max-blocks", type=int, default=512,
                     help="per-tree action-block arena; a depth-2 Driving-v1 tree uses ~170 "
                          "(overflow is detected and fails the run)")
+    ap.add_argument("--env", default="Driving-v1", choices=["Driving-v1", "PursuitEvasion-v1"],
+                    help="Driving-v1 is BASELINE.json's metric; PursuitEvasion-v1 is config 3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-sims", type=int, default=16384)
     ap.add_argument("--cpu-sample-trees", type=int, default=4)
@@ -53,7 +64,7 @@ TEST_CFG = dict(discount=0.95, search_time_limit=0.1, c=math.sqrt(2), truncated=
                 step_limit=None, epsilon=0.92, state_belief_only=True)
 
 
-def cpu_baseline(sims, trees, seed):
+def cpu_baseline(sims, trees, seed, env="Driving-v1"):
     """The oracle (pure-Python restatement of the reference planner, pinned to it by
     tests/golden) timed on one host core over a bounded sample of the same workload."""
     from oracle.episode import run_episode
@@ -61,7 +72,7 @@ def cpu_baseline(sims, trees, seed):
     cfg = dict(TEST_CFG, seed=seed)
     t_search = 0.0
     for b in range(trees):
-        p = make_oracle(cfg, sims, tree=b)
+        p = make_oracle(cfg, sims, tree=b, env=env)
 
         def step(obs, p=p):
             nonlocal t_search
@@ -71,7 +82,7 @@ def cpu_baseline(sims, trees, seed):
             t_search += time.perf_counter() - t0
             return a
 
-        run_episode(step, 1000 + b, max_steps=1)
+        run_episode(step, 1000 + b, max_steps=1, env=env)
     return {"value": sims * trees / t_search, "unit": "simulations/s", "cores": 1, "kind": "port",
             "sample": f"{trees} roots x {sims} sims (get_action only), oracle/pomcp.py, 1 thread"}
 
@@ -97,14 +108,14 @@ def main():
         nb.build()
     if world > 1:
         dist.barrier()
-    from posggym_baselines_amd.envs import DrivingModel
+    from posggym_baselines_amd.envs import DrivingModel, PursuitEvasionModel
     from posggym_baselines_amd.planning import BatchedPOMCP, MCTSConfig
     from posggym_baselines_amd.planning.engine import plan_capacities
     from posggym_baselines_amd.planning.parallel import merge_buffer_tensor, root_parallel_merge
 
     B, S = args.trees, args.sims
     cfg = MCTSConfig(seed=args.seed, num_sims=S, **TEST_CFG)
-    model = DrivingModel()
+    model = PursuitEvasionModel() if args.env == "PursuitEvasion-v1" else DrivingModel()
     caps = plan_capacities(cfg, model.spec.max_episode_steps, S, 1, reroot=False,
                            max_blocks=min(args.max_blocks, S + 64),
                            overflow_slots=1024)
@@ -152,7 +163,7 @@ def main():
     levels = sum(s.n_levels for s in st)
     expands = sum(s.n_expansions for s in st)
     new_nodes = sum(s.n_new_nodes for s in st)
-    alg_bytes = B_SIM * sims + B_LEVEL * levels + B_EXPAND * expands + B_NEW_NODE * new_nodes
+    alg_bytes = B_SIM * sims + b_level(A) * levels + b_expand(A) * expands + B_NEW_NODE * new_nodes
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     total_sims = world * B * S * args.steps
     value = total_sims / elapsed
@@ -161,12 +172,15 @@ def main():
     if os.path.exists(prof):
         try:
             pm = json.load(open(prof))
-            if pm.get("trees") == B and pm.get("sims") == S:
+            if (pm.get("trees") == B and pm.get("sims") == S
+                    and pm.get("env", "Driving-v1") == args.env):
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    env_desc = ("PursuitEvasion-v1 16x16 max_obs_distance=12" if args.env == "PursuitEvasion-v1"
+                else "Driving-v1 14x14RoundAbout")
     out = {
-        "metric": "MCTS simulations/sec on Driving-v1 (POMCP exact search)",
+        "metric": f"MCTS simulations/sec on {args.env} (POMCP exact search)",
         "value": value,
         "unit": "simulations/s",
         "n_gpus": world,
@@ -177,8 +191,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic Driving-v1 belief states (env seed 1000+b), build's Driving-v1 restatement",
-        "config": {"workload": f"POMCP Driving-v1 14x14RoundAbout exact search, {B} roots x {S} "
+        "data": f"synthetic {args.env} belief states (env seed 1000+b), build's {args.env} "
+                "restatement",
+        "config": {"workload": f"POMCP {env_desc} exact search, {B} roots x {S} "
                                f"sims per GPU, ucb c=sqrt2 gamma=0.95 depth_limit=2, root-parallel "
                                f"all-reduce over {world} GPU(s)",
                    "trees_per_gpu": B, "sims_per_tree": S, "depth_limit": cfg.depth_limit,
@@ -193,7 +208,8 @@ def main():
                      "alg_bytes_per_launch": alg_bytes},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_sample_sims, args.cpu_sample_trees, args.seed)
+        out["cpu_baseline"] = cpu_baseline(args.cpu_sample_sims, args.cpu_sample_trees, args.seed,
+                                           args.env)
     if rank == 0:
         print(json.dumps(out), flush=True)
     bp.close()
