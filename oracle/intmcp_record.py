@@ -1,0 +1,54 @@
+"""Per-step record of an I-NTMCP planner (shared by the reference harness, the
+oracle and the GPU tests).  TEST INFRASTRUCTURE (see ``oracle/__init__.py``).
+
+Hashes cover the level-1 root's particles (t, state words, the other agent's
+history as (action | -1, obs key) steps) and, for each distinct other-agent
+history in that belief (first-occurrence order), the level-0 node's visits,
+registered children (registration order) and particles."""
+import hashlib
+import json
+import struct
+
+
+def _fhex(x):
+    return float(x).hex()
+
+
+def hist_digest(h):
+    m = hashlib.sha1()
+    for a, k in h:
+        m.update(struct.pack("<iQ", a, k))
+    return m.hexdigest()
+
+
+def intmcp_record(rec, num_sims, search_depth, root_visits, kids, mn, mx, parts, nested_nodes,
+                  full=False):
+    rec["num_sims"] = num_sims
+    if num_sims > 0:
+        rec["search_depth"] = search_depth
+        rec["root_visits"] = int(root_visits)
+        rec["children"] = [[a, int(v), _fhex(val), _fhex(tot)] for a, v, val, tot in kids]
+        rec["min_value"] = _fhex(mn)
+        rec["max_value"] = _fhex(mx)
+    m = hashlib.sha1()
+    for t, (v0, v1), h in parts:
+        m.update(struct.pack("<III", t, v0, v1))
+        m.update(hist_digest(h).encode())
+    rec["belief_size"] = len(parts)
+    rec["belief_digest"] = m.hexdigest()
+    out = []
+    for h, node in nested_nodes:
+        if node is None:
+            out.append([hist_digest(h), None])
+            continue
+        visits, nkids, nparts = node
+        mm = hashlib.sha1()
+        for t, (v0, v1) in nparts:
+            mm.update(struct.pack("<III", t, v0, v1))
+        out.append([hist_digest(h), int(visits),
+                    [[a, int(v), _fhex(val)] for a, v, val in nkids], len(nparts), mm.hexdigest()])
+    rec["nested_count"] = len(out)
+    rec["nested_digest"] = hashlib.sha1(json.dumps(out, separators=(",", ":")).encode()).hexdigest()
+    if full:
+        rec["nested"] = out
+    return rec

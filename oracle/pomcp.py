@@ -41,7 +41,7 @@ class OracleConfig:
         self.step_limit = step_limit
         self.epsilon = epsilon
         self.seed = seed
-        self.state_belief_only = True
+        self.state_belief_only = state_belief_only
         self.num_sims = num_sims
         # config.py:461-469
         self.num_particles = math.ceil(100 * search_time_limit)

@@ -65,7 +65,8 @@ def import_reference():
     mod("posggym.agents.utils.action_distributions", DiscreteActionDistribution=_Any)
     pg.utils = mod("posggym.utils")
     pg.utils.__path__ = []
-    mod("posggym.utils.history", JointHistory=_Any, AgentHistory=_Any)
+    from oracle.history import AgentHistory, JointHistory
+    mod("posggym.utils.history", JointHistory=JointHistory, AgentHistory=AgentHistory)
     mod("posggym_baselines.ppo").__path__ = [os.path.join(REF_ROOT, "posggym_baselines", "ppo")]
     if REF_ROOT not in sys.path:
         sys.path.insert(0, REF_ROOT)
@@ -167,5 +168,130 @@ def reference_episode(cfg_kwargs, num_sims, env_seed, ego="0", grid=None,
         return a
 
     trace = run_episode(step, env_seed, ego=ego, grid=grid, max_steps=max_steps, env=env)
+    planner.close()
+    return trace, records
+
+
+# ----------------------------------------------------------------- I-NTMCP
+def make_reference_intmcp(model, agent_id, cfg_kwargs, num_sims, streams):
+    """``INTMCP.initialize(model, agent_id, config, 1, None)`` wired to ``streams``
+    with ``num_sims`` simulations per nesting level (intmcp.py:385-399: the
+    wrapped top-level ``_nested_sim`` jumps the fake clock after num_sims calls).
+    ``random.Random(seed)`` is called once per planner, the nested planner first
+    (intmcp.py:964-986): first call -> S_BELIEF_NESTED, second -> S_BELIEF."""
+    P = import_reference()
+    import posggym_baselines.planning.intmcp as im
+    import posggym_baselines.planning.belief as B
+    from oracle.intmcp import S_BELIEF_NESTED
+    from oracle.rng import S_BELIEF, S_SELECT, StreamRandom
+
+    select = StreamRandom(streams, S_SELECT)
+    order = [StreamRandom(streams, S_BELIEF_NESTED), StreamRandom(streams, S_BELIEF)]
+    made = []
+
+    def new_random(seed=None):
+        r = order[len(made)]
+        made.append(r)
+        return r
+
+    rnd = types.ModuleType("random_shim")
+    rnd.Random = new_random
+    rnd.choice = select.choice
+    rnd.choices = select.choices
+    rnd.random = select.random
+    im.random = rnd
+    B.random = rnd
+    clock = _FakeClock()
+    im.time = clock
+    from posggym_baselines.planning.utils import KnownBounds
+    kw = dict(cfg_kwargs)
+    if kw.get("known_bounds") is not None:
+        kw["known_bounds"] = KnownBounds(*kw["known_bounds"])
+    config = P.MCTSConfig(**kw)
+    planner = P.INTMCP.initialize(model, agent_id, config, nesting_level=1, search_policies=None)
+    assert len(made) == 2
+    inner = planner._nested_sim
+    count = [0]
+
+    def nested_sim(history, search_level, top_level=False):
+        r = inner(history, search_level, top_level)
+        if top_level:
+            count[0] += 1
+            if count[0] >= num_sims:
+                clock.now += 1e9
+                count[0] = 0
+        return r
+
+    planner._nested_sim = nested_sim
+    return planner
+
+
+def _hist_key(model, agent_hist):
+    return tuple((-1 if a is None else int(a), model.pack_obs(o)) for a, o in agent_hist)
+
+
+def _walk(root, agent_hist):
+    node = root
+    for a, o in agent_hist:
+        an = node.children.get(a)
+        if an is None:
+            return None
+        node = an.children.get(o)
+        if node is None:
+            return None
+    return node
+
+
+def reference_intmcp_record(planner, searched, action):
+    from oracle.intmcp_record import intmcp_record
+    model = planner.model
+    rec = {"searched": searched, "action": int(action)}
+    if not searched:
+        return rec
+    root = _walk(planner.root, planner.history)
+    other = [i for i in model.possible_agents if i != planner.agent_id][0]
+    nested = planner.other_agent_policies[other]
+    parts = [(p.t, model.pack_words(p.state), _hist_key(model, p.history.get_agent_history(other)))
+             for p in root.belief.particles]
+    kids = [(int(c.action), c.visits, c.value, c.total_value) for c in root.get_child_nodes()]
+    nested_nodes = []
+    seen = []
+    for p in root.belief.particles:
+        h = p.history.get_agent_history(other)
+        if h in seen:
+            continue
+        seen.append(h)
+        n = _walk(nested.root, h)
+        if n is None:
+            nested_nodes.append((_hist_key(model, h), None))
+            continue
+        nparts = [(q.t, model.pack_words(q.state)) for q in n.belief.particles]
+        nkids = [(int(c.action), c.visits, c.value) for c in n.get_child_nodes()]
+        nested_nodes.append((_hist_key(model, h), (n.visits, nkids, nparts)))
+    st = planner.step_statistics
+    return intmcp_record(rec, int(st["num_sims"]), int(st["search_depth"]), root.visits, kids,
+                         st["min_value"], st["max_value"], parts, nested_nodes)
+
+
+def reference_intmcp_episode(cfg_kwargs, num_sims, env_seed, ego="0", tree=0, max_steps=50,
+                             env="Driving-v1"):
+    from oracle.envs import make_model
+    from oracle.episode import run_episode
+    from oracle.rng import Streams
+
+    streams = Streams(cfg_kwargs.get("seed") or 0, tree)
+    model = make_model(env, streams)
+    planner = make_reference_intmcp(model, ego, cfg_kwargs, num_sims, streams)
+    planner.reset()
+    records = []
+
+    def step(obs):
+        root = _walk(planner.root, planner.history)
+        searched = not root.is_absorbing
+        a = planner.step(obs)
+        records.append(reference_intmcp_record(planner, searched, a))
+        return a
+
+    trace = run_episode(step, env_seed, ego=ego, max_steps=max_steps, env=env)
     planner.close()
     return trace, records

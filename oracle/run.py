@@ -67,3 +67,51 @@ def oracle_first_step(cfg_kwargs, num_sims, tree, env_seed, rekey=None, env="Dri
 
     run_episode(step, env_seed, max_steps=1, env=env)
     return recs[0], p
+
+
+# ----------------------------------------------------------------- I-NTMCP
+def make_oracle_intmcp(cfg_kwargs, num_sims, ego="0", tree=0, env="Driving-v1"):
+    from oracle.intmcp import OracleINTMCP
+    streams = Streams(cfg_kwargs.get("seed") or 0, tree)
+    model = make_model(env, streams)
+    cfg = OracleConfig(num_sims=num_sims, **cfg_kwargs)
+    return OracleINTMCP(model, ego, cfg, streams)
+
+
+def oracle_intmcp_record(p, searched, action):
+    from oracle.intmcp_record import intmcp_record
+    rec = {"searched": searched, "action": int(action)}
+    if not searched:
+        return rec
+    top, nested = p.top, p.nested
+    tr, n = top.tree, top.cur
+    parts = [(q[2], p.model.pack_words(q[0]), p.history(nested.tree, q[1])) for q in tr.belief[n]]
+    kids = [(a,) + tuple(tr.stats[(n, a)][:3]) for a in tr.order[n]]
+    nested_nodes, seen = [], []
+    for q in tr.belief[n]:
+        if q[1] in seen:
+            continue
+        seen.append(q[1])
+        nt = nested.tree
+        m = q[1]
+        nkids = [(a, nt.stats[(m, a)][0], nt.stats[(m, a)][1]) for a in nt.order[m]]
+        nparts = [(r[1], p.model.pack_words(r[0])) for r in nt.belief[m]]
+        nested_nodes.append((p.history(nt, m), (nt.visits[m], nkids, nparts)))
+    return intmcp_record(rec, top.num_sims, top.search_depth, tr.visits[n], kids,
+                         top.mm_min, top.mm_max, parts, nested_nodes)
+
+
+def oracle_intmcp_episode(cfg_kwargs, num_sims, env_seed, ego="0", tree=0, max_steps=50,
+                          env="Driving-v1"):
+    p = make_oracle_intmcp(cfg_kwargs, num_sims, ego=ego, tree=tree, env=env)
+    p.reset()
+    records = []
+
+    def step(obs):
+        searched = not p.top.tree.absorbing[p.top.cur]
+        a = p.step(obs)
+        records.append(oracle_intmcp_record(p, searched, a))
+        return a
+
+    trace = run_episode(step, env_seed, ego=ego, max_steps=max_steps, env=env)
+    return trace, records

@@ -16,8 +16,9 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 
-from oracle.ref_harness import import_reference, reference_available, reference_episode  # noqa: E402
-from oracle.run import oracle_episode  # noqa: E402
+from oracle.ref_harness import (  # noqa: E402
+    import_reference, reference_available, reference_episode, reference_intmcp_episode)
+from oracle.run import oracle_episode, oracle_intmcp_episode  # noqa: E402
 
 SQRT2 = math.sqrt(2)
 # tests/planning/test_pomcp.py:38-50 (config 1 of BASELINE.json)
@@ -61,6 +62,38 @@ def run_case(name):
     return out
 
 
+# BASELINE config 5: I-NTMCP nesting_level=1 (tests/planning/test_intmcp.py:34-71:
+# search_time_limit = 0.1 * (nesting_level + 1), state_belief_only=False); the
+# simulation count is per nesting level
+INTMCP_CFG = dict(TEST_CFG, search_time_limit=0.2, state_belief_only=False)
+INTMCP_CASES = {
+    "intmcp_ucb": ({}, 64, [(0, 0), (1, 1)], "0", 50, "Driving-v1"),
+    "intmcp_ego1": ({}, 48, [(2, 2)], "1", 50, "Driving-v1"),
+    "intmcp_uniform": ({"action_selection": "uniform"}, 32, [(3, 3)], "0", 50, "Driving-v1"),
+    "intmcp_deep": ({"discount": 0.99, "epsilon": 0.01}, 16, [(4, 4)], "0", 20, "Driving-v1"),
+    "intmcp_pe": ({}, 48, [(5, 5)], "0", 100, "PursuitEvasion-v1"),
+}
+
+
+def run_intmcp_case(name):
+    over, num_sims, pairs, ego, max_steps, env = INTMCP_CASES[name]
+    out = {"case": name, "env": env, "num_sims": num_sims, "ego": ego, "max_steps": max_steps,
+           "episodes": []}
+    for seed, env_seed in pairs:
+        cfg = dict(INTMCP_CFG)
+        cfg.update(over)
+        cfg["seed"] = seed
+        tr, rr = reference_intmcp_episode(cfg, num_sims, env_seed, ego=ego, max_steps=max_steps,
+                                          env=env)
+        to, ro = oracle_intmcp_episode(cfg, num_sims, env_seed, ego=ego, max_steps=max_steps,
+                                       env=env)
+        if tr != to or rr != ro:
+            raise SystemExit(f"oracle disagrees with reference in case {name} seed {seed}")
+        out["episodes"].append({"config": dict(cfg), "env_seed": env_seed, "trace": tr,
+                                "records": rr})
+    return out
+
+
 def config_kats():
     """MCTSConfig derived fields (config.py:461-469) from the reference itself."""
     P = import_reference()
@@ -86,6 +119,12 @@ def main():
         raise SystemExit("reference not available (container-only script)")
     for name in CASES:
         data = run_case(name)
+        with open(os.path.join(HERE, f"{name}.json"), "w") as f:
+            json.dump(data, f, separators=(",", ":"))
+        n = sum(len(e["records"]) for e in data["episodes"])
+        print(f"{name}: {len(data['episodes'])} episodes, {n} records")
+    for name in INTMCP_CASES:
+        data = run_intmcp_case(name)
         with open(os.path.join(HERE, f"{name}.json"), "w") as f:
             json.dump(data, f, separators=(",", ":"))
         n = sum(len(e["records"]) for e in data["episodes"])

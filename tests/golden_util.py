@@ -27,3 +27,6 @@ def cfg_kwargs(cfg):
     if kw.get("known_bounds") is not None:
         kw["known_bounds"] = tuple(kw["known_bounds"])
     return kw
+
+
+INTMCP_CASES = ["intmcp_ucb", "intmcp_ego1", "intmcp_uniform", "intmcp_deep", "intmcp_pe"]

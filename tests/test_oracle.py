@@ -68,3 +68,21 @@ def test_oracle_matches_reference_goldens(case):
         assert len(records) == len(ep["records"])
         for t, (got, exp) in enumerate(zip(records, ep["records"])):
             assert got == exp, f"{case} step {t}"
+
+
+@pytest.mark.parametrize("case", ["intmcp_ucb", "intmcp_ego1", "intmcp_uniform", "intmcp_deep",
+                                  "intmcp_pe"])
+def test_intmcp_oracle_matches_reference_goldens(case):
+    """I-NTMCP nesting 1 (BASELINE config 5): the oracle restatement against the
+    real reference planner's records (root children, beliefs with the other
+    agent's histories, the level-0 nodes of every history in the belief)."""
+    from oracle.run import oracle_intmcp_episode
+    data = load(case)
+    for ep in data["episodes"]:
+        trace, records = oracle_intmcp_episode(ep["config"], data["num_sims"], ep["env_seed"],
+                                               ego=data["ego"], max_steps=data["max_steps"],
+                                               env=case_env(data))
+        assert trace == ep["trace"]
+        for t, (got, exp) in enumerate(zip(records, ep["records"])):
+            assert got == exp, f"{case} step {t}"
+        assert len(records) == len(ep["records"])
