@@ -1,0 +1,104 @@
+/* intmcp.h — C ABI of the I-NTMCP engine in libpomcp_hip.so (BASELINE config 5).
+ *
+ * Drop-in boundary for posggym_baselines.planning.intmcp.INTMCP at nesting
+ * level 1 with two agents, as built by
+ * INTMCP.initialize(model, ego, config, nesting_level=1, search_policies=None)
+ * (intmcp.py:949-994): the ego's level-1 tree and the other agent's level-0
+ * tree, random search policies.  One planner pair per "tree" index; many
+ * pairs per call (a batched launch).  Paths relative to
+ * posggym_baselines/planning/ in the reference.
+ *
+ * Same conventions as pomcp.h (plain pointers, POMCP_* status codes, a
+ * context is not thread-safe).
+ */
+#ifndef INTMCP_H_
+#define INTMCP_H_
+
+#include <stdint.h>
+
+#include "pomcp.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct intmcp_config {
+  pomcp_config base;              /* MCTSConfig + model + tables (num_trees = planner pairs) */
+  int32_t state_belief_only;      /* MCTSConfig.state_belief_only (test config: 0) */
+  int32_t pad;
+  int64_t max_nodes;              /* obs nodes per tree */
+  int64_t max_stats;              /* action-node statistics entries per tree (A per expanded node) */
+  int64_t max_log;                /* particle log records per tree (16 B) */
+  int64_t hash_slots;             /* obs-child map slots per tree, power of two */
+  int64_t max_root_belief;        /* level-1 root particles (and level-0 support entries) */
+  int64_t max_support_particles;  /* materialised level-0 particles per pair */
+} intmcp_config;
+
+typedef struct intmcp_root_stats {
+  int32_t action;                 /* _final_action_selection of the level-1 root */
+  int32_t num_sims;               /* simulations over both levels */
+  int32_t search_depth;
+  int32_t root_visits;
+  int32_t root_absorbing;
+  int32_t belief_size;
+  int32_t error;
+  int32_t num_children;           /* registered children of the root, registration order: */
+  int32_t child_action[POMCP_MAX_ACTIONS];
+  int32_t child_visits[POMCP_MAX_ACTIONS];
+  double child_values[POMCP_MAX_ACTIONS];
+  double child_totals[POMCP_MAX_ACTIONS];
+  double min_value, max_value;    /* the level-1 planner's MinMaxStats */
+  int32_t n_nodes[2], n_log[2];
+  int32_t n_support, pad;
+} intmcp_root_stats;
+
+typedef struct intmcp_ctx intmcp_ctx;
+
+/* INTMCP.initialize (intmcp.py:949-994) for every pair. */
+int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, intmcp_ctx** out);
+void intmcp_destroy(intmcp_ctx* ctx);
+const char* intmcp_last_error(const intmcp_ctx* ctx);
+/* INTMCP.reset (intmcp.py:154-176). */
+int intmcp_reset(intmcp_ctx* ctx);
+/* INTMCP.update (intmcp.py:198-300): t == 0 -> _initial_nested_update, else
+ * _nested_update (re-root, reinvigoration, the level-0 update of every
+ * other-agent history in the new root belief). */
+int intmcp_update(intmcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_keys,
+                  int32_t* root_absorbing_out);
+/* INTMCP.get_action (intmcp.py:368-408) with num_sims simulations per nesting level. */
+int intmcp_search(intmcp_ctx* ctx, int32_t num_sims_per_level, int32_t* actions_out);
+/* One chunk of get_action: level0_sims simulations at level 0 then
+ * level1_sims at level 1.  flags: INTMCP_BEGIN resets the step's counters,
+ * INTMCP_FINAL runs _final_action_selection (actions_out is then valid).  The
+ * reference's wall-clock loop (per-level time budget) is a sequence of chunks;
+ * intmcp_search(n) == intmcp_search_levels(n, n, BEGIN | FINAL). */
+#define INTMCP_BEGIN 1
+#define INTMCP_FINAL 2
+int intmcp_search_levels(intmcp_ctx* ctx, int32_t level0_sims, int32_t level1_sims, int32_t flags,
+                         int32_t* actions_out);
+int intmcp_get_root_stats(intmcp_ctx* ctx, intmcp_root_stats* out);
+/* Level-1 root particles of one pair as (v0, v1, level-0 node id) u32 triples. */
+int intmcp_get_root_belief(intmcp_ctx* ctx, int32_t pair, uint32_t* out, int32_t capacity,
+                           int32_t* count);
+/* Diagnostics: one tree's node records (32 B each: parent i32, info u32,
+ * visits i32, t i32, stats i32, -, obs key u64; info = parent action:3 |
+ * absorbing:1 | path_ok:1 | registered:3 | registration order 6 x 3 bits) and
+ * statistics entries (32 B: visits i32, -, value f64, total f64, agg f64);
+ * tree 0 = level 1, tree 1 = level 0. */
+int intmcp_get_nodes(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int32_t capacity,
+                     int32_t* count);
+int intmcp_get_stats(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int32_t capacity,
+                     int32_t* count);
+/* The materialised level-0 beliefs: entries (node, offset, size, capacity) and
+ * their (v0, v1) particles. */
+int intmcp_get_support(intmcp_ctx* ctx, int32_t pair, int32_t* entries, int32_t capacity_entries,
+                       int32_t* n_entries, uint32_t* particles, int32_t capacity_particles,
+                       int32_t* n_particles);
+/* Synthetic roots (as pomcp_synthetic_obs). */
+int intmcp_synthetic_obs(intmcp_ctx* ctx, uint64_t env_seed_base, uint64_t* obs_keys_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* INTMCP_H_ */

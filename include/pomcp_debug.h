@@ -8,6 +8,8 @@ extern "C" {
 /* out[4*i + k] = {sqrt(a), a / b, a + 0.95 * b, (a - b) / (a + b)} computed on
  * device 0 in FP64 (checks the device FP64 path is correctly rounded). */
 int pomcp_debug_fp_selftest(const double* a, const double* b, int32_t n, double* out);
+/* out[i] = exp(x[i]) on device 0 (FP64). */
+int pomcp_debug_exp(const double* x, int32_t n, double* out);
 /* k_search phase cycles per wave, [waves][16] (libpomcp_hip built with
  * -DPOMCP_PHASE_TIMING; POMCP_E_UNSUPPORTED otherwise).  The first call
  * enables collection (count = 0); later calls copy the last search's values

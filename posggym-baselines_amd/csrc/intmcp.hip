@@ -1,0 +1,888 @@
+// I-NTMCP, nesting level 1, two agents: the ego's level-1 tree and the other
+// agent's level-0 tree, ONE planner pair per lane.
+//
+// Replaces posggym_baselines/planning/intmcp.py:198-517, 547-593, 634-862 as
+// built by INTMCP.initialize(model, ego, config, 1, None) (random search
+// policies at both levels).  Restates oracle/intmcp.py, which the real
+// reference pins (tests/golden/intmcp_*.json); the representation is the
+// oracle's (DESIGN.md "I-NTMCP"):
+//   * obs nodes are keyed by the agent's history; a node records its parent
+//     edge (node, action) -- the None action of the initial observation is
+//     action A -- and which of its actions are registered as children, in
+//     registration order (what ObsNode.get_child_nodes() iterates);
+//   * a particle of the level-1 tree carries the other agent's history as its
+//     node id in the level-0 tree: created with the particle, registered on the
+//     path only when the reference traverses (INTMCP.traverse, intmcp.py:797);
+//   * beliefs: an append-only particle log per tree (the node a particle
+//     entered), materialised at every update into the level-1 root belief and
+//     the beliefs of the level-0 nodes the root belief's histories name (the
+//     "support"), both ping-ponged (the previous ones are the parents of the
+//     reinvigoration).
+// Serial per planner pair; many pairs per launch (config 5: nested trees as a
+// batched launch).  No atomics: a pair is touched by one lane.
+#pragma clang fp contract(off)
+
+namespace pb {
+
+constexpr int kImPath = 128;          // tree levels per simulation
+constexpr uint32_t kImNoSupport = 0xFFFFFFFFu;
+
+struct INode {          // 32 B
+  int32_t parent;
+  uint32_t info;        // paction:3 | absorbing:1 | path_ok:1 | nreg:3 | order 6 x 3 bits
+  int32_t visits;
+  int32_t t;
+  int32_t stats;        // first of A IStat entries (-1: none registered yet)
+  uint32_t support;     // support slot while materialising beliefs (level-0 tree)
+  uint64_t okey;
+};
+struct IStat {          // 32 B: ActionNode visits / value / total_value / agg
+  int32_t visits, pad;
+  double value, total, agg;
+};
+struct IHash {          // 16 B: (parent, action, obs key) -> child
+  uint64_t okey;
+  uint32_t na;          // parent << 3 | action
+  int32_t child;        // -1: empty
+};
+struct IRec {           // particle log record: the particle (v0, v1[, other's node]) entered `node`
+  uint32_t node, v0, v1, nested;
+};
+struct ISup {           // a materialised level-0 belief
+  int32_t node, off, size, cap;
+};
+
+struct IHdr {
+  int32_t n_nodes[2], n_stats[2], n_log[2];
+  int32_t cur, root_sel, root_size, sup_sel, n_sup, sup_used, err, last_action;
+  int32_t num_sims, search_depth, sims_done, pad;
+  double mm_min[2], mm_max[2];
+  uint64_t seed;
+  uint32_t tree_key;
+  uint32_t ctr[6];      // belief (level 1), select, model, act0, act1, belief (level 0)
+};
+
+struct ImParams {
+  int32_t B, A, ego, other, sel, depth_limit, step_limit, n_target, extra, has_kb,
+      state_belief_only, pad;
+  double discount, c, limit_factor, kb_min, kb_max;
+  int64_t Nn, Ns, Nl, H, Nr, Nsp;   // per tree: nodes, stat entries, log records, hash slots;
+                                    // per pair: root belief, support particles
+  IHdr* hdr;
+  INode* nodes;         // [B][2][Nn]
+  IStat* stats;         // [B][2][Ns]
+  IHash* hash;          // [B][2][H]
+  IRec* log;            // [B][2][Nl]
+  uint4* root;          // [B][2][Nr] {v0, v1, nested, support slot}
+  ISup* sup;            // [B][2][Nr]
+  uint2* supp;          // [B][2][Nsp]
+  int4* path;           // [B][kImPath][2] path of the running simulation
+  double* prob;         // [B][Nr] support probabilities (update scratch)
+  const double* logtab;
+  int64_t logtab_n;
+  const double* dpow;
+  int32_t dpow_n;
+  const void* model;
+  const int32_t* in_actions;
+  const uint64_t* in_obs;
+  int32_t* out;         // [B][2] {root absorbing, error}
+  uint64_t* out_obs;    // [B] synthetic roots
+};
+
+__device__ __forceinline__ uint32_t im_paction(uint32_t info) { return info & 7u; }
+__host__ __device__ __forceinline__ bool im_absorbing(uint32_t info) { return (info >> 3) & 1u; }
+__device__ __forceinline__ bool im_path_ok(uint32_t info) { return (info >> 4) & 1u; }
+__host__ __device__ __forceinline__ int im_nreg(uint32_t info) { return (int)((info >> 5) & 7u); }
+__host__ __device__ __forceinline__ int im_order(uint32_t info, int k) { return (int)((info >> (8 + 3 * k)) & 7u); }
+
+// One planner pair (lane): pointers, counters, RNG.
+template <class Env>
+struct ImPair {
+  using Model = typename Env::Model;
+  const ImParams& p;
+  const Model& m;
+  int pair;
+  INode* nd[2];
+  IStat* st[2];
+  IHash* hs[2];
+  IRec* lg[2];
+  uint4* rootb;   // [2][Nr]
+  ISup* sup;      // [2][Nr]
+  uint2* supp;    // [2][Nsp]
+  int4* path;
+  double* prob;   // [Nr]
+  IHdr h;
+
+  __device__ ImPair(const ImParams& pp, const Model& mm, int b) : p(pp), m(mm), pair(b) {
+    for (int k = 0; k < 2; ++k) {
+      nd[k] = p.nodes + ((int64_t)b * 2 + k) * p.Nn;
+      st[k] = p.stats + ((int64_t)b * 2 + k) * p.Ns;
+      hs[k] = p.hash + ((int64_t)b * 2 + k) * p.H;
+      lg[k] = p.log + ((int64_t)b * 2 + k) * p.Nl;
+    }
+    rootb = p.root + (int64_t)b * 2 * p.Nr;
+    sup = p.sup + (int64_t)b * 2 * p.Nr;
+    supp = p.supp + (int64_t)b * 2 * p.Nsp;
+    path = p.path + (int64_t)b * kImPath * 2;
+    prob = p.prob + (int64_t)b * p.Nr;
+    h = p.hdr[b];
+  }
+  __device__ void store() { p.hdr[pair] = h; }
+  __device__ void fail(int code) {
+    if (h.err == 0) h.err = code;
+  }
+
+  // ------------------------------------------------------------------ RNG
+  __device__ uint32_t draw(int slot, uint32_t stream) {
+    return philox_word(h.seed, h.tree_key, stream, h.ctr[slot]++);
+  }
+  __device__ uint32_t d_bel(int level, uint32_t n) {   // planner random.Random(seed)
+    return level == 1 ? uniform_int(draw(0, S_BELIEF), n) : uniform_int(draw(5, S_BELIEF_NESTED), n);
+  }
+  __device__ uint32_t d_sel(uint32_t n) { return uniform_int(draw(1, S_SELECT), n); }
+  __device__ double d_sel_float() { return uniform_float(draw(1, S_SELECT)); }
+  __device__ uint32_t d_model(uint32_t n) { return uniform_int(draw(2, S_MODEL), n); }
+  __device__ uint32_t d_act(int agent, uint32_t n) {   // model.action_spaces[agent].sample()
+    return agent == 0 ? uniform_int(draw(3, S_ACT_BASE), n) : uniform_int(draw(4, S_ACT_BASE + 1), n);
+  }
+
+  // ---------------------------------------------------------------- trees
+  // k = 0: the level-1 (ego) tree, k = 1: the level-0 (other agent) tree
+  __device__ uint32_t hkey(uint32_t na, uint64_t okey) const {
+    return ovf_hash(na, okey) & (uint32_t)(p.H - 1);
+  }
+  __device__ int find(int k, int n, int a, uint64_t okey) {
+    const uint32_t na = ((uint32_t)n << 3) | (uint32_t)a;
+    uint32_t s = hkey(na, okey);
+    for (int64_t probe = 0; probe < p.H; ++probe) {
+      const IHash e = hs[k][s];
+      if (e.child < 0) return -1;
+      if (e.na == na && e.okey == okey) return e.child;
+      s = (s + 1) & (uint32_t)(p.H - 1);
+    }
+    return -1;
+  }
+  // The obs child (n, a, okey); created (visits 0) if missing (INTMCP.traverse /
+  // history extension, intmcp.py:797-809, 466).
+  __device__ int child(int k, int n, int a, uint64_t okey) {
+    const uint32_t na = ((uint32_t)n << 3) | (uint32_t)a;
+    uint32_t s = hkey(na, okey);
+    for (int64_t probe = 0; probe < p.H; ++probe) {
+      const IHash e = hs[k][s];
+      if (e.child >= 0 && e.na == na && e.okey == okey) return e.child;
+      if (e.child < 0) {
+        if (h.n_nodes[k] >= p.Nn) {
+          fail(POMCP_E_ARENA);
+          return -1;
+        }
+        const int c = h.n_nodes[k]++;
+        INode x;
+        x.parent = n;
+        x.info = (uint32_t)a;
+        x.visits = 0;
+        x.t = nd[k][n].t + 1;
+        x.stats = -1;
+        x.support = kImNoSupport;
+        x.okey = okey;
+        nd[k][c] = x;
+        IHash ne;
+        ne.okey = okey;
+        ne.na = na;
+        ne.child = c;
+        hs[k][s] = ne;
+        return c;
+      }
+      s = (s + 1) & (uint32_t)(p.H - 1);
+    }
+    fail(POMCP_E_ARENA);
+    return -1;
+  }
+  // ObsNode.add_child(a) (node.py:68-80) if not a child yet
+  __device__ void reg(int k, int n, int a) {
+    INode& x = nd[k][n];
+    const int nr = im_nreg(x.info);
+    for (int i = 0; i < nr; ++i)
+      if (im_order(x.info, i) == a) return;
+    if (nr >= 6) {
+      fail(POMCP_E_INVALID);
+      return;
+    }
+    x.info = (x.info & ~(7u << 5)) | ((uint32_t)(nr + 1) << 5) | ((uint32_t)a << (8 + 3 * nr));
+    if (a < p.A && x.stats < 0) {
+      if (h.n_stats[k] + p.A > p.Ns) {
+        fail(POMCP_E_ARENA);
+        return;
+      }
+      x.stats = h.n_stats[k];
+      h.n_stats[k] += p.A;
+      for (int q = 0; q < p.A; ++q) {
+        IStat z;
+        z.visits = 0;
+        z.pad = 0;
+        z.value = 0.0;
+        z.total = 0.0;
+        z.agg = 0.0;
+        st[k][x.stats + q] = z;
+      }
+    }
+  }
+  __device__ void traverse(int k, int n) {   // intmcp.py:797-809
+    while (n > 0 && !im_path_ok(nd[k][n].info)) {
+      const int par = nd[k][n].parent;
+      reg(k, par, (int)im_paction(nd[k][n].info));
+      nd[k][n].info |= 1u << 4;
+      n = par;
+    }
+  }
+  __device__ void expand(int k, int n) {
+    for (int a = 0; a < p.A; ++a) reg(k, n, a);
+  }
+
+  __device__ void mm_update(int k, double v) {
+    if (v > h.mm_max[k]) h.mm_max[k] = v;
+    if (v < h.mm_min[k]) h.mm_min[k] = v;
+  }
+  __device__ double normalize(int k, double v) const {
+    return h.mm_max[k] > h.mm_min[k] ? (v - h.mm_min[k]) / (h.mm_max[k] - h.mm_min[k]) : v;
+  }
+  __device__ double logn(int n) {
+    if (n >= p.logtab_n) {
+      fail(POMCP_E_ARENA);
+      return 0.0;
+    }
+    return p.logtab[n];
+  }
+
+  // ------------------------------------------------------------- selection
+  // the agent of tree k: k = 0 the ego, k = 1 the other agent
+  __device__ int agent(int k) const { return k == 0 ? p.ego : p.other; }
+
+  __device__ int select(int k, int n) {          // intmcp.py:670-701
+    const INode x = nd[k][n];
+    if (x.visits == 0) return (int)d_sel((uint32_t)p.A);
+    const int nr = im_nreg(x.info);
+    if (p.sel == POMCP_SEL_UCB) {
+      const double log_n = logn(x.visits);
+      double best = -__builtin_inf();
+      int ba = 0;
+      for (int i = 0; i < nr; ++i) {
+        const int a = im_order(x.info, i);
+        const IStat s = st[k][x.stats + a];
+        if (s.visits == 0) return a;
+        const double v = normalize(k, s.value) + p.c * sqrt(log_n / (double)s.visits);
+        if (v > best) {
+          best = v;
+          ba = a;
+        }
+      }
+      return ba;
+    }
+    int min_n = x.visits + 1, nxt = 0;            // min_visit_action_selection
+    for (int i = 0; i < nr; ++i) {
+      const int a = im_order(x.info, i);
+      const int v = st[k][x.stats + a].visits;
+      if (v < min_n) {
+        min_n = v;
+        nxt = a;
+      }
+    }
+    return nxt;
+  }
+
+  // INTMCP.sample_action of the level-0 planner (intmcp.py:763-791) at node n
+  __device__ int sample_action(int n) {
+    traverse(1, n);
+    const INode x = nd[1][n];
+    const int nr = im_nreg(x.info);
+    if (x.visits == 0 || nr == 0) return (int)d_act(p.other, (uint32_t)p.A);
+    const double sq = sqrt((double)x.visits);
+    double pr[6];
+    double total = 0.0;
+    for (int i = 0; i < nr; ++i) {
+      pr[i] = exp((double)st[1][x.stats + im_order(x.info, i)].visits / sq);
+      total = i == 0 ? pr[i] : total + pr[i];
+    }
+    // random.choices(children, weights=p / sum): cum weights, x = random() * total
+    double cum[6];
+    double acc = 0.0;
+    for (int i = 0; i < nr; ++i) {
+      const double w = pr[i] / total;
+      acc = i == 0 ? w : acc + w;
+      cum[i] = acc;
+    }
+    const double u = d_sel_float() * (cum[nr - 1] + 0.0);
+    int lo = 0, hi = nr - 1;   // bisect_right(cum, u, 0, n - 1)
+    while (lo < hi) {
+      const int mid = (lo + hi) / 2;
+      if (u < cum[mid]) hi = mid;
+      else lo = mid + 1;
+    }
+    return im_order(x.info, lo);
+  }
+
+  // the other agent's action from a particle of tree k (intmcp.py:602-615)
+  __device__ int other_action(int k, uint32_t nested) {
+    if (k == 1 || p.state_belief_only) return (int)d_bel(k == 0 ? 1 : 0, (uint32_t)p.A);
+    return sample_action((int)nested);
+  }
+
+  // joint step for tree k's agent; the next particle's other-agent node
+  __device__ void step(int k, uint32_t s0, uint32_t s1, uint32_t nested, int a_self,
+                       int a_other, uint32_t* n0, uint32_t* n1, double* r, int* done,
+                       uint64_t* okey, uint32_t* nested_out) {
+    const int me = agent(k);
+    const uint32_t j = Env::kStepDraws ? d_model(2) : 0u;
+    Env::step(m, me, s0, s1, (uint32_t)a_self, (uint32_t)a_other, j, n0, n1, r, done);
+    *okey = Env::obs_key(m, me, *n0, *n1);
+    *nested_out = 0;
+    if (k == 0) {
+      const uint64_t ok = Env::obs_key(m, p.other, *n0, *n1);
+      const int c = child(1, (int)nested, a_other, ok);
+      *nested_out = c < 0 ? 0u : (uint32_t)c;
+    }
+  }
+
+  __device__ void log_add(int k, int node, uint32_t v0, uint32_t v1, uint32_t nested) {
+    if (h.n_log[k] >= p.Nl) {
+      fail(POMCP_E_ARENA);
+      return;
+    }
+    IRec r;
+    r.node = (uint32_t)node;
+    r.v0 = v0;
+    r.v1 = v1;
+    r.nested = nested;
+    lg[k][h.n_log[k]++] = r;
+  }
+
+  // ------------------------------------------------------------ rollout
+  __device__ double rollout(int k, uint32_t s0, uint32_t s1, int t, int depth) {   // intmcp.py:547-593
+    double ret = 0.0;
+    int kk = 0;
+    const int me = agent(k);
+    while (depth <= p.depth_limit && t <= p.step_limit) {
+      const uint32_t a0 = d_act(0, (uint32_t)p.A);
+      const uint32_t a1 = d_act(1, (uint32_t)p.A);
+      const uint32_t j = Env::kStepDraws ? d_model(2) : 0u;
+      uint32_t n0, n1;
+      double r;
+      int done;
+      Env::step(m, me, s0, s1, me == 0 ? a0 : a1, me == 0 ? a1 : a0, j, &n0, &n1, &r, &done);
+      if (kk >= p.dpow_n) {
+        fail(POMCP_E_ARENA);
+        return ret;
+      }
+      ret += p.dpow[kk] * r;
+      if (done) break;
+      s0 = n0;
+      s1 = n1;
+      ++t;
+      ++depth;
+      ++kk;
+    }
+    return ret;
+  }
+
+  // ----------------------------------------------------------- simulate
+  // INTMCP._simulate (intmcp.py:444-517) from node n of tree k; returns the
+  // search depth.
+  __device__ int simulate(int k, uint32_t s0, uint32_t s1, uint32_t nested, int n) {
+    int depth = 0, plen = 0;
+    double leaf = 0.0;
+    const int me = agent(k);
+    for (;;) {
+      const INode x = nd[k][n];
+      if (depth > p.depth_limit || x.t + depth > p.step_limit) break;
+      if (im_nreg(x.info) < p.A) {                 // leaf: add the missing children
+        expand(k, n);
+        leaf = rollout(k, s0, s1, x.t, depth);
+        break;
+      }
+      const int a = select(k, n);
+      const int ao = other_action(k, nested);
+      uint32_t n0, n1, nn;
+      double r;
+      int done;
+      uint64_t okey;
+      step(k, s0, s1, nested, a, ao, &n0, &n1, &r, &done, &okey, &nn);
+      int c = find(k, n, a, okey);
+      if (c >= 0) {
+        nd[k][c].visits += 1;
+      } else {
+        c = child(k, n, a, okey);
+        if (c < 0) return depth;
+        nd[k][c].visits = 1;
+      }
+      uint32_t info = nd[k][c].info;
+      if (im_path_ok(nd[k][n].info)) info |= 1u << 4;
+      info = done ? (info | 8u) : (info & ~8u);
+      nd[k][c].info = info;
+      log_add(k, c, n0, n1, nn);
+      if (plen >= kImPath) {
+        fail(POMCP_E_ARENA);
+        return depth;
+      }
+      path[plen * 2] = make_int4(n, a, done, 0);
+      path[plen * 2 + 1] = make_int4(__double2loint(r), __double2hiint(r), 0, 0);
+      ++plen;
+      (void)me;
+      if (done) break;
+      n = c;
+      s0 = n0;
+      s1 = n1;
+      nested = nn;
+      ++depth;
+    }
+    double g = leaf;
+    for (int l = plen - 1; l >= 0; --l) {            // backup, node.py:166-178
+      const int4 e = path[l * 2], f = path[l * 2 + 1];
+      const double r = __hiloint2double(f.y, f.x);
+      g = e.z ? r : r + p.discount * g;
+      IStat& s = st[k][nd[k][e.x].stats + e.y];
+      s.visits += 1;
+      s.total += g;
+      const double delta = g - s.value;
+      s.value += delta / (double)s.visits;
+      s.agg += delta * (g - s.value);
+      mm_update(k, s.value);
+    }
+    return depth;
+  }
+
+  // ------------------------------------------------------ beliefs / update
+  __device__ uint4* root_buf(int sel) { return rootb + (int64_t)sel * p.Nr; }
+  __device__ ISup* sup_tab(int sel) { return sup + (int64_t)sel * p.Nr; }
+  __device__ uint2* sup_parts(int sel) { return supp + (int64_t)sel * p.Nsp; }
+
+  __device__ int find_support(int sel, int n, int count) {
+    const ISup* t = sup_tab(sel);
+    for (int i = 0; i < count; ++i)
+      if (t[i].node == n) return i;
+    return -1;
+  }
+
+  // BeliefRejectionSampler (belief.py:145-194, use_rejected_samples=True) for a
+  // level-1 node n: parent particles from the previous root buffer; appends to
+  // the current root buffer
+  __device__ void reinvig_top(int n, int action, uint64_t okey, int target, int* size) {
+    const int to_add = target - *size;
+    if (to_add <= 0) return;
+    const uint4* par = root_buf(h.root_sel ^ 1);
+    const int psize = h.pad;   // previous root size (kept in pad during update)
+    if (psize <= 0) {
+      fail(POMCP_E_STATE);
+      return;
+    }
+    uint4* cur = root_buf(h.root_sel);
+    const double limit = p.limit_factor * (double)to_add;
+    int count = 0, attempts = 0, nrej = 0;
+    const int base = *size;
+    if (base + 2 * to_add > p.Nr) {
+      fail(POMCP_E_ARENA);
+      return;
+    }
+    // accepted go to [base, base + to_add), rejected to [base + to_add, ...)
+    while (count < to_add && (double)attempts < limit) {
+      ++attempts;
+      const uint4 hp = par[d_bel(1, (uint32_t)psize)];
+      const int ao = other_action(0, hp.z);
+      uint32_t n0, n1, nn;
+      double r;
+      int done;
+      uint64_t k2;
+      step(0, hp.x, hp.y, hp.z, action, ao, &n0, &n1, &r, &done, &k2, &nn);
+      const uint4 rec = make_uint4(n0, n1, nn, 0u);
+      if (k2 == okey) {
+        cur[base + count++] = rec;
+      } else if (nrej < to_add) {
+        cur[base + to_add + nrej++] = rec;
+      }
+    }
+    int fill = to_add - count;
+    if (fill > nrej) fill = nrej;
+    for (int q = 0; q < fill; ++q) cur[base + count + q] = cur[base + to_add + q];
+    *size = base + count + fill;
+  }
+
+  // the same for a level-0 node: parent particles from the previous support
+  // table; appends to support entry `si` of table `sel`
+  __device__ void reinvig_nested(int n, int action, uint64_t okey, int target, int sel, int si) {
+    ISup& e = sup_tab(sel)[si];
+    const int to_add = target - e.size;
+    if (to_add <= 0) return;
+    const int par = nd[1][n].parent;
+    const int pi = find_support(sel ^ 1, par, h.pad);   // previous support count in pad
+    if (pi < 0) {
+      fail(POMCP_E_UNSUPPORTED);   // parent belief not materialised
+      return;
+    }
+    const ISup pe = sup_tab(sel ^ 1)[pi];
+    if (pe.size <= 0) {
+      fail(POMCP_E_STATE);
+      return;
+    }
+    const uint2* pp = sup_parts(sel ^ 1) + pe.off;
+    uint2* cur = sup_parts(sel) + e.off;
+    if (e.size + 2 * to_add > e.cap) {
+      fail(POMCP_E_ARENA);
+      return;
+    }
+    const double limit = p.limit_factor * (double)to_add;
+    int count = 0, attempts = 0, nrej = 0;
+    const int base = e.size;
+    while (count < to_add && (double)attempts < limit) {
+      ++attempts;
+      const uint2 hp = pp[d_bel(0, (uint32_t)pe.size)];
+      const int ao = (int)d_bel(0, (uint32_t)p.A);      // self._rng.choice (level 0)
+      uint32_t n0, n1, nn;
+      double r;
+      int done;
+      uint64_t k2;
+      step(1, hp.x, hp.y, 0u, action, ao, &n0, &n1, &r, &done, &k2, &nn);
+      const uint2 rec = make_uint2(n0, n1);
+      if (k2 == okey) {
+        cur[base + count++] = rec;
+      } else if (nrej < to_add) {
+        cur[base + to_add + nrej++] = rec;
+      }
+    }
+    int fill = to_add - count;
+    if (fill > nrej) fill = nrej;
+    for (int q = 0; q < fill; ++q) cur[base + count + q] = cur[base + to_add + q];
+    e.size = base + count + fill;
+  }
+};
+
+// Level-0 support of the root belief: distinct other-agent nodes in
+// first-occurrence order with probability count / size (intmcp.py:334-362);
+// writes support slots into the root buffer's .w.
+template <class Env>
+__device__ void im_support(ImPair<Env>& P, int sel, int size, int* nsup) {
+  double* prob = P.prob;
+  uint4* rb = P.root_buf(P.h.root_sel);
+  ISup* tab = P.sup_tab(sel);
+  int n = 0;
+  for (int i = 0; i < size; ++i) {
+    const int nodeid = (int)rb[i].z;
+    int s = -1;
+    for (int q = 0; q < n; ++q)
+      if (tab[q].node == nodeid) s = q;
+    if (s < 0) {
+      s = n++;
+      tab[s].node = nodeid;
+      tab[s].size = 0;   // count for now
+    }
+    tab[s].size += 1;
+    rb[i].w = (uint32_t)s;
+  }
+  for (int q = 0; q < n; ++q) {
+    prob[q] = 0.0 + 1.0 * ((double)tab[q].size / (double)size);
+    tab[q].size = 0;
+  }
+  *nsup = n;
+}
+
+// Materialise the level-0 support beliefs from the level-0 log (insertion
+// order), leaving `slack` free slots per entry for reinvigoration.
+template <class Env>
+__device__ void im_extract_support(ImPair<Env>& P, int sel, int nsup) {
+  ISup* tab = P.sup_tab(sel);
+  for (int q = 0; q < nsup; ++q) P.nd[1][tab[q].node].support = (uint32_t)q;
+  for (int q = 0; q < nsup; ++q) tab[q].cap = 0;
+  for (int i = 0; i < P.h.n_log[1]; ++i) {
+    const uint32_t s = P.nd[1][P.lg[1][i].node].support;
+    if (s != kImNoSupport) tab[s].cap += 1;
+  }
+  int off = 0;
+  for (int q = 0; q < nsup; ++q) {   // room for the reinvigoration (accepted + rejected)
+    tab[q].off = off;
+    tab[q].size = 0;
+    tab[q].cap += 2 * (int)ceil(P.prob[q] * (double)P.p.n_target) + 2;
+    off += tab[q].cap;
+  }
+  if (off > P.p.Nsp) {
+    P.fail(POMCP_E_ARENA);
+    for (int q = 0; q < nsup; ++q) P.nd[1][tab[q].node].support = kImNoSupport;
+    return;
+  }
+  uint2* parts = P.sup_parts(sel);
+  for (int i = 0; i < P.h.n_log[1]; ++i) {
+    const IRec r = P.lg[1][i];
+    const uint32_t s = P.nd[1][r.node].support;
+    if (s != kImNoSupport) parts[tab[s].off + tab[s].size++] = make_uint2(r.v0, r.v1);
+  }
+  for (int q = 0; q < nsup; ++q) P.nd[1][tab[q].node].support = kImNoSupport;
+}
+
+template <class Env>
+__global__ __launch_bounds__(64) void k_im_reset(ImParams p) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= p.B) return;
+  IHdr h = p.hdr[b];
+  for (int k = 0; k < 2; ++k) {
+    IHash* hs = p.hash + ((int64_t)b * 2 + k) * p.H;
+    for (int64_t i = 0; i < p.H; ++i) {
+      IHash e;
+      e.okey = 0;
+      e.na = 0;
+      e.child = -1;
+      hs[i] = e;
+    }
+    INode r;
+    r.parent = -1;
+    r.info = 1u << 4;   // path_ok
+    r.visits = 0;
+    r.t = 0;
+    r.stats = -1;
+    r.support = kImNoSupport;
+    r.okey = 0;
+    p.nodes[((int64_t)b * 2 + k) * p.Nn] = r;
+    h.n_nodes[k] = 1;
+    h.n_stats[k] = 0;
+    h.n_log[k] = 0;
+    h.mm_max[k] = p.has_kb ? p.kb_max : -__builtin_inf();
+    h.mm_min[k] = p.has_kb ? p.kb_min : __builtin_inf();
+  }
+  h.cur = 0;
+  h.root_sel = 0;
+  h.root_size = 0;
+  h.sup_sel = 0;
+  h.n_sup = 0;
+  h.sup_used = 0;
+  h.err = 0;
+  h.last_action = -1;
+  h.num_sims = 0;
+  h.search_depth = 0;
+  h.sims_done = 0;
+  h.pad = 0;
+  p.hdr[b] = h;
+}
+
+// INTMCP.update (intmcp.py:198-300) for every pair.
+template <class Env>
+__global__ __launch_bounds__(64) void k_im_update(ImParams p) {
+  __shared__ typename Env::Model sm;
+  stage_model(p.model, sm);
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= p.B) return;
+  ImPair<Env> P(p, sm, b);
+  const uint64_t obs = p.in_obs[b];
+  P.h.num_sims = 0;         // the step's counters (intmcp.py:114-136 resets them first)
+  P.h.search_depth = 0;
+  if (P.h.err == 0 && !im_absorbing(P.nd[0][P.h.cur].info)) {
+    auto draw_model = [&](uint32_t n) { return P.d_model(n); };
+    const double* prob = P.prob;
+    int nsup = 0;
+    if (P.nd[0][P.h.cur].t == 0) {
+      // _initial_nested_update (intmcp.py:216-268), level 1
+      const int node = P.child(0, 0, p.A, obs);
+      if (node >= 0) {
+        P.traverse(0, node);
+        uint32_t s0, s1;
+        if (!Env::sample_agent_initial(sm, p.ego, obs, draw_model, &s0, &s1)) P.fail(POMCP_E_INVALID);
+        P.h.root_sel ^= 1;
+        uint4* rb = P.root_buf(P.h.root_sel);
+        int n = 0;
+        while (P.h.err == 0 && (double)n < 1.0 * (double)p.n_target) {
+          if (n >= p.Nr) {
+            P.fail(POMCP_E_ARENA);
+            break;
+          }
+          Env::sample_agent_initial(sm, p.ego, obs, draw_model, &s0, &s1);
+          const uint64_t ok = Env::obs_key(sm, p.other, s0, s1);
+          const int c = P.child(1, 0, p.A, ok);
+          rb[n++] = make_uint4(s0, s1, (uint32_t)(c < 0 ? 0 : c), 0u);
+        }
+        P.h.cur = node;
+        P.h.root_size = n;
+        if (P.h.err == 0 && n > 0) {
+          // level 0: support of the histories, their initial beliefs
+          const int sel = P.h.sup_sel ^ 1;
+          im_support(P, sel, n, &nsup);
+          ISup* tab = P.sup_tab(sel);
+          const uint64_t o0 = P.nd[1][tab[0].node].okey;
+          Env::sample_agent_initial(sm, p.other, o0, draw_model, &s0, &s1);   // probe
+          int off = 0;
+          for (int q = 0; q < nsup && P.h.err == 0; ++q) {
+            P.traverse(1, tab[q].node);
+            const uint64_t oq = P.nd[1][tab[q].node].okey;
+            tab[q].off = off;
+            tab[q].size = 0;
+            uint2* pp = P.sup_parts(sel) + off;
+            int m = 0;
+            while ((double)m < prob[q] * (double)p.n_target) {
+              if (off + m >= p.Nsp) {
+                P.fail(POMCP_E_ARENA);
+                break;
+              }
+              Env::sample_agent_initial(sm, p.other, oq, draw_model, &s0, &s1);
+              pp[m++] = make_uint2(s0, s1);
+            }
+            tab[q].size = m;
+            tab[q].cap = m;
+            off += m;
+          }
+          P.h.sup_sel = sel;
+          P.h.n_sup = nsup;
+          P.h.sup_used = off;
+        }
+      }
+    } else {
+      // _nested_update (intmcp.py:270-300), level 1: re-root to (action, obs)
+      const int action = p.in_actions[b];
+      const int node = (action >= 0 && action < p.A) ? P.child(0, P.h.cur, action, obs) : -1;
+      if (node < 0) {
+        P.fail(POMCP_E_NOT_FOUND);
+      } else {
+        P.traverse(0, node);
+        // its belief: log records of `node`, insertion order
+        const int prev_size = P.h.root_size;
+        P.h.root_sel ^= 1;
+        uint4* rb = P.root_buf(P.h.root_sel);
+        int n = 0;
+        for (int i = 0; i < P.h.n_log[0]; ++i) {
+          const IRec r = P.lg[0][i];
+          if ((int)r.node == node) {
+            if (n >= p.Nr) {
+              P.fail(POMCP_E_ARENA);
+              break;
+            }
+            rb[n++] = make_uint4(r.v0, r.v1, r.nested, 0u);
+          }
+        }
+        P.h.pad = prev_size;
+        if (!im_absorbing(P.nd[0][node].info) && P.h.err == 0)
+          P.reinvig_top(node, action, obs, p.n_target, &n);   // ceil(1.0 * target)
+        P.h.cur = node;
+        P.h.root_size = n;
+        // level 0: support of the new root belief, materialised + reinvigorated
+        if (P.h.err == 0 && n > 0) {
+          const int sel = P.h.sup_sel ^ 1;
+          im_support(P, sel, n, &nsup);
+          im_extract_support(P, sel, nsup);
+          ISup* tab = P.sup_tab(sel);
+          P.h.pad = P.h.n_sup;   // previous support count (parents)
+          for (int q = 0; q < nsup && P.h.err == 0; ++q) {
+            const int m = tab[q].node;
+            P.traverse(1, m);
+            if (im_absorbing(P.nd[1][m].info)) continue;
+            const int tq = (int)ceil(prob[q] * (double)p.n_target);
+            P.reinvig_nested(m, (int)im_paction(P.nd[1][m].info), P.nd[1][m].okey, tq, sel, q);
+          }
+          int used = 0;
+          for (int q = 0; q < nsup; ++q) used = max(used, tab[q].off + tab[q].cap);
+          P.h.sup_sel = sel;
+          P.h.n_sup = nsup;
+          P.h.sup_used = used;
+        } else {
+          P.h.sup_sel ^= 1;
+          P.h.n_sup = 0;
+          P.h.sup_used = 0;
+        }
+      }
+    }
+  }
+  P.h.pad = 0;
+  P.store();
+  p.out[2 * b] = im_absorbing(P.nd[0][P.h.cur].info) ? 1 : 0;
+  p.out[2 * b + 1] = P.h.err;
+}
+
+// INTMCP.get_action (intmcp.py:368-408): sims[0] simulations at level 0, then
+// sims[1] at level 1; kImBegin resets the step's counters, kImFinal runs the
+// final action selection.  A fixed-count search is one launch with both flags;
+// the wall-clock loop of the reference is several launches.
+constexpr int kImBegin = 1, kImFinal = 2;
+template <class Env>
+__global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sims1, int flags) {
+  __shared__ typename Env::Model sm;
+  stage_model(p.model, sm);
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= p.B) return;
+  ImPair<Env> P(p, sm, b);
+  if (flags & kImBegin) {
+    P.h.num_sims = 0;
+    P.h.search_depth = 0;
+  }
+  const int root = P.h.cur;
+  int action = 0;
+  if (P.h.err == 0 && !im_absorbing(P.nd[0][root].info) && P.nd[0][root].t > 0) {
+    uint4* rb = P.root_buf(P.h.root_sel);
+    for (int level = 0; level < 2 && P.h.err == 0; ++level) {
+      const int num_sims = level == 0 ? sims0 : sims1;
+      for (int s = 0; s < num_sims && P.h.err == 0; ++s) {
+        // _nested_sim(history, level, top_level=True) of the level-1 planner
+        P.traverse(0, root);
+        if (im_nreg(P.nd[0][root].info) == 0) P.expand(0, root);
+        if (P.h.root_size == 0 || P.h.root_size < p.extra) {
+          P.fail(POMCP_E_UNSUPPORTED);   // depleted root (needs the top-level reinvigoration)
+          break;
+        }
+        const uint4 hp = rb[P.d_bel(1, (uint32_t)P.h.root_size)];
+        if (level == 0) {
+          // the level-0 planner's _nested_sim at the particle's history
+          const int n = (int)hp.z;
+          P.traverse(1, n);
+          if (im_nreg(P.nd[1][n].info) == 0) P.expand(1, n);
+          ISup& e = P.sup_tab(P.h.sup_sel)[hp.w];
+          if (e.size == 0) {
+            P.fail(POMCP_E_UNSUPPORTED);   // depleted level-0 node
+            break;
+          }
+          const uint2 q = P.sup_parts(P.h.sup_sel)[e.off + P.d_bel(0, (uint32_t)e.size)];
+          P.simulate(1, q.x, q.y, 0u, n);
+          P.nd[1][n].visits += 1;
+        } else {
+          const int d = P.simulate(0, hp.x, hp.y, hp.z, root);
+          P.nd[0][root].visits += 1;
+          if (d > P.h.search_depth) P.h.search_depth = d;
+        }
+        P.h.num_sims += 1;
+      }
+    }
+    if (!(flags & kImFinal)) {
+      P.store();
+      return;
+    }
+    // max_value_action_selection (intmcp.py:718-732)
+    const INode x = P.nd[0][root];
+    const int nr = im_nreg(x.info);
+    if (nr == 0) {
+      action = (int)P.d_sel((uint32_t)p.A);
+    } else {
+      double mx = -__builtin_inf();
+      int ties[6], nt = 0;
+      for (int i = 0; i < nr; ++i) {
+        const int a = im_order(x.info, i);
+        const double v = P.st[0][x.stats + a].value;
+        if (v == mx) {
+          ties[nt++] = a;
+        } else if (v > mx) {
+          mx = v;
+          ties[0] = a;
+          nt = 1;
+        }
+      }
+      action = ties[P.d_sel((uint32_t)nt)];
+    }
+  }
+  if (flags & kImFinal) P.h.last_action = action;
+  P.store();
+}
+
+template <class Env>
+__global__ __launch_bounds__(64) void k_im_synthetic(ImParams p, uint64_t env_seed_base) {
+  __shared__ typename Env::Model sm;
+  stage_model(p.model, sm);
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= p.B) return;
+  Streams env;
+  env.seed = env_seed_base + (uint64_t)b;
+  env.tree = 0x40000000u;
+  for (int k = 0; k < 5; ++k) env.ctr[k] = 0;
+  uint32_t s0, s1;
+  Env::sample_initial(sm, [&](uint32_t n) { return env.model(n); }, &s0, &s1);
+  p.out_obs[b] = Env::obs_key(sm, p.ego, s0, s1);
+}
+
+}  // namespace pb

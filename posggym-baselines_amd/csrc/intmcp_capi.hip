@@ -1,0 +1,415 @@
+// C-ABI host side of the I-NTMCP engine (include/intmcp.h).  Part of the
+// single translation unit of pomcp_capi.hip.
+#include "../../include/intmcp.h"
+
+struct intmcp_ctx {
+  intmcp_config cfg;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  ImParams ip{};
+  std::vector<void*> allocs;
+  std::string err;
+  DrvModel host_drv;
+  PeModel host_pe;
+  const void* host_model = nullptr;
+  size_t model_bytes = 0;
+  std::vector<int32_t> host_out;
+  std::vector<IHdr> host_hdr;
+};
+
+#define IM_TRY(ctx, expr)                                                           \
+  do {                                                                              \
+    hipError_t e_ = (expr);                                                         \
+    if (e_ != hipSuccess) {                                                         \
+      (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);              \
+      return POMCP_E_HIP;                                                           \
+    }                                                                               \
+  } while (0)
+
+#define IM_LAUNCH(ctx, KERNEL, grid, block, ...)                                              \
+  do {                                                                                         \
+    if ((ctx)->cfg.base.env_id == POMCP_ENV_PURSUIT_EVASION)                                   \
+      hipLaunchKernelGGL(KERNEL<EnvPursuitEvasion>, grid, block, 0, (ctx)->stream, __VA_ARGS__); \
+    else                                                                                       \
+      hipLaunchKernelGGL(KERNEL<EnvDriving>, grid, block, 0, (ctx)->stream, __VA_ARGS__);    \
+  } while (0)
+
+static unsigned im_blocks(int B) { return (unsigned)((B + 63) / 64); }
+
+static int im_alloc(intmcp_ctx* ctx, void** out, size_t bytes) {
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, bytes ? bytes : 16);
+  if (e != hipSuccess) {
+    ctx->err = "hipMalloc(" + std::to_string(bytes) + " B): " + hipGetErrorString(e);
+    return POMCP_E_HIP;
+  }
+  ctx->allocs.push_back(p);
+  *out = p;
+  return POMCP_OK;
+}
+
+template <class T>
+static int im_copy(intmcp_ctx* ctx, T* dst, const T* src, size_t n) {
+  if (n == 0) return POMCP_OK;
+  IM_TRY(ctx, hipMemcpyAsync(dst, src, sizeof(T) * n, hipMemcpyDeviceToHost, ctx->stream));
+  IM_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return POMCP_OK;
+}
+
+extern "C" {
+
+const char* intmcp_last_error(const intmcp_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+void intmcp_destroy(intmcp_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  for (void* p : ctx->allocs) (void)hipFree(p);
+  if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, intmcp_ctx** out) {
+  if (!cfg || !out) return POMCP_E_INVALID;
+  *out = nullptr;
+  const pomcp_config& c = cfg->base;
+  auto* ctx = new intmcp_ctx();
+  ctx->cfg = *cfg;
+  auto bad = [&](int code, const char* m) {
+    ctx->err = m;
+    int rc = code;
+    delete ctx;
+    return rc;
+  };
+  if (c.abi_version != POMCP_ABI_VERSION) return bad(POMCP_E_INVALID, "ABI version mismatch");
+  if (c.env_id != POMCP_ENV_DRIVING && c.env_id != POMCP_ENV_PURSUIT_EVASION)
+    return bad(POMCP_E_UNSUPPORTED, "env_id");
+  if (c.num_agents != 2) return bad(POMCP_E_UNSUPPORTED, "2 agents");
+  if (c.num_actions != (c.env_id == POMCP_ENV_DRIVING ? 5 : 4)) return bad(POMCP_E_INVALID, "num_actions");
+  if (c.action_selection != POMCP_SEL_UCB && c.action_selection != POMCP_SEL_UNIFORM)
+    return bad(POMCP_E_UNSUPPORTED, "I-NTMCP pucb reads self.action_space (intmcp.py:645): ucb / uniform only");
+  if (c.ego_agent < 0 || c.ego_agent > 1 || c.num_trees < 1) return bad(POMCP_E_INVALID, "ego / pairs");
+  if (c.depth_limit < 0 || c.step_limit < 0 || c.num_particles < 1) return bad(POMCP_E_INVALID, "limits");
+  if (cfg->max_nodes < 2 || cfg->max_nodes >= (1ll << 28) || cfg->max_stats < c.num_actions ||
+      cfg->max_log < 1 || cfg->hash_slots < 16 || (cfg->hash_slots & (cfg->hash_slots - 1)) ||
+      cfg->hash_slots > (1ll << 31) || cfg->max_root_belief < 2 * (c.num_particles + c.extra_particles) ||
+      cfg->max_support_particles < 1)
+    return bad(POMCP_E_INVALID, "capacities");
+  if (!c.log_table || c.log_table_size < 2 || !c.discount_pow || c.discount_pow_size < 1)
+    return bad(POMCP_E_INVALID, "tables");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) {
+    delete ctx;
+    return POMCP_E_NO_DEVICE;
+  }
+  ctx->device = device;
+  if (hipSetDevice(device) != hipSuccess) {
+    delete ctx;
+    return POMCP_E_NO_DEVICE;
+  }
+  if (hip_stream) {
+    ctx->stream = (hipStream_t)hip_stream;
+  } else {
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+      delete ctx;
+      return POMCP_E_HIP;
+    }
+    ctx->own_stream = true;
+  }
+  if (c.env_id == POMCP_ENV_PURSUIT_EVASION) {
+    build_pe_model(c.pe_grid, &ctx->host_pe);
+    ctx->host_model = &ctx->host_pe;
+    ctx->model_bytes = sizeof(PeModel);
+  } else {
+    std::memcpy(&ctx->host_drv.g, &c.grid, sizeof(DrvGrid));
+    build_model_tables(ctx->host_drv.g, &ctx->host_drv);
+    ctx->host_model = &ctx->host_drv;
+    ctx->model_bytes = sizeof(DrvModel);
+  }
+  ImParams& d = ctx->ip;
+  d.B = c.num_trees;
+  d.A = c.num_actions;
+  d.ego = c.ego_agent;
+  d.other = 1 - c.ego_agent;
+  d.sel = c.action_selection;
+  d.depth_limit = c.depth_limit;
+  d.step_limit = c.step_limit;
+  d.n_target = c.num_particles + c.extra_particles;
+  d.extra = c.extra_particles;
+  d.has_kb = c.has_known_bounds;
+  d.state_belief_only = cfg->state_belief_only;
+  d.discount = c.discount;
+  d.c = c.c;
+  d.limit_factor = c.reinvigoration_sample_limit_factor;
+  d.kb_min = c.known_min;
+  d.kb_max = c.known_max;
+  d.Nn = cfg->max_nodes;
+  d.Ns = cfg->max_stats;
+  d.Nl = cfg->max_log;
+  d.H = cfg->hash_slots;
+  d.Nr = cfg->max_root_belief;
+  d.Nsp = cfg->max_support_particles;
+  const int64_t B = c.num_trees;
+  int rc;
+  void* p;
+#define IM_ALLOC(field, type, count)                                            \
+  do {                                                                          \
+    if ((rc = im_alloc(ctx, &p, sizeof(type) * (size_t)(count))) != POMCP_OK) {\
+      intmcp_destroy(ctx);                                                      \
+      return rc;                                                                \
+    }                                                                           \
+    d.field = reinterpret_cast<decltype(d.field)>(p);                           \
+  } while (0)
+  IM_ALLOC(hdr, IHdr, B);
+  IM_ALLOC(nodes, INode, B * 2 * d.Nn);
+  IM_ALLOC(stats, IStat, B * 2 * d.Ns);
+  IM_ALLOC(hash, IHash, B * 2 * d.H);
+  IM_ALLOC(log, IRec, B * 2 * d.Nl);
+  IM_ALLOC(root, uint4, B * 2 * d.Nr);
+  IM_ALLOC(sup, ISup, B * 2 * d.Nr);
+  IM_ALLOC(supp, uint2, B * 2 * d.Nsp);
+  IM_ALLOC(path, int4, B * kImPath * 2);
+  IM_ALLOC(prob, double, B * d.Nr);
+  IM_ALLOC(logtab, double, c.log_table_size);
+  IM_ALLOC(dpow, double, c.discount_pow_size);
+  IM_ALLOC(model, uint8_t, ctx->model_bytes);
+  IM_ALLOC(in_actions, int32_t, B);
+  IM_ALLOC(in_obs, uint64_t, B);
+  IM_ALLOC(out, int32_t, B * 2);
+  IM_ALLOC(out_obs, uint64_t, B);
+#undef IM_ALLOC
+  d.logtab_n = c.log_table_size;
+  d.dpow_n = (int32_t)(c.discount_pow_size > INT32_MAX ? INT32_MAX : c.discount_pow_size);
+  std::vector<IHdr> h((size_t)B);
+  for (int64_t t = 0; t < B; ++t) {
+    std::memset(&h[t], 0, sizeof(IHdr));
+    h[t].seed = c.seed;
+    h[t].tree_key = c.tree_key_base + (uint32_t)t;
+  }
+  hipStream_t s = ctx->stream;
+  if (hipMemcpyAsync((void*)d.logtab, c.log_table, sizeof(double) * c.log_table_size,
+                     hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync((void*)d.dpow, c.discount_pow, sizeof(double) * c.discount_pow_size,
+                     hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync((void*)d.model, ctx->host_model, ctx->model_bytes, hipMemcpyHostToDevice,
+                     s) != hipSuccess ||
+      hipMemcpyAsync(d.hdr, h.data(), sizeof(IHdr) * (size_t)B, hipMemcpyHostToDevice, s) !=
+          hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess) {
+    ctx->err = "initial upload failed";
+    intmcp_destroy(ctx);
+    return POMCP_E_HIP;
+  }
+  ctx->host_out.resize((size_t)(2 * B));
+  ctx->host_hdr.resize((size_t)B);
+  rc = intmcp_reset(ctx);
+  if (rc != POMCP_OK) {
+    intmcp_destroy(ctx);
+    return rc;
+  }
+  *out = ctx;
+  return POMCP_OK;
+}
+
+int intmcp_reset(intmcp_ctx* ctx) {
+  if (!ctx) return POMCP_E_INVALID;
+  IM_TRY(ctx, hipSetDevice(ctx->device));
+  IM_LAUNCH(ctx, k_im_reset, dim3(im_blocks(ctx->ip.B)), dim3(64), ctx->ip);
+  IM_TRY(ctx, hipGetLastError());
+  IM_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return POMCP_OK;
+}
+
+static int im_first_error(intmcp_ctx* ctx, const char* what) {
+  for (int t = 0; t < ctx->ip.B; ++t) {
+    const int e = ctx->host_out[2 * t + 1];
+    if (e != 0) {
+      ctx->err = std::string(what) + ": pair " + std::to_string(t) + ": status " + std::to_string(e);
+      return e;
+    }
+  }
+  return POMCP_OK;
+}
+
+int intmcp_update(intmcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_keys,
+                  int32_t* root_absorbing_out) {
+  if (!ctx || !obs_keys) return POMCP_E_INVALID;
+  IM_TRY(ctx, hipSetDevice(ctx->device));
+  const int B = ctx->ip.B;
+  std::vector<int32_t> acts((size_t)B, -1);
+  if (actions) std::memcpy(acts.data(), actions, sizeof(int32_t) * (size_t)B);
+  IM_TRY(ctx, hipMemcpyAsync((void*)ctx->ip.in_actions, acts.data(), sizeof(int32_t) * B,
+                             hipMemcpyHostToDevice, ctx->stream));
+  IM_TRY(ctx, hipMemcpyAsync((void*)ctx->ip.in_obs, obs_keys, sizeof(uint64_t) * B,
+                             hipMemcpyHostToDevice, ctx->stream));
+  IM_LAUNCH(ctx, k_im_update, dim3(im_blocks(B)), dim3(64), ctx->ip);
+  IM_TRY(ctx, hipGetLastError());
+  IM_TRY(ctx, hipMemcpyAsync(ctx->host_out.data(), ctx->ip.out, sizeof(int32_t) * 2 * B,
+                             hipMemcpyDeviceToHost, ctx->stream));
+  IM_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  if (root_absorbing_out)
+    for (int t = 0; t < B; ++t) root_absorbing_out[t] = ctx->host_out[2 * t];
+  return im_first_error(ctx, "update");
+}
+
+static int im_fetch_hdr(intmcp_ctx* ctx) {
+  IM_TRY(ctx, hipMemcpyAsync(ctx->host_hdr.data(), ctx->ip.hdr, sizeof(IHdr) * ctx->ip.B,
+                             hipMemcpyDeviceToHost, ctx->stream));
+  IM_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return POMCP_OK;
+}
+
+int intmcp_search_levels(intmcp_ctx* ctx, int32_t level0_sims, int32_t level1_sims,
+                         int32_t flags, int32_t* actions_out) {
+  if (!ctx || level0_sims < 0 || level1_sims < 0 || (flags & ~(kImBegin | kImFinal)))
+    return POMCP_E_INVALID;
+  IM_TRY(ctx, hipSetDevice(ctx->device));
+  IM_LAUNCH(ctx, k_im_search, dim3(im_blocks(ctx->ip.B)), dim3(64), ctx->ip, (int)level0_sims,
+            (int)level1_sims, (int)flags);
+  IM_TRY(ctx, hipGetLastError());
+  if (!actions_out) return POMCP_OK;
+  int rc = im_fetch_hdr(ctx);
+  if (rc != POMCP_OK) return rc;
+  for (int t = 0; t < ctx->ip.B; ++t) {
+    if (ctx->host_hdr[t].err != 0) {
+      ctx->err = "search: pair " + std::to_string(t) + ": status " + std::to_string(ctx->host_hdr[t].err);
+      return ctx->host_hdr[t].err;
+    }
+    actions_out[t] = ctx->host_hdr[t].last_action;
+  }
+  return POMCP_OK;
+}
+
+int intmcp_search(intmcp_ctx* ctx, int32_t num_sims, int32_t* actions_out) {
+  if (!ctx || num_sims < 0) return POMCP_E_INVALID;
+  return intmcp_search_levels(ctx, num_sims, num_sims, kImBegin | kImFinal, actions_out);
+}
+
+int intmcp_get_root_stats(intmcp_ctx* ctx, intmcp_root_stats* out) {
+  if (!ctx || !out) return POMCP_E_INVALID;
+  IM_TRY(ctx, hipSetDevice(ctx->device));
+  int rc = im_fetch_hdr(ctx);
+  if (rc != POMCP_OK) return rc;
+  const ImParams& d = ctx->ip;
+  for (int t = 0; t < d.B; ++t) {
+    const IHdr& h = ctx->host_hdr[t];
+    intmcp_root_stats& o = out[t];
+    std::memset(&o, 0, sizeof(o));
+    INode node;
+    rc = im_copy(ctx, &node, d.nodes + (int64_t)t * 2 * d.Nn + h.cur, 1);
+    if (rc != POMCP_OK) return rc;
+    o.action = h.last_action;
+    o.num_sims = h.num_sims;
+    o.search_depth = h.search_depth;
+    o.root_visits = node.visits;
+    o.root_absorbing = im_absorbing(node.info) ? 1 : 0;
+    o.belief_size = h.root_size;
+    o.error = h.err;
+    const int nr = im_nreg(node.info);
+    o.num_children = nr;
+    if (node.stats >= 0) {
+      std::vector<IStat> stv((size_t)d.A);
+      rc = im_copy(ctx, stv.data(), d.stats + (int64_t)t * 2 * d.Ns + node.stats, (size_t)d.A);
+      if (rc != POMCP_OK) return rc;
+      for (int i = 0; i < nr && i < POMCP_MAX_ACTIONS; ++i) {
+        const int a = im_order(node.info, i);
+        o.child_action[i] = a;
+        if (a < d.A) {
+          o.child_visits[i] = stv[a].visits;
+          o.child_values[i] = stv[a].value;
+          o.child_totals[i] = stv[a].total;
+        }
+      }
+    }
+    o.min_value = h.mm_min[0];
+    o.max_value = h.mm_max[0];
+    for (int k = 0; k < 2; ++k) {
+      o.n_nodes[k] = h.n_nodes[k];
+      o.n_log[k] = h.n_log[k];
+    }
+    o.n_support = h.n_sup;
+  }
+  return POMCP_OK;
+}
+
+int intmcp_get_root_belief(intmcp_ctx* ctx, int32_t pair, uint32_t* out, int32_t capacity,
+                           int32_t* count) {
+  if (!ctx || !count || pair < 0 || pair >= ctx->ip.B) return POMCP_E_INVALID;
+  int rc = im_fetch_hdr(ctx);
+  if (rc != POMCP_OK) return rc;
+  const IHdr& h = ctx->host_hdr[pair];
+  *count = h.root_size;
+  if (!out || capacity < h.root_size) return POMCP_OK;
+  std::vector<uint4> buf((size_t)h.root_size);
+  rc = im_copy(ctx, buf.data(), ctx->ip.root + ((int64_t)pair * 2 + h.root_sel) * ctx->ip.Nr,
+               (size_t)h.root_size);
+  if (rc != POMCP_OK) return rc;
+  for (int i = 0; i < h.root_size; ++i) {
+    out[3 * i] = buf[i].x;
+    out[3 * i + 1] = buf[i].y;
+    out[3 * i + 2] = buf[i].z;
+  }
+  return POMCP_OK;
+}
+
+int intmcp_get_nodes(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int32_t capacity,
+                     int32_t* count) {
+  if (!ctx || !count || pair < 0 || pair >= ctx->ip.B || tree < 0 || tree > 1) return POMCP_E_INVALID;
+  int rc = im_fetch_hdr(ctx);
+  if (rc != POMCP_OK) return rc;
+  const int n = ctx->host_hdr[pair].n_nodes[tree];
+  *count = n;
+  if (!out || capacity < n) return POMCP_OK;
+  return im_copy(ctx, reinterpret_cast<INode*>(out), ctx->ip.nodes + ((int64_t)pair * 2 + tree) * ctx->ip.Nn,
+                 (size_t)n);
+}
+
+int intmcp_get_stats(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int32_t capacity,
+                     int32_t* count) {
+  if (!ctx || !count || pair < 0 || pair >= ctx->ip.B || tree < 0 || tree > 1) return POMCP_E_INVALID;
+  int rc = im_fetch_hdr(ctx);
+  if (rc != POMCP_OK) return rc;
+  const int n = ctx->host_hdr[pair].n_stats[tree];
+  *count = n;
+  if (!out || capacity < n) return POMCP_OK;
+  return im_copy(ctx, reinterpret_cast<IStat*>(out), ctx->ip.stats + ((int64_t)pair * 2 + tree) * ctx->ip.Ns,
+                 (size_t)n);
+}
+
+int intmcp_get_support(intmcp_ctx* ctx, int32_t pair, int32_t* entries, int32_t capacity_entries,
+                       int32_t* n_entries, uint32_t* particles, int32_t capacity_particles,
+                       int32_t* n_particles) {
+  if (!ctx || !n_entries || !n_particles || pair < 0 || pair >= ctx->ip.B) return POMCP_E_INVALID;
+  int rc = im_fetch_hdr(ctx);
+  if (rc != POMCP_OK) return rc;
+  const IHdr& h = ctx->host_hdr[pair];
+  *n_entries = h.n_sup;
+  *n_particles = h.sup_used;
+  if (entries && capacity_entries >= h.n_sup) {
+    rc = im_copy(ctx, reinterpret_cast<ISup*>(entries),
+                 ctx->ip.sup + ((int64_t)pair * 2 + h.sup_sel) * ctx->ip.Nr, (size_t)h.n_sup);
+    if (rc != POMCP_OK) return rc;
+  }
+  if (particles && capacity_particles >= h.sup_used) {
+    rc = im_copy(ctx, reinterpret_cast<uint2*>(particles),
+                 ctx->ip.supp + ((int64_t)pair * 2 + h.sup_sel) * ctx->ip.Nsp, (size_t)h.sup_used);
+    if (rc != POMCP_OK) return rc;
+  }
+  return POMCP_OK;
+}
+
+int intmcp_synthetic_obs(intmcp_ctx* ctx, uint64_t env_seed_base, uint64_t* obs_keys_out) {
+  if (!ctx) return POMCP_E_INVALID;
+  IM_TRY(ctx, hipSetDevice(ctx->device));
+  IM_LAUNCH(ctx, k_im_synthetic, dim3(im_blocks(ctx->ip.B)), dim3(64), ctx->ip, env_seed_base);
+  IM_TRY(ctx, hipGetLastError());
+  if (obs_keys_out) {
+    IM_TRY(ctx, hipMemcpyAsync(obs_keys_out, ctx->ip.out_obs, sizeof(uint64_t) * ctx->ip.B,
+                               hipMemcpyDeviceToHost, ctx->stream));
+  }
+  IM_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return POMCP_OK;
+}
+
+}  // extern "C"

@@ -15,6 +15,7 @@
 // Single translation unit: the kernels are compiled together with their launchers.
 #include "pomcp_kernels.hip"
 #include "pomcp_search.hip"
+#include "intmcp.hip"
 #include "../../include/pomcp_debug.h"
 
 using namespace pb;
@@ -604,6 +605,21 @@ int pomcp_debug_fp_selftest(const double* a, const double* b, int32_t n, double*
   return e == hipSuccess ? POMCP_OK : POMCP_E_HIP;
 }
 
+// Debug: device exp (the I-NTMCP softmax, intmcp.py:784-786) for comparison
+// with the host's math.exp.
+int pomcp_debug_exp(const double* x, int32_t n, double* out) {
+  if (!x || !out || n <= 0) return POMCP_E_INVALID;
+  double *dx = nullptr, *dout = nullptr;
+  if (hipMalloc(&dx, sizeof(double) * n) != hipSuccess) return POMCP_E_HIP;
+  (void)hipMalloc(&dout, sizeof(double) * n);
+  (void)hipMemcpy(dx, x, sizeof(double) * n, hipMemcpyHostToDevice);
+  hipLaunchKernelGGL(k_exp_selftest, dim3((n + 255) / 256), dim3(256), 0, 0, dx, n, dout);
+  hipError_t e = hipMemcpy(out, dout, sizeof(double) * n, hipMemcpyDeviceToHost);
+  (void)hipFree(dx);
+  (void)hipFree(dout);
+  return e == hipSuccess ? POMCP_OK : POMCP_E_HIP;
+}
+
 // Debug: per-wave phase cycles of k_search (diagnostics build only).
 int pomcp_debug_phase_timing(pomcp_ctx* ctx, uint64_t* out, int32_t capacity, int32_t* count) {
   if (!ctx || !count) return POMCP_E_INVALID;
@@ -634,3 +650,6 @@ int pomcp_debug_phase_timing(pomcp_ctx* ctx, uint64_t* out, int32_t capacity, in
 }
 
 }  // extern "C"
+
+// I-NTMCP (include/intmcp.h)
+#include "intmcp_capi.hip"

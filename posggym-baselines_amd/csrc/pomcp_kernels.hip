@@ -562,6 +562,11 @@ __global__ __launch_bounds__(256) void k_restore(DevParams p, const TreeHdr* sna
   }
 }
 
+__global__ void k_exp_selftest(const double* x, int n, double* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = exp(x[i]);
+}
+
 __global__ void k_fp_selftest(const double* a, const double* b, int n, double* out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;

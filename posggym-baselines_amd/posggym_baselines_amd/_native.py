@@ -171,8 +171,76 @@ SIGNATURES = [
 ]
 DEBUG_SIGNATURES = [
     ("pomcp_debug_fp_selftest", C.c_int, [_PD, _PD, C.c_int32, _PD]),
+    ("pomcp_debug_exp", C.c_int, [_PD, C.c_int32, _PD]),
     ("pomcp_debug_phase_timing", C.c_int,
      [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32, C.POINTER(C.c_int32)]),
+]
+
+
+
+class IntmcpConfig(C.Structure):
+    """``intmcp_config`` (include/intmcp.h)."""
+    _fields_ = [
+        ("base", PomcpConfig),
+        ("state_belief_only", C.c_int32),
+        ("pad", C.c_int32),
+        ("max_nodes", C.c_int64),
+        ("max_stats", C.c_int64),
+        ("max_log", C.c_int64),
+        ("hash_slots", C.c_int64),
+        ("max_root_belief", C.c_int64),
+        ("max_support_particles", C.c_int64),
+    ]
+
+
+class IntmcpRootStats(C.Structure):
+    """``intmcp_root_stats`` (include/intmcp.h)."""
+    _fields_ = [
+        ("action", C.c_int32),
+        ("num_sims", C.c_int32),
+        ("search_depth", C.c_int32),
+        ("root_visits", C.c_int32),
+        ("root_absorbing", C.c_int32),
+        ("belief_size", C.c_int32),
+        ("error", C.c_int32),
+        ("num_children", C.c_int32),
+        ("child_action", C.c_int32 * POMCP_MAX_ACTIONS),
+        ("child_visits", C.c_int32 * POMCP_MAX_ACTIONS),
+        ("child_values", C.c_double * POMCP_MAX_ACTIONS),
+        ("child_totals", C.c_double * POMCP_MAX_ACTIONS),
+        ("min_value", C.c_double),
+        ("max_value", C.c_double),
+        ("n_nodes", C.c_int32 * 2),
+        ("n_log", C.c_int32 * 2),
+        ("n_support", C.c_int32),
+        ("pad", C.c_int32),
+    ]
+
+
+INTMCP_BEGIN, INTMCP_FINAL = 1, 2
+
+# numpy views of the diagnostic records (include/intmcp.h)
+INTMCP_NODE_DTYPE = [("parent", "<i4"), ("info", "<u4"), ("visits", "<i4"), ("t", "<i4"),
+                     ("stats", "<i4"), ("support", "<u4"), ("okey", "<u8")]
+INTMCP_STAT_DTYPE = [("visits", "<i4"), ("pad", "<i4"), ("value", "<f8"), ("total", "<f8"),
+                     ("agg", "<f8")]
+INTMCP_SUPPORT_DTYPE = [("node", "<i4"), ("off", "<i4"), ("size", "<i4"), ("cap", "<i4")]
+
+INTMCP_SIGNATURES = [
+    ("intmcp_create", C.c_int, [C.POINTER(IntmcpConfig), C.c_int32, C.c_void_p, C.POINTER(_CTX)]),
+    ("intmcp_destroy", None, [_CTX]),
+    ("intmcp_last_error", C.c_char_p, [_CTX]),
+    ("intmcp_reset", C.c_int, [_CTX]),
+    ("intmcp_update", C.c_int, [_CTX, _P32, _PU64, _P32]),
+    ("intmcp_search", C.c_int, [_CTX, C.c_int32, _P32]),
+    ("intmcp_search_levels", C.c_int, [_CTX, C.c_int32, C.c_int32, C.c_int32, _P32]),
+    ("intmcp_get_root_stats", C.c_int, [_CTX, C.POINTER(IntmcpRootStats)]),
+    ("intmcp_get_root_belief", C.c_int, [_CTX, C.c_int32, _PU32, C.c_int32, _P32]),
+    ("intmcp_get_nodes", C.c_int, [_CTX, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, _P32]),
+    ("intmcp_get_stats", C.c_int, [_CTX, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, _P32]),
+    ("intmcp_get_support", C.c_int,
+     [_CTX, C.c_int32, _P32, C.c_int32, _P32, _PU32, C.c_int32, _P32]),
+    ("intmcp_synthetic_obs", C.c_int, [_CTX, C.c_uint64, _PU64]),
 ]
 
 _lib = None
@@ -194,7 +262,7 @@ def load():
             f"{LIB_PATH} is missing: build it with `python -m posggym_baselines_amd.build` "
             "(or __graft_entry__.build()); there is no CPU fallback for the planner")
     lib = C.CDLL(LIB_PATH)
-    for name, res, args in SIGNATURES + DEBUG_SIGNATURES:
+    for name, res, args in SIGNATURES + DEBUG_SIGNATURES + INTMCP_SIGNATURES:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -204,11 +272,11 @@ def load():
     return lib
 
 
-def check(rc, ctx=None, what=""):
+def check(rc, ctx=None, what="", last_error="pomcp_last_error"):
     if rc != POMCP_OK:
         msg = what
         if ctx is not None:
-            err = load().pomcp_last_error(ctx)
+            err = getattr(load(), last_error)(ctx)
             if err:
                 msg = f"{what}: {err.decode()}"
         raise PomcpError(rc, msg)

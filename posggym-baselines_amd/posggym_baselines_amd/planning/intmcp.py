@@ -1,0 +1,504 @@
+"""I-NTMCP drop-in: the reference's ``INTMCP`` API (``intmcp.py:22-994``) at
+nesting level 1 with two agents, both planners' trees, beliefs and generative
+model on the GPU (``include/intmcp.h``, ``csrc/intmcp.hip``).
+
+Public surface kept from the reference: ``INTMCP.initialize(model,
+ego_agent_id, config, nesting_level, search_policies)``, ``step(obs)``,
+``reset()``, ``update(action, obs)``, ``get_action()``, ``close()``, and the
+attributes ``model``, ``agent_id``, ``config``, ``nesting_level``,
+``num_agents``, ``other_agent_policies`` (the level-0 planner, a view of the
+same device state), ``search_policies``, ``action_spaces``, ``step_limit``,
+``step_statistics``, ``stat_tracker``, ``root``.
+
+``BatchedINTMCP`` runs many independent planner pairs in one launch (BASELINE
+config 5: nested trees as a batched launch).
+
+Scope (DESIGN.md "I-NTMCP"): nesting level 1, random search policies
+(``search_policies=None``), ``ucb`` / ``uniform`` selection (the reference's
+``pucb_action_selection`` reads ``self.action_space``, which INTMCP does not
+define, ``intmcp.py:645``).  The reinvigoration of a depleted root during the
+search (``intmcp.py:426-431``) reports POMCP_E_UNSUPPORTED instead of running.
+"""
+import ctypes as C
+import dataclasses
+import logging
+import math
+import time
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import psutil
+
+from posggym_baselines_amd import _native as N
+from posggym_baselines_amd.planning.config import MCTSConfig
+from posggym_baselines_amd.planning.search_policy import RandomSearchPolicy
+from posggym_baselines_amd.planning.utils import PlanningStatTracker
+
+INT32_MAX = 2**31 - 1
+
+
+@dataclass
+class IntmcpCapacities:
+    max_nodes: int              # obs nodes per tree (32 B)
+    max_stats: int              # action statistics per tree (32 B)
+    max_log: int                # particle log records per tree (16 B)
+    hash_slots: int             # obs-child map slots per tree (16 B)
+    max_root_belief: int        # level-1 root particles (16 B, x2) and support entries (16 B, x2)
+    max_support_particles: int  # materialised level-0 particles (8 B, x2)
+    log_table_size: int
+    discount_pow_size: int
+
+    def bytes_per_pair(self) -> int:
+        return (2 * (self.max_nodes * 32 + self.max_stats * 32 + self.max_log * 16
+                     + self.hash_slots * 16) + 4 * self.max_root_belief * 16
+                + 2 * self.max_support_particles * 8 + self.max_root_belief * 8)
+
+
+def _next_pow2(n: int) -> int:
+    return 1 << max(4, (int(n) - 1).bit_length())
+
+
+def plan_intmcp_capacities(config, step_limit: int, num_sims: int, searches: int,
+                           num_actions: int) -> IntmcpCapacities:
+    """Worst-case sizes for ``searches`` steps of ``num_sims`` simulations per level.
+
+    Per step and tree: every simulation steps at most ``L = min(depth_limit,
+    step_limit) + 1`` levels (one node + one log record each); a level-1
+    simulation also extends the other agent's history in the level-0 tree;
+    each reinvigoration attempt (at most ``limit_factor x target`` per belief)
+    creates a level-0 node.  A root / level-0 belief gathers records of the
+    last ``L`` searches plus its reinvigoration (accepted and rejected).
+    """
+    L = min(config.depth_limit, step_limit) + 1
+    S = num_sims
+    target = config.num_particles + config.extra_particles
+    lf = config.reinvigoration_sample_limit_factor
+    reinv = int(math.ceil(lf * target)) + target
+    per_step = 2 * S * L + 2 * reinv + 2 * target + 8
+    nodes = searches * per_step + 16
+    nr = S * L + 4 * target + 64
+    nsp = S * L + 2 * nr + 4 * target + 64
+    total_sims = 2 * S * searches
+    return IntmcpCapacities(
+        max_nodes=nodes, max_stats=num_actions * nodes, max_log=nodes,
+        hash_slots=_next_pow2(2 * nodes), max_root_belief=nr, max_support_particles=nsp,
+        log_table_size=total_sims + 2, discount_pow_size=min(L, 4096) + 2)
+
+
+class IntmcpEngine:
+    """Python handle on one ``intmcp_ctx`` (``num_pairs`` planner pairs)."""
+
+    SELECTION = {"ucb": N.SEL_UCB, "uniform": N.SEL_UNIFORM}
+
+    def __init__(self, model, agent_id, config, num_pairs=1, capacities=None, num_sims=None,
+                 searches=None, device=None, stream=None, tree_key_base=0, seed=None):
+        lib = N.load()
+        if not hasattr(model, "configure_engine"):
+            raise NotImplementedError(
+                f"{type(model).__name__} has no GPU generative model; the engine implements "
+                "Driving-v1 and PursuitEvasion-v1 (posggym_baselines_amd.envs)")
+        if len(model.possible_agents) != 2:
+            raise NotImplementedError("the I-NTMCP engine plans for two agents")
+        if config.action_selection not in self.SELECTION:
+            raise NotImplementedError(
+                "INTMCP pucb_action_selection reads self.action_space, which INTMCP does not "
+                "define (intmcp.py:645); use 'ucb' or 'uniform'")
+        self.model = model
+        self.config = config
+        self.num_pairs = int(num_pairs)
+        self.ego = model.possible_agents.index(agent_id)
+        self.A = model.action_spaces[agent_id].n
+        other = model.possible_agents[1 - self.ego]
+        if model.action_spaces[other].n != self.A:
+            raise NotImplementedError("both agents need the same action count")
+        if config.step_limit is not None:
+            step_limit = int(config.step_limit)
+        elif getattr(model, "spec", None) is not None and model.spec.max_episode_steps:
+            step_limit = int(model.spec.max_episode_steps)
+        else:
+            step_limit = INT32_MAX
+        self.step_limit = step_limit
+        if capacities is None:
+            sims = num_sims if num_sims is not None else (config.num_sims or 1024)
+            budget = searches if searches is not None else (
+                (step_limit if step_limit < INT32_MAX else 100) + 1)
+            capacities = plan_intmcp_capacities(config, step_limit, sims, budget, self.A)
+        self.capacities = capacities
+        ic = N.IntmcpConfig()
+        c = ic.base
+        c.abi_version = N.POMCP_ABI_VERSION
+        c.num_agents = 2
+        c.ego_agent = self.ego
+        c.num_actions = self.A
+        c.action_selection = self.SELECTION[config.action_selection]
+        c.depth_limit = min(config.depth_limit, INT32_MAX)
+        c.step_limit = step_limit
+        c.num_particles = config.num_particles
+        c.extra_particles = config.extra_particles
+        kb = config.known_bounds
+        c.has_known_bounds = 1 if kb else 0
+        if kb:
+            c.known_min, c.known_max = float(kb[0]), float(kb[1])
+        c.num_trees = self.num_pairs
+        c.discount = config.discount
+        c.c = config.c
+        c.pucb_exploration_fraction = config.pucb_exploration_fraction
+        c.reinvigoration_sample_limit_factor = config.reinvigoration_sample_limit_factor
+        s = config.seed if seed is None else seed
+        if s is None:
+            s = int(np.random.SeedSequence().entropy) & (2**63 - 1)
+        c.seed = int(s) & (2**64 - 1)
+        c.tree_key_base = int(tree_key_base)
+        self._logtab = np.array([0.0] + [math.log(n) for n in range(1, capacities.log_table_size)],
+                                dtype=np.float64)
+        self._dpow = np.array([config.discount ** k for k in range(capacities.discount_pow_size)],
+                              dtype=np.float64)
+        c.log_table = self._logtab.ctypes.data_as(C.POINTER(C.c_double))
+        c.log_table_size = len(self._logtab)
+        c.discount_pow = self._dpow.ctypes.data_as(C.POINTER(C.c_double))
+        c.discount_pow_size = len(self._dpow)
+        model.configure_engine(c)
+        ic.state_belief_only = 1 if config.state_belief_only else 0
+        ic.max_nodes = capacities.max_nodes
+        ic.max_stats = capacities.max_stats
+        ic.max_log = capacities.max_log
+        ic.hash_slots = capacities.hash_slots
+        ic.max_root_belief = capacities.max_root_belief
+        ic.max_support_particles = capacities.max_support_particles
+        self._cfg = ic
+        dev = config.device if device is None else device
+        ctx = C.c_void_p()
+        rc = lib.intmcp_create(C.byref(ic), int(dev), stream, C.byref(ctx))
+        if rc != N.POMCP_OK:
+            raise N.PomcpError(rc, "intmcp_create failed (no GPU, bad config or out of memory)")
+        self._ctx = ctx
+        self._lib = lib
+        self._stats = (N.IntmcpRootStats * self.num_pairs)()
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self._lib.intmcp_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        N.check(rc, self._ctx, what, last_error="intmcp_last_error")
+
+    def reset(self):
+        self._check(self._lib.intmcp_reset(self._ctx), "reset")
+
+    def update(self, actions, obs_keys):
+        B = self.num_pairs
+        a = np.ascontiguousarray(np.broadcast_to(np.asarray(actions, dtype=np.int32), (B,)))
+        o = np.ascontiguousarray(np.broadcast_to(np.asarray(obs_keys, dtype=np.uint64), (B,)))
+        absorbing = np.zeros(B, dtype=np.int32)
+        self._check(self._lib.intmcp_update(
+            self._ctx, a.ctypes.data_as(C.POINTER(C.c_int32)),
+            o.ctypes.data_as(C.POINTER(C.c_uint64)),
+            absorbing.ctypes.data_as(C.POINTER(C.c_int32))), "update")
+        return absorbing.astype(bool)
+
+    def search(self, num_sims, fetch=True):
+        if not fetch:
+            self._check(self._lib.intmcp_search(self._ctx, int(num_sims), None), "search")
+            return None
+        out = np.zeros(self.num_pairs, dtype=np.int32)
+        self._check(self._lib.intmcp_search(self._ctx, int(num_sims),
+                                            out.ctypes.data_as(C.POINTER(C.c_int32))), "search")
+        return out
+
+    def search_levels(self, level0_sims, level1_sims, flags, fetch=False):
+        out = np.zeros(self.num_pairs, dtype=np.int32) if fetch else None
+        ptr = out.ctypes.data_as(C.POINTER(C.c_int32)) if fetch else None
+        self._check(self._lib.intmcp_search_levels(self._ctx, int(level0_sims), int(level1_sims),
+                                                   int(flags), ptr), "search_levels")
+        return out
+
+    def root_stats(self):
+        self._check(self._lib.intmcp_get_root_stats(self._ctx, self._stats), "get_root_stats")
+        return self._stats
+
+    def root_belief(self, pair=0):
+        """Level-1 root particles as (v0, v1, level-0 node) u32 rows."""
+        n = C.c_int32()
+        self._check(self._lib.intmcp_get_root_belief(self._ctx, pair, None, 0, C.byref(n)),
+                    "get_root_belief")
+        buf = np.zeros(3 * max(n.value, 1), dtype=np.uint32)
+        self._check(self._lib.intmcp_get_root_belief(
+            self._ctx, pair, buf.ctypes.data_as(C.POINTER(C.c_uint32)), n.value, C.byref(n)),
+            "get_root_belief")
+        return buf[:3 * n.value].reshape(-1, 3)
+
+    def _records(self, fn, pair, tree, dtype):
+        n = C.c_int32()
+        self._check(fn(self._ctx, pair, tree, None, 0, C.byref(n)), fn.__name__)
+        out = np.zeros(max(n.value, 1), dtype=dtype)
+        self._check(fn(self._ctx, pair, tree, out.ctypes.data_as(C.c_void_p), n.value,
+                       C.byref(n)), fn.__name__)
+        return out[:n.value]
+
+    def nodes(self, pair=0, tree=0):
+        """Obs nodes of one tree (0: level 1, 1: level 0) as a structured array."""
+        return self._records(self._lib.intmcp_get_nodes, pair, tree, N.INTMCP_NODE_DTYPE)
+
+    def stats(self, pair=0, tree=0):
+        return self._records(self._lib.intmcp_get_stats, pair, tree, N.INTMCP_STAT_DTYPE)
+
+    def support(self, pair=0):
+        """The materialised level-0 beliefs: (entries, (v0, v1) particles)."""
+        ne, npart = C.c_int32(), C.c_int32()
+        self._check(self._lib.intmcp_get_support(self._ctx, pair, None, 0, C.byref(ne), None, 0,
+                                                 C.byref(npart)), "get_support")
+        ent = np.zeros(max(ne.value, 1), dtype=N.INTMCP_SUPPORT_DTYPE)
+        parts = np.zeros(2 * max(npart.value, 1), dtype=np.uint32)
+        self._check(self._lib.intmcp_get_support(
+            self._ctx, pair, ent.ctypes.data_as(C.POINTER(C.c_int32)), ne.value, C.byref(ne),
+            parts.ctypes.data_as(C.POINTER(C.c_uint32)), npart.value, C.byref(npart)),
+            "get_support")
+        return ent[:ne.value], parts[:2 * npart.value].reshape(-1, 2)
+
+    def synthetic_obs(self, env_seed_base):
+        out = np.zeros(self.num_pairs, dtype=np.uint64)
+        self._check(self._lib.intmcp_synthetic_obs(
+            self._ctx, int(env_seed_base), out.ctypes.data_as(C.POINTER(C.c_uint64))),
+            "synthetic_obs")
+        return out
+
+
+def node_order(info: int):
+    """Registered actions of a node, registration order (``ObsNode.children``)."""
+    n = (int(info) >> 5) & 7
+    return [(int(info) >> (8 + 3 * i)) & 7 for i in range(n)]
+
+
+@dataclasses.dataclass
+class RootView:
+    """Read-only view of the level-1 root node."""
+
+    t: int = 0
+    is_absorbing: bool = False
+    visits: int = 0
+    children: tuple = ()          # (action, visits, value, total), registration order
+    belief_size: int = 0
+
+
+class _NestedPlanner:
+    """The level-0 planner of the other agent (``other_agent_policies[j]``):
+    a view of the device state shared with the level-1 planner."""
+
+    def __init__(self, parent, agent_id):
+        self._parent = parent
+        self.model = parent.model
+        self.agent_id = agent_id
+        self.config = parent.config
+        self.nesting_level = 0
+        self.other_agent_policies = {}
+        self.step_statistics = {"reinvigoration_time": 0.0}
+
+    def reset(self):
+        pass
+
+    def close(self):
+        pass
+
+    def _collect_nested_statistics(self):
+        return {"reinvigoration_time": 0.0}
+
+    def __str__(self):
+        return "INTMCP"
+
+
+class INTMCP:
+    """Interactive Nested Tree Monte-Carlo Planning, GPU-resident trees.
+
+    Built with :meth:`initialize` (as in the reference).  With ``num_sims``
+    set (``MCTSConfig.num_sims`` or the keyword) every ``get_action`` runs
+    exactly that many simulations per nesting level; otherwise the
+    ``search_time_limit`` is split evenly over the levels (``intmcp.py:383-397``).
+    """
+
+    def __init__(self, model, agent_id: str, config: MCTSConfig, nesting_level: int,
+                 other_agent_policies=None, search_policies=None, *,
+                 num_sims: Optional[int] = None):
+        if nesting_level != 1:
+            raise NotImplementedError("the GPU I-NTMCP engine runs nesting level 1")
+        if search_policies is not None and not all(
+                isinstance(p, RandomSearchPolicy) for p in search_policies.values()):
+            raise NotImplementedError("only RandomSearchPolicy search policies run in-kernel")
+        assert agent_id in model.possible_agents
+        self.model = model
+        self.agent_id = agent_id
+        self.config = config
+        self.nesting_level = nesting_level
+        self.num_agents = len(model.possible_agents)
+        self.search_policies = search_policies or {
+            i: RandomSearchPolicy(model, i) for i in model.possible_agents}
+        self.action_spaces = {i: list(range(model.action_spaces[i].n))
+                              for i in model.possible_agents}
+        other = [i for i in model.possible_agents if i != agent_id][0]
+        self.other_agent_policies = {other: _NestedPlanner(self, other)}
+        self._num_sims = num_sims if num_sims is not None else config.num_sims
+        self._engine = IntmcpEngine(model, agent_id, config, num_pairs=1,
+                                    num_sims=self._num_sims or 1024)
+        self.step_limit = self._engine.step_limit
+        self._logger = logging.getLogger()
+        self._last_action = None
+        self._step_num = 0
+        self.root = RootView()
+        self._min_value, self._max_value = self._initial_bounds()
+        self.step_statistics = {}
+        self._reset_step_statistics()
+        self.stat_tracker = PlanningStatTracker(self)
+
+    @classmethod
+    def initialize(cls, model, ego_agent_id: str, config: MCTSConfig, nesting_level: int,
+                   search_policies=None, *, num_sims: Optional[int] = None) -> "INTMCP":
+        """``intmcp.py:949-994``; ``search_policies`` is ``{level: {agent: policy}}``."""
+        if search_policies is not None:
+            flat = {}
+            for level_pols in search_policies.values():
+                for i, p in level_pols.items():
+                    if not isinstance(p, RandomSearchPolicy):
+                        raise NotImplementedError(
+                            "only RandomSearchPolicy search policies run in-kernel")
+                    flat[i] = p
+            search_policies = flat
+        return cls(model, ego_agent_id, config, nesting_level, None, search_policies,
+                   num_sims=num_sims)
+
+    # ---------------------------------------------------------------- step
+    def step(self, obs):
+        """``intmcp.py:114-136``."""
+        assert self.step_limit is None or self.root.t <= self.step_limit
+        if self.root.is_absorbing:
+            for k in self.step_statistics:
+                self.step_statistics[k] = np.nan
+            return self._last_action
+        self._reset_step_statistics()
+        self.update(self._last_action, obs)
+        self._last_action = self.get_action()
+        self._step_num += 1
+        self.step_statistics["mem_usage"] = psutil.Process().memory_info().rss / 1024**2
+        self.stat_tracker.step()
+        return self._last_action
+
+    def reset(self):
+        """``intmcp.py:158-177``."""
+        self.stat_tracker.reset_episode()
+        self._step_num = 0
+        self._engine.reset()
+        self.root = RootView()
+        self._min_value, self._max_value = self._initial_bounds()
+        self._reset_step_statistics()
+        self._last_action = None
+        for pi in self.other_agent_policies.values():
+            pi.reset()
+
+    def _initial_bounds(self):
+        kb = self.config.known_bounds
+        return (kb[0], kb[1]) if kb else (float("inf"), -float("inf"))
+
+    def _reset_step_statistics(self):
+        self.step_statistics = {
+            "search_time": 0.0, "update_time": 0.0, "reinvigoration_time": 0.0,
+            "evaluation_time": 0.0, "policy_calls": 0, "inference_time": 0.0,
+            "search_depth": 0, "num_sims": 0, "mem_usage": 0,
+            "min_value": self._min_value, "max_value": self._max_value,
+        }
+
+    # -------------------------------------------------------------- update
+    def update(self, action, obs):
+        """``intmcp.py:198-214``: ``_initial_nested_update`` at t == 0, else
+        ``_nested_update`` of both levels."""
+        if self.root.is_absorbing:
+            return
+        start = time.time()
+        a = -1 if self.root.t == 0 else int(action)
+        key = self.model.obs_key(obs)
+        absorbing = self._engine.update([a], [key])
+        self.root = dataclasses.replace(self.root, t=self.root.t + 1,
+                                        is_absorbing=bool(absorbing[0]))
+        self.step_statistics["update_time"] = time.time() - start
+
+    # -------------------------------------------------------------- search
+    def get_action(self):
+        """``intmcp.py:368-408``."""
+        if self.root.is_absorbing:
+            return self.action_spaces[self.agent_id][0]
+        start = time.time()
+        if self._num_sims is not None:
+            self._engine.search(self._num_sims, fetch=False)
+        else:
+            per_level = self.config.search_time_limit / (self.nesting_level + 1)
+            flags = N.INTMCP_BEGIN
+            for level in range(self.nesting_level + 1):
+                t0, chunk = time.time(), 16
+                while time.time() - t0 < per_level:
+                    sims = (chunk, 0) if level == 0 else (0, chunk)
+                    self._engine.search_levels(sims[0], sims[1], flags)
+                    flags = 0
+                    self._engine.root_stats()          # synchronises
+                    chunk = min(chunk * 2, 4096)
+            self._engine.search_levels(0, 0, flags | N.INTMCP_FINAL)
+        st = self._engine.root_stats()[0]
+        search_time = time.time() - start
+        self._min_value, self._max_value = st.min_value, st.max_value
+        kids = tuple((int(st.child_action[i]), int(st.child_visits[i]), st.child_values[i],
+                      st.child_totals[i]) for i in range(st.num_children))
+        self.root = dataclasses.replace(self.root, visits=st.root_visits,
+                                        belief_size=st.belief_size, children=kids)
+        self.step_statistics.update(
+            search_time=search_time, search_depth=st.search_depth, num_sims=int(st.num_sims),
+            min_value=st.min_value, max_value=st.max_value)
+        return int(st.action)
+
+    def root_belief(self):
+        """Level-1 root particles as (v0, v1, level-0 node id) rows."""
+        return self._engine.root_belief(0)
+
+    def close(self):
+        for p in self.search_policies.values():
+            p.close()
+        self._engine.close()
+
+    def __str__(self):
+        return "INTMCP"
+
+
+class BatchedINTMCP:
+    """``num_pairs`` independent I-NTMCP planner pairs searched by one launch.
+
+    Pair ``b`` uses RNG key ``(seed, tree_key_base + b)``: bit-identical to a
+    single ``INTMCP`` (and to the oracle) with that key.
+    """
+
+    def __init__(self, model, agent_id, config: MCTSConfig, num_pairs: int, num_sims: int, *,
+                 searches: int = 1, capacities=None, stream=None, tree_key_base: int = 0,
+                 device: Optional[int] = None):
+        if capacities is None:
+            step_limit = config.step_limit or model.spec.max_episode_steps
+            capacities = plan_intmcp_capacities(config, step_limit, num_sims, searches,
+                                                model.action_spaces[agent_id].n)
+        self.num_pairs = num_pairs
+        self.num_sims = num_sims
+        self.engine = IntmcpEngine(model, agent_id, config, num_pairs=num_pairs,
+                                   capacities=capacities, stream=stream,
+                                   tree_key_base=tree_key_base, device=device)
+        self.engine.reset()
+
+    def init_synthetic(self, env_seed_base: int = 1000):
+        keys = self.engine.synthetic_obs(env_seed_base)
+        self.engine.update(np.full(self.num_pairs, -1, dtype=np.int32), keys)
+        return keys
+
+    def search(self, fetch=True):
+        return self.engine.search(self.num_sims, fetch=fetch)
+
+    def close(self):
+        self.engine.close()

@@ -112,3 +112,69 @@ def batched_episodes(cfg_kwargs, num_sims, env_seeds, steps):
         last = actions.astype(np.int32)
     bp.close()
     return records
+
+
+def intmcp_state_record(eng, pair, searched, action):
+    """The oracle's I-NTMCP step record (oracle/run.py oracle_intmcp_record)
+    rebuilt from the device state of one planner pair."""
+    from oracle.intmcp_record import intmcp_record
+    from posggym_baselines_amd.planning.intmcp import node_order
+    rec = {"searched": searched, "action": int(action)}
+    if not searched:
+        return rec
+    st = eng.root_stats()[pair]
+    A = eng.A
+    n1 = eng.nodes(pair, 1)
+    s1 = eng.stats(pair, 1)
+    ent, sparts = eng.support(pair)
+    rows = eng.root_belief(pair)
+
+    def history(n):
+        out = []
+        while n != 0:
+            a = int(n1[n]["info"]) & 7
+            out.append((-1 if a == A else a, int(n1[n]["okey"])))
+            n = int(n1[n]["parent"])
+        return tuple(reversed(out))
+
+    # the root's t: every root particle's other-agent history has that length
+    t_root = int(n1[int(rows[0][2])]["t"]) if len(rows) else 0
+    parts = [(t_root, (int(r[0]), int(r[1])), history(int(r[2]))) for r in rows]
+    kids = [(int(st.child_action[i]), int(st.child_visits[i]), st.child_values[i],
+             st.child_totals[i]) for i in range(st.num_children)]
+    nested, seen = [], []
+    for r in rows:
+        m = int(r[2])
+        if m in seen:
+            continue
+        seen.append(m)
+        nd = n1[m]
+        nk = [(a, int(s1[int(nd["stats"]) + a]["visits"]), float(s1[int(nd["stats"]) + a]["value"]))
+              for a in node_order(int(nd["info"])) if a < A]
+        hit = [e for e in ent if int(e["node"]) == m]
+        npart = []
+        if hit:
+            e = hit[0]
+            npart = [(int(nd["t"]), (int(q[0]), int(q[1])))
+                     for q in sparts[int(e["off"]):int(e["off"]) + int(e["size"])]]
+        nested.append((history(m), (int(nd["visits"]), nk, npart)))
+    return intmcp_record(rec, int(st.num_sims), int(st.search_depth), int(st.root_visits), kids,
+                         st.min_value, st.max_value, parts, nested)
+
+
+def gpu_intmcp_episode(cfg_kwargs, num_sims, env_seed, ego="0", max_steps=50, env="Driving-v1"):
+    from posggym_baselines_amd.planning import INTMCP
+    model = product_model(env)
+    planner = INTMCP.initialize(model, ego, product_config(cfg_kwargs, num_sims), 1, None)
+    planner.reset()
+    records = []
+
+    def step(obs):
+        searched = not planner.root.is_absorbing
+        a = planner.step(obs)
+        records.append(intmcp_state_record(planner._engine, 0, searched, a))
+        return a
+
+    trace = run_episode(step, env_seed, ego=ego, max_steps=max_steps, env=env)
+    planner.close()
+    return trace, records

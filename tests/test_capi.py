@@ -10,7 +10,8 @@ import pytest
 from posggym_baselines_amd import _native as N
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("pomcp.h", "pomcp_debug.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("pomcp.h", "pomcp_debug.h",
+                                                                  "intmcp.h")]
 
 
 def declared_functions():
@@ -18,7 +19,7 @@ def declared_functions():
     for h in HEADERS:
         src = open(h).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-        names += re.findall(r"^\s*(?:int|void|int32_t|const char\s*\*)\s+(pomcp_\w+)\s*\(", src, re.M)
+        names += re.findall(r"^\s*(?:int|void|int32_t|const char\s*\*)\s+((?:pomcp|intmcp)_\w+)\s*\(", src, re.M)
     return names
 
 
@@ -28,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     assert len(names) >= 19
     for n in names:
         assert hasattr(lib, n), n
-    bound = {s[0] for s in N.SIGNATURES + N.DEBUG_SIGNATURES}
+    bound = {s[0] for s in N.SIGNATURES + N.DEBUG_SIGNATURES + N.INTMCP_SIGNATURES}
     assert set(names) == bound
     assert lib.pomcp_abi_version() == N.POMCP_ABI_VERSION
 
@@ -40,8 +41,10 @@ def test_struct_layout_matches_header(tmp_path):
         "pomcp_root_stats": [f[0] for f in N.PomcpRootStats._fields_],
         "pomcp_grid": [f[0] for f in N.PomcpGrid._fields_],
         "pomcp_pe_grid": [f[0] for f in N.PomcpPeGrid._fields_],
+        "intmcp_config": [f[0] for f in N.IntmcpConfig._fields_],
+        "intmcp_root_stats": [f[0] for f in N.IntmcpRootStats._fields_],
     }
-    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "pomcp.h"', "int main(void){"]
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "intmcp.h"', "int main(void){"]
     for st, fs in fields.items():
         lines.append(f'printf("{st} %zu\\n", sizeof({st}));')
         for f in fs:
@@ -54,7 +57,8 @@ def test_struct_layout_matches_header(tmp_path):
     out = dict(line.rsplit(" ", 1) for line in subprocess.run(
         [str(exe)], check=True, capture_output=True, text=True).stdout.split("\n") if line)
     for st, cls in (("pomcp_config", N.PomcpConfig), ("pomcp_root_stats", N.PomcpRootStats),
-                    ("pomcp_grid", N.PomcpGrid), ("pomcp_pe_grid", N.PomcpPeGrid)):
+                    ("pomcp_grid", N.PomcpGrid), ("pomcp_pe_grid", N.PomcpPeGrid),
+                    ("intmcp_config", N.IntmcpConfig), ("intmcp_root_stats", N.IntmcpRootStats)):
         assert int(out[st]) == ctypes.sizeof(cls), st
         for f in fields[st]:
             assert int(out[f"{st}.{f}"]) == getattr(cls, f).offset, f"{st}.{f}"
