@@ -65,6 +65,8 @@ int intmcp_reset(intmcp_ctx* ctx);
  * other-agent history in the new root belief). */
 int intmcp_update(intmcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_keys,
                   int32_t* root_absorbing_out);
+/* intmcp_update action of a pair to leave untouched (its episode has ended). */
+#define INTMCP_SKIP (-2)
 /* INTMCP.get_action (intmcp.py:368-408) with num_sims simulations per nesting level. */
 int intmcp_search(intmcp_ctx* ctx, int32_t num_sims_per_level, int32_t* actions_out);
 /* One chunk of get_action: level0_sims simulations at level 0 then

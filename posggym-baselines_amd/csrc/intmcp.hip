@@ -26,6 +26,7 @@ namespace pb {
 
 constexpr int kImPath = 128;          // tree levels per simulation
 constexpr uint32_t kImNoSupport = 0xFFFFFFFFu;
+constexpr int32_t kImSkip = -2;       // intmcp_update action: leave the pair untouched
 
 struct INode {          // 32 B
   int32_t parent;
@@ -667,6 +668,11 @@ __global__ __launch_bounds__(64) void k_im_update(ImParams p) {
   if (b >= p.B) return;
   ImPair<Env> P(p, sm, b);
   const uint64_t obs = p.in_obs[b];
+  if (p.in_actions[b] == kImSkip) {   // a pair whose episode has ended: untouched
+    p.out[2 * b] = im_absorbing(P.nd[0][P.h.cur].info) ? 1 : 0;
+    p.out[2 * b + 1] = P.h.err;
+    return;
+  }
   P.h.num_sims = 0;         // the step's counters (intmcp.py:114-136 resets them first)
   P.h.search_depth = 0;
   if (P.h.err == 0 && !im_absorbing(P.nd[0][P.h.cur].info)) {

@@ -218,6 +218,7 @@ class IntmcpRootStats(C.Structure):
 
 
 INTMCP_BEGIN, INTMCP_FINAL = 1, 2
+INTMCP_SKIP = -2
 
 # numpy views of the diagnostic records (include/intmcp.h)
 INTMCP_NODE_DTYPE = [("parent", "<i4"), ("info", "<u4"), ("visits", "<i4"), ("t", "<i4"),

@@ -178,3 +178,56 @@ def gpu_intmcp_episode(cfg_kwargs, num_sims, env_seed, ego="0", max_steps=50, en
     trace = run_episode(step, env_seed, ego=ego, max_steps=max_steps, env=env)
     planner.close()
     return trace, records
+
+
+def batched_intmcp_episodes(cfg_kwargs, num_sims, env_seeds, steps, env="Driving-v1", ego="0"):
+    """Lockstep I-NTMCP episodes of len(env_seeds) planner pairs in ONE engine
+    (pair b = tree key b, env seed env_seeds[b]), at most `steps` real steps;
+    a pair whose episode ended is skipped (INTMCP_SKIP).  Per-pair record lists
+    in the oracle format (oracle/run.py oracle_intmcp_episode)."""
+    import numpy as np
+    from oracle.envs import make_model
+    from oracle.episode import ENV_TREE_BASE
+    from oracle.rng import S_ENV_POLICY_BASE, Streams
+    from posggym_baselines_amd import _native as N
+    from posggym_baselines_amd.planning import BatchedINTMCP
+    model = product_model(env)
+    B = len(env_seeds)
+    bp = BatchedINTMCP(model, ego, product_config(cfg_kwargs, num_sims), B, num_sims,
+                       searches=steps)
+    envs = []
+    for s in env_seeds:
+        es = Streams(s, ENV_TREE_BASE)
+        e = make_model(env, es)
+        st = e.sample_initial_state()
+        envs.append([es, e, st, e.sample_initial_obs(st), False])
+    records = [[] for _ in range(B)]
+    last = np.full(B, -1, dtype=np.int32)
+    absorbing = np.zeros(B, dtype=bool)
+    for t in range(steps):
+        acts_in = last.copy()
+        keys = np.zeros(B, dtype=np.uint64)
+        searched = ~absorbing
+        for b in range(B):
+            if envs[b][4] or absorbing[b]:
+                acts_in[b] = N.INTMCP_SKIP
+            else:
+                keys[b] = envs[b][1].pack_obs(envs[b][3][ego])
+        absorbing = bp.engine.update(acts_in, keys)
+        actions = bp.search()
+        for b in range(B):
+            if envs[b][4]:
+                continue
+            a = int(actions[b]) if searched[b] else int(last[b])
+            records[b].append(intmcp_state_record(bp.engine, b, bool(searched[b]), a))
+            es, e, st, obs, _ = envs[b]
+            ja = {}
+            for i in e.possible_agents:
+                ja[i] = a if i == ego else es.randint(S_ENV_POLICY_BASE + int(i),
+                                                      e.action_spaces[i].n)
+            ts = e.step(st, ja)
+            envs[b][2], envs[b][3] = ts.state, ts.observations
+            envs[b][4] = bool(ts.all_done)
+            last[b] = a
+    bp.close()
+    return records

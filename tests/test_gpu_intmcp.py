@@ -22,3 +22,48 @@ def test_gpu_intmcp_matches_reference_goldens(case):
         for t, (got, exp) in enumerate(zip(records, ep["records"])):
             assert got == exp, f"{case} env_seed {ep['env_seed']} step {t}"
         assert trace == ep["trace"]
+
+
+TEST_CFG = dict(discount=0.95, search_time_limit=0.1, c=2 ** 0.5, truncated=False,
+                action_selection="ucb", pucb_exploration_fraction=0.25, known_bounds=None,
+                step_limit=None, epsilon=0.92, seed=3, state_belief_only=False)
+
+
+@pytest.mark.parametrize("env,ego,sel", [("Driving-v1", "0", "ucb"),
+                                         ("PursuitEvasion-v1", "1", "uniform")])
+def test_batched_pairs_match_oracle(env, ego, sel):
+    """150 planner pairs (3 launch blocks) in one engine, lockstep episodes:
+    pair b equals the oracle planner with tree key b."""
+    from gpu_util import batched_intmcp_episodes
+    from oracle.run import oracle_intmcp_episode
+    cfg = dict(TEST_CFG, action_selection=sel)
+    seeds = [500 + b for b in range(150)]
+    steps, sims = 4, 48
+    got = batched_intmcp_episodes(cfg, sims, seeds, steps, env=env, ego=ego)
+    for b in (0, 1, 63, 64, 100, 127, 128, 149):
+        _, exp = oracle_intmcp_episode(cfg, sims, seeds[b], ego=ego, tree=b, max_steps=steps,
+                                       env=env)
+        assert got[b] == exp, f"pair {b}"
+
+
+def test_batched_many_pairs_properties():
+    """4096 pairs, one step: every pair searched 2 x num_sims simulations, its
+    level-1 root visits equal num_sims, and the root's children visits sum to it."""
+    import numpy as np
+    from gpu_util import product_config, product_model
+    from posggym_baselines_amd.planning import BatchedINTMCP
+    model = product_model("Driving-v1")
+    B, S = 4096, 256
+    bp = BatchedINTMCP(model, "0", product_config(TEST_CFG, S), B, S)
+    bp.init_synthetic(1000)
+    actions = bp.search()
+    st = bp.engine.root_stats()
+    assert np.all((actions >= 0) & (actions < 5))
+    for s in st:
+        assert s.error == 0
+        if s.root_absorbing:
+            continue
+        assert s.num_sims == 2 * S
+        assert s.root_visits == S
+        assert sum(s.child_visits[i] for i in range(s.num_children)) == S
+    bp.close()
