@@ -53,6 +53,13 @@ def parse():
                          "(overflow is detected and fails the run)")
     ap.add_argument("--env", default="Driving-v1", choices=["Driving-v1", "PursuitEvasion-v1"],
                     help="Driving-v1 is BASELINE.json's metric; PursuitEvasion-v1 is config 3")
+    ap.add_argument("--planner", default="pomcp", choices=["pomcp", "intmcp"],
+                    help="pomcp: BASELINE.json's metric (C2/C3); intmcp: config 5, I-NTMCP "
+                         "nesting level 1, one planner pair per lane (--trees pairs, --sims "
+                         "simulations per nesting level)")
+    ap.add_argument("--arena", default=None,
+                    help="intmcp: per-tree NODES,STATS,LOG arena sizes (skips the calibration "
+                         "probe, e.g. for profiling runs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-sims", type=int, default=16384)
     ap.add_argument("--cpu-sample-trees", type=int, default=4)
@@ -87,8 +94,164 @@ def cpu_baseline(sims, trees, seed, env="Driving-v1"):
             "sample": f"{trees} roots x {sims} sims (get_action only), oracle/pomcp.py, 1 thread"}
 
 
+def b_other(A):
+    """I-NTMCP level-1 tree level: the other agent's softmax over its level-0
+    node (node 8 + A visits x 4) and the level-0 child lookup (16)."""
+    return 8 + 4 * A + 16
+
+
+B_STAT, B_NODE_HASH = 32, 48
+
+
+def cpu_baseline_intmcp(sims, pairs, seed, env="Driving-v1"):
+    """oracle/intmcp.py (pinned to the reference by tests/golden/intmcp_*) timed on
+    one host core: get_action of `sims` simulations per level on `pairs` roots."""
+    from oracle.episode import run_episode
+    from oracle.run import make_oracle_intmcp
+    cfg = dict(TEST_CFG, seed=seed, state_belief_only=False)
+    t_search = 0.0
+    for b in range(pairs):
+        p = make_oracle_intmcp(cfg, sims, tree=b, env=env)
+        p.reset()
+
+        def step(obs, p=p):
+            nonlocal t_search
+            top = p.top
+            top.update(None, obs)
+            t0 = time.perf_counter()
+            a = top.get_action(sims)
+            t_search += time.perf_counter() - t0
+            return a
+
+        run_episode(step, 1000 + b, max_steps=1, env=env)
+    return {"value": 2 * sims * pairs / t_search, "unit": "simulations/s", "cores": 1,
+            "kind": "port",
+            "sample": f"{pairs} roots x {sims} sims per level x 2 levels (get_action only), "
+                      "oracle/intmcp.py, 1 thread"}
+
+
+def main_intmcp(args):
+    import torch
+    torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        raise SystemExit("--planner intmcp is a single-GPU configuration (BASELINE config 5)")
+    from posggym_baselines_amd import build as nb
+    nb.build()
+    from posggym_baselines_amd.envs import DrivingModel, PursuitEvasionModel
+    from posggym_baselines_amd.planning import BatchedINTMCP, MCTSConfig
+    from posggym_baselines_amd.planning.intmcp import plan_intmcp_capacities
+    B, S = args.trees, args.sims
+    cfg = MCTSConfig(seed=args.seed, num_sims=S, **dict(TEST_CFG, state_belief_only=False))
+    model = PursuitEvasionModel() if args.env == "PursuitEvasion-v1" else DrivingModel()
+    A = model.action_spaces["0"].n
+    searches = args.warmup + args.steps + 1
+    caps = plan_intmcp_capacities(cfg, model.spec.max_episode_steps, S, searches, A)
+    if args.arena:
+        nodes, nstats, nlog = (int(x) for x in args.arena.split(","))
+        caps.max_nodes, caps.max_stats, caps.max_log = nodes, nstats, nlog
+        caps.hash_slots = 1 << max(4, (2 * nodes - 1).bit_length())
+    elif B > 1024:
+        # calibrated arenas: worst-case sizes are ~5x what a search uses; size the
+        # per-pair arenas from a 1024-pair probe of the same workload (an overflow
+        # would still be detected and fail the run, never be silent)
+        probe = BatchedINTMCP(model, "0", cfg, 1024, S, capacities=caps, device=dev)
+        probe.init_synthetic(1000 + B)
+        for _ in range(searches - 1):
+            probe.search(fetch=False)
+        ps = probe.engine.root_stats()
+        mx = lambda f: max(f(s) for s in ps)
+        nodes = int(1.5 * mx(lambda s: max(s.n_nodes[0], s.n_nodes[1]))) + 256
+        caps.max_nodes = min(caps.max_nodes, nodes)
+        caps.max_log = min(caps.max_log, int(1.5 * mx(lambda s: max(s.n_log[0], s.n_log[1])))
+                           + 256)
+        caps.max_stats = min(caps.max_stats,
+                             int(1.5 * mx(lambda s: max(s.n_stats[0], s.n_stats[1]))) + 64 * A)
+        caps.hash_slots = min(caps.hash_slots, 1 << max(4, (2 * nodes - 1).bit_length()))
+        probe.close()
+    stream = torch.cuda.Stream(device=dev)
+    bp = BatchedINTMCP(model, "0", cfg, B, S, capacities=caps, stream=stream.cuda_stream,
+                       device=dev)
+    bp.init_synthetic(1000)
+    for _ in range(args.warmup):
+        with torch.cuda.stream(stream):
+            bp.search(fetch=False)
+    torch.cuda.synchronize()
+    st0 = [(s.n_log[0], s.n_log[1], s.n_nodes[0] + s.n_nodes[1], s.n_stats[0] + s.n_stats[1])
+           for s in bp.engine.root_stats()]
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        with torch.cuda.stream(stream):
+            ev[k][0].record(stream)
+            bp.search(fetch=False)
+            ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    st = bp.engine.root_stats()
+    if any(s.error for s in st):
+        raise SystemExit("I-NTMCP search reported an error")
+    searched = sum(1 for s in st if not s.root_absorbing)
+    lv0 = lv1 = nodes = stats = 0
+    for s, s0 in zip(st, st0):
+        lv1 += s.n_log[0] - s0[0]
+        lv0 += s.n_log[1] - s0[1]
+        nodes += s.n_nodes[0] + s.n_nodes[1] - s0[2]
+        stats += s.n_stats[0] + s.n_stats[1] - s0[3]
+    sims_timed = 2 * S * searched * args.steps
+    alg_bytes = (B_SIM * sims_timed + b_level(A) * (lv0 + lv1) + b_other(A) * lv1
+                 + B_STAT * stats + B_NODE_HASH * nodes) / args.steps
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    traffic = None
+    prof = os.path.join(ROOT, "profiles", "pmc_intmcp.json")
+    if os.path.exists(prof):
+        try:
+            pm = json.load(open(prof))
+            if pm.get("trees") == B and pm.get("sims") == S and pm.get("env") == args.env:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    out = {
+        "metric": f"I-NTMCP simulations/sec on {args.env} (nesting level 1, exact search)",
+        "value": sims_timed / elapsed,
+        "unit": "simulations/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": f"synthetic {args.env} roots (env seed 1000+b), build's {args.env} restatement",
+        "config": {"workload": f"I-NTMCP nesting 1 {args.env}, {B} planner pairs x {S} sims per "
+                               "level x 2 levels per step (one batched launch), ucb c=sqrt2 "
+                               "gamma=0.95 depth_limit=2",
+                   "pairs": B, "sims_per_level": S, "pairs_searched": searched,
+                   "arena_per_pair": {"max_nodes": caps.max_nodes, "max_stats": caps.max_stats,
+                                      "max_log": caps.max_log, "hash_slots": caps.hash_slots,
+                                      "bytes": caps.bytes_per_pair(),
+                                      "nodes_used": max(max(s.n_nodes[0], s.n_nodes[1])
+                                                        for s in st)}},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "k_im_search", "kernel_ms": kernel_ms,
+                     "alg_bytes_per_launch": alg_bytes},
+    }
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_intmcp(2048, 16, args.seed, args.env)
+    print(json.dumps(out), flush=True)
+    bp.close()
+
+
 def main():
     args = parse()
+    if args.planner == "intmcp":
+        return main_intmcp(args)
     import torch
     import torch.distributed as dist
 

@@ -48,7 +48,7 @@ typedef struct intmcp_root_stats {
   double child_values[POMCP_MAX_ACTIONS];
   double child_totals[POMCP_MAX_ACTIONS];
   double min_value, max_value;    /* the level-1 planner's MinMaxStats */
-  int32_t n_nodes[2], n_log[2];
+  int32_t n_nodes[2], n_log[2], n_stats[2];
   int32_t n_support, pad;
 } intmcp_root_stats;
 

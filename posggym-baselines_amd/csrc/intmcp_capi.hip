@@ -327,6 +327,7 @@ int intmcp_get_root_stats(intmcp_ctx* ctx, intmcp_root_stats* out) {
     for (int k = 0; k < 2; ++k) {
       o.n_nodes[k] = h.n_nodes[k];
       o.n_log[k] = h.n_log[k];
+      o.n_stats[k] = h.n_stats[k];
     }
     o.n_support = h.n_sup;
   }

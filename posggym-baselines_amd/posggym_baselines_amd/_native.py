@@ -212,6 +212,7 @@ class IntmcpRootStats(C.Structure):
         ("max_value", C.c_double),
         ("n_nodes", C.c_int32 * 2),
         ("n_log", C.c_int32 * 2),
+        ("n_stats", C.c_int32 * 2),
         ("n_support", C.c_int32),
         ("pad", C.c_int32),
     ]

@@ -1,6 +1,7 @@
 #!/bin/bash
-# Profile the default bench command on the GPU box (run via gpurun).
+# Profile a bench command on the GPU box (run via gpurun).
 #   kernel trace + stats, then separate PMC passes for HBM bytes.
+# usage: tools/profile.sh TAG [bench args...]  -> gpurun_out/prof_TAG/
 set -e
 TAG=${1:-r1}
 shift || true
@@ -11,4 +12,19 @@ mkdir -p $OUT
 timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/bench_trace.log 2>&1
 timeout -k 10 500 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 bench.py --no-cpu-baseline $ARGS > $OUT/bench_fetch.log 2>&1
 timeout -k 10 500 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 bench.py --no-cpu-baseline $ARGS > $OUT/bench_write.log 2>&1
+# keep only what tools/summarize_profile.py reads (the merge-back limit is 64 MiB)
+du -ab $OUT | sort -n | tail -8
+find $OUT -type f ! -name '*kernel_stats.csv' ! -name '*counter_collection.csv' ! -name '*.log' -delete
+for f in $(find $OUT -name '*counter_collection.csv'); do
+  python3 - "$f" <<'PY'
+import csv, sys
+p = sys.argv[1]
+rows = [r for r in csv.DictReader(open(p)) if "k_" in r.get("Kernel_Name", "")]
+if rows:
+    w = csv.DictWriter(open(p, "w"), fieldnames=list(rows[0].keys()))
+    w.writeheader()
+    w.writerows(rows)
+PY
+done
+du -sh $OUT
 echo profile-done

@@ -39,6 +39,10 @@ def bench_line(log):
 def main():
     tag = sys.argv[1]
     current = "--current" in sys.argv
+    kernel = "k_search"
+    pmc_out = "pmc_search.json"
+    if "--intmcp" in sys.argv:
+        kernel, pmc_out = "k_im_search", "pmc_intmcp.json"
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
@@ -47,12 +51,14 @@ def main():
     stats = {}
     with open(os.path.join(src, "trace", "run_kernel_stats.csv")) as f:
         for row in csv.DictReader(f):
-            if "k_search" in row["Name"]:
+            if kernel in row["Name"]:
                 stats = {"name": row["Name"], "calls": int(row["Calls"]),
                          "avg_ms": float(row["AverageNs"]) / 1e6,
                          "min_ms": float(row["MinNs"]) / 1e6, "max_ms": float(row["MaxNs"]) / 1e6}
-    fetch = read_counter(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
-    write = read_counter(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    fetch = read_counter(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE",
+                         kernel)
+    write = read_counter(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE",
+                         kernel)
     # skip the warmup launch: every timed launch re-searches the same restored roots
     f_avg = sum(fetch[1:]) / max(1, len(fetch) - 1) if len(fetch) > 1 else fetch[0]
     w_avg = sum(write[1:]) / max(1, len(write) - 1) if len(write) > 1 else write[0]
@@ -60,7 +66,7 @@ def main():
     b = bench_line(os.path.join(src, "bench_trace.log"))
     cfg = b["config"]
     summary = {
-        "tag": tag, "bench": b, "k_search": stats,
+        "tag": tag, "bench": b, kernel: stats,
         "pmc": {"FETCH_SIZE_KiB_per_launch": f_avg, "WRITE_SIZE_KiB_per_launch": w_avg,
                 "hbm_bytes_per_launch": hbm,
                 "hbm_GBps": hbm / (stats["avg_ms"] * 1e-3) / 1e9,
@@ -70,8 +76,11 @@ def main():
     with open(os.path.join(out, f"{tag}_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     if current:
-        with open(os.path.join(out, "pmc_search.json"), "w") as f:
-            json.dump({"tag": tag, "trees": cfg["trees_per_gpu"], "sims": cfg["sims_per_tree"],
+        with open(os.path.join(out, pmc_out), "w") as f:
+            trees = cfg.get("trees_per_gpu", cfg.get("pairs"))
+            sims = cfg.get("sims_per_tree", cfg.get("sims_per_level"))
+            json.dump({"tag": tag, "trees": trees, "sims": sims,
+                       "env": b["metric"].split(" on ")[1].split(" ")[0],
                        "hbm_bytes_per_launch": hbm,
                        "source": f"profiles/{tag}_summary.json"}, f, indent=1)
     print(json.dumps(summary["pmc"], indent=1), stats)
