@@ -42,7 +42,17 @@ namespace pb {
 
 constexpr int kMaxA = 5;     // LDS root cache: A <= 5 (Driving-v1 5, PursuitEvasion-v1 4)
 constexpr int kTPB = 256;    // lanes per workgroup
-constexpr int kRootParts = kMaxA * (1 + kSlots);   // stats0[a], then slots[a][k]
+// Root cache layout: the root's stats0[a] (always) and, when kRootSlotsInLds,
+// its inline child slots[a][k].  Without the slots a tree needs 80 B of LDS,
+// which leaves room for more than one workgroup per CU.
+#ifndef POMCP_ROOT_SLOTS_LDS
+#define POMCP_ROOT_SLOTS_LDS 1
+#endif
+#ifndef POMCP_WAVES_PER_EU
+#define POMCP_WAVES_PER_EU 1
+#endif
+constexpr bool kRootSlotsInLds = POMCP_ROOT_SLOTS_LDS != 0;
+constexpr int kRootParts = kMaxA * (kRootSlotsInLds ? 1 + kSlots : 1);
 __host__ __device__ constexpr int rc_stats(int a) { return a; }
 __host__ __device__ constexpr int rc_slot(int a, int k) { return kMaxA + a * kSlots + k; }
 
@@ -75,7 +85,7 @@ struct PathEntry {
 enum : int { TP_LEVEL = 0, TP_ROLL = 1, TP_BACKUP = 2, TP_START = 3, TP_DONE = 4 };
 
 template <class Env, int SEL, int NA>
-__global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
+__global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES_PER_EU, POMCP_WAVES_PER_EU))) void k_search(DevParams p, int num_sims) {
   static_assert(NA >= 2 && NA <= kMaxA, "action count");
   __shared__ typename Env::Model sm;
   __shared__ uint4 rc[kRootParts][kTPB];   // the root block of every lane's tree
@@ -261,8 +271,10 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
     for (int a = 0; a < kMaxA; ++a) {
       if (a < A) {
         rc[rc_stats(a)][lid] = rb[a];
+        if (kRootSlotsInLds) {
 #pragma unroll
-        for (int q = 0; q < kSlots; ++q) rc[rc_slot(a, q)][lid] = rb[part_slot(a, q)];
+          for (int q = 0; q < kSlots; ++q) rc[rc_slot(a, q)][lid] = rb[part_slot(a, q)];
+        }
       }
     }
     pf = rbel[d_belief((uint32_t)bsize)];   // the first simulation's particle
@@ -405,7 +417,8 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
           for (int q = 1; q < kMaxA; ++q)
             if (q == a) sa = st[q];
 #pragma unroll
-          for (int q = 0; q < kSlots; ++q) sl[q] = rc[rc_slot(a, q)][lid];
+          for (int q = 0; q < kSlots; ++q)
+            sl[q] = kRootSlotsInLds ? rc[rc_slot(a, q)][lid] : rb[part_slot(a, q)];
           r0_s1 = rb[part_stats1(a)];   // no wait: consumed by the backup
           uint32_t n0, n1;
           double r;
@@ -429,9 +442,17 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
               ++n_nodes;
             }
             const uint64_t nk = okey | kValidBit | ((uint64_t)done << 63);
-            rc[rc_slot(a, ks)][lid] = make_uint4((uint32_t)nk, (uint32_t)(nk >> 32), (uint32_t)cblk, (uint32_t)cvis);
+            const uint4 nsl = make_uint4((uint32_t)nk, (uint32_t)(nk >> 32), (uint32_t)cblk, (uint32_t)cvis);
             cid = ani * kSlots + (uint32_t)ks + 1u;
-            leaf_rc = rc_slot(a, ks);
+            if (kRootSlotsInLds) {
+              rc[rc_slot(a, ks)][lid] = nsl;
+              leaf_rc = rc_slot(a, ks);
+            } else {
+              uint4* slot = const_cast<uint4*>(rb) + part_slot(a, ks);
+              *slot = nsl;
+              leaf_ptr = reinterpret_cast<int32_t*>(slot) + 2;
+              leaf_rc = -1;
+            }
           } else {
             ovf_child(ani, okey, done, &cid, &cblk, &cvis, &leaf_ptr);
             leaf_rc = -1;
@@ -638,8 +659,10 @@ __global__ __launch_bounds__(kTPB) void k_search(DevParams p, int num_sims) {
     for (int a = 0; a < kMaxA; ++a) {
       if (a < A) {
         const_cast<uint4*>(rb)[a] = rc[rc_stats(a)][lid];
+        if (kRootSlotsInLds) {
 #pragma unroll
-        for (int q = 0; q < kSlots; ++q) const_cast<uint4*>(rb)[part_slot(a, q)] = rc[rc_slot(a, q)][lid];
+          for (int q = 0; q < kSlots; ++q) const_cast<uint4*>(rb)[part_slot(a, q)] = rc[rc_slot(a, q)][lid];
+        }
       }
     }
   }
