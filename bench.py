@@ -46,7 +46,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--trees", type=int, default=65536)
-    ap.add_argument("--sims", type=int, default=65536)
+    ap.add_argument("--sims", type=int, default=None,
+                    help="simulations per search (default 65536; intmcp: 256 per nesting level)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--max-blocks", type=int, default=512,
                     help="per-tree action-block arena; a depth-2 Driving-v1 tree uses ~170 "
@@ -63,7 +64,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-sims", type=int, default=16384)
     ap.add_argument("--cpu-sample-trees", type=int, default=4)
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.sims is None:
+        args.sims = 256 if args.planner == "intmcp" else 65536
+    return args
 
 
 TEST_CFG = dict(discount=0.95, search_time_limit=0.1, c=math.sqrt(2), truncated=False,

@@ -57,6 +57,7 @@ typedef struct intmcp_ctx intmcp_ctx;
 /* INTMCP.initialize (intmcp.py:949-994) for every pair. */
 int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, intmcp_ctx** out);
 void intmcp_destroy(intmcp_ctx* ctx);
+/* ctx == NULL: the reason the calling thread's last intmcp_create failed. */
 const char* intmcp_last_error(const intmcp_ctx* ctx);
 /* INTMCP.reset (intmcp.py:154-176). */
 int intmcp_reset(intmcp_ctx* ctx);

@@ -59,7 +59,9 @@ static int im_copy(intmcp_ctx* ctx, T* dst, const T* src, size_t n) {
 
 extern "C" {
 
-const char* intmcp_last_error(const intmcp_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+// ctx == NULL: why the last intmcp_create of this thread failed
+static thread_local std::string g_create_err;
+const char* intmcp_last_error(const intmcp_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_err.c_str(); }
 
 void intmcp_destroy(intmcp_ctx* ctx) {
   if (!ctx) return;
@@ -76,8 +78,9 @@ int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, in
   const pomcp_config& c = cfg->base;
   auto* ctx = new intmcp_ctx();
   ctx->cfg = *cfg;
+  g_create_err.clear();
   auto bad = [&](int code, const char* m) {
-    ctx->err = m;
+    g_create_err = m;
     int rc = code;
     delete ctx;
     return rc;
@@ -156,6 +159,7 @@ int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, in
 #define IM_ALLOC(field, type, count)                                            \
   do {                                                                          \
     if ((rc = im_alloc(ctx, &p, sizeof(type) * (size_t)(count))) != POMCP_OK) {\
+      g_create_err = ctx->err;                                                  \
       intmcp_destroy(ctx);                                                      \
       return rc;                                                                \
     }                                                                           \
@@ -197,7 +201,7 @@ int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, in
       hipMemcpyAsync(d.hdr, h.data(), sizeof(IHdr) * (size_t)B, hipMemcpyHostToDevice, s) !=
           hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess) {
-    ctx->err = "initial upload failed";
+    g_create_err = "initial upload failed";
     intmcp_destroy(ctx);
     return POMCP_E_HIP;
   }
@@ -205,6 +209,7 @@ int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, in
   ctx->host_hdr.resize((size_t)B);
   rc = intmcp_reset(ctx);
   if (rc != POMCP_OK) {
+    g_create_err = "reset: " + ctx->err;
     intmcp_destroy(ctx);
     return rc;
   }

@@ -232,7 +232,7 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
     d.field = reinterpret_cast<decltype(d.field)>(p);                           \
   } while (0)
   ALLOC(hdr, TreeHdr, B);
-  ALLOC(an, Line, B * d.Nb * blk_lines(d.A));
+  ALLOC(an, Line, arena_lines((int)B, d.Nb, d.A));   // interleaved by search wave
   ALLOC(ovf, OvfSlot, B * d.H);
   ALLOC(plog, LogRec, (int64_t)search_waves((int)B) * kWave * d.Np);
   ALLOC(wlog, uint32_t, search_waves((int)B));

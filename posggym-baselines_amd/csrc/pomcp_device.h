@@ -68,6 +68,24 @@ __host__ __device__ constexpr int blk_parts(int A) { return kLine * (A + 1); }
 __host__ __device__ constexpr int part_stats1(int a) { return kLine * (1 + a); }
 __host__ __device__ constexpr int part_slot(int a, int k) { return kLine * (1 + a) + 1 + k; }
 
+// The block arena is interleaved by search wave ([wave][block][lane] of
+// (A + 1)-line blocks): block b of tree t starts at line
+//   ((t / 64 * Nb + b) * 64 + t % 64) * (A + 1)
+// so the 64 trees of a k_search wave (one per lane) keep their blocks in one
+// contiguous region whose size follows the blocks in use, not Nb.  With a
+// per-tree layout a wave's accesses spread over 64 regions of Nb blocks each
+// and the address translation caches thrash (tools/ubench).
+// A block is still one contiguous (A + 1) x 128 B piece (coalesced loads of
+// the wave-per-tree kernels are unchanged); consecutive blocks of one tree
+// are blk_stride_lines(A) apart.
+__host__ __device__ inline int64_t tree_base_lines(int t, int64_t Nb, int A) {
+  return ((int64_t)(t / kWave) * Nb * kWave + (t % kWave)) * blk_lines(A);
+}
+__host__ __device__ constexpr int64_t blk_stride_lines(int A) { return (int64_t)kWave * blk_lines(A); }
+__host__ __device__ inline int64_t arena_lines(int B, int64_t Nb, int A) {
+  return (int64_t)((B + kWave - 1) / kWave) * kWave * Nb * blk_lines(A);
+}
+
 // Overflow children (> kSlots per action node): open-addressing map keyed by
 // (action node, obs).  32 B entries; valid when key's epoch matches.
 struct OvfSlot {

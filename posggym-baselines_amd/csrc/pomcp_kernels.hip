@@ -60,7 +60,7 @@ struct Tree {
 
   __device__ Tree(const DevParams& pp, const Model& mm, int t) : p(pp), m(mm), tree(t) {
     lane = lane_id();
-    an = p.an + (int64_t)t * p.Nb * blk_lines(p.A);
+    an = p.an + tree_base_lines(t, p.Nb, p.A);
     ovf = p.ovf + (int64_t)t * p.H;
     bel = p.belief + (int64_t)t * 2 * p.Nr;
     const TreeHdr h = p.hdr[t];
@@ -151,7 +151,7 @@ struct Tree {
 
   __device__ uint4 load_block(int blk) const {
     uint4 q = make_uint4(0, 0, 0, 0);
-    if (lane < blk_parts(p.A)) q = reinterpret_cast<const uint4*>(an + (int64_t)blk * blk_lines(p.A))[lane];
+    if (lane < blk_parts(p.A)) q = reinterpret_cast<const uint4*>(an + (int64_t)blk * blk_stride_lines(p.A))[lane];
     return q;
   }
 
@@ -163,7 +163,7 @@ struct Tree {
     }
     const int b = n_blocks++;
     if (lane < blk_parts(p.A))
-      reinterpret_cast<uint4*>(an + (int64_t)b * blk_lines(p.A))[lane] = make_uint4(0, 0, 0, 0);
+      reinterpret_cast<uint4*>(an + (int64_t)b * blk_stride_lines(p.A))[lane] = make_uint4(0, 0, 0, 0);
     ++c_expand;
     return b;
   }
@@ -257,7 +257,7 @@ struct Tree {
     const uint64_t skey = (uint64_t)q.x | ((uint64_t)q.y << 32);
     const bool valid = cl && (skey & kValidBit) != 0;
     const uint64_t m = __ballot(valid && (skey & kObsMask) == okey);
-    uint4* slots = reinterpret_cast<uint4*>(an + (int64_t)blk * blk_lines(p.A)) + lo;
+    uint4* slots = reinterpret_cast<uint4*>(an + (int64_t)blk * blk_stride_lines(p.A)) + lo;
     int L;
     bool is_new = false;
     if (m) {

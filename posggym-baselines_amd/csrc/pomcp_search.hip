@@ -58,9 +58,16 @@ __host__ __device__ constexpr int rc_slot(int a, int k) { return kMaxA + a * kSl
 
 constexpr int kRegPath = 3;  // levels 1..kRegPath held in registers (deeper ones in p.path)
 
-// One level (depth >= 1) of the running simulation's path: {stats0 byte
-// offset | done << 31, visits before, r}, {value before, total before},
-// {agg before, stats1 byte offset, -}.
+// One level (depth >= 1) of the running simulation's path: {block << 3 |
+// action | done << 31, visits before, r}, {value before, total before},
+// {agg before, child hint after, -}.
+//
+// Child hint: the otherwise unused word of an action's stats0 part holds
+// 1 + the block of the obs child that has the majority of the action's
+// visits (0: none).  Right after selecting an action the search issues a
+// load of that child's statistics line, so when the observation then picks
+// that child (the likeliest case) its statistics are already on their way to
+// L2 when descend() asks for them.  Search results do not depend on it.
 struct PathEntry {
   uint4 e0, e1, e2;
 };
@@ -97,8 +104,9 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVE
   const bool valid = tree < p.B;
   const int tt = valid ? tree : 0;
   constexpr int A = NA;   // == p.A (host dispatch)
-  char* const an = reinterpret_cast<char*>(p.an + (int64_t)tt * p.Nb * blk_lines(A));
-  const int blk_bytes = blk_lines(A) * 128;
+  // this tree's blocks: interleaved with the wave's other trees (pomcp_device.h)
+  char* const an = reinterpret_cast<char*>(p.an + tree_base_lines(tt, p.Nb, A));
+  const int64_t blk_bytes = blk_stride_lines(A) * 128;   // block b at an + b * blk_bytes
   // the wave's shared particle log (pomcp_device.h LogRec); wpos is the same in
   // every lane still in the loop (advanced by ballot at convergent points)
   LogRec* const wl = p.plog + (int64_t)wave * kWave * p.Np;
@@ -539,12 +547,12 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVE
           rec = LogRec{cid | ((uint32_t)lane << kIdBits), n0, n1};   // mcts.py:371
           app = true;
           ++n_log;
-          const uint32_t off = (uint32_t)(blk * blk_bytes + a * 16);
+          const uint32_t ba = ((uint32_t)blk << 3) | (uint32_t)a;   // blk < 2^26 / 30
           const PathEntry pe = {
-              make_uint4(off | ((uint32_t)done << 31), sa.x, (uint32_t)__double2loint(r),
+              make_uint4(ba | ((uint32_t)done << 31), sa.x, (uint32_t)__double2loint(r),
                          (uint32_t)__double2hiint(r)),
               make_uint4(sa.z, sa.w, s1a.x, s1a.y),
-              make_uint4(s1a.z, s1a.w, (uint32_t)(blk * blk_bytes + part_stats1(a) * 16), 0u)};
+              make_uint4(s1a.z, s1a.w, 0u, 0u)};
           if (plen < kRegPath) {
   #pragma unroll
             for (int l = 0; l < kRegPath; ++l)
@@ -604,10 +612,11 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVE
         const double delta = gr - value0;
         const double value = value0 + delta / (double)n;
         const double agg = hilo_d(e2.x, e2.y) + delta * (gr - value);
-        *reinterpret_cast<uint4*>(an + (e0.x & 0x7FFFFFFFu)) =
-            make_uint4((uint32_t)n, 0u, (uint32_t)__double2loint(value),
-                       (uint32_t)__double2hiint(value));
-        *reinterpret_cast<uint4*>(an + e2.z) = make_uint4(
+        const uint32_t ba = e0.x & 0x7FFFFFFFu;
+        uint4* const bp = reinterpret_cast<uint4*>(an + (int64_t)(ba >> 3) * blk_bytes);
+        bp[ba & 7u] = make_uint4((uint32_t)n, 0u, (uint32_t)__double2loint(value),
+                                 (uint32_t)__double2hiint(value));
+        bp[part_stats1((int)(ba & 7u))] = make_uint4(
             (uint32_t)__double2loint(total), (uint32_t)__double2hiint(total),
             (uint32_t)__double2loint(agg), (uint32_t)__double2hiint(agg));
         if (value > mm_max) mm_max = value;   // utils.py:29-32

@@ -171,7 +171,9 @@ class IntmcpEngine:
         ctx = C.c_void_p()
         rc = lib.intmcp_create(C.byref(ic), int(dev), stream, C.byref(ctx))
         if rc != N.POMCP_OK:
-            raise N.PomcpError(rc, "intmcp_create failed (no GPU, bad config or out of memory)")
+            why = (lib.intmcp_last_error(None) or b"").decode(errors="replace")
+            raise N.PomcpError(rc, "intmcp_create failed: "
+                               + (why or "no GPU, bad config or out of memory"))
         self._ctx = ctx
         self._lib = lib
         self._stats = (N.IntmcpRootStats * self.num_pairs)()
