@@ -83,8 +83,9 @@ class _FakeClock:
         return self.now
 
 
-def make_reference_pomcp(model, agent_id, cfg_kwargs, num_sims, streams):
-    """Build a reference ``POMCP`` wired to ``streams`` and a fixed sim count."""
+def make_reference_pomcp(model, agent_id, cfg_kwargs, num_sims, streams, planner_cls="POMCP"):
+    """Build a reference ``POMCP`` (or ``IPOMCP`` with random other agents,
+    ``ipomcp.py:11-38``) wired to ``streams`` and a fixed sim count."""
     P = import_reference()
     import posggym_baselines.planning.belief as B
     import posggym_baselines.planning.mcts as mcts_mod
@@ -107,7 +108,14 @@ def make_reference_pomcp(model, agent_id, cfg_kwargs, num_sims, streams):
     if kw.get("known_bounds") is not None:
         kw["known_bounds"] = KnownBounds(*kw["known_bounds"])
     config = P.MCTSConfig(**kw)
-    planner = P.POMCP(model, agent_id, config, search_policy=P.RandomSearchPolicy(model, agent_id))
+    if planner_cls == "IPOMCP":
+        others = {i: P.RandomOtherAgentPolicy(model, i)
+                  for i in model.possible_agents if i != agent_id}
+        planner = P.IPOMCP(model, agent_id, config, others,
+                           search_policy=P.RandomSearchPolicy(model, agent_id))
+    else:
+        planner = P.POMCP(model, agent_id, config,
+                          search_policy=P.RandomSearchPolicy(model, agent_id))
     inner = planner._simulate
     count = [0]
 
@@ -149,7 +157,7 @@ def reference_record(planner, searched, action):
 
 
 def reference_episode(cfg_kwargs, num_sims, env_seed, ego="0", grid=None,
-                      tree=0, max_steps=50, env="Driving-v1"):
+                      tree=0, max_steps=50, env="Driving-v1", planner_cls="POMCP"):
     """One full episode with the real reference POMCP. Returns (trace, records)."""
     from oracle.envs import make_model
     from oracle.episode import run_episode
@@ -157,7 +165,7 @@ def reference_episode(cfg_kwargs, num_sims, env_seed, ego="0", grid=None,
 
     streams = Streams(cfg_kwargs.get("seed") or 0, tree)
     model = make_model(env, streams, grid=grid)
-    planner = make_reference_pomcp(model, ego, cfg_kwargs, num_sims, streams)
+    planner = make_reference_pomcp(model, ego, cfg_kwargs, num_sims, streams, planner_cls)
     planner.reset()
     records = []
 

@@ -60,14 +60,7 @@ constexpr int kRegPath = 3;  // levels 1..kRegPath held in registers (deeper one
 
 // One level (depth >= 1) of the running simulation's path: {block << 3 |
 // action | done << 31, visits before, r}, {value before, total before},
-// {agg before, child hint after, -}.
-//
-// Child hint: the otherwise unused word of an action's stats0 part holds
-// 1 + the block of the obs child that has the majority of the action's
-// visits (0: none).  Right after selecting an action the search issues a
-// load of that child's statistics line, so when the observation then picks
-// that child (the likeliest case) its statistics are already on their way to
-// L2 when descend() asks for them.  Search results do not depend on it.
+// {agg before, -, -}.
 struct PathEntry {
   uint4 e0, e1, e2;
 };
@@ -131,7 +124,9 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVE
   const int bsize = h->belief_size, epoch = h->epoch, root_abs = h->root_abs;
   int err = h->error;
   double mm_min = h->mm_min, mm_max = h->mm_max;
-  const uint64_t seed = h->seed;
+  // every tree of a context has the same seed (pomcp_create / pomcp_rekey): as a
+  // wave-uniform value the Philox key word k0 and its schedule live in SGPRs
+  const uint64_t seed = uni64(h->seed);
   const uint32_t tkey = h->tree_key;
   uint32_t c_bel = h->ctr[0], c_sel = h->ctr[1], c_mod = h->ctr[2], c_a0 = h->ctr[3],
            c_a1 = h->ctr[4];

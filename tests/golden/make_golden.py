@@ -42,16 +42,30 @@ CASES = {
 }
 
 
-def run_case(name):
-    over, num_sims, pairs, ego, max_steps = CASES[name][:5]
-    env = CASES[name][5] if len(CASES[name]) > 5 else "Driving-v1"
+# IPOMCP (ipomcp.py:11-38) with random other-agent policies and histories in
+# the particles (state_belief_only=False): the reference must produce exactly
+# the POMCP oracle's records (the other agents' random policies are stateless)
+IPOMCP_CASES = {
+    "ipomcp_ucb": ({"state_belief_only": False}, 128, [(20, 20), (21, 21)], "0", 50),
+    "ipomcp_pucb_ego1": ({"state_belief_only": False, "action_selection": "pucb"}, 96,
+                         [(22, 22)], "1", 50),
+}
+
+
+def run_case(name, cases=CASES, planner_cls="POMCP"):
+    over, num_sims, pairs, ego, max_steps = cases[name][:5]
+    env = cases[name][5] if len(cases[name]) > 5 else "Driving-v1"
     out = {"case": name, "env": env, "num_sims": num_sims, "ego": ego, "episodes": []}
+    if planner_cls != "POMCP":
+        out["planner"] = planner_cls
     for seed, env_seed in pairs:
         cfg = dict(TEST_CFG)
         cfg.update(over)
         cfg["seed"] = seed
-        tr, rr = reference_episode(cfg, num_sims, env_seed, ego=ego, max_steps=max_steps, env=env)
-        to, ro = oracle_episode(cfg, num_sims, env_seed, ego=ego, max_steps=max_steps, env=env)
+        tr, rr = reference_episode(cfg, num_sims, env_seed, ego=ego, max_steps=max_steps, env=env,
+                                   planner_cls=planner_cls)
+        to, ro = oracle_episode(dict(cfg, state_belief_only=True), num_sims, env_seed, ego=ego,
+                                max_steps=max_steps, env=env)
         if tr != to or rr != ro:
             raise SystemExit(f"oracle disagrees with reference in case {name} seed {seed}")
         cfg_json = dict(cfg)
@@ -114,25 +128,33 @@ def config_kats():
     return rows
 
 
-def main():
+def main(only=None):
     if not reference_available():
         raise SystemExit("reference not available (container-only script)")
-    for name in CASES:
+    for name in CASES if only is None else ():
         data = run_case(name)
         with open(os.path.join(HERE, f"{name}.json"), "w") as f:
             json.dump(data, f, separators=(",", ":"))
         n = sum(len(e["records"]) for e in data["episodes"])
         print(f"{name}: {len(data['episodes'])} episodes, {n} records")
-    for name in INTMCP_CASES:
+    for name in IPOMCP_CASES:
+        data = run_case(name, IPOMCP_CASES, "IPOMCP")
+        with open(os.path.join(HERE, f"{name}.json"), "w") as f:
+            json.dump(data, f, separators=(",", ":"))
+        n = sum(len(e["records"]) for e in data["episodes"])
+        print(f"{name}: {len(data['episodes'])} episodes, {n} records")
+    for name in INTMCP_CASES if only is None else ():
         data = run_intmcp_case(name)
         with open(os.path.join(HERE, f"{name}.json"), "w") as f:
             json.dump(data, f, separators=(",", ":"))
         n = sum(len(e["records"]) for e in data["episodes"])
         print(f"{name}: {len(data['episodes'])} episodes, {n} records")
-    with open(os.path.join(HERE, "config_kats.json"), "w") as f:
-        json.dump(config_kats(), f, separators=(",", ":"))
-    print("config_kats written")
+    if only is None:
+        with open(os.path.join(HERE, "config_kats.json"), "w") as f:
+            json.dump(config_kats(), f, separators=(",", ":"))
+        print("config_kats written")
 
 
 if __name__ == "__main__":
-    main()
+    # --ipomcp: (re)generate only the IPOMCP fixtures
+    main(only="ipomcp" if "--ipomcp" in sys.argv else None)

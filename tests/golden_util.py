@@ -29,4 +29,8 @@ def cfg_kwargs(cfg):
     return kw
 
 
+# reference IPOMCP (ipomcp.py:11-38), random other agents, state_belief_only=False:
+# the same records as POMCP (tests/golden/make_golden.py IPOMCP_CASES)
+IPOMCP_CASES = ["ipomcp_ucb", "ipomcp_pucb_ego1"]
+
 INTMCP_CASES = ["intmcp_ucb", "intmcp_ego1", "intmcp_uniform", "intmcp_deep", "intmcp_pe"]

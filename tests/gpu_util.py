@@ -44,11 +44,17 @@ def stats_record(st, A, searched, action, rows):
     return rec
 
 
-def gpu_episode(cfg_kwargs, num_sims, env_seed, ego="0", max_steps=50, env="Driving-v1"):
-    from posggym_baselines_amd.planning import POMCP, RandomSearchPolicy
+def gpu_episode(cfg_kwargs, num_sims, env_seed, ego="0", max_steps=50, env="Driving-v1",
+                planner_cls="POMCP"):
+    from posggym_baselines_amd.planning import (IPOMCP, POMCP, RandomOtherAgentPolicy,
+                                                RandomSearchPolicy)
     model = product_model(env)
-    planner = POMCP(model, ego, product_config(cfg_kwargs, num_sims),
-                    RandomSearchPolicy(model, ego))
+    config = product_config(cfg_kwargs, num_sims)
+    if planner_cls == "IPOMCP":
+        others = {i: RandomOtherAgentPolicy(model, i) for i in model.possible_agents if i != ego}
+        planner = IPOMCP(model, ego, config, others, RandomSearchPolicy(model, ego))
+    else:
+        planner = POMCP(model, ego, config, RandomSearchPolicy(model, ego))
     planner.reset()
     records = []
     A = model.action_spaces[ego].n

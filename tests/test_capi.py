@@ -93,3 +93,26 @@ def test_engine_rejects_unsupported_search_policy():
     cfg = MCTSConfig(discount=0.95, search_time_limit=0.1, c=1.4, truncated=False, seed=0)
     with pytest.raises(NotImplementedError):
         POMCP(m, "0", cfg, Other(m, "0", "x"))
+
+
+def test_ipomcp_validates_other_agent_policies():
+    """IPOMCP / MCTS (ipomcp.py:11-38, mcts.py:22-91): every other agent needs a
+    policy; only RandomOtherAgentPolicy runs in-kernel (checked before any GPU use)."""
+    from posggym_baselines_amd.envs import DrivingModel
+    from posggym_baselines_amd.planning import (IPOMCP, MCTS, MCTSConfig, OtherAgentPolicy,
+                                                RandomSearchPolicy)
+
+    class Scripted(OtherAgentPolicy):
+        def sample_initial_state(self): return {}
+        def get_next_state(self, a, o, s): return {}
+        def sample_action(self, s): return 0
+        def get_pi(self, s): return {0: 1.0}
+
+    m = DrivingModel()
+    cfg = MCTSConfig(discount=0.95, search_time_limit=0.1, c=1.4, truncated=False, seed=0,
+                     state_belief_only=False, num_sims=16)
+    for cls in (IPOMCP, MCTS):
+        with pytest.raises(AssertionError):
+            cls(m, "0", cfg, {}, RandomSearchPolicy(m, "0"))
+        with pytest.raises(NotImplementedError):
+            cls(m, "0", cfg, {"1": Scripted(m, "1")}, RandomSearchPolicy(m, "0"))

@@ -5,7 +5,7 @@ import math
 import numpy as np
 import pytest
 
-from golden_util import EPISODE_CASES, case_env, case_max_steps, cfg_kwargs, load
+from golden_util import EPISODE_CASES, IPOMCP_CASES, case_env, case_max_steps, cfg_kwargs, load
 from gpu_util import gpu_episode, product_config, stats_record
 from oracle.episode import run_episode
 from oracle.run import make_oracle, oracle_record
@@ -46,6 +46,21 @@ def test_gpu_matches_reference_goldens(case):
         assert len(records) == len(ep["records"])
         for t, (got, exp) in enumerate(zip(records, ep["records"])):
             assert got == exp, f"{case} step {t}"
+        assert trace == ep["trace"]
+
+
+@pytest.mark.parametrize("case", IPOMCP_CASES)
+def test_gpu_ipomcp_matches_reference_goldens(case):
+    """The IPOMCP drop-in (random other agents) against the real reference
+    IPOMCP run with state_belief_only=False (ipomcp.py:11-38)."""
+    data = load(case)
+    for ep in data["episodes"]:
+        kw = cfg_kwargs(ep["config"])
+        assert kw["state_belief_only"] is False
+        trace, records = gpu_episode(kw, data["num_sims"], ep["env_seed"], ego=data["ego"],
+                                     max_steps=case_max_steps(case, data), env=case_env(data),
+                                     planner_cls="IPOMCP")
+        assert records == ep["records"]
         assert trace == ep["trace"]
 
 

@@ -1,7 +1,7 @@
 """Oracle pinning: the CPU restatement against the reference's golden vectors."""
 import pytest
 
-from golden_util import EPISODE_CASES, case_env, case_max_steps, cfg_kwargs, load
+from golden_util import EPISODE_CASES, IPOMCP_CASES, case_env, case_max_steps, cfg_kwargs, load
 from oracle.pomcp import OracleConfig
 from oracle.rng import Streams, StreamRandom, philox4x32_10
 from oracle.run import oracle_episode
@@ -56,11 +56,13 @@ def test_config_kats():
             row["num_particles"], row["extra_particles"], row["depth_limit"])
 
 
-@pytest.mark.parametrize("case", EPISODE_CASES)
+@pytest.mark.parametrize("case", EPISODE_CASES + IPOMCP_CASES)
 def test_oracle_matches_reference_goldens(case):
     data = load(case)
     for ep in data["episodes"]:
-        kw = cfg_kwargs(ep["config"])
+        # IPOMCP cases: the reference ran with histories in the particles; the
+        # POMCP restatement (state beliefs) must give the same records
+        kw = dict(cfg_kwargs(ep["config"]), state_belief_only=True)
         trace, records = oracle_episode(kw, data["num_sims"], ep["env_seed"], ego=data["ego"],
                                         max_steps=case_max_steps(case, data),
                                         env=case_env(data))
