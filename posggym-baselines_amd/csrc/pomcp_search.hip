@@ -140,12 +140,36 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVE
 
   // ---- RNG streams (philox.h): one stateless Philox block per draw
   auto d_belief = [&](uint32_t n) { return uniform_int(philox_word(seed, tkey, S_BELIEF, c_bel++), n); };
-  auto d_model = [&](uint32_t n) { return uniform_int(philox_word(seed, tkey, S_MODEL, c_mod++), n); };
   auto d_select = [&](uint32_t n) { return uniform_int(philox_word(seed, tkey, S_SELECT, c_sel++), n); };
   auto d_act = [&](int agent, uint32_t n) {
     return agent == 0 ? uniform_int(philox_word(seed, tkey, S_ACT_BASE, c_a0++), n)
                       : uniform_int(philox_word(seed, tkey, S_ACT_BASE + 1, c_a1++), n);
   };
+  // One-draw lookahead of the streams every tree step consumes (the other
+  // agent's action, the model's shuffle draw) and of the belief stream: the
+  // next word of each is computed right after the current one is consumed, at
+  // a point where the wave waits on memory anyway (after a level's loads are
+  // issued), so no Philox block is computed on the root level's critical
+  // path.  Each stream is still consumed in order, so results are unchanged;
+  // the stored counters exclude a computed-but-unconsumed word (pend_*).
+  uint32_t w_oth = 0u, w_mod = 0u, w_bel = 0u;
+  int pend_s = 0, pend_b = 0;   // a lookahead word is held (step streams / belief)
+  auto la_step = [&]() {
+    if (!pend_s) {
+      w_oth = p.other == 0 ? philox_word(seed, tkey, S_ACT_BASE, c_a0++)
+                           : philox_word(seed, tkey, S_ACT_BASE + 1, c_a1++);
+      if (Env::kStepDraws) w_mod = philox_word(seed, tkey, S_MODEL, c_mod++);
+      pend_s = 1;
+    }
+  };
+  auto la_bel = [&]() {
+    if (!pend_b) {
+      w_bel = philox_word(seed, tkey, S_BELIEF, c_bel++);
+      pend_b = 1;
+    }
+  };
+  auto take_oth = [&](uint32_t n) { pend_s = 0; return uniform_int(w_oth, n); };
+  auto take_mod = [&](uint32_t n) { return Env::kStepDraws ? uniform_int(w_mod, n) : 0u; };
   // ObsNode.add_child for every action (mcts.py:279-281, 318-321): zeroed block
   auto alloc_block = [&]() -> int {
     if (n_blocks >= p.Nb) {
@@ -281,6 +305,8 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVE
       }
     }
     pf = rbel[d_belief((uint32_t)bsize)];   // the first simulation's particle
+    la_bel();
+    la_step();
   }
 
   // Overflow children (beyond the kSlots inline ones) of action node ani.
@@ -397,7 +423,10 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVE
     if (phase == TP_START) {
       {
         const uint4 pr = pf;                                     // belief.py:55
-        if (sims + 1 < num_sims) pf = rbel[d_belief((uint32_t)bsize)];
+        if (sims + 1 < num_sims) {
+          pf = rbel[uniform_int(w_bel, (uint32_t)bsize)];
+          pend_b = 0;
+        }
         t = (int)pr.x;
         s0 = pr.y;
         s1 = pr.z;
@@ -408,8 +437,8 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVE
           ret = 0.0;
           phase = TP_BACKUP;
         } else {
-          const uint32_t ao = d_act(p.other, (uint32_t)A);
-          const uint32_t j = Env::kStepDraws ? d_model(2) : 0u;
+          const uint32_t j = take_mod(2);
+          const uint32_t ao = take_oth((uint32_t)A);
           uint4 st[kMaxA];
 #pragma unroll
           for (int q = 0; q < kMaxA; ++q) st[q] = q < A ? rc[rc_stats(q)][lid] : make_uint4(0, 0, 0, 0);
@@ -480,12 +509,18 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVE
       PT_MARK(0);
     }
     append();
+    // refill the lookahead words the root level consumed while the first level's
+    // statistics line (issued by descend) is in flight
+    if (phase != TP_DONE) {
+      la_step();
+      la_bel();
+    }
     // ------------------------------------------------- the levels below the root
     while (__ballot(phase == TP_LEVEL) != 0ull) {
       if (phase == TP_LEVEL) {
         const uint4* const ap = reinterpret_cast<const uint4*>(an + (int64_t)blk * blk_bytes);
-        const uint32_t ao = d_act(p.other, (uint32_t)A);
-        const uint32_t j = Env::kStepDraws ? d_model(2) : 0u;
+        const uint32_t j = take_mod(2);
+        const uint32_t ao = take_oth((uint32_t)A);
         PT_MARK(8);
         uint4 st[kMaxA];   // prefetched by descend()
   #pragma unroll
@@ -502,6 +537,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVE
         uint4 sl[kSlots];
   #pragma unroll
         for (int q = 0; q < kSlots; ++q) sl[q] = ap[part_slot(a, q)];
+        la_step();   // the next step's draws, while the child line is in flight
         PT_MARK(3);
         uint32_t n0, n1;
         double r;
@@ -569,8 +605,9 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVE
         phase = TP_BACKUP;
       } else {
         const uint32_t ae = d_act(p.ego, (uint32_t)A);       // search_policy.py:177
-        const uint32_t ao = d_act(p.other, (uint32_t)A);     // other_policy.py:151
-        const uint32_t j = Env::kStepDraws ? d_model(2) : 0u;
+        const uint32_t j = take_mod(2);
+        const uint32_t ao = take_oth((uint32_t)A);           // other_policy.py:151
+        la_step();
         uint32_t n0, n1;
         double r;
         int dn;
@@ -734,11 +771,11 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVE
   hw->root_visits = root_visits;
   hw->mm_min = mm_min;
   hw->mm_max = mm_max;
-  hw->ctr[0] = c_bel;
+  hw->ctr[0] = c_bel - (uint32_t)pend_b;   // draws consumed, not looked ahead
   hw->ctr[1] = c_sel;
-  hw->ctr[2] = c_mod;
-  hw->ctr[3] = c_a0;
-  hw->ctr[4] = c_a1;
+  hw->ctr[2] = c_mod - (Env::kStepDraws ? (uint32_t)pend_s : 0u);
+  hw->ctr[3] = c_a0 - (p.other == 0 ? (uint32_t)pend_s : 0u);
+  hw->ctr[4] = c_a1 - (p.other == 1 ? (uint32_t)pend_s : 0u);
   pomcp_root_stats* const so = p.stats + tree;
 #pragma unroll
   for (int a = 0; a < kMaxA; ++a) {
