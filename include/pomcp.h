@@ -198,6 +198,13 @@ int pomcp_pe_step(const pomcp_pe_grid* g, const uint32_t state[2], const int32_t
                   uint64_t obs_keys_out[2]);
 int pomcp_pe_obs(const pomcp_pe_grid* g, const uint32_t state[2], uint64_t obs_keys_out[2]);
 
+/* ---- Host RNG streams (csrc/philox.h) -----------------------------------
+ * out[k] = word (first + k) of Philox stream `stream` under key (seed, tree):
+ * the draws of the episode loop's non-planning agents (the reference's
+ * UniformOtherAgentFn / Random-v0 policies, baseline_exps/exp_utils.py:481). */
+int pomcp_philox_words(uint64_t seed, uint32_t tree, uint32_t stream, uint32_t first, int32_t n,
+                       uint32_t* out);
+
 #ifdef __cplusplus
 }
 #endif

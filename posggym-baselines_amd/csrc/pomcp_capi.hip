@@ -542,6 +542,15 @@ int pomcp_driving_obs(const pomcp_grid* g, const uint32_t state[2], uint64_t obs
   return POMCP_OK;
 }
 
+// ---------------------------------------------------------- host RNG streams
+
+int pomcp_philox_words(uint64_t seed, uint32_t tree, uint32_t stream, uint32_t first, int32_t n,
+                       uint32_t* out) {
+  if (n < 0 || (n > 0 && !out)) return POMCP_E_INVALID;
+  for (int32_t k = 0; k < n; ++k) out[k] = philox_word(seed, tree, stream, first + (uint32_t)k);
+  return POMCP_OK;
+}
+
 // ---------------------------------------------------------- host PursuitEvasion
 
 int pomcp_pe_sample_initial_state(const pomcp_pe_grid* g, uint64_t seed, uint32_t tree,

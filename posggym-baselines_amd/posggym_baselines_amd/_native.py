@@ -168,6 +168,8 @@ SIGNATURES = [
      [C.POINTER(PomcpPeGrid), C.c_uint64, C.c_uint32, _PU32, _PU32]),
     ("pomcp_pe_step", C.c_int, [C.POINTER(PomcpPeGrid), _PU32, _P32, _PU32, _PD, _P32, _PU64]),
     ("pomcp_pe_obs", C.c_int, [C.POINTER(PomcpPeGrid), _PU32, _PU64]),
+    ("pomcp_philox_words", C.c_int, [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int32,
+                                     _PU32]),
 ]
 DEBUG_SIGNATURES = [
     ("pomcp_debug_fp_selftest", C.c_int, [_PD, _PD, C.c_int32, _PD]),

@@ -116,3 +116,76 @@ def test_ipomcp_validates_other_agent_policies():
             cls(m, "0", cfg, {}, RandomSearchPolicy(m, "0"))
         with pytest.raises(NotImplementedError):
             cls(m, "0", cfg, {"1": Scripted(m, "1")}, RandomSearchPolicy(m, "0"))
+
+
+def test_episode_results_header_matches_reference(tmp_path):
+    """episode_results.csv columns of run_planning_exp (exp_utils.py:325-331)."""
+    from posggym_baselines_amd.planning.episodes import EPISODE_RESULT_HEADS, EpisodeResultsWriter
+    assert EPISODE_RESULT_HEADS == [
+        "num", "len", "return", "discounted_return", "time", "search_time", "update_time",
+        "reinvigoration_time", "evaluation_time", "policy_calls", "inference_time",
+        "search_depth", "num_sims", "mem_usage", "min_value", "max_value"]
+    w = EpisodeResultsWriter(str(tmp_path / "episode_results.csv"))
+    w({k: 1 for k in EPISODE_RESULT_HEADS})
+    lines = open(tmp_path / "episode_results.csv").read().splitlines()
+    assert lines[0].split(",") == EPISODE_RESULT_HEADS and len(lines) == 2
+
+
+def test_host_philox_words_match_the_oracle():
+    """pomcp_philox_words (the episode loop's random agents) == oracle/rng.py."""
+    import ctypes
+    from oracle.rng import Streams
+    out = (ctypes.c_uint32 * 8)()
+    assert N.load().pomcp_philox_words(7, 0x40000000, 41, 0, 8, out) == 0
+    s = Streams(7, 0x40000000)
+    assert list(out) == [s.u32(41) for _ in range(8)]
+
+
+def test_episode_loop_replays_golden_trajectories_on_cpu():
+    """run_planning_episodes with a planner that replays the reference planner's
+    recorded actions: the host environment (same driving.h / pursuit_evasion.h
+    through the C ABI) and the random other agents reproduce the golden
+    trajectories exactly (other agent's actions, rewards, length, return)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from golden_util import load
+    from oracle.episode import fhex
+    from posggym_baselines_amd.envs import DrivingModel, PursuitEvasionModel
+    from posggym_baselines_amd.planning.episodes import run_planning_episodes
+
+    class Replay:
+        class config:
+            discount = 0.95
+
+        def __init__(self, actions):
+            self.actions, self.t = actions, 0
+
+            class _T:
+                def get_episode(self_inner):
+                    return {}
+            self.stat_tracker = _T()
+
+        def reset(self):
+            self.t = 0
+
+        def step(self, obs):
+            a = self.actions[self.t]
+            self.t += 1
+            return a
+
+    for case, Model in (("c1_ucb", DrivingModel), ("c1_pucb", DrivingModel),
+                        ("pe_evader_ucb", PursuitEvasionModel)):
+        data = load(case)
+        ego = int(data["ego"])
+        for ep in data["episodes"]:
+            steps = ep["trace"]["steps"]
+            seen = []
+            rows = run_planning_episodes(
+                Replay([s["actions"][ego] for s in steps]), Model(), 1, data["ego"],
+                env_seeds=[ep["env_seed"]], until="all_done",
+                on_step=lambda t, o, acts, ts: seen.append(
+                    ([acts[i] for i in sorted(acts)], fhex(ts.rewards[data["ego"]]))))
+            assert [s[0] for s in seen] == [s["actions"] for s in steps], case
+            assert [s[1] for s in seen] == [s["reward"] for s in steps], case
+            assert rows[0]["len"] == ep["trace"]["len"]
+            assert fhex(rows[0]["return"]) == ep["trace"]["return"]
