@@ -40,6 +40,16 @@ def b_expand(A):
 HBM_PEAK_GBS = 8000.0
 
 
+def _device_info(dev):
+    """Name and compute-unit count of the GPU (the same code measures 3.75-4.73 G
+    sims/s across boxes of the pool, DESIGN.md §6: recorded to tell boxes apart)."""
+    import torch
+    p = torch.cuda.get_device_properties(dev)
+    return {"name": p.name, "gcn_arch": getattr(p, "gcnArchName", ""),
+            "compute_units": p.multi_processor_count,
+            "hbm_gib": round(p.total_memory / 2**30, 1)}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -365,6 +375,7 @@ def main():
                                f"all-reduce over {world} GPU(s)",
                    "trees_per_gpu": B, "sims_per_tree": S, "depth_limit": cfg.depth_limit,
                    "parallelism": f"root-parallel x{world}",
+                   "device": _device_info(dev),
                    "arena": {"max_blocks": caps.max_blocks,
                              "max_blocks_used": max(s.n_blocks for s in st),
                              "max_particles": caps.max_particles,
