@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-sims", type=int, default=16384)
     ap.add_argument("--cpu-sample-trees", type=int, default=4)
+    ap.add_argument("--cpu-procs", type=int, default=16,
+                    help="host processes for the CPU baseline (capped by os.cpu_count(); the "
+                         "GPU box's CPU share is 16)")
     args = ap.parse_args()
     if args.sims is None:
         args.sims = 256 if args.planner == "intmcp" else 65536
@@ -85,14 +88,14 @@ TEST_CFG = dict(discount=0.95, search_time_limit=0.1, c=math.sqrt(2), truncated=
                 step_limit=None, epsilon=0.92, state_belief_only=True)
 
 
-def cpu_baseline(sims, trees, seed, env="Driving-v1"):
+def cpu_baseline(sims, trees, seed, env="Driving-v1", first_tree=0):
     """The oracle (pure-Python restatement of the reference planner, pinned to it by
     tests/golden) timed on one host core over a bounded sample of the same workload."""
     from oracle.episode import run_episode
     from oracle.run import make_oracle
     cfg = dict(TEST_CFG, seed=seed)
     t_search = 0.0
-    for b in range(trees):
+    for b in range(first_tree, first_tree + trees):
         p = make_oracle(cfg, sims, tree=b, env=env)
 
         def step(obs, p=p):
@@ -106,6 +109,26 @@ def cpu_baseline(sims, trees, seed, env="Driving-v1"):
         run_episode(step, 1000 + b, max_steps=1, env=env)
     return {"value": sims * trees / t_search, "unit": "simulations/s", "cores": 1, "kind": "port",
             "sample": f"{trees} roots x {sims} sims (get_action only), oracle/pomcp.py, 1 thread"}
+
+
+def _cpu_worker(job):
+    sims, tree, seed, env = job
+    r = cpu_baseline(sims, 1, seed, env, first_tree=tree)
+    return sims, sims / r["value"]
+
+
+def cpu_baseline_parallel(sims, procs, seed, env="Driving-v1"):
+    """The oracle on `procs` host cores at once (one process per core, one root
+    each); rate = all simulations / the slowest process's
+    search time.  Forked before this process touches the GPU."""
+    import multiprocessing as mp
+    with mp.get_context("fork").Pool(procs) as pool:
+        res = pool.map(_cpu_worker, [(sims, b, seed, env) for b in range(procs)])
+    total = sum(r[0] for r in res)
+    return {"value": total / max(r[1] for r in res), "unit": "simulations/s", "cores": procs,
+            "kind": "port",
+            "sample": f"{procs} roots x {sims} sims (get_action only), oracle/pomcp.py, "
+                      f"{procs} processes x 1 thread"}
 
 
 def b_other(A):
@@ -272,6 +295,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # before any GPU call: the worker processes are forked from this one
+        procs = max(1, min(args.cpu_procs, os.cpu_count() or 1))
+        cpu = cpu_baseline_parallel(args.cpu_sample_sims, procs, args.seed, args.env)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
@@ -385,9 +413,8 @@ def main():
                      "kernel": "k_search", "kernel_ms": kernel_ms,
                      "alg_bytes_per_launch": alg_bytes},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_sample_sims, args.cpu_sample_trees, args.seed,
-                                           args.env)
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(out), flush=True)
     bp.close()
