@@ -150,6 +150,12 @@ int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_key
  * simulations each (the time-bounded loop of mcts.py:285 becomes a count).
  * actions_out (host, [num_trees]) may be NULL: results stay on device. */
 int pomcp_search(pomcp_ctx* ctx, int32_t num_sims, int32_t* actions_out);
+/* num_sims more simulations WITHOUT the final action choice (mcts.py:299-306):
+ * a get_action split over several launches -- the wall-clock loop of
+ * mcts.py:285 -- is pomcp_search_continue(n1), ..., (nk) then
+ * pomcp_search(ctx, 0, ...), and consumes exactly the draws of one
+ * pomcp_search(n1 + ... + nk).  Root stats' action is -1 after it. */
+int pomcp_search_continue(pomcp_ctx* ctx, int32_t num_sims);
 
 /* Copy every tree's pomcp_root_stats of the last search to host. */
 int pomcp_get_root_stats(pomcp_ctx* ctx, pomcp_root_stats* out);

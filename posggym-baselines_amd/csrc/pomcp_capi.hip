@@ -362,26 +362,34 @@ int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_key
   return first_tree_error(ctx, ctx->host_upd.data(), 2, 1, "update");
 }
 
-int pomcp_search(pomcp_ctx* ctx, int32_t num_sims, int32_t* actions_out) {
+static int launch_search(pomcp_ctx* ctx, int32_t num_sims, int final_sel) {
   if (!ctx || num_sims < 0) return POMCP_E_INVALID;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   const dim3 grid(search_blocks(ctx->dp.B)), block(kTPB);
   // kernel per (environment, selection rule); the action count is the model's
-  using KFn = void (*)(DevParams, int);
+  using KFn = void (*)(DevParams, int, int);
   static const KFn table[2][3] = {
       {k_search<EnvDriving, POMCP_SEL_PUCB, 5>, k_search<EnvDriving, POMCP_SEL_UCB, 5>,
        k_search<EnvDriving, POMCP_SEL_UNIFORM, 5>},
       {k_search<EnvPursuitEvasion, POMCP_SEL_PUCB, 4>, k_search<EnvPursuitEvasion, POMCP_SEL_UCB, 4>,
        k_search<EnvPursuitEvasion, POMCP_SEL_UNIFORM, 4>}};
   const int e = ctx->dp.env == POMCP_ENV_PURSUIT_EVASION ? 1 : 0;
-  hipLaunchKernelGGL(table[e][ctx->dp.sel], grid, block, 0, ctx->stream, ctx->dp, (int)num_sims);
+  hipLaunchKernelGGL(table[e][ctx->dp.sel], grid, block, 0, ctx->stream, ctx->dp, (int)num_sims,
+                     final_sel);
   HIP_TRY(ctx, hipGetLastError());
-  if (!actions_out) return POMCP_OK;
-  const int rc = pomcp_get_root_stats(ctx, ctx->host_stats.data());
+  return POMCP_OK;
+}
+
+int pomcp_search(pomcp_ctx* ctx, int32_t num_sims, int32_t* actions_out) {
+  int rc = launch_search(ctx, num_sims, 1);
+  if (rc != POMCP_OK || !actions_out) return rc;
+  rc = pomcp_get_root_stats(ctx, ctx->host_stats.data());
   if (rc != POMCP_OK) return rc;
   for (int t = 0; t < ctx->dp.B; ++t) actions_out[t] = ctx->host_stats[t].action;
   return POMCP_OK;
 }
+
+int pomcp_search_continue(pomcp_ctx* ctx, int32_t num_sims) { return launch_search(ctx, num_sims, 0); }
 
 int pomcp_get_root_stats(pomcp_ctx* ctx, pomcp_root_stats* out) {
   if (!ctx || !out) return POMCP_E_INVALID;

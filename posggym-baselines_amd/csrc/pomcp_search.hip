@@ -85,7 +85,7 @@ struct PathEntry {
 enum : int { TP_LEVEL = 0, TP_ROLL = 1, TP_BACKUP = 2, TP_START = 3, TP_DONE = 4 };
 
 template <class Env, int SEL, int NA>
-__global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES_PER_EU, POMCP_WAVES_PER_EU))) void k_search(DevParams p, int num_sims) {
+__global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES_PER_EU, POMCP_WAVES_PER_EU))) void k_search(DevParams p, int num_sims, int final_sel) {
   static_assert(NA >= 2 && NA <= kMaxA, "action count");
   __shared__ typename Env::Model sm;
   __shared__ uint4 rc[kRootParts][kTPB];   // the root block of every lane's tree
@@ -719,8 +719,11 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVE
       s1s[a] = reinterpret_cast<const uint4*>(an + (int64_t)root_blk * blk_bytes)[part_stats1(a)];
     }
   }
-  int action = 0;
-  if (have) {   // _final_action_selection (mcts.py:565-600)
+  // _final_action_selection (mcts.py:565-600) ends get_action; a search split
+  // over several launches (final_sel = 0 for all but the last) draws it once
+  int action = -1;
+  if (have && final_sel) {
+    action = 0;
     uint32_t ties = 0;
     int nt = 0;
     bool direct = false;
@@ -809,9 +812,9 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVE
 }
 
 #define PB_SEARCH_INST(E, NA)                                                 \
-  template __global__ void k_search<E, POMCP_SEL_PUCB, NA>(DevParams, int);  \
-  template __global__ void k_search<E, POMCP_SEL_UCB, NA>(DevParams, int);   \
-  template __global__ void k_search<E, POMCP_SEL_UNIFORM, NA>(DevParams, int);
+  template __global__ void k_search<E, POMCP_SEL_PUCB, NA>(DevParams, int, int);  \
+  template __global__ void k_search<E, POMCP_SEL_UCB, NA>(DevParams, int, int);   \
+  template __global__ void k_search<E, POMCP_SEL_UNIFORM, NA>(DevParams, int, int);
 PB_SEARCH_INST(EnvDriving, 5)
 PB_SEARCH_INST(EnvPursuitEvasion, 4)
 #undef PB_SEARCH_INST

@@ -152,6 +152,7 @@ SIGNATURES = [
     ("pomcp_reset", C.c_int, [_CTX]),
     ("pomcp_update", C.c_int, [_CTX, _P32, _PU64, _P32]),
     ("pomcp_search", C.c_int, [_CTX, C.c_int32, _P32]),
+    ("pomcp_search_continue", C.c_int, [_CTX, C.c_int32]),
     ("pomcp_get_root_stats", C.c_int, [_CTX, C.POINTER(PomcpRootStats)]),
     ("pomcp_get_root_belief", C.c_int, [_CTX, C.c_int32, _PU32, C.c_int32, _P32]),
     ("pomcp_rekey", C.c_int, [_CTX, C.c_uint64]),

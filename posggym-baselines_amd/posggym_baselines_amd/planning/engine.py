@@ -171,7 +171,12 @@ class PomcpEngine:
             absorbing.ctypes.data_as(C.POINTER(C.c_int32))), "update")
         return absorbing.astype(bool)
 
-    def search(self, num_sims, fetch=True):
+    def search(self, num_sims, fetch=True, final=True):
+        """``num_sims`` simulations per tree; ``final=False`` leaves out the final
+        action choice (more launches of the same get_action follow)."""
+        if not final:
+            self._check(self._lib.pomcp_search_continue(self._ctx, int(num_sims)), "search")
+            return None
         if not fetch:
             self._check(self._lib.pomcp_search(self._ctx, int(num_sims), None), "search")
             return None

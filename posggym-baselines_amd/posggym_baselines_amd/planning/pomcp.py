@@ -143,16 +143,20 @@ class POMCP:
         if self.root.is_absorbing:
             return self.action_space[0]
         start = time.time()
+        depth = 0
         if self._num_sims is not None:
             self._engine.search(self._num_sims, fetch=False)
             n_sims = self._num_sims
         else:
+            # the wall-clock loop (mcts.py:285) as launches of growing chunks; the
+            # final action choice is drawn once, after the last one
             n_sims, chunk = 0, 16
             while time.time() - start < self.config.search_time_limit:
-                self._engine.search(chunk, fetch=False)
-                self._engine.root_stats()          # synchronises
+                self._engine.search(chunk, final=False)
+                depth = max(depth, self._engine.root_stats()[0].search_depth)   # synchronises
                 n_sims += chunk
                 chunk = min(chunk * 2, 4096)
+            self._engine.search(0, fetch=False)
         st = self._engine.root_stats()[0]
         search_time = time.time() - start
         A = len(self.action_space)
@@ -162,11 +166,8 @@ class POMCP:
             child_visits=tuple(st.child_visits[:A]), child_values=tuple(st.child_values[:A]),
             child_totals=tuple(st.child_totals[:A]))
         self.step_statistics.update(
-            search_time=search_time, search_depth=st.search_depth, num_sims=n_sims,
+            search_time=search_time, search_depth=max(depth, st.search_depth), num_sims=n_sims,
             min_value=st.min_value, max_value=st.max_value)
-        if self._num_sims is None:
-            # the time-bounded loop ran several launches; the last one chose the action
-            pass
         return int(st.action)
 
     def root_belief(self):
