@@ -258,19 +258,29 @@ struct ImPair {
   // the agent of tree k: k = 0 the ego, k = 1 the other agent
   __device__ int agent(int k) const { return k == 0 ? p.ego : p.other; }
 
-  __device__ int select(int k, int n) {          // intmcp.py:670-701
-    const INode x = nd[k][n];
+  // {visits, -, value} of the registered children of node x, all loads issued
+  // before any is used (one memory round trip instead of one per child)
+  __device__ void child_stats(int k, const INode& x, int nr, uint4 (&q)[6]) const {
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+      q[i] = i < nr ? *reinterpret_cast<const uint4*>(&st[k][x.stats + im_order(x.info, i)])
+                    : make_uint4(0, 0, 0, 0);
+  }
+
+  __device__ int select(int k, const INode& x) {   // intmcp.py:670-701
     if (x.visits == 0) return (int)d_sel((uint32_t)p.A);
     const int nr = im_nreg(x.info);
+    uint4 q[6];
+    child_stats(k, x, nr, q);
     if (p.sel == POMCP_SEL_UCB) {
       const double log_n = logn(x.visits);
       double best = -__builtin_inf();
       int ba = 0;
       for (int i = 0; i < nr; ++i) {
         const int a = im_order(x.info, i);
-        const IStat s = st[k][x.stats + a];
-        if (s.visits == 0) return a;
-        const double v = normalize(k, s.value) + p.c * sqrt(log_n / (double)s.visits);
+        const int sv = (int)q[i].x;
+        if (sv == 0) return a;
+        const double v = normalize(k, hilo_d(q[i].z, q[i].w)) + p.c * sqrt(log_n / (double)sv);
         if (v > best) {
           best = v;
           ba = a;
@@ -281,7 +291,7 @@ struct ImPair {
     int min_n = x.visits + 1, nxt = 0;            // min_visit_action_selection
     for (int i = 0; i < nr; ++i) {
       const int a = im_order(x.info, i);
-      const int v = st[k][x.stats + a].visits;
+      const int v = (int)q[i].x;
       if (v < min_n) {
         min_n = v;
         nxt = a;
@@ -297,10 +307,12 @@ struct ImPair {
     const int nr = im_nreg(x.info);
     if (x.visits == 0 || nr == 0) return (int)d_act(p.other, (uint32_t)p.A);
     const double sq = sqrt((double)x.visits);
+    uint4 q[6];
+    child_stats(1, x, nr, q);
     double pr[6];
     double total = 0.0;
     for (int i = 0; i < nr; ++i) {
-      pr[i] = exp((double)st[1][x.stats + im_order(x.info, i)].visits / sq);
+      pr[i] = exp((double)(int)q[i].x / sq);
       total = i == 0 ? pr[i] : total + pr[i];
     }
     // random.choices(children, weights=p / sum): cum weights, x = random() * total
@@ -399,7 +411,7 @@ struct ImPair {
         leaf = rollout(k, s0, s1, x.t, depth);
         break;
       }
-      const int a = select(k, n);
+      const int a = select(k, x);
       const int ao = other_action(k, nested);
       uint32_t n0, n1, nn;
       double r;
@@ -415,7 +427,7 @@ struct ImPair {
         nd[k][c].visits = 1;
       }
       uint32_t info = nd[k][c].info;
-      if (im_path_ok(nd[k][n].info)) info |= 1u << 4;
+      if (im_path_ok(x.info)) info |= 1u << 4;   // x: node n, unchanged since loaded
       info = done ? (info | 8u) : (info & ~8u);
       nd[k][c].info = info;
       log_add(k, c, n0, n1, nn);
@@ -423,7 +435,7 @@ struct ImPair {
         fail(POMCP_E_ARENA);
         return depth;
       }
-      path[plen * 2] = make_int4(n, a, done, 0);
+      path[plen * 2] = make_int4(n, a, done, x.stats);   // the backup needs no node load
       path[plen * 2 + 1] = make_int4(__double2loint(r), __double2hiint(r), 0, 0);
       ++plen;
       (void)me;
@@ -439,7 +451,7 @@ struct ImPair {
       const int4 e = path[l * 2], f = path[l * 2 + 1];
       const double r = __hiloint2double(f.y, f.x);
       g = e.z ? r : r + p.discount * g;
-      IStat& s = st[k][nd[k][e.x].stats + e.y];
+      IStat& s = st[k][e.w + e.y];
       s.visits += 1;
       s.total += g;
       const double delta = g - s.value;
