@@ -16,7 +16,49 @@ struct intmcp_ctx {
   size_t model_bytes = 0;
   std::vector<int32_t> host_out;
   std::vector<IHdr> host_hdr;
+  intmcp_root_stats* dev_rstats = nullptr;   // device staging of intmcp_get_root_stats
 };
+
+// intmcp_root_stats of every pair's level-1 root (was a host loop with two
+// synchronous copies per pair: seconds at 65,536 pairs)
+__global__ __launch_bounds__(64) void k_im_root_stats(ImParams d, intmcp_root_stats* out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= d.B) return;
+  const IHdr h = d.hdr[t];
+  const INode node = d.nodes[(int64_t)t * 2 * d.Nn + h.cur];
+  intmcp_root_stats o;
+  memset(&o, 0, sizeof(o));
+  o.action = h.last_action;
+  o.num_sims = h.num_sims;
+  o.search_depth = h.search_depth;
+  o.root_visits = node.visits;
+  o.root_absorbing = im_absorbing(node.info) ? 1 : 0;
+  o.belief_size = h.root_size;
+  o.error = h.err;
+  const int nr = im_nreg(node.info);
+  o.num_children = nr;
+  if (node.stats >= 0) {
+    const IStat* sv = d.stats + (int64_t)t * 2 * d.Ns + node.stats;
+    for (int i = 0; i < nr && i < POMCP_MAX_ACTIONS; ++i) {
+      const int a = im_order(node.info, i);
+      o.child_action[i] = a;
+      if (a < d.A) {
+        o.child_visits[i] = sv[a].visits;
+        o.child_values[i] = sv[a].value;
+        o.child_totals[i] = sv[a].total;
+      }
+    }
+  }
+  o.min_value = h.mm_min[0];
+  o.max_value = h.mm_max[0];
+  for (int k = 0; k < 2; ++k) {
+    o.n_nodes[k] = h.n_nodes[k];
+    o.n_log[k] = h.n_log[k];
+    o.n_stats[k] = h.n_stats[k];
+  }
+  o.n_support = h.n_sup;
+  out[t] = o;
+}
 
 #define IM_TRY(ctx, expr)                                                           \
   do {                                                                              \
@@ -294,49 +336,18 @@ int intmcp_search(intmcp_ctx* ctx, int32_t num_sims, int32_t* actions_out) {
 int intmcp_get_root_stats(intmcp_ctx* ctx, intmcp_root_stats* out) {
   if (!ctx || !out) return POMCP_E_INVALID;
   IM_TRY(ctx, hipSetDevice(ctx->device));
-  int rc = im_fetch_hdr(ctx);
-  if (rc != POMCP_OK) return rc;
-  const ImParams& d = ctx->ip;
-  for (int t = 0; t < d.B; ++t) {
-    const IHdr& h = ctx->host_hdr[t];
-    intmcp_root_stats& o = out[t];
-    std::memset(&o, 0, sizeof(o));
-    INode node;
-    rc = im_copy(ctx, &node, d.nodes + (int64_t)t * 2 * d.Nn + h.cur, 1);
+  const int B = ctx->ip.B;
+  if (!ctx->dev_rstats) {
+    void* p = nullptr;
+    const int rc = im_alloc(ctx, &p, sizeof(intmcp_root_stats) * (size_t)B);
     if (rc != POMCP_OK) return rc;
-    o.action = h.last_action;
-    o.num_sims = h.num_sims;
-    o.search_depth = h.search_depth;
-    o.root_visits = node.visits;
-    o.root_absorbing = im_absorbing(node.info) ? 1 : 0;
-    o.belief_size = h.root_size;
-    o.error = h.err;
-    const int nr = im_nreg(node.info);
-    o.num_children = nr;
-    if (node.stats >= 0) {
-      std::vector<IStat> stv((size_t)d.A);
-      rc = im_copy(ctx, stv.data(), d.stats + (int64_t)t * 2 * d.Ns + node.stats, (size_t)d.A);
-      if (rc != POMCP_OK) return rc;
-      for (int i = 0; i < nr && i < POMCP_MAX_ACTIONS; ++i) {
-        const int a = im_order(node.info, i);
-        o.child_action[i] = a;
-        if (a < d.A) {
-          o.child_visits[i] = stv[a].visits;
-          o.child_values[i] = stv[a].value;
-          o.child_totals[i] = stv[a].total;
-        }
-      }
-    }
-    o.min_value = h.mm_min[0];
-    o.max_value = h.mm_max[0];
-    for (int k = 0; k < 2; ++k) {
-      o.n_nodes[k] = h.n_nodes[k];
-      o.n_log[k] = h.n_log[k];
-      o.n_stats[k] = h.n_stats[k];
-    }
-    o.n_support = h.n_sup;
+    ctx->dev_rstats = reinterpret_cast<intmcp_root_stats*>(p);
   }
-  return POMCP_OK;
+  // one lane per pair gathers its root's record, then a single copy
+  hipLaunchKernelGGL(k_im_root_stats, dim3(im_blocks(B)), dim3(64), 0, ctx->stream, ctx->ip,
+                     ctx->dev_rstats);
+  IM_TRY(ctx, hipGetLastError());
+  return im_copy(ctx, out, ctx->dev_rstats, (size_t)B);
 }
 
 int intmcp_get_root_belief(intmcp_ctx* ctx, int32_t pair, uint32_t* out, int32_t capacity,
