@@ -8,8 +8,11 @@ extern "C" {
 /* out[4*i + k] = {sqrt(a), a / b, a + 0.95 * b, (a - b) / (a + b)} computed on
  * device 0 in FP64 (checks the device FP64 path is correctly rounded). */
 int pomcp_debug_fp_selftest(const double* a, const double* b, int32_t n, double* out);
-/* out[i] = exp(x[i]) on device 0 (FP64). */
+/* out[i] = host_exp(x[i]) on device 0 (FP64): the I-NTMCP softmax's exp, a
+ * bit-exact restatement of the host libm's exp (csrc/host_exp.h). */
 int pomcp_debug_exp(const double* x, int32_t n, double* out);
+/* The same function evaluated on the host CPU (no GPU needed). */
+int pomcp_debug_host_exp(const double* x, int32_t n, double* out);
 /* k_search phase cycles per wave, [waves][16] (libpomcp_hip built with
  * -DPOMCP_PHASE_TIMING; POMCP_E_UNSUPPORTED otherwise).  The first call
  * enables collection (count = 0); later calls copy the last search's values

@@ -312,7 +312,7 @@ struct ImPair {
     double pr[6];
     double total = 0.0;
     for (int i = 0; i < nr; ++i) {
-      pr[i] = exp((double)(int)q[i].x / sq);
+      pr[i] = host_exp((double)(int)q[i].x / sq);   // == math.exp (host_exp.h)
       total = i == 0 ? pr[i] : total + pr[i];
     }
     // random.choices(children, weights=p / sum): cum weights, x = random() * total
@@ -858,7 +858,8 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
         P.h.num_sims += 1;
       }
     }
-    if (!(flags & kImFinal)) {
+    if (!(flags & kImFinal) || P.h.err != 0) {   // no action from a failed search
+      if (P.h.err != 0 && (flags & kImFinal)) P.h.last_action = -1;
       P.store();
       return;
     }

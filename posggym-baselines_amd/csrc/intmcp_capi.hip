@@ -347,7 +347,17 @@ int intmcp_get_root_stats(intmcp_ctx* ctx, intmcp_root_stats* out) {
   hipLaunchKernelGGL(k_im_root_stats, dim3(im_blocks(B)), dim3(64), 0, ctx->stream, ctx->ip,
                      ctx->dev_rstats);
   IM_TRY(ctx, hipGetLastError());
-  return im_copy(ctx, out, ctx->dev_rstats, (size_t)B);
+  const int rc = im_copy(ctx, out, ctx->dev_rstats, (size_t)B);
+  if (rc != POMCP_OK) return rc;
+  // a failed search (arena, depleted root, ...) is reported here, as
+  // pomcp_get_root_stats does: its partial tree's action must not be used
+  for (int t = 0; t < B; ++t) {
+    if (out[t].error != 0) {
+      ctx->err = "search: pair " + std::to_string(t) + ": status " + std::to_string(out[t].error);
+      return out[t].error;
+    }
+  }
+  return POMCP_OK;
 }
 
 int intmcp_get_root_belief(intmcp_ctx* ctx, int32_t pair, uint32_t* out, int32_t capacity,

@@ -637,6 +637,14 @@ int pomcp_debug_exp(const double* x, int32_t n, double* out) {
   return e == hipSuccess ? POMCP_OK : POMCP_E_HIP;
 }
 
+// Debug: the same host_exp on the host CPU (tests/test_host_exp.py compares it
+// with math.exp without a GPU).
+int pomcp_debug_host_exp(const double* x, int32_t n, double* out) {
+  if (!x || !out || n < 0) return POMCP_E_INVALID;
+  for (int32_t i = 0; i < n; ++i) out[i] = host_exp(x[i]);
+  return POMCP_OK;
+}
+
 // Debug: per-wave phase cycles of k_search (diagnostics build only).
 int pomcp_debug_phase_timing(pomcp_ctx* ctx, uint64_t* out, int32_t capacity, int32_t* count) {
   if (!ctx || !count) return POMCP_E_INVALID;

@@ -14,6 +14,7 @@
 
 #include "pomcp_device.h"
 #include "envs.h"
+#include "host_exp.h"
 
 namespace pb {
 
@@ -544,12 +545,15 @@ __global__ __launch_bounds__(256) void k_synthetic_obs(DevParams p, uint64_t env
   if (lane_id() == 0) p.out_obs[tree] = key;
 }
 
-// Restore of the post-initial-update root state (see pomcp_snapshot).
+// Restore of the post-initial-update root state (see pomcp_snapshot).  The
+// live stream key (seed) is kept: a pomcp_rekey after the snapshot (root-
+// parallel ranks, bench.py) must survive every restore.
 __global__ __launch_bounds__(256) void k_restore(DevParams p, const TreeHdr* snap) {
   const int tree = blockIdx.x * kTreesPerBlock + (threadIdx.x >> 6);
   if (tree >= p.B) return;
   const int lane = lane_id();
-  int epoch = (p.hdr[tree].epoch + 1) & (int)kEpochMask;
+  const TreeHdr live = p.hdr[tree];
+  int epoch = (live.epoch + 1) & (int)kEpochMask;
   if (epoch == 0) {
     clear_ovf(p, tree, lane);
     epoch = 1;
@@ -558,13 +562,14 @@ __global__ __launch_bounds__(256) void k_restore(DevParams p, const TreeHdr* sna
   if (lane == 0) {
     TreeHdr h = snap[tree];
     h.epoch = epoch;
+    h.seed = live.seed;
     p.hdr[tree] = h;
   }
 }
 
 __global__ void k_exp_selftest(const double* x, int n, double* out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = exp(x[i]);
+  if (i < n) out[i] = host_exp(x[i]);   // the I-NTMCP softmax's exp (host_exp.h)
 }
 
 __global__ void k_fp_selftest(const double* a, const double* b, int n, double* out) {

@@ -175,6 +175,7 @@ SIGNATURES = [
 DEBUG_SIGNATURES = [
     ("pomcp_debug_fp_selftest", C.c_int, [_PD, _PD, C.c_int32, _PD]),
     ("pomcp_debug_exp", C.c_int, [_PD, C.c_int32, _PD]),
+    ("pomcp_debug_host_exp", C.c_int, [_PD, C.c_int32, _PD]),
     ("pomcp_debug_phase_timing", C.c_int,
      [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32, C.POINTER(C.c_int32)]),
 ]

@@ -114,6 +114,37 @@ def test_root_parallel_rekey():
     _batched_vs_oracle(TEST_CFG, 6, 200, range(6), rekey=seed ^ (3 << 32))
 
 
+def test_rekey_survives_restore():
+    """bench.py's root-parallel ranks: snapshot, rekey, then restore + search
+    every step.  The restore must keep the rank's key (it used to copy the
+    snapshot's seed back), so two keys give different statistics, each equal to
+    the oracle under its own key."""
+    from posggym_baselines_amd.planning import BatchedPOMCP
+    from gpu_util import product_model
+    model = product_model("Driving-v1")
+    S, B = 200, 4
+    key = lambda st: [(s.action, tuple(s.child_visits[:5]), tuple(s.child_values[:5])) for s in st]
+    runs = []
+    for r in (0, 1):
+        seed = TEST_CFG["seed"] ^ (r << 32)
+        bp = BatchedPOMCP(model, "0", product_config(TEST_CFG, S), B, S)
+        bp.init_synthetic(1000)
+        bp.engine.rekey(seed)
+        bp.restore()
+        bp.search()
+        first = key(bp.engine.root_stats())
+        bp.restore()
+        actions = bp.search()
+        stats = bp.engine.root_stats()
+        assert key(stats) == first
+        for b in range(B):
+            exp = _oracle_first_step(TEST_CFG, S, b, 1000 + b, rekey=seed)
+            assert stats_record(stats[b], 5, True, actions[b], bp.engine.root_belief(b)) == exp
+        runs.append(first)
+        bp.close()
+    assert runs[0] != runs[1]
+
+
 def test_full_size_65536_sims():
     """BASELINE config 2 size: 65,536 simulations from one root, bit-exact."""
     stats = _batched_vs_oracle(TEST_CFG, 2, 65536, [0])
