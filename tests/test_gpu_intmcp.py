@@ -67,3 +67,24 @@ def test_batched_many_pairs_properties():
         assert s.root_visits == S
         assert sum(s.child_visits[i] for i in range(s.num_children)) == S
     bp.close()
+
+
+def test_device_softmax_exp_equals_math_exp():
+    """The softmax exp of the other agent's action draw (intmcp.py:782-790) runs
+    on the device as host_exp (csrc/host_exp.h): it must equal this host's
+    math.exp bit for bit on every v / sqrt(N) the softmax can see (all of them
+    for N <= 4096, a sample up to N = 65,536) plus random and special
+    arguments, > 9 M in all.  math.exp is evaluated here, on the GPU box's host."""
+    import ctypes as C
+    import numpy as np
+    from posggym_baselines_amd import _native as N
+    from test_host_exp import _py_exp, _same, softmax_arguments, special_arguments
+    rng = np.random.default_rng(1)
+    x = np.concatenate([softmax_arguments(rng), special_arguments(rng)])
+    assert len(x) > 9_000_000
+    out = np.zeros_like(x)
+    P = C.POINTER(C.c_double)
+    assert N.load().pomcp_debug_exp(x.ctypes.data_as(P), len(x), out.ctypes.data_as(P)) == 0
+    ref = _py_exp(x)
+    bad = np.nonzero(~_same(out, ref))[0]
+    assert len(bad) == 0, [(x[i].hex(), out[i].hex(), ref[i].hex()) for i in bad[:5]]
