@@ -11,7 +11,15 @@ grows (weak scaling).  Inputs are resident in HBM before timing starts; each
 timed step restores the post-update root state (a few KB per tree) and
 re-searches it.
 
-    python bench.py [--gpus N --steps K --warmup W --trees B --sims S]
+Single-root modes (BASELINE config 2 as ONE planner): ``--trees 1`` is the
+exact planner (one tree, one lane); ``--trees K --root-parallel K --sims S/K``
+gives one planner K replica trees of S/K simulations each, merged on the
+device (``pomcp_merge_roots``), so ``ms_per_step`` is that planner's
+``get_action`` latency for S simulations.  ``--deep`` is SURVEY §8(d)'s
+rollout-dominated point (gamma 0.99, epsilon 0.01: depth_limit 459).
+
+    python bench.py [--gpus N --steps K --warmup W --trees B --sims S
+                     --root-parallel K --deep --env E --planner P]
 """
 import argparse
 import json
@@ -71,6 +79,11 @@ def parse():
     ap.add_argument("--arena", default=None,
                     help="intmcp: per-tree NODES,STATS,LOG arena sizes (skips the calibration "
                          "probe, e.g. for profiling runs)")
+    ap.add_argument("--root-parallel", type=int, default=1,
+                    help="replica trees per planner: consecutive groups of K trees are one "
+                         "planner, merged on the device each step (1 = independent planners)")
+    ap.add_argument("--deep", action="store_true",
+                    help="gamma=0.99, epsilon=0.01 (depth_limit 459, rollout-dominated)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-sims", type=int, default=16384)
     ap.add_argument("--cpu-sample-trees", type=int, default=4)
@@ -80,20 +93,23 @@ def parse():
     args = ap.parse_args()
     if args.sims is None:
         args.sims = 256 if args.planner == "intmcp" else 65536
+    if args.trees % args.root_parallel:
+        ap.error("--trees must be a multiple of --root-parallel")
     return args
 
 
 TEST_CFG = dict(discount=0.95, search_time_limit=0.1, c=math.sqrt(2), truncated=False,
                 action_selection="ucb", pucb_exploration_fraction=0.25, known_bounds=None,
                 step_limit=None, epsilon=0.92, state_belief_only=True)
+DEEP_CFG = dict(TEST_CFG, discount=0.99, epsilon=0.01)   # depth_limit 459
 
 
-def cpu_baseline(sims, trees, seed, env="Driving-v1", first_tree=0):
+def cpu_baseline(sims, trees, seed, env="Driving-v1", first_tree=0, base=None):
     """The oracle (pure-Python restatement of the reference planner, pinned to it by
     tests/golden) timed on one host core over a bounded sample of the same workload."""
     from oracle.episode import run_episode
     from oracle.run import make_oracle
-    cfg = dict(TEST_CFG, seed=seed)
+    cfg = dict(base or TEST_CFG, seed=seed)
     t_search = 0.0
     for b in range(first_tree, first_tree + trees):
         p = make_oracle(cfg, sims, tree=b, env=env)
@@ -112,18 +128,18 @@ def cpu_baseline(sims, trees, seed, env="Driving-v1", first_tree=0):
 
 
 def _cpu_worker(job):
-    sims, tree, seed, env = job
-    r = cpu_baseline(sims, 1, seed, env, first_tree=tree)
+    sims, tree, seed, env, base = job
+    r = cpu_baseline(sims, 1, seed, env, first_tree=tree, base=base)
     return sims, sims / r["value"]
 
 
-def cpu_baseline_parallel(sims, procs, seed, env="Driving-v1"):
+def cpu_baseline_parallel(sims, procs, seed, env="Driving-v1", base=None):
     """The oracle on `procs` host cores at once (one process per core, one root
     each); rate = all simulations / the slowest process's
     search time.  Forked before this process touches the GPU."""
     import multiprocessing as mp
     with mp.get_context("fork").Pool(procs) as pool:
-        res = pool.map(_cpu_worker, [(sims, b, seed, env) for b in range(procs)])
+        res = pool.map(_cpu_worker, [(sims, b, seed, env, base) for b in range(procs)])
     total = sum(r[0] for r in res)
     return {"value": total / max(r[1] for r in res), "unit": "simulations/s", "cores": procs,
             "kind": "port",
@@ -296,10 +312,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     cpu = None
+    base_cfg = DEEP_CFG if args.deep else TEST_CFG
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # before any GPU call: the worker processes are forked from this one
         procs = max(1, min(args.cpu_procs, os.cpu_count() or 1))
-        cpu = cpu_baseline_parallel(args.cpu_sample_sims, procs, args.seed, args.env)
+        sample = args.cpu_sample_sims if not args.deep else max(64, args.cpu_sample_sims // 8)
+        cpu = cpu_baseline_parallel(sample, procs, args.seed, args.env, base_cfg)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
@@ -316,10 +334,10 @@ def main():
     from posggym_baselines_amd.envs import DrivingModel, PursuitEvasionModel
     from posggym_baselines_amd.planning import BatchedPOMCP, MCTSConfig
     from posggym_baselines_amd.planning.engine import plan_capacities
-    from posggym_baselines_amd.planning.parallel import merge_buffer_tensor, root_parallel_merge
+    from posggym_baselines_amd.planning.parallel import merge_buffer_tensor
 
-    B, S = args.trees, args.sims
-    cfg = MCTSConfig(seed=args.seed, num_sims=S, **TEST_CFG)
+    B, S, K = args.trees, args.sims, args.root_parallel
+    cfg = MCTSConfig(seed=args.seed, num_sims=S, **base_cfg)
     model = PursuitEvasionModel() if args.env == "PursuitEvasion-v1" else DrivingModel()
     caps = plan_capacities(cfg, model.spec.max_episode_steps, S, 1, reroot=False,
                            max_blocks=min(args.max_blocks, S + 64),
@@ -340,7 +358,12 @@ def main():
             bp.search(fetch=False)
             if events is not None:
                 events[1].record(stream)
-            return root_parallel_merge(merge, A, world)
+            # the root-parallel decision: one all-reduce of (visits, total) per
+            # root action (RCCL, same stream), then the device merge of each
+            # planner's K replicas (pomcp_merge_roots) -- the same on every rank
+            if world > 1:
+                dist.all_reduce(merge)
+            bp.engine.merge_roots(K, fetch=False)
 
     for _ in range(args.warmup):
         step()
@@ -372,6 +395,9 @@ def main():
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     total_sims = world * B * S * args.steps
     value = total_sims / elapsed
+    merged = bp.engine.merge_roots(K)   # the last step's decisions (checks replica errors)
+    if not all(0 <= m.action < A for m in merged):
+        raise SystemExit("merged action out of range")
     traffic = None
     prof = os.path.join(ROOT, "profiles", "pmc_search.json")
     if os.path.exists(prof):
@@ -399,9 +425,15 @@ def main():
         "data": f"synthetic {args.env} belief states (env seed 1000+b), build's {args.env} "
                 "restatement",
         "config": {"workload": f"POMCP {env_desc} exact search, {B} roots x {S} "
-                               f"sims per GPU, ucb c=sqrt2 gamma=0.95 depth_limit=2, root-parallel "
-                               f"all-reduce over {world} GPU(s)",
+                               f"sims per GPU, ucb c=sqrt2 gamma={cfg.discount} "
+                               f"depth_limit={cfg.depth_limit}, "
+                               + (f"{B // K} planner(s) x {K} replica trees merged on the device, "
+                                  if K > 1 else "")
+                               + f"root-parallel all-reduce over {world} GPU(s)",
                    "trees_per_gpu": B, "sims_per_tree": S, "depth_limit": cfg.depth_limit,
+                   "root_parallel": K, "planners_per_gpu": B // K,
+                   "sims_per_planner_step": S * K,
+                   "rollout_steps_per_sim": sum(s.n_rollout_steps for s in st) / max(sims, 1),
                    "parallelism": f"root-parallel x{world}",
                    "device": _device_info(dev),
                    "arena": {"max_blocks": caps.max_blocks,

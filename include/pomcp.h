@@ -72,10 +72,10 @@ typedef struct pomcp_config {
   int32_t ego_agent;            /* index of agent_id in possible_agents */
   int32_t num_actions;          /* model.action_spaces[agent_id].n */
   int32_t action_selection;     /* pomcp_selection */
-  int32_t depth_limit;          /* config.py:464-469 */
+  int32_t depth_limit;          /* config.py:50-55 */
   int32_t step_limit;           /* mcts.py:53-58; INT32_MAX = unbounded */
-  int32_t num_particles;        /* config.py:461 */
-  int32_t extra_particles;      /* config.py:462 */
+  int32_t num_particles;        /* config.py:47 */
+  int32_t extra_particles;      /* config.py:48 */
   int32_t has_known_bounds;
   int32_t num_trees;            /* independent planners (batched roots) */
   double discount;
@@ -172,6 +172,31 @@ int pomcp_rekey(pomcp_ctx* ctx, uint64_t seed);
  * double[num_trees][num_actions][2] = (child visits, child total value),
  * the operand of the RCCL all-reduce at action-selection time. */
 int pomcp_root_merge_buffer(pomcp_ctx* ctx, void** device_ptr);
+
+/* Root-parallel decision of one planner. */
+typedef struct pomcp_merged_root {
+  int32_t action;               /* merged final action (see pomcp_merge_roots) */
+  int32_t num_trees;            /* replicas merged */
+  int32_t search_depth;         /* max over the replicas */
+  int32_t error;                /* first non-zero replica error, in tree order */
+  int64_t num_sims;             /* summed over the replicas */
+  int64_t root_visits;          /* summed */
+  double min_value, max_value;  /* min / max over the replicas' MinMaxStats */
+  double visits[POMCP_MAX_ACTIONS];   /* summed root child visits */
+  double totals[POMCP_MAX_ACTIONS];   /* summed root child total values */
+} pomcp_merged_root;
+
+/* Root-parallel merge on the device: trees [g*group, (g+1)*group) are the
+ * replicas of planner g (num_trees % group == 0); their entries of the merge
+ * buffer (as last written by pomcp_search, or after an all-reduce of it across
+ * GPUs) are summed in a fixed order and the merged action is
+ *   PUCB: argmax summed visits (the merged max_visit_action_selection,
+ *         mcts.py:565-581);  UCB / uniform: argmax summed total / summed visits
+ *         over visited actions (max_value_action_selection, mcts.py:583-600);
+ * lowest action on ties, 0 if nothing was visited.  Replaces the reference's
+ * single-tree _final_action_selection when one planner runs many trees.
+ * out (host, [num_trees / group]) may be NULL: the result stays on device. */
+int pomcp_merge_roots(pomcp_ctx* ctx, int32_t group, pomcp_merged_root* out);
 
 /* Bench / batch helpers: synthetic roots (the configured environment).  Tree b samples s0 from
  * the model's b0 under env key (env_seed_base + b, 0x40000000) and the ego's

@@ -43,7 +43,7 @@ class OracleConfig:
         self.seed = seed
         self.state_belief_only = state_belief_only
         self.num_sims = num_sims
-        # config.py:461-469
+        # config.py:47-55
         self.num_particles = math.ceil(100 * search_time_limit)
         self.extra_particles = math.ceil(self.num_particles * extra_particles_prop)
         if discount == 0.0:

@@ -1,7 +1,7 @@
 // C-ABI host side of libpomcp_hip.so (include/pomcp.h).
 //
 // Owns every device allocation of a planner batch, validates the
-// MCTSConfig-derived parameters (config.py:447-469 asserts) and launches the
+// MCTSConfig-derived parameters (config.py:33-55 asserts) and launches the
 // kernels of pomcp_kernels.hip on one HIP stream.
 #include <hip/hip_runtime.h>
 
@@ -41,6 +41,7 @@ struct pomcp_ctx {
   PeModel host_pe;
   const void* host_model = nullptr;
   size_t model_bytes = 0;
+  pomcp_merged_root* merged = nullptr;   // [B] device results of pomcp_merge_roots
 };
 
 static void make_model(const pomcp_grid* g, DrvModel* m) {
@@ -85,6 +86,11 @@ static int dev_alloc(pomcp_ctx* ctx, void** out, size_t bytes) {
 
 static unsigned grid_blocks(int B) { return (unsigned)((B + kTreesPerBlock - 1) / kTreesPerBlock); }
 static unsigned search_blocks(int B) { return (unsigned)((B + kTPB - 1) / kTPB); }
+// Workgroup size of a search launch: one-wave workgroups while the launch has
+// at most 3 waves per CU (3 such workgroups fit a CU's LDS: root cache 35 KB +
+// model tables each), so a small launch's waves spread over all 256 CUs; a
+// full launch uses 256-lane workgroups, one per CU.
+static int search_tpb(int B) { return (B + kWave - 1) / kWave <= 3 * 256 ? kTPBSmall : kTPB; }
 static int search_waves(int B) { return (B + kWave - 1) / kWave; }
 
 extern "C" {
@@ -250,6 +256,11 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
   ALLOC(in_obs, uint64_t, B);
   ALLOC(out_obs, uint64_t, B);
 #undef ALLOC
+  if ((rc = dev_alloc(ctx, &p, sizeof(pomcp_merged_root) * (size_t)B)) != POMCP_OK) {
+    pomcp_destroy(ctx);
+    return rc;
+  }
+  ctx->merged = reinterpret_cast<pomcp_merged_root*>(p);
   d.logtab_n = c.log_table_size;
   d.dpow_n = (int32_t)(c.discount_pow_size > INT32_MAX ? INT32_MAX : c.discount_pow_size);
   hipStream_t s = ctx->stream;
@@ -365,17 +376,20 @@ int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_key
 static int launch_search(pomcp_ctx* ctx, int32_t num_sims, int final_sel) {
   if (!ctx || num_sims < 0) return POMCP_E_INVALID;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
-  const dim3 grid(search_blocks(ctx->dp.B)), block(kTPB);
-  // kernel per (environment, selection rule); the action count is the model's
+  const int tpb = search_tpb(ctx->dp.B);
+  const dim3 grid((unsigned)((ctx->dp.B + tpb - 1) / tpb)), block((unsigned)tpb);
+  // kernel per (environment, selection rule, workgroup size); the action count is the model's
   using KFn = void (*)(DevParams, int, int);
-  static const KFn table[2][3] = {
-      {k_search<EnvDriving, POMCP_SEL_PUCB, 5>, k_search<EnvDriving, POMCP_SEL_UCB, 5>,
-       k_search<EnvDriving, POMCP_SEL_UNIFORM, 5>},
-      {k_search<EnvPursuitEvasion, POMCP_SEL_PUCB, 4>, k_search<EnvPursuitEvasion, POMCP_SEL_UCB, 4>,
-       k_search<EnvPursuitEvasion, POMCP_SEL_UNIFORM, 4>}};
+#define PB_SEARCH_ROW(T)                                                                          \
+  {{k_search<EnvDriving, POMCP_SEL_PUCB, 5, T>, k_search<EnvDriving, POMCP_SEL_UCB, 5, T>,        \
+    k_search<EnvDriving, POMCP_SEL_UNIFORM, 5, T>},                                               \
+   {k_search<EnvPursuitEvasion, POMCP_SEL_PUCB, 4, T>, k_search<EnvPursuitEvasion, POMCP_SEL_UCB, 4, T>, \
+    k_search<EnvPursuitEvasion, POMCP_SEL_UNIFORM, 4, T>}}
+  static const KFn table[2][2][3] = {PB_SEARCH_ROW(kTPB), PB_SEARCH_ROW(kTPBSmall)};
+#undef PB_SEARCH_ROW
   const int e = ctx->dp.env == POMCP_ENV_PURSUIT_EVASION ? 1 : 0;
-  hipLaunchKernelGGL(table[e][ctx->dp.sel], grid, block, 0, ctx->stream, ctx->dp, (int)num_sims,
-                     final_sel);
+  hipLaunchKernelGGL(table[tpb == kTPB ? 0 : 1][e][ctx->dp.sel], grid, block, 0, ctx->stream,
+                     ctx->dp, (int)num_sims, final_sel);
   HIP_TRY(ctx, hipGetLastError());
   return POMCP_OK;
 }
@@ -449,6 +463,25 @@ int pomcp_rekey(pomcp_ctx* ctx, uint64_t seed) {
 int pomcp_root_merge_buffer(pomcp_ctx* ctx, void** device_ptr) {
   if (!ctx || !device_ptr) return POMCP_E_INVALID;
   *device_ptr = ctx->dp.merge;
+  return POMCP_OK;
+}
+
+int pomcp_merge_roots(pomcp_ctx* ctx, int32_t group, pomcp_merged_root* out) {
+  if (!ctx || group < 1 || ctx->dp.B % group != 0)
+    return fail(ctx, POMCP_E_INVALID, "merge_roots: group must divide num_trees");
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  const int G = ctx->dp.B / group;
+  hipLaunchKernelGGL(k_merge_roots, dim3((unsigned)G), dim3(kWave), 0, ctx->stream, ctx->dp,
+                     (int)group, ctx->merged);
+  HIP_TRY(ctx, hipGetLastError());
+  if (!out) return POMCP_OK;
+  HIP_TRY(ctx, hipMemcpyAsync(out, ctx->merged, sizeof(pomcp_merged_root) * (size_t)G,
+                              hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  for (int g = 0; g < G; ++g)
+    if (out[g].error != 0)
+      return fail(ctx, out[g].error, "search: planner " + std::to_string(g) + ": replica error " +
+                                         std::to_string(out[g].error));
   return POMCP_OK;
 }
 
@@ -654,8 +687,7 @@ int pomcp_debug_phase_timing(pomcp_ctx* ctx, uint64_t* out, int32_t capacity, in
   *count = 0;
   return POMCP_E_UNSUPPORTED;
 #else
-  const int per_block = kTPB / kWave;
-  const int64_t waves = (int64_t)search_blocks(ctx->dp.B) * per_block;
+  const int64_t waves = search_waves(ctx->dp.B);
   if (ctx->dp.timing == nullptr) {   // first call: allocate; the next search fills it
     void* p = nullptr;
     if (dev_alloc(ctx, &p, sizeof(uint64_t) * 16 * (size_t)waves) != POMCP_OK) return POMCP_E_HIP;

@@ -567,6 +567,105 @@ __global__ __launch_bounds__(256) void k_restore(DevParams p, const TreeHdr* sna
   }
 }
 
+// Root-parallel merge: trees [g * group, (g + 1) * group) are
+// the root-parallel replicas of planner g; their root statistics in the merge
+// buffer ([B][A][2] = (visits, total), written by k_search and possibly
+// all-reduced across GPUs since) are summed and the merged action chosen:
+//   * PUCB  (max_visit_action_selection, mcts.py:565-581): argmax of summed visits;
+//   * UCB / uniform (max_value_action_selection, mcts.py:583-600): argmax of
+//     summed total / summed visits over the visited actions;
+// lowest action on ties (the replicas' choice must be the same everywhere, so
+// the reference's random tie-break is not drawn); 0 when nothing was visited
+// (action_space[0], mcts.py:270-272).  Summation order is fixed: lane l of the
+// group's wave sums trees [l * c, (l + 1) * c), c = ceil(group / 64), in tree
+// order from 0.0, then lane 0 sums the 64 partials in lane order from 0.0
+// (restated by oracle/root_parallel.py, bit-exact).  The step statistics of
+// the replicas (search depth, simulations, root visits, MinMaxStats, errors)
+// are reduced alongside.
+__global__ __launch_bounds__(64) void k_merge_roots(DevParams p, int group,
+                                                    pomcp_merged_root* out) {
+  __shared__ double part[2][POMCP_MAX_ACTIONS][kWave];
+  __shared__ double pmm[2][kWave];
+  __shared__ int64_t pn[2][kWave];
+  __shared__ int32_t pi[2][kWave];
+  const int g = blockIdx.x, lane = lane_id(), A = p.A;
+  const int c = (group + kWave - 1) / kWave;
+  const int k0 = min(lane * c, group), k1 = min(k0 + c, group);
+  const int64_t t0 = (int64_t)g * group;
+  const double* m = p.merge + t0 * A * 2;
+  double v[POMCP_MAX_ACTIONS], t[POMCP_MAX_ACTIONS];
+#pragma unroll
+  for (int a = 0; a < POMCP_MAX_ACTIONS; ++a) v[a] = t[a] = 0.0;
+  double mn = __builtin_inf(), mx = -__builtin_inf();
+  int64_t sims = 0, rv = 0;
+  int depth = 0, err = 0;
+  for (int k = k0; k < k1; ++k) {
+#pragma unroll
+    for (int a = 0; a < POMCP_MAX_ACTIONS; ++a)
+      if (a < A) {
+        v[a] = v[a] + m[((int64_t)k * A + a) * 2];
+        t[a] = t[a] + m[((int64_t)k * A + a) * 2 + 1];
+      }
+    const pomcp_root_stats& s = p.stats[t0 + k];
+    depth = max(depth, s.search_depth);
+    sims += s.num_sims;
+    rv += s.root_visits;
+    if (s.min_value < mn) mn = s.min_value;
+    if (s.max_value > mx) mx = s.max_value;
+    if (err == 0) err = s.error;
+  }
+#pragma unroll
+  for (int a = 0; a < POMCP_MAX_ACTIONS; ++a) {
+    part[0][a][lane] = v[a];
+    part[1][a][lane] = t[a];
+  }
+  pmm[0][lane] = mn;
+  pmm[1][lane] = mx;
+  pn[0][lane] = sims;
+  pn[1][lane] = rv;
+  pi[0][lane] = depth;
+  pi[1][lane] = err;
+  __syncthreads();
+  if (lane != 0) return;
+  pomcp_merged_root r;
+  r.action = 0;
+  r.num_trees = group;
+  r.search_depth = 0;
+  r.error = 0;
+  r.num_sims = 0;
+  r.root_visits = 0;
+  r.min_value = __builtin_inf();
+  r.max_value = -__builtin_inf();
+  for (int l = 0; l < kWave; ++l) {
+    r.search_depth = max(r.search_depth, pi[0][l]);
+    if (r.error == 0) r.error = pi[1][l];
+    r.num_sims += pn[0][l];
+    r.root_visits += pn[1][l];
+    if (pmm[0][l] < r.min_value) r.min_value = pmm[0][l];
+    if (pmm[1][l] > r.max_value) r.max_value = pmm[1][l];
+  }
+  double best = 0.0;
+  bool any = false;
+  for (int a = 0; a < POMCP_MAX_ACTIONS; ++a) {
+    double sv = 0.0, st = 0.0;
+    if (a < A)
+      for (int l = 0; l < kWave; ++l) {
+        sv = sv + part[0][a][l];
+        st = st + part[1][a][l];
+      }
+    r.visits[a] = sv;
+    r.totals[a] = st;
+    if (a >= A || !(sv > 0.0)) continue;
+    const double score = p.sel == POMCP_SEL_PUCB ? sv : st / sv;
+    if (!any || score > best) {
+      best = score;
+      r.action = a;
+      any = true;
+    }
+  }
+  out[g] = r;
+}
+
 __global__ void k_exp_selftest(const double* x, int n, double* out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = host_exp(x[i]);   // the I-NTMCP softmax's exp (host_exp.h)

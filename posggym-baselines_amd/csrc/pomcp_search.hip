@@ -41,7 +41,11 @@
 namespace pb {
 
 constexpr int kMaxA = 5;     // LDS root cache: A <= 5 (Driving-v1 5, PursuitEvasion-v1 4)
-constexpr int kTPB = 256;    // lanes per workgroup
+constexpr int kTPB = 256;    // lanes per workgroup of a full launch (one workgroup per CU)
+// Small launches (root-parallel trees of one planner, few batched roots) use
+// one-wave workgroups so their waves spread over the CUs instead of filling
+// a few of them (pomcp_capi.hip search_tpb).
+constexpr int kTPBSmall = 64;
 // Root cache layout: the root's stats0[a] (always) and, when kRootSlotsInLds,
 // its inline child slots[a][k].  Without the slots a tree needs 80 B of LDS,
 // which leaves room for more than one workgroup per CU.
@@ -84,15 +88,15 @@ struct PathEntry {
 
 enum : int { TP_LEVEL = 0, TP_ROLL = 1, TP_BACKUP = 2, TP_START = 3, TP_DONE = 4 };
 
-template <class Env, int SEL, int NA>
-__global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES_PER_EU, POMCP_WAVES_PER_EU))) void k_search(DevParams p, int num_sims, int final_sel) {
+template <class Env, int SEL, int NA, int TPB>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES_PER_EU, POMCP_WAVES_PER_EU))) void k_search(DevParams p, int num_sims, int final_sel) {
   static_assert(NA >= 2 && NA <= kMaxA, "action count");
   __shared__ typename Env::Model sm;
-  __shared__ uint4 rc[kRootParts][kTPB];   // the root block of every lane's tree
+  __shared__ uint4 rc[kRootParts][TPB];   // the root block of every lane's tree
   stage_model(p.model, sm);
   const int lid = (int)threadIdx.x;
   const int lane = lid & (kWave - 1);
-  const int wave = (int)(blockIdx.x * (kTPB / kWave) + (threadIdx.x >> 6));
+  const int wave = (int)(blockIdx.x * (TPB / kWave) + (threadIdx.x >> 6));
   const int tree = wave * kWave + lane;
   const bool valid = tree < p.B;
   const int tt = valid ? tree : 0;
@@ -682,7 +686,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVE
     }
   }
 #ifdef POMCP_PHASE_TIMING
-  if (p.timing != nullptr && (threadIdx.x & (kWave - 1)) == 0) {
+  if (p.timing != nullptr && (threadIdx.x & (kWave - 1)) == 0 && wave * kWave < p.B) {
     for (int i = 0; i < 16; ++i) p.timing[wave * 16 + i] = pt[i];
   }
 #endif
@@ -811,12 +815,14 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVE
   so->pad = 0;
 }
 
-#define PB_SEARCH_INST(E, NA)                                                 \
-  template __global__ void k_search<E, POMCP_SEL_PUCB, NA>(DevParams, int, int);  \
-  template __global__ void k_search<E, POMCP_SEL_UCB, NA>(DevParams, int, int);   \
-  template __global__ void k_search<E, POMCP_SEL_UNIFORM, NA>(DevParams, int, int);
-PB_SEARCH_INST(EnvDriving, 5)
-PB_SEARCH_INST(EnvPursuitEvasion, 4)
+#define PB_SEARCH_INST(E, NA, T)                                                 \
+  template __global__ void k_search<E, POMCP_SEL_PUCB, NA, T>(DevParams, int, int);  \
+  template __global__ void k_search<E, POMCP_SEL_UCB, NA, T>(DevParams, int, int);   \
+  template __global__ void k_search<E, POMCP_SEL_UNIFORM, NA, T>(DevParams, int, int);
+PB_SEARCH_INST(EnvDriving, 5, kTPB)
+PB_SEARCH_INST(EnvPursuitEvasion, 4, kTPB)
+PB_SEARCH_INST(EnvDriving, 5, kTPBSmall)
+PB_SEARCH_INST(EnvPursuitEvasion, 4, kTPBSmall)
 #undef PB_SEARCH_INST
 
 }  // namespace pb

@@ -137,6 +137,22 @@ class PomcpRootStats(C.Structure):
     ]
 
 
+class PomcpMergedRoot(C.Structure):
+    """``pomcp_merged_root`` (include/pomcp.h)."""
+    _fields_ = [
+        ("action", C.c_int32),
+        ("num_trees", C.c_int32),
+        ("search_depth", C.c_int32),
+        ("error", C.c_int32),
+        ("num_sims", C.c_int64),
+        ("root_visits", C.c_int64),
+        ("min_value", C.c_double),
+        ("max_value", C.c_double),
+        ("visits", C.c_double * POMCP_MAX_ACTIONS),
+        ("totals", C.c_double * POMCP_MAX_ACTIONS),
+    ]
+
+
 # (name, restype, argtypes) for every symbol include/pomcp.h declares.
 _CTX = C.c_void_p
 _P32 = C.POINTER(C.c_int32)
@@ -157,6 +173,7 @@ SIGNATURES = [
     ("pomcp_get_root_belief", C.c_int, [_CTX, C.c_int32, _PU32, C.c_int32, _P32]),
     ("pomcp_rekey", C.c_int, [_CTX, C.c_uint64]),
     ("pomcp_root_merge_buffer", C.c_int, [_CTX, C.POINTER(C.c_void_p)]),
+    ("pomcp_merge_roots", C.c_int, [_CTX, C.c_int32, C.POINTER(PomcpMergedRoot)]),
     ("pomcp_synthetic_obs", C.c_int, [_CTX, C.c_uint64, _PU64]),
     ("pomcp_snapshot", C.c_int, [_CTX]),
     ("pomcp_restore", C.c_int, [_CTX]),

@@ -4,7 +4,12 @@
 Additive fields (defaults keep the reference behaviour):
   * ``num_sims``: run exactly this many simulations per ``get_action`` instead
     of the wall-clock loop of ``mcts.py:285`` (needed for reproducible parity);
-  * ``device``: HIP device ordinal of the engine.
+  * ``device``: HIP device ordinal of the engine;
+  * ``root_parallel``: K replica trees for one planner on the GPU (replica k =
+    the exact planner with RNG key (seed, k); ``num_sims`` is split as
+    ceil(num_sims / K) per replica; the final action is the device merge of the
+    replicas' root statistics, ``pomcp_merge_roots``).  1 (default) = the
+    reference's single tree, bit-exact.
 """
 import math
 from dataclasses import dataclass, field
@@ -31,13 +36,14 @@ class MCTSConfig:
     use_rollout_if_no_value: bool = True
     num_sims: Optional[int] = None
     device: int = 0
+    root_parallel: int = 1
 
     num_particles: int = field(init=False)
     extra_particles: int = field(init=False)
     depth_limit: int = field(init=False)
 
     def __post_init__(self):
-        # same assertions (AssertionError) as config.py:448-459
+        # same assertions (AssertionError) as config.py:34-45
         assert 0.0 <= self.discount <= 1.0
         assert self.search_time_limit > 0.0
         assert self.c > 0.0
@@ -47,7 +53,8 @@ class MCTSConfig:
         self.action_selection = self.action_selection.lower()
         assert self.action_selection in ("pucb", "ucb", "uniform")
         assert self.num_sims is None or self.num_sims >= 0
-        # derived sizes, config.py:461-469 (discount == 1 raises ZeroDivisionError there too)
+        assert self.root_parallel >= 1
+        # derived sizes, config.py:47-55 (discount == 1 raises ZeroDivisionError there too)
         self.num_particles = math.ceil(self.search_time_limit * 100)
         self.extra_particles = math.ceil(self.extra_particles_prop * self.num_particles)
         self.depth_limit = 0 if self.discount == 0.0 else math.ceil(

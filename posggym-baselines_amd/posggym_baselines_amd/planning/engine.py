@@ -207,6 +207,18 @@ class PomcpEngine:
         self._check(self._lib.pomcp_root_merge_buffer(self._ctx, C.byref(p)), "merge_buffer")
         return p.value
 
+    def merge_roots(self, group, fetch=True):
+        """Device merge of root-parallel replicas (``pomcp_merge_roots``): trees
+        [g * group, (g + 1) * group) are planner g.  Returns the
+        ``PomcpMergedRoot`` array (or None with ``fetch=False``)."""
+        G = self.num_trees // group
+        if not fetch:
+            self._check(self._lib.pomcp_merge_roots(self._ctx, int(group), None), "merge_roots")
+            return None
+        out = (N.PomcpMergedRoot * G)()
+        self._check(self._lib.pomcp_merge_roots(self._ctx, int(group), out), "merge_roots")
+        return out
+
     def synthetic_obs(self, env_seed_base):
         out = np.zeros(self.num_trees, dtype=np.uint64)
         self._check(self._lib.pomcp_synthetic_obs(

@@ -10,6 +10,20 @@ search_policy)``, ``step(obs)``, ``reset()``, ``update(action, obs)``,
 
 ``BatchedPOMCP`` runs many independent planners (one tree each) in one kernel
 launch; it is what the bench and batch experiments use.
+
+``MCTSConfig.root_parallel = K > 1`` gives ONE planner K replica trees on the
+GPU (root parallelisation): replica k is the exact single-tree planner with
+RNG key (seed, k), every replica is updated with the played action and the
+real observation, searches ceil(num_sims / K) simulations, and the played
+action is the device merge of the replicas' root statistics
+(``pomcp_merge_roots``: summed visits for PUCB, summed total / summed visits
+otherwise).  K = 1 (default) is the reference's planner, bit-exact.
+
+``POMCP(..., process_group=pg)`` spreads the replicas over the ranks of a
+``torch.distributed`` group (one process per GPU, backend "nccl" = RCCL):
+rank r's replicas take keys (seed, r*K .. r*K+K-1), and before the decision
+one all-reduce sums the merge buffer over the ranks (``parallel.allreduce_roots``),
+so every rank plays the same action.
 """
 import dataclasses
 import logging
@@ -50,7 +64,7 @@ class POMCP:
     """
 
     def __init__(self, model, agent_id: str, config: MCTSConfig, search_policy: SearchPolicy,
-                 *, num_sims: Optional[int] = None):
+                 *, num_sims: Optional[int] = None, process_group=None):
         if not isinstance(search_policy, RandomSearchPolicy):
             raise NotImplementedError(
                 "the GPU POMCP engine runs the uniform random rollout policy in-kernel; "
@@ -69,8 +83,17 @@ class POMCP:
         self.num_agents = len(model.possible_agents)
         self.action_space = list(range(model.action_spaces[agent_id].n))
         self._num_sims = num_sims if num_sims is not None else config.num_sims
-        self._engine = PomcpEngine(model, agent_id, config, num_trees=1,
-                                   num_sims=self._num_sims or 4096)
+        self._K = int(config.root_parallel)
+        per = math.ceil(self._num_sims / self._K) if self._num_sims is not None else None
+        self._per_replica = per
+        self._pg = process_group
+        self._rank, self._world = 0, 1
+        if process_group is not None:
+            import torch.distributed as dist
+            self._rank = dist.get_rank(process_group)
+            self._world = dist.get_world_size(process_group)
+        self._engine = PomcpEngine(model, agent_id, config, num_trees=self._K,
+                                   num_sims=per or 4096, tree_key_base=self._rank * self._K)
         self.step_limit = self._engine.step_limit
         self._logger = logging.getLogger()
         self._last_action = None
@@ -132,9 +155,11 @@ class POMCP:
         else:
             a = int(action)
         key = self.model.obs_key(obs)
-        absorbing = self._engine.update([a], [key])
+        absorbing = self._engine.update([a], [key])   # broadcast to every replica
+        # a replica whose root is absorbing stops searching and merges as zeros;
+        # the planner is absorbing once all of them are (oracle/root_parallel.py)
         self.root = dataclasses.replace(self.root, t=self.root.t + 1,
-                                        is_absorbing=bool(absorbing[0]))
+                                        is_absorbing=bool(np.all(absorbing)))
         self.step_statistics["update_time"] = time.time() - start
 
     # -------------------------------------------------------------- search
@@ -144,35 +169,56 @@ class POMCP:
             return self.action_space[0]
         start = time.time()
         depth = 0
+        K = self._K
         if self._num_sims is not None:
-            self._engine.search(self._num_sims, fetch=False)
-            n_sims = self._num_sims
+            self._engine.search(self._per_replica, fetch=False)
+            n_sims = self._per_replica * K
         else:
             # the wall-clock loop (mcts.py:285) as launches of growing chunks; the
             # final action choice is drawn once, after the last one
             n_sims, chunk = 0, 16
             while time.time() - start < self.config.search_time_limit:
                 self._engine.search(chunk, final=False)
-                depth = max(depth, self._engine.root_stats()[0].search_depth)   # synchronises
-                n_sims += chunk
+                depth = max(depth, self._depth())   # synchronises
+                n_sims += chunk * K
                 chunk = min(chunk * 2, 4096)
             self._engine.search(0, fetch=False)
-        st = self._engine.root_stats()[0]
-        search_time = time.time() - start
         A = len(self.action_space)
+        if self._world > 1:
+            from posggym_baselines_amd.planning.parallel import allreduce_roots
+            self._engine.root_stats()   # synchronises the engine (raises on a replica error)
+            allreduce_roots(self._engine, f"cuda:{self.config.device}", self._pg)
+        if K == 1 and self._world == 1:
+            st = self._engine.root_stats()[0]
+            action = int(st.action)
+            visits, belief_size = st.root_visits, st.belief_size
+            cv, cval, ctot = (tuple(st.child_visits[:A]), tuple(st.child_values[:A]),
+                              tuple(st.child_totals[:A]))
+        else:
+            st = self._engine.merge_roots(K)[0]
+            action = int(st.action)
+            visits, belief_size = st.root_visits, None
+            cv = tuple(int(v) for v in st.visits[:A])
+            ctot = tuple(st.totals[:A])
+            cval = tuple(t / v if v > 0 else 0.0 for t, v in zip(ctot, cv))
+        search_time = time.time() - start
         self._min_value, self._max_value = st.min_value, st.max_value
         self.root = dataclasses.replace(
-            self.root, visits=st.root_visits, belief_size=st.belief_size,
-            child_visits=tuple(st.child_visits[:A]), child_values=tuple(st.child_values[:A]),
-            child_totals=tuple(st.child_totals[:A]))
+            self.root, visits=visits, belief_size=belief_size, child_visits=cv,
+            child_values=cval, child_totals=ctot)
         self.step_statistics.update(
             search_time=search_time, search_depth=max(depth, st.search_depth), num_sims=n_sims,
             min_value=st.min_value, max_value=st.max_value)
-        return int(st.action)
+        return action
 
-    def root_belief(self):
-        """Root particles as (t, v0, v1) packed u32 rows."""
-        return self._engine.root_belief(0)
+    def _depth(self):
+        if self._K == 1:
+            return self._engine.root_stats()[0].search_depth
+        return self._engine.merge_roots(self._K)[0].search_depth
+
+    def root_belief(self, replica: int = 0):
+        """Root particles as (t, v0, v1) packed u32 rows (of one replica)."""
+        return self._engine.root_belief(replica)
 
     def close(self):
         self.search_policy.close()

@@ -109,7 +109,7 @@ def run_intmcp_case(name):
 
 
 def config_kats():
-    """MCTSConfig derived fields (config.py:461-469) from the reference itself."""
+    """MCTSConfig derived fields (config.py:47-55) from the reference itself."""
     P = import_reference()
     rows = []
     for T in (0.1, 0.5, 1.0, 5.0, 20.0):

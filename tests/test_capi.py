@@ -41,6 +41,7 @@ def test_struct_layout_matches_header(tmp_path):
         "pomcp_root_stats": [f[0] for f in N.PomcpRootStats._fields_],
         "pomcp_grid": [f[0] for f in N.PomcpGrid._fields_],
         "pomcp_pe_grid": [f[0] for f in N.PomcpPeGrid._fields_],
+        "pomcp_merged_root": [f[0] for f in N.PomcpMergedRoot._fields_],
         "intmcp_config": [f[0] for f in N.IntmcpConfig._fields_],
         "intmcp_root_stats": [f[0] for f in N.IntmcpRootStats._fields_],
     }
@@ -58,6 +59,7 @@ def test_struct_layout_matches_header(tmp_path):
         [str(exe)], check=True, capture_output=True, text=True).stdout.split("\n") if line)
     for st, cls in (("pomcp_config", N.PomcpConfig), ("pomcp_root_stats", N.PomcpRootStats),
                     ("pomcp_grid", N.PomcpGrid), ("pomcp_pe_grid", N.PomcpPeGrid),
+                    ("pomcp_merged_root", N.PomcpMergedRoot),
                     ("intmcp_config", N.IntmcpConfig), ("intmcp_root_stats", N.IntmcpRootStats)):
         assert int(out[st]) == ctypes.sizeof(cls), st
         for f in fields[st]:
