@@ -160,9 +160,22 @@ int pomcp_search_continue(pomcp_ctx* ctx, int32_t num_sims);
 /* Copy every tree's pomcp_root_stats of the last search to host. */
 int pomcp_get_root_stats(pomcp_ctx* ctx, pomcp_root_stats* out);
 
+/* Host particles as the root belief of one FRESH tree (after pomcp_reset,
+ * before its first update): `particles` = count (t, v0, v1) u32 triples in
+ * insertion order (ParticleBelief, belief.py:47-64), all with the same t >= 1.
+ * The root becomes an unexpanded obs node at time t holding them -- what
+ * _initial_update builds (mcts.py:175-227), from the caller's particles
+ * instead of b0 samples (no RNG draws).  Searches and updates follow as usual. */
+int pomcp_set_root_belief(pomcp_ctx* ctx, int32_t tree, const uint32_t* particles, int32_t count);
+
 /* Root belief particles of one tree as (t, v0, v1) u32 triples (belief.py:47-64). */
 int pomcp_get_root_belief(pomcp_ctx* ctx, int32_t tree, uint32_t* out, int32_t capacity,
                           int32_t* count);
+
+/* Arena use: the largest block count and particle-log record count over the
+ * trees (after the last update's subtree compaction / the last search).  The
+ * wall-clock loop sizes its chunks from it (never overflowing the arenas). */
+int pomcp_arena_usage(pomcp_ctx* ctx, int32_t* max_blocks_used, int32_t* max_log_used);
 
 /* Root-parallel search: re-key every tree's streams to `seed`
  * keeping counters (rank g uses seed ^ (g << 32)). */

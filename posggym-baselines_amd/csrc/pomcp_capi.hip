@@ -345,6 +345,26 @@ static int first_tree_error(pomcp_ctx* ctx, const int32_t* codes, int stride, in
   return POMCP_OK;
 }
 
+// Scratch of the subtree compaction (k_compact), allocated on the first
+// re-root: a batch that is only ever searched from its initial update (the
+// bench's restore loop) never pays for it.
+static int ensure_compaction_scratch(pomcp_ctx* ctx) {
+  DevParams& d = ctx->dp;
+  if (d.cmap) return POMCP_OK;
+  const int64_t B = d.B;
+  void* p = nullptr;
+  int rc;
+  if ((rc = dev_alloc(ctx, &p, sizeof(int32_t) * (size_t)(B * d.Nb))) != POMCP_OK) return rc;
+  d.cmap = reinterpret_cast<int32_t*>(p);
+  if ((rc = dev_alloc(ctx, &p, sizeof(int32_t) * (size_t)(B * d.Nb))) != POMCP_OK) return rc;
+  d.cpar = reinterpret_cast<int32_t*>(p);
+  if ((rc = dev_alloc(ctx, &p, sizeof(int32_t) * (size_t)(B * d.H))) != POMCP_OK) return rc;
+  d.ovf_new = reinterpret_cast<int32_t*>(p);
+  if ((rc = dev_alloc(ctx, &p, sizeof(OvfSlot) * (size_t)(B * d.H))) != POMCP_OK) return rc;
+  d.ovf_tmp = reinterpret_cast<OvfSlot*>(p);
+  return POMCP_OK;
+}
+
 int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_keys,
                  int32_t* root_absorbing_out) {
   if (!ctx || !obs_keys) return POMCP_E_INVALID;
@@ -365,6 +385,18 @@ int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_key
   HIP_TRY(ctx, hipGetLastError());
   PB_ENV_LAUNCH(ctx, k_update, dim3(grid_blocks(B)), dim3(256), ctx->dp);
   HIP_TRY(ctx, hipGetLastError());
+  // subtree compaction (re-roots only: an initial update leaves an empty arena)
+  bool reroot = false;
+  for (int t = 0; t < B && !reroot; ++t) reroot = acts[t] >= 0;
+  if (reroot) {
+    int rc = ensure_compaction_scratch(ctx);
+    if (rc != POMCP_OK) return rc;
+    hipLaunchKernelGGL(k_compact, dim3(grid_blocks(B)), dim3(256), 0, ctx->stream, ctx->dp);
+    HIP_TRY(ctx, hipGetLastError());
+    hipLaunchKernelGGL(k_compact_log, dim3(grid_blocks(search_waves(B))), dim3(256), 0,
+                       ctx->stream, ctx->dp);
+    HIP_TRY(ctx, hipGetLastError());
+  }
   HIP_TRY(ctx, hipMemcpyAsync(ctx->host_upd.data(), ctx->dp.upd_out, sizeof(int32_t) * 2 * B,
                               hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -420,6 +452,42 @@ int pomcp_get_root_stats(pomcp_ctx* ctx, pomcp_root_stats* out) {
   return POMCP_OK;
 }
 
+int pomcp_set_root_belief(pomcp_ctx* ctx, int32_t tree, const uint32_t* particles, int32_t count) {
+  if (!ctx || tree < 0 || tree >= ctx->dp.B || count < 1 || !particles)
+    return fail(ctx, POMCP_E_INVALID, "set_root_belief: bad arguments");
+  if (count > ctx->dp.Nr) return fail(ctx, POMCP_E_ARENA, "set_root_belief: more particles than max_belief");
+  const uint32_t t = particles[0];
+  for (int32_t i = 0; i < count; ++i)
+    if (particles[3 * i] != t || t < 1u)
+      return fail(ctx, POMCP_E_INVALID, "set_root_belief: every particle needs the same t >= 1");
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  TreeHdr h;
+  HIP_TRY(ctx, hipMemcpyAsync(&h, ctx->dp.hdr + tree, sizeof(TreeHdr), hipMemcpyDeviceToHost,
+                              ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  if (h.root_t != 0 || h.n_blocks != 0 || h.error != 0)
+    return fail(ctx, POMCP_E_STATE, "set_root_belief: the tree must be fresh (pomcp_reset)");
+  std::vector<uint4> b((size_t)count);
+  for (int32_t i = 0; i < count; ++i)
+    b[i] = make_uint4(particles[3 * i], particles[3 * i + 1], particles[3 * i + 2], 0u);
+  const int sel = h.belief_sel ^ 1;
+  uint4* dst = ctx->dp.belief + (int64_t)tree * 2 * ctx->dp.Nr + (int64_t)sel * ctx->dp.Nr;
+  HIP_TRY(ctx, hipMemcpyAsync(dst, b.data(), sizeof(uint4) * (size_t)count, hipMemcpyHostToDevice,
+                              ctx->stream));
+  h.belief_sel = sel;
+  h.belief_size = count;
+  h.root_t = (int32_t)t;
+  h.root_id = kRootId;
+  h.root_blk = -1;
+  h.root_visits = 0;
+  h.root_abs = 0;
+  h.n_nodes += 1;
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->dp.hdr + tree, &h, sizeof(TreeHdr), hipMemcpyHostToDevice,
+                              ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return POMCP_OK;
+}
+
 int pomcp_get_root_belief(pomcp_ctx* ctx, int32_t tree, uint32_t* out, int32_t capacity,
                           int32_t* count) {
   if (!ctx || !count || tree < 0 || tree >= ctx->dp.B) return POMCP_E_INVALID;
@@ -443,6 +511,23 @@ int pomcp_get_root_belief(pomcp_ctx* ctx, int32_t tree, uint32_t* out, int32_t c
     out[3 * i + 1] = tmp[i].y;
     out[3 * i + 2] = tmp[i].z;
   }
+  return POMCP_OK;
+}
+
+int pomcp_arena_usage(pomcp_ctx* ctx, int32_t* max_blocks_used, int32_t* max_log_used) {
+  if (!ctx || !max_blocks_used || !max_log_used) return POMCP_E_INVALID;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  std::vector<TreeHdr> h((size_t)ctx->dp.B);
+  HIP_TRY(ctx, hipMemcpyAsync(h.data(), ctx->dp.hdr, sizeof(TreeHdr) * h.size(),
+                              hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  int32_t nb = 0, nl = 0;
+  for (const auto& x : h) {
+    nb = x.n_blocks > nb ? x.n_blocks : nb;
+    nl = x.n_log > nl ? x.n_log : nl;
+  }
+  *max_blocks_used = nb;
+  *max_log_used = nl;
   return POMCP_OK;
 }
 

@@ -138,6 +138,14 @@ struct DevParams {
   const uint64_t* in_obs;
   uint64_t* out_obs;
   uint64_t* timing;     // [waves][16] phase cycles (diagnostics build only), may be null
+  // subtree compaction at re-root (k_compact / k_compact_log), allocated on the
+  // first re-root: block -> new index (-1: not in the new root's subtree), the
+  // parent block / alive list, overflow slot -> new obs node id, the live
+  // overflow entries being re-inserted
+  int32_t* cmap;        // [B][Nb]
+  int32_t* cpar;        // [B][Nb]
+  int32_t* ovf_new;     // [B][H]
+  OvfSlot* ovf_tmp;     // [B][H]
 };
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }

@@ -484,26 +484,65 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
               const uint4* pbel = T.root_belief();
               const double limit = p.limit_factor * (double)need;
               int got = 0, tries = 0, nrej = 0;
+              // 64 tries per pass, one per lane: try i draws word (counter + i) of
+              // the belief, the other agent's action and the model stream (one
+              // each, independent of the outcomes), so the serial loop's tries
+              // are computed in parallel; the ones it would run are the prefix
+              // up to the try that completes `need` acceptances (or `limit`),
+              // accepted / rejected particles keep their order (ballot ranks)
+              const int oth = p.other;
+              uint32_t& c_oth = oth == 0 ? T.c_act0 : T.c_act1;
+              const uint32_t s_oth = S_ACT_BASE + (uint32_t)oth;
+              const uint64_t lt = (1ull << lane) - 1ull;
               while (got < need && (double)tries < limit) {
-                ++tries;
-                const uint4 hp = pbel[T.d_belief((uint32_t)T.bsize)];
-                const int ao = (int)T.d_act(p.other, (uint32_t)p.A);
+                const bool valid = (double)(tries + lane) < limit;
+                const uint32_t wb = philox_word(T.seed, T.tkey, S_BELIEF, T.c_belief + (uint32_t)lane);
+                const uint32_t wa = philox_word(T.seed, T.tkey, s_oth, c_oth + (uint32_t)lane);
+                const uint32_t wm = Env::kStepDraws
+                                        ? philox_word(T.seed, T.tkey, S_MODEL, T.c_model + (uint32_t)lane)
+                                        : 0u;
+                const uint4 hp = pbel[uniform_int(wb, (uint32_t)T.bsize)];
                 uint32_t n0, n1;
-                uint64_t k;
-                T.joint_step(uniu(hp.y), uniu(hp.z), action, ao, &n0, &n1, &k);
-                const uint4 rec = make_uint4(uniu(hp.x) + 1u, n0, n1, 0u);
-                if (k == obs) {
-                  if (lane == 0) nb[n + got] = rec;
-                  ++got;
-                } else if (nrej < need) {
-                  if (lane == 0) nb[n + need + nrej] = rec;
-                  ++nrej;
+                double r;
+                int done;
+                Env::step(sm, p.ego, hp.y, hp.z, (uint32_t)action, uniform_int(wa, (uint32_t)p.A),
+                          Env::kStepDraws ? uniform_int(wm, 2u) : 0u, &n0, &n1, &r, &done);
+                const bool acc = valid && Env::obs_key(sm, p.ego, n0, n1) == obs;
+                const uint64_t am = __ballot(acc);
+                const int pa = __popcll(am & lt);
+                const bool run = valid && got + pa < need;   // the loop head's test before this try
+                const uint64_t rm = __ballot(run);
+                const uint64_t jm = __ballot(run && !acc);
+                const uint4 rec = make_uint4(hp.x + 1u, n0, n1, 0u);
+                if (run && acc) nb[n + got + pa] = rec;
+                const int rr = nrej + __popcll(jm & lt);
+                if (run && !acc && rr < need) nb[n + need + rr] = rec;
+                const int ran = __popcll(rm);
+                got += __popcll(am & rm);
+                nrej = min(need, nrej + __popcll(jm));
+                tries += ran;
+                T.c_belief += (uint32_t)ran;
+                c_oth += (uint32_t)ran;
+                if (Env::kStepDraws) T.c_model += (uint32_t)ran;
+              }
+              // the LDS pages of the streams advanced here are stale
+              T.r_belief.refill(T.seed, T.tkey, S_BELIEF, T.c_belief / kRngPage);
+              T.r_model.refill(T.seed, T.tkey, S_MODEL, T.c_model / kRngPage);
+              if (oth == 0) T.r_act0.refill(T.seed, T.tkey, S_ACT_BASE, T.c_act0 / kRngPage);
+              else T.r_act1.refill(T.seed, T.tkey, S_ACT_BASE + 1, T.c_act1 / kRngPage);
+              __builtin_amdgcn_s_waitcnt(0);
+              __threadfence_block();
+              int fill = need - got;   // rejected samples fill up (belief.py:186-192)
+              if (fill > nrej) fill = nrej;
+              for (int q0 = 0; q0 < fill; q0 += kWave) {   // disjoint ranges: got < need
+                const int q2 = q0 + lane;
+                if (q2 < fill) {   // written by other lanes: read past the L1
+                  const uint64_t* src = reinterpret_cast<const uint64_t*>(nb + n + need + q2);
+                  uint64_t* dst = reinterpret_cast<uint64_t*>(nb + n + got + q2);
+                  dst[0] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                  dst[1] = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
               }
-              int fill = need - got;
-              if (fill > nrej) fill = nrej;
-              for (int q2 = 0; q2 < fill; ++q2)
-                if (lane == 0) nb[n + got + q2] = nb[n + need + q2];
               n += got + fill;
             }
           }
@@ -525,6 +564,254 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
     p.upd_out[2 * tree] = T.root_abs;
     p.upd_out[2 * tree + 1] = T.err;
   }
+}
+
+// ------------------------------------------------------- subtree compaction
+// MCTS._update drops the old root (mcts.py:261-263: `obs_node.parent = None`,
+// the rest of the tree is garbage-collected).  Here the arena is compacted
+// after every re-root so that it only ever holds the new root's subtree: a
+// per-step bound on blocks, overflow entries, particle records and node ids
+// (wall-clock searches of the reference's 0.1-20 s budgets, exp_utils.py:27).
+// Relabelling only: block order, node ids and overflow slots carry no meaning
+// to the search (a node's particles keep their insertion order), so results
+// are unchanged -- every golden episode runs through it.
+//
+// Blocks are allocated when a leaf is expanded, after its parent, so a child's
+// block index is always larger than its parent's; the new numbering keeps that
+// order (the alive blocks in ascending old order), which lets one ascending pass
+// decide reachability and move blocks in place.
+
+__device__ __forceinline__ int32_t ld_agent(const int32_t* p) {   // bypass the (stale) L1
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_agent_u32(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One wave per tree: reachability from the new root, block move, overflow map
+// rebuild.  Runs after k_update for trees re-rooted without error.
+__global__ __launch_bounds__(256) void k_compact(DevParams p) {
+  const int tree = blockIdx.x * kTreesPerBlock + (threadIdx.x >> 6);
+  if (tree >= p.B) return;
+  const int lane = lane_id();
+  TreeHdr h = p.hdr[tree];
+  const bool on = uni(h.error) == 0 && uni(h.root_t) >= 2;
+  if (lane == 0) p.cnt[tree] = on ? 1 : 0;   // read by k_compact_log
+  if (!on) return;
+  const int A = p.A;
+  const int nb = uni(h.n_blocks);
+  const int R = uni(h.root_blk);
+  Line* const an = p.an + tree_base_lines(tree, p.Nb, A);
+  const int64_t bstride = blk_stride_lines(A);
+  int32_t* const cmap = p.cmap + (int64_t)tree * p.Nb;
+  int32_t* const cpar = p.cpar + (int64_t)tree * p.Nb;
+  OvfSlot* const ovf = p.ovf + (int64_t)tree * p.H;
+  int32_t* const onew = p.ovf_new + (int64_t)tree * p.H;
+  OvfSlot* const otmp = p.ovf_tmp + (int64_t)tree * p.H;
+  const uint32_t epoch = (uint32_t)uni(h.epoch);
+  // 1. parent of every block: the inline child slots of each block, then the
+  //    live overflow entries
+  for (int b = lane; b < nb; b += kWave) cpar[b] = -1;
+  __threadfence();
+  for (int b = lane; b < nb; b += kWave) {
+    const uint4* blk = reinterpret_cast<const uint4*>(an + (int64_t)b * bstride);
+    for (int a = 0; a < A; ++a) {
+#pragma unroll
+      for (int k = 0; k < kSlots; ++k) {
+        const uint4 sl = blk[part_slot(a, k)];
+        if ((sl.y & (uint32_t)(kValidBit >> 32)) != 0u && (int)sl.z >= 0) cpar[(int)sl.z] = b;
+      }
+    }
+  }
+  for (int64_t s = lane; s < p.H; s += kWave) {
+    const uint4 w0 = reinterpret_cast<const uint4*>(ovf + s)[0];
+    const uint4 w1 = reinterpret_cast<const uint4*>(ovf + s)[1];
+    const uint64_t key = (uint64_t)w0.x | ((uint64_t)w0.y << 32);
+    if ((uint32_t)(key >> kEpochShift) == epoch && (int)w1.x >= 0) cpar[(int)w1.x] = (int)(w0.z / (uint32_t)A);
+  }
+  __threadfence();
+  // 2. reachability and the new numbering (ascending), alive list into cpar
+  for (int b = lane; b < (R < 0 ? nb : R); b += kWave) cmap[b] = -1;
+  int m = 0;
+  for (int base = R < 0 ? nb : R; base < nb; base += kWave) {
+    const int b = base + lane;
+    const bool in = b < nb;
+    const int par = in ? ld_agent(cpar + b) : -1;
+    // parents in earlier chunks are final; parents inside this chunk propagate
+    // by shuffles (child > parent, so this converges within the chunk depth)
+    bool alive = in && (b == R || (par >= 0 && par < base && ld_agent(cmap + par) >= 0));
+    const bool local = in && par >= base;
+    for (;;) {
+      const int src = local ? par - base : lane;
+      const bool pa = __shfl((int)alive, src) != 0;
+      const bool nw = alive || (local && pa);
+      if (__ballot(nw != alive) == 0ull) break;
+      alive = nw;
+    }
+    const uint64_t mk = __ballot(alive);
+    const int idx = m + __popcll(mk & ((1ull << lane) - 1ull));
+    if (in) cmap[b] = alive ? idx : -1;
+    if (alive) cpar[idx] = b;   // idx <= b: entries of this and later chunks already read
+    m += __popcll(mk);
+    __threadfence();
+  }
+  __threadfence();
+  // 3. move the alive blocks down (in place, ascending), remapping the child
+  //    block of every valid inline slot.  8 blocks per pass: all of a pass's
+  //    parts are loaded before any is stored (a destination may be a source
+  //    of the same pass, never of a later one).
+  constexpr int kMoveBlocks = 8;
+  const int parts = blk_parts(A);   // <= 48
+  for (int i0 = 0; i0 < m; i0 += kMoveBlocks) {
+    constexpr int kPer = (kMoveBlocks * 48 + kWave - 1) / kWave;
+    uint4 v[kPer];
+    int dst[kPer], prt[kPer];
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const int e = lane + q * kWave;
+      const int j = e / parts, pp = e % parts;
+      dst[q] = -1;
+      prt[q] = pp;
+      v[q] = make_uint4(0, 0, 0, 0);
+      if (j < kMoveBlocks && e < kMoveBlocks * parts && i0 + j < m) {
+        const int src = ld_agent(cpar + i0 + j);
+        dst[q] = i0 + j;
+        v[q] = reinterpret_cast<const uint4*>(an + (int64_t)src * bstride)[pp];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const int pp = prt[q];
+      const bool slot = pp >= kLine && (pp % kLine) >= 1 && (pp % kLine) <= kSlots;
+      if (dst[q] >= 0 && slot && (v[q].y & (uint32_t)(kValidBit >> 32)) != 0u && (int)v[q].z >= 0)
+        v[q].z = (uint32_t)ld_agent(cmap + (int)v[q].z);
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int q = 0; q < kPer; ++q)
+      if (dst[q] >= 0) reinterpret_cast<uint4*>(an + (int64_t)dst[q] * bstride)[prt[q]] = v[q];
+    __threadfence();
+  }
+  // 4. overflow map: live entries of alive action nodes are copied out (with the
+  //    new action node and child block), the generation is bumped, and they are
+  //    re-inserted in slot order; ovf_new maps an old slot to its new node id
+  int nlive = 0;
+  for (int64_t s0 = 0; s0 < p.H; s0 += kWave) {
+    const int64_t s = s0 + lane;
+    uint4 w0 = make_uint4(0, 0, 0, 0), w1 = w0;
+    bool keep = false;
+    if (s < p.H) {
+      w0 = reinterpret_cast<const uint4*>(ovf + s)[0];
+      w1 = reinterpret_cast<const uint4*>(ovf + s)[1];
+      const uint64_t key = (uint64_t)w0.x | ((uint64_t)w0.y << 32);
+      if ((uint32_t)(key >> kEpochShift) == epoch) {
+        const int pb = ld_agent(cmap + (int)(w0.z / (uint32_t)A));
+        if (pb >= 0) {
+          keep = true;
+          w0.z = (uint32_t)pb * (uint32_t)A + w0.z % (uint32_t)A;
+          if ((int)w1.x >= 0) w1.x = (uint32_t)ld_agent(cmap + (int)w1.x);
+          w1.z = (uint32_t)s;   // the old slot (pad word)
+        }
+      }
+      onew[s] = -1;
+    }
+    const uint64_t mk = __ballot(keep);
+    if (keep) {
+      const int at = nlive + __popcll(mk & ((1ull << lane) - 1ull));
+      reinterpret_cast<uint4*>(otmp + at)[0] = w0;
+      reinterpret_cast<uint4*>(otmp + at)[1] = w1;
+    }
+    nlive += __popcll(mk);
+  }
+  uint32_t ne = (epoch + 1u) & kEpochMask;
+  if (ne == 0u) {   // generation counter wrapped: clear the map
+    clear_ovf(p, tree, lane);
+    ne = 1u;
+  }
+  __threadfence();
+  for (int i = 0; i < nlive; ++i) {
+    const uint4 w0 = reinterpret_cast<const uint4*>(otmp + i)[0];
+    const uint4 w1 = reinterpret_cast<const uint4*>(otmp + i)[1];
+    const uint64_t okey = ((uint64_t)w0.x | ((uint64_t)w0.y << 32)) & kObsMask;
+    uint32_t b = ovf_hash(w0.z, okey) & p.bucket_mask;
+    for (uint32_t probe = 0; probe <= p.bucket_mask; ++probe) {
+      OvfSlot* e = ovf + (int64_t)b * kBucket + (lane & (kBucket - 1));
+      uint32_t ky = 0u;   // the key's high word (generation); this loop's inserts are not in L1
+      if (lane < kBucket) ky = ld_agent_u32(reinterpret_cast<const uint32_t*>(e) + 1);
+      const uint64_t em = __ballot(lane < kBucket && (ky >> (kEpochShift - 32)) != ne);
+      if (em) {
+        const int L = __ffsll((long long)em) - 1;
+        if (lane == L) {
+          const uint64_t key = okey | ((uint64_t)ne << kEpochShift);
+          reinterpret_cast<uint4*>(e)[0] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), w0.z, w0.w);
+          reinterpret_cast<uint4*>(e)[1] = make_uint4(w1.x, w1.y, 0u, 0u);
+          onew[w1.z] = (int32_t)(p.ovf_base + b * kBucket + (uint32_t)L);
+        }
+        __threadfence();
+        break;
+      }
+      b = (b + 1) & p.bucket_mask;
+    }
+  }
+  if (lane == 0) {
+    h.n_blocks = m;
+    h.root_blk = R >= 0 ? 0 : -1;
+    h.epoch = (int32_t)ne;
+    p.hdr[tree] = h;
+  }
+}
+
+// One wave per SEARCH wave: filter that wave's shared particle log to the
+// records of obs nodes that survived k_compact (insertion order kept) and
+// relabel them; every tree's record count is recounted.
+__global__ __launch_bounds__(256) void k_compact_log(DevParams p) {
+  const int sw = blockIdx.x * kTreesPerBlock + (threadIdx.x >> 6);
+  const int wi = threadIdx.x >> 6;
+  const int lane = lane_id();
+  if (sw >= (p.B + kWave - 1) / kWave) return;
+  __shared__ int32_t kept[kTreesPerBlock][kWave];
+  __shared__ int32_t act[kTreesPerBlock][kWave];
+  const int mytree = sw * kWave + lane;
+  kept[wi][lane] = 0;
+  act[wi][lane] = mytree < p.B ? p.cnt[mytree] : 0;
+  __builtin_amdgcn_wave_barrier();
+  LogRec* const wl = p.plog + (int64_t)sw * kWave * p.Np;
+  const uint32_t n = p.wlog[sw];
+  const uint32_t A = (uint32_t)p.A;
+  uint32_t out = 0;
+  for (uint32_t base = 0; base < n; base += kWave) {
+    const uint32_t i = base + (uint32_t)lane;
+    LogRec r = {0u, 0u, 0u};
+    bool keep = false;
+    if (i < n) {
+      r = wl[i];
+      const uint32_t l = r.id >> kIdBits;
+      const uint32_t id = r.id & kIdMask;
+      const int tree = sw * kWave + (int)l;
+      keep = true;
+      if (act[wi][l]) {
+        int32_t nid = -1;
+        if (id >= p.ovf_base) {
+          nid = ld_agent(p.ovf_new + (int64_t)tree * p.H + (id - p.ovf_base));
+        } else if (id >= 1u) {
+          const uint32_t ani = (id - 1u) / kSlots, k = (id - 1u) % kSlots;
+          const int nb = ld_agent(p.cmap + (int64_t)tree * p.Nb + (int)(ani / A));
+          if (nb >= 0) nid = (int32_t)(((uint32_t)nb * A + ani % A) * kSlots + k + 1u);
+        }
+        keep = nid >= 0;
+        r.id = (uint32_t)nid | (l << kIdBits);
+      }
+      if (keep) atomicAdd(&kept[wi][l], 1);
+    }
+    const uint64_t mk = __ballot(keep);
+    __builtin_amdgcn_s_waitcnt(0);   // the whole chunk is loaded before any store
+    if (keep) wl[out + (uint32_t)__popcll(mk & ((1ull << lane) - 1ull))] = r;
+    out += (uint32_t)__popcll(mk);
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (mytree < p.B) p.hdr[mytree].n_log = kept[wi][lane];
+  if (lane == 0) p.wlog[sw] = out;
 }
 
 // Synthetic roots: env b0 sample for tree b under key (env_seed_base + b,

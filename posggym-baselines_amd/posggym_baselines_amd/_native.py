@@ -170,7 +170,9 @@ SIGNATURES = [
     ("pomcp_search", C.c_int, [_CTX, C.c_int32, _P32]),
     ("pomcp_search_continue", C.c_int, [_CTX, C.c_int32]),
     ("pomcp_get_root_stats", C.c_int, [_CTX, C.POINTER(PomcpRootStats)]),
+    ("pomcp_set_root_belief", C.c_int, [_CTX, C.c_int32, _PU32, C.c_int32]),
     ("pomcp_get_root_belief", C.c_int, [_CTX, C.c_int32, _PU32, C.c_int32, _P32]),
+    ("pomcp_arena_usage", C.c_int, [_CTX, _P32, _P32]),
     ("pomcp_rekey", C.c_int, [_CTX, C.c_uint64]),
     ("pomcp_root_merge_buffer", C.c_int, [_CTX, C.POINTER(C.c_void_p)]),
     ("pomcp_merge_roots", C.c_int, [_CTX, C.c_int32, C.POINTER(PomcpMergedRoot)]),

@@ -1,3 +1,5 @@
+"""Environment models the GPU engine implements (Driving-v1, PursuitEvasion-v1)
+and the recognition of a posggym-style ``env.model``."""
 from posggym_baselines_amd.envs.driving import (  # noqa: F401
     GRIDS,
     DrivingModel,
@@ -5,3 +7,48 @@ from posggym_baselines_amd.envs.driving import (  # noqa: F401
     unpack_obs,
 )
 from posggym_baselines_amd.envs.pursuit_evasion import PursuitEvasionModel  # noqa: F401
+
+# posggym registrations the engine restates, with the env kwargs each accepts
+# and their posggym defaults (the reference's experiments: Driving-v1
+# "14x14RoundAbout", PursuitEvasion-v1 "16x16", baseline_exps/exp_utils.py)
+_SUPPORTED = {
+    "Driving-v1": (DrivingModel, {"grid": "14x14RoundAbout", "num_agents": 2,
+                                  "obs_dim": (3, 1, 1)}),
+    "PursuitEvasion-v1": (PursuitEvasionModel, {"grid": "16x16", "max_obs_distance": 12,
+                                                "use_progress_reward": True}),
+}
+# posggym env kwargs that do not change the generative model
+_IGNORED_KWARGS = {"render_mode", "normalize_reward", "max_episode_steps"}
+
+
+def engine_model(model):
+    """The engine-side model for ``model``: the builder's own models as they are;
+    a posggym-style model (``model.spec.id`` + ``model.spec.kwargs``, e.g. the
+    ``env.model`` the reference's planners receive) is mapped to the engine's
+    restatement of that registration.  Anything else raises
+    ``NotImplementedError`` -- the engine has no generic (Python) model path."""
+    if hasattr(model, "configure_engine"):
+        return model
+    spec = getattr(model, "spec", None)
+    env_id = getattr(spec, "id", None)
+    if env_id not in _SUPPORTED:
+        raise NotImplementedError(
+            f"no GPU generative model for {env_id or type(model).__name__}; the engine "
+            f"implements {sorted(_SUPPORTED)}")
+    cls, defaults = _SUPPORTED[env_id]
+    kwargs = dict(getattr(spec, "kwargs", None) or {})
+    for k in _IGNORED_KWARGS:
+        kwargs.pop(k, None)
+    unknown = set(kwargs) - set(defaults)
+    if unknown:
+        raise NotImplementedError(f"{env_id}: unsupported env kwargs {sorted(unknown)}")
+    args = dict(defaults, **kwargs)
+    if "obs_dim" in args:
+        args["obs_dim"] = tuple(args["obs_dim"])
+    if isinstance(args.get("grid"), str) and args["grid"] not in GRIDS and \
+            env_id == "Driving-v1":
+        raise NotImplementedError(f"Driving-v1 grid {args['grid']!r} is not restated")
+    try:
+        return cls(**args)
+    except KeyError as e:
+        raise NotImplementedError(f"{env_id}: grid {e} is not restated") from None

@@ -62,16 +62,46 @@ def plan_capacities(config, step_limit: int, num_sims: int, searches: int = 1,
         log_table_size=total + 2, discount_pow_size=min(levels, 4096) + 2)
 
 
+# Wall-clock mode (num_sims=None, the reference's default, mcts.py:285) sizes
+# the arenas from the time limit: an upper bound on one tree's simulation rate
+# (measured 89-110 k simulations/s for a lone tree on MI355X, DESIGN.md §6;
+# 2.5x margin) times search_time_limit per search.  The arena holds one
+# search plus the subtree kept by the re-root (subtree compaction at update,
+# pomcp_kernels.hip k_compact), and get_action stops launching chunks before
+# a chunk could overflow it (POMCP.get_action), so a time-limited episode never
+# fails with POMCP_E_ARENA.  HBM budget for all trees of one engine:
+WALL_CLOCK_SIMS_PER_S = 250_000
+WALL_CLOCK_HBM_BUDGET = 64 << 30
+
+
+def plan_wallclock_capacities(config, step_limit: int, num_trees: int = 1, num_actions: int = 5):
+    """Capacities of a wall-clock (num_sims=None) engine; returns (capacities,
+    per-search simulation bound)."""
+    levels = min(config.depth_limit, step_limit) + 1
+    per_sim = num_actions * 128 + 16 * min(levels, 64)   # block + particle records, worst case
+    sims = math.ceil(config.search_time_limit * WALL_CLOCK_SIMS_PER_S)
+    sims = min(sims, WALL_CLOCK_HBM_BUDGET // (2 * per_sim * max(1, num_trees)))
+    ovf = 1 << 16
+    nb_id = (ID_LIMIT - 1 - ovf) // (num_actions * 6)
+    sims = max(256, min(sims, nb_id // 2 - 64))
+    caps = plan_capacities(config, step_limit, sims, 2, num_actions=num_actions,
+                           overflow_slots=ovf)
+    # log(N) of a node's visit count: a node at depth d of a search was visited
+    # by at most one search's simulations in each of the d searches before it
+    # became the root (depth <= min(depth_limit, step_limit) + 1)
+    caps.log_table_size = (min(levels, 64) + 1) * sims + 2
+    return caps, sims
+
+
 class PomcpEngine:
     SELECTION = {"pucb": N.SEL_PUCB, "ucb": N.SEL_UCB, "uniform": N.SEL_UNIFORM}
 
     def __init__(self, model, agent_id, config, num_trees=1, capacities=None, num_sims=None,
-                 searches=None, device=None, stream=None, tree_key_base=0, seed=None):
+                 searches=None, device=None, stream=None, tree_key_base=0, seed=None,
+                 wall_clock=False):
         lib = N.load()
-        if not hasattr(model, "configure_engine"):
-            raise NotImplementedError(
-                f"{type(model).__name__} has no GPU generative model; the engine implements "
-                "Driving-v1 and PursuitEvasion-v1 (posggym_baselines_amd.envs)")
+        from posggym_baselines_amd.envs import engine_model
+        model = engine_model(model)   # posggym-style models by spec.id + kwargs
         if config.truncated and not config.use_rollout_if_no_value:
             raise NotImplementedError("truncated search needs a value function (none on GPU)")
         self.model = model
@@ -86,6 +116,10 @@ class PomcpEngine:
         else:
             step_limit = INT32_MAX
         self.step_limit = step_limit
+        self.wall_clock_sims = None
+        if capacities is None and wall_clock:
+            capacities, self.wall_clock_sims = plan_wallclock_capacities(
+                config, step_limit, self.num_trees, model.action_spaces[agent_id].n)
         if capacities is None:
             sims = num_sims if num_sims is not None else (config.num_sims or 4096)
             budget = searches if searches is not None else (
@@ -199,6 +233,13 @@ class PomcpEngine:
             "get_root_belief")
         return buf[:3 * n.value].reshape(-1, 3)
 
+    def set_root_belief(self, tree, rows):
+        """Root belief of a fresh tree from host particles ((t, v0, v1) rows)."""
+        a = np.ascontiguousarray(np.asarray(rows, dtype=np.uint32).reshape(-1, 3))
+        self._check(self._lib.pomcp_set_root_belief(
+            self._ctx, int(tree), a.ctypes.data_as(C.POINTER(C.c_uint32)), len(a)),
+            "set_root_belief")
+
     def rekey(self, seed):
         self._check(self._lib.pomcp_rekey(self._ctx, int(seed) & (2**64 - 1)), "rekey")
 
@@ -206,6 +247,17 @@ class PomcpEngine:
         p = C.c_void_p()
         self._check(self._lib.pomcp_root_merge_buffer(self._ctx, C.byref(p)), "merge_buffer")
         return p.value
+
+    def headroom(self):
+        """Simulations every tree can still run before its block arena or particle
+        log could overflow (worst case: one expansion and min(depth, step) + 1
+        particle records per simulation)."""
+        nb, nl = C.c_int32(), C.c_int32()
+        self._check(self._lib.pomcp_arena_usage(self._ctx, C.byref(nb), C.byref(nl)), "arena_usage")
+        nb, nl = nb.value, nl.value
+        cap = self.capacities
+        levels = min(self.config.depth_limit, self.step_limit) + 1
+        return max(0, min(cap.max_blocks - nb - 1, (cap.max_particles - nl - 1) // min(levels, 64)))
 
     def merge_roots(self, group, fetch=True):
         """Device merge of root-parallel replicas (``pomcp_merge_roots``): trees

@@ -30,6 +30,8 @@ from typing import Optional
 import numpy as np
 import psutil
 
+from posggym_baselines_amd.envs import engine_model
+
 from posggym_baselines_amd import _native as N
 from posggym_baselines_amd.planning.config import MCTSConfig
 from posggym_baselines_amd.planning.search_policy import RandomSearchPolicy
@@ -94,10 +96,7 @@ class IntmcpEngine:
     def __init__(self, model, agent_id, config, num_pairs=1, capacities=None, num_sims=None,
                  searches=None, device=None, stream=None, tree_key_base=0, seed=None):
         lib = N.load()
-        if not hasattr(model, "configure_engine"):
-            raise NotImplementedError(
-                f"{type(model).__name__} has no GPU generative model; the engine implements "
-                "Driving-v1 and PursuitEvasion-v1 (posggym_baselines_amd.envs)")
+        model = engine_model(model)   # posggym-style models by spec.id + kwargs
         if len(model.possible_agents) != 2:
             raise NotImplementedError("the I-NTMCP engine plans for two agents")
         if config.action_selection not in self.SELECTION:
@@ -105,6 +104,7 @@ class IntmcpEngine:
                 "INTMCP pucb_action_selection reads self.action_space, which INTMCP does not "
                 "define (intmcp.py:645); use 'ucb' or 'uniform'")
         self.model = model
+        self._emodel = engine_model(model)
         self.config = config
         self.num_pairs = int(num_pairs)
         self.ego = model.possible_agents.index(agent_id)
@@ -335,6 +335,7 @@ class INTMCP:
             raise NotImplementedError("only RandomSearchPolicy search policies run in-kernel")
         assert agent_id in model.possible_agents
         self.model = model
+        self._emodel = engine_model(model)
         self.agent_id = agent_id
         self.config = config
         self.nesting_level = nesting_level
@@ -422,7 +423,7 @@ class INTMCP:
             return
         start = time.time()
         a = -1 if self.root.t == 0 else int(action)
-        key = self.model.obs_key(obs)
+        key = self._emodel.obs_key(obs)
         absorbing = self._engine.update([a], [key])
         self.root = dataclasses.replace(self.root, t=self.root.t + 1,
                                         is_absorbing=bool(absorbing[0]))

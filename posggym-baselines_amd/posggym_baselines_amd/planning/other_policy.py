@@ -55,3 +55,43 @@ class RandomOtherAgentPolicy(OtherAgentPolicy):
     def get_pi(self, state) -> Dict[int, float]:
         n = self._action_space.n
         return {a: 1.0 / n for a in range(n)}
+
+
+class OtherAgentMixturePolicy(OtherAgentPolicy):
+    """Mixture over posggym.agents policies (``other_policy.py:157-230``): the
+    policy is drawn at ``sample_initial_state`` and kept in the state.  The GPU
+    planners accept random other agents only; this class keeps the surface."""
+
+    def __init__(self, model, agent_id: str, policies: Dict[str, object],
+                 policy_distribution: Optional[Dict[str, float]] = None):
+        super().__init__(model, agent_id)
+        self.policies = policies
+        if policy_distribution is None:
+            policy_distribution = {k: 1.0 / len(policies) for k in policies}
+        self.policy_distribution = policy_distribution
+
+    def sample_initial_state(self):
+        import random
+        pid = random.choices(list(self.policy_distribution),
+                             weights=list(self.policy_distribution.values()), k=1)[0]
+        return {"policy_id": pid, "policy_state": self.policies[pid].get_initial_state()}
+
+    def get_next_state(self, action, obs, state):
+        pid = state["policy_id"]
+        return {"policy_id": pid,
+                "policy_state": self.policies[pid].get_next_state(action, obs,
+                                                                  state["policy_state"])}
+
+    def sample_action(self, state):
+        return self.policies[state["policy_id"]].sample_action(state["policy_state"])
+
+    def get_pi(self, state):
+        return self.policies[state["policy_id"]].get_pi(state["policy_state"])
+
+    def close(self):
+        for p in self.policies.values():
+            p.close()
+
+    @staticmethod
+    def load_posggym_agents_policy(model, agent_id, policy_dist):
+        raise NotImplementedError("posggym.agents policies are not available to the MI355X engine")

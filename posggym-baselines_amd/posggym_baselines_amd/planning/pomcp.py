@@ -34,6 +34,8 @@ from typing import Optional
 import numpy as np
 import psutil
 
+from posggym_baselines_amd.envs import engine_model
+
 from posggym_baselines_amd.planning.config import MCTSConfig
 from posggym_baselines_amd.planning.engine import PomcpEngine
 from posggym_baselines_amd.planning.other_policy import RandomOtherAgentPolicy
@@ -75,6 +77,7 @@ class POMCP:
             # what it means.  Recorded in DESIGN.md.
             config = dataclasses.replace(config, state_belief_only=True)
         self.model = model
+        self._emodel = engine_model(model)
         self.agent_id = agent_id
         self.config = config
         self.search_policy = search_policy
@@ -93,7 +96,8 @@ class POMCP:
             self._rank = dist.get_rank(process_group)
             self._world = dist.get_world_size(process_group)
         self._engine = PomcpEngine(model, agent_id, config, num_trees=self._K,
-                                   num_sims=per or 4096, tree_key_base=self._rank * self._K)
+                                   num_sims=per, tree_key_base=self._rank * self._K,
+                                   wall_clock=per is None)
         self.step_limit = self._engine.step_limit
         self._logger = logging.getLogger()
         self._last_action = None
@@ -154,7 +158,7 @@ class POMCP:
             a = -1
         else:
             a = int(action)
-        key = self.model.obs_key(obs)
+        key = self._emodel.obs_key(obs)
         absorbing = self._engine.update([a], [key])   # broadcast to every replica
         # a replica whose root is absorbing stops searching and merges as zeros;
         # the planner is absorbing once all of them are (oracle/root_parallel.py)
@@ -175,12 +179,21 @@ class POMCP:
             n_sims = self._per_replica * K
         else:
             # the wall-clock loop (mcts.py:285) as launches of growing chunks; the
-            # final action choice is drawn once, after the last one
+            # final action choice is drawn once, after the last one.  A chunk is
+            # never larger than the arena headroom (PomcpEngine.headroom): when
+            # the arena is full the search ends early (step_statistics
+            # "arena_full"), it does not fail.
             n_sims, chunk = 0, 16
+            room = self._engine.headroom()
             while time.time() - start < self.config.search_time_limit:
-                self._engine.search(chunk, final=False)
-                depth = max(depth, self._depth())   # synchronises
-                n_sims += chunk * K
+                n = min(chunk, room)
+                if n <= 0:
+                    self.step_statistics["arena_full"] = True
+                    break
+                self._engine.search(n, final=False)
+                room = self._engine.headroom()    # synchronises
+                depth = max(depth, self._depth())
+                n_sims += n * K
                 chunk = min(chunk * 2, 4096)
             self._engine.search(0, fetch=False)
         A = len(self.action_space)
@@ -215,6 +228,16 @@ class POMCP:
         if self._K == 1:
             return self._engine.root_stats()[0].search_depth
         return self._engine.merge_roots(self._K)[0].search_depth
+
+    def set_root_belief(self, rows):
+        """Search from a caller-supplied belief: after ``reset()``, the root
+        becomes an unexpanded node at time t holding ``rows`` ((t, v0, v1) packed
+        particles, insertion order; ``pomcp_set_root_belief``) in every replica,
+        in place of the initial update's b0 samples (mcts.py:175-227)."""
+        rows = np.asarray(rows, dtype=np.uint32).reshape(-1, 3)
+        for k in range(self._K):
+            self._engine.set_root_belief(k, rows)
+        self.root = RootView(t=int(rows[0, 0]), belief_size=len(rows))
 
     def root_belief(self, replica: int = 0):
         """Root particles as (t, v0, v1) packed u32 rows (of one replica)."""

@@ -67,3 +67,42 @@ class RandomSearchPolicy(SearchPolicy):
 
     def get_value(self, state) -> float:
         raise NotImplementedError("RandomSearchPolicy does not support value estimates.")
+
+
+class SearchPolicyWrapper(SearchPolicy):
+    """A posggym.agents ``Policy`` as a search policy (``search_policy.py:188-224``)."""
+
+    def __init__(self, policy):
+        super().__init__(policy.model, policy.agent_id, policy.policy_id)
+        self.policy = policy
+
+    def get_initial_state(self):
+        return self.policy.get_initial_state()
+
+    def get_next_state(self, action, obs, state):
+        return self.policy.get_next_state(action, obs, state)
+
+    def sample_action(self, state):
+        return self.policy.sample_action(state)
+
+    def get_pi(self, state):
+        return self.policy.get_pi(state)
+
+    def get_value(self, state):
+        return self.policy.get_value(state)
+
+    def close(self):
+        self.policy.close()
+
+
+def load_posggym_agents_search_policy(model, agent_id: str, policy_id: str):
+    """``search_policy.py:226-232``: needs posggym.agents (absent from this build)."""
+    raise NotImplementedError("posggym.agents policies are not available to the MI355X engine")
+
+
+class PPOLSTMSearchPolicy(SearchPolicy):
+    """``search_policy.py:235-290``: a PPO-LSTM network as search policy --
+    neural inference on the search path, out of this build's scope."""
+
+    def __new__(cls, *args, **kwargs):
+        raise NotImplementedError("PPO-LSTM search policies are out of the GPU engine's scope")

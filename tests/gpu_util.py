@@ -81,7 +81,14 @@ def gpu_episode(cfg_kwargs, num_sims, env_seed, ego="0", max_steps=50, env="Driv
     return trace, records
 
 
-def batched_episodes(cfg_kwargs, num_sims, env_seeds, steps):
+def _arena_usage(engine):
+    import ctypes as C
+    nb, nl = C.c_int32(), C.c_int32()
+    assert engine._lib.pomcp_arena_usage(engine._ctx, C.byref(nb), C.byref(nl)) == 0
+    return nb.value, nl.value
+
+
+def batched_episodes(cfg_kwargs, num_sims, env_seeds, steps, capacities=None, usage=None):
     """Lockstep episodes of len(env_seeds) independent planners in ONE engine
     (tree b = planner b, env seed env_seeds[b]), `steps` real steps each.
     Returns per-tree record lists in the oracle format."""
@@ -95,7 +102,7 @@ def batched_episodes(cfg_kwargs, num_sims, env_seeds, steps):
     model = DrivingModel()
     B = len(env_seeds)
     bp = BatchedPOMCP(model, "0", product_config(cfg_kwargs, num_sims), B, num_sims,
-                      searches=steps, reroot=True)
+                      searches=steps, reroot=True, capacities=capacities)
     envs = []
     for s in env_seeds:
         es = Streams(s, ENV_TREE_BASE)
@@ -106,7 +113,11 @@ def batched_episodes(cfg_kwargs, num_sims, env_seeds, steps):
     last = np.full(B, -1, dtype=np.int32)
     for t in range(steps):
         keys = np.array([pack_obs(e[3]["0"]) for e in envs], dtype=np.uint64)
+        if usage is not None:
+            usage.append(("before_update", _arena_usage(bp.engine)))
         bp.engine.update(last, keys)
+        if usage is not None:
+            usage.append(("after_update", _arena_usage(bp.engine)))
         actions = bp.search()
         stats = bp.engine.root_stats()
         for b in range(B):

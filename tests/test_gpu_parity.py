@@ -295,3 +295,136 @@ def test_wall_clock_search_mode():
     assert 0 <= a < 5 and st["num_sims"] >= 16 and st["search_depth"] >= 1
     assert planner.root.visits == st["num_sims"] == sum(planner.root.child_visits)
     planner.close()
+
+
+def test_subtree_compaction_forced_small_arena():
+    """Arenas sized for ~2 searches carry 8-step episodes: every update compacts
+    the tree to the new root's subtree (k_compact / k_compact_log: blocks moved,
+    overflow map rebuilt, particle log filtered and relabelled) and every tree
+    stays bit-exact with the oracle, whose tree is never compacted."""
+    from posggym_baselines_amd.planning.engine import plan_capacities
+    from posggym_baselines_amd.planning import MCTSConfig
+    from gpu_util import batched_episodes
+    S, steps, B = 64, 8, 70
+    cfg = MCTSConfig(num_sims=S, **TEST_CFG)
+    caps = plan_capacities(cfg, 50, S, 2, num_actions=5, overflow_slots=64)
+    # one search plus the kept subtree (the new root and its expanded children,
+    # at most its visits): no room for 8 searches without compaction
+    caps.max_blocks = S + S // 2 + 16
+    levels = cfg.depth_limit + 1
+    caps.max_particles = 2 * S * levels + 2 * (cfg.num_particles + cfg.extra_particles) + 64
+    caps.log_table_size = S * (steps + 1) + 2   # math.log(N): root visits accumulate
+    from oracle.run import oracle_episode
+    usage, seeds, exp = [], [], []
+    s = 7000
+    while len(seeds) < B:   # planners whose episodes last >= steps (searched every step)
+        trace, recs = oracle_episode(TEST_CFG, S, s, tree=len(seeds), max_steps=steps)
+        if trace["len"] >= steps and all(r["searched"] and r["num_sims"] for r in recs):
+            seeds.append(s)
+            exp.append(recs)
+        s += 1
+    got = batched_episodes(TEST_CFG, S, seeds, steps, capacities=caps, usage=usage)
+    for b in range(B):
+        assert got[b] == exp[b], f"tree {b} (env seed {seeds[b]})"
+    before = [u for k, u in usage if k == "before_update"][1:]
+    after = [u for k, u in usage if k == "after_update"][1:]
+    assert all(a[0] < bb[0] and a[1] < bb[1] for a, bb in zip(after, before)), (before, after)
+    assert sum(bb[1] for bb in before) > 2 * caps.max_particles   # several logs' worth in all
+
+
+def test_wall_clock_episode_one_second():
+    """The reference's default mode (num_sims=None, mcts.py:285) over a full
+    Driving-v1 episode at search_time_limit=1.0 (exp_utils.py:27 budgets): the
+    arenas are sized from the time limit, compacted at every update, and the
+    chunk loop never overflows them."""
+    from oracle.episode import run_episode
+    from posggym_baselines_amd.planning import MCTSConfig, POMCP, RandomSearchPolicy
+    from gpu_util import product_model
+    model = product_model("Driving-v1")
+    cfg = MCTSConfig(**dict(TEST_CFG, search_time_limit=1.0))
+    planner = POMCP(model, "0", cfg, RandomSearchPolicy(model, "0"))
+    planner.reset()
+    sims = []
+
+    def step(obs):
+        a = planner.step(obs)
+        if not planner.root.is_absorbing:
+            st = planner.step_statistics
+            assert not st.get("arena_full"), len(sims)
+            assert 0.9 <= st["search_time"] < 3.0
+            sims.append(st["num_sims"])
+        return a
+
+    trace = run_episode(step, 31, max_steps=50)
+    assert trace["len"] >= 3 and min(sims) > 1000
+    planner.close()
+
+
+@pytest.mark.parametrize("time_limit", [1.0, 20.0])
+def test_reinvigoration_many_particles(time_limit):
+    """The rejection reinvigoration (mcts.py:651-700, belief.py:145-194) at the
+    reference's particle counts for 1 s and 20 s budgets (100 + 7 and 2000 + 125
+    particles, config.py:47-48): k_update runs 64 tries per pass (one per lane,
+    ballot-ranked accepts / rejects); beliefs equal the oracle's, insertion order
+    included (belief digests), over 3 real steps."""
+    from gpu_util import batched_episodes
+    from oracle.run import oracle_episode
+    cfg = dict(TEST_CFG, search_time_limit=time_limit)
+    S, K, B = 32, 3, 5
+    seeds, exp = [], []
+    s = 9100
+    while len(seeds) < B:
+        trace, recs = oracle_episode(cfg, S, s, tree=len(seeds), max_steps=K)
+        if trace["len"] >= K and all(r["searched"] for r in recs):
+            seeds.append(s)
+            exp.append(recs)
+        s += 1
+    got = batched_episodes(cfg, S, seeds, K)
+    for b in range(B):
+        assert got[b] == exp[b], f"tree {b} (env seed {seeds[b]})"
+        assert got[b][-1]["belief_size"] >= 100
+
+
+def test_search_from_host_belief():
+    """pomcp_set_root_belief: a fresh planner searches from caller-supplied
+    particles (another planner's b0 particles, insertion order kept) and then
+    re-roots as usual; both steps equal the oracle holding the same belief."""
+    from oracle.envs import make_model
+    from oracle.rng import Streams
+    from posggym_baselines_amd.planning import POMCP, RandomSearchPolicy
+    from gpu_util import product_model
+    donor = make_oracle(TEST_CFG, 8, tree=9)
+    run_episode(lambda obs: (donor.update(None, obs), 0)[1], 55, max_steps=1)
+    parts = list(donor.belief[donor.root])
+    rows = [(t,) + tuple(donor.model.pack_words(st)) for st, t in parts]
+    S = 300
+    model = product_model("Driving-v1")
+    planner = POMCP(model, "0", product_config(TEST_CFG, S), RandomSearchPolicy(model, "0"))
+    planner.reset()
+    planner.set_root_belief(rows)
+    p = make_oracle(TEST_CFG, S, tree=0)
+    node = p._new_obs_node(rows[0][0], 0)
+    p.belief[node] = list(parts)
+    p.root = node
+
+    def both_records(a, b):
+        p.stats["searched"] = True
+        p.stats["belief"] = list(p.belief[p.root])
+        st = planner._engine.root_stats()[0]
+        return (stats_record(st, 5, True, a, planner.root_belief()), oracle_record(p, True, b))
+
+    a = planner.get_action()
+    p.stats = {}
+    b = p.get_action()
+    got, exp = both_records(a, b)
+    assert got == exp
+    # one real step on: an observation from the belief's first particle
+    env = make_model("Driving-v1", Streams(77, 0x40000000))
+    obs = env.step(parts[0][0], {"0": a, "1": 0}).observations["0"]
+    planner.update(a, obs)
+    p.stats = {}
+    p.update(b, obs)
+    a2, b2 = planner.get_action(), p.get_action()
+    got, exp = both_records(a2, b2)
+    assert got == exp
+    planner.close()

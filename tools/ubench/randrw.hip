@@ -15,7 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 
-template <int PARTS, bool WRITE, int MODE>
+template <int PARTS, int WPARTS, int MODE>
 __global__ __launch_bounds__(256) void k_rw(uint4* buf, int lg, int lg_region, int iters, uint32_t* sink) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = gid & 63u, wave = gid >> 6;
@@ -34,10 +34,8 @@ __global__ __launch_bounds__(256) void k_rw(uint4* buf, int lg, int lg_region, i
     for (int q = 0; q < PARTS; ++q) v[q] = p[q];
 #pragma unroll
     for (int q = 0; q < PARTS; ++q) { v[q].x += 1; acc += v[q].y; }
-    if (WRITE) {
 #pragma unroll
-      for (int q = 0; q < PARTS; ++q) p[q] = v[q];
-    }
+    for (int q = 0; q < WPARTS; ++q) p[q] = v[q];   // write back the first WPARTS parts
     x += acc & 1;   // next address depends on the data: one chain per lane
   }
   if (acc == 0x12345678u) sink[0] = acc;
@@ -66,14 +64,21 @@ int main(int argc, char** argv) {
     printf("%-22s %6.2f G acc/s  %6.2f us/access/lane  useful %7.1f GB/s\n", name, acc / ms / 1e6,
            ms * 1e3 / iters, acc * bytes * rw / ms / 1e6);
   };
-  run("global r16", k_rw<1, false, 0>, 16, 1);
-  run("global r128(8x16B)", k_rw<8, false, 0>, 128, 1);
-  run("global rw112(7x16B)", k_rw<7, true, 0>, 112, 2);
-  run("per-lane r16", k_rw<1, false, 1>, 16, 1);
-  run("per-lane r128", k_rw<8, false, 1>, 128, 1);
-  run("per-lane rw112", k_rw<7, true, 1>, 112, 2);
-  run("interleaved r16", k_rw<1, false, 2>, 16, 1);
-  run("interleaved r128", k_rw<8, false, 2>, 128, 1);
-  run("interleaved rw112", k_rw<7, true, 2>, 112, 2);
+  // bytes column: bytes read + written per access (useful bytes)
+  run("global r16", k_rw<1, 0, 0>, 16, 1);
+  run("global r128(8x16B)", k_rw<8, 0, 0>, 128, 1);
+  run("global rw112(7x16B)", k_rw<7, 7, 0>, 112, 2);
+  run("per-lane r16", k_rw<1, 0, 1>, 16, 1);
+  run("per-lane r128", k_rw<8, 0, 1>, 128, 1);
+  run("per-lane rw112", k_rw<7, 7, 1>, 112, 2);
+  run("interleaved r16", k_rw<1, 0, 2>, 16, 1);
+  run("interleaved r128", k_rw<8, 0, 2>, 128, 1);
+  run("interleaved rw112", k_rw<7, 7, 2>, 112, 2);
+  // k_search's own shapes (FETCH_SIZE / WRITE_SIZE calibration, tools/calib_fetch.sh):
+  // the node statistics line (5 x 16 B), the chosen action's line (7 x 16 B),
+  // and a line read then one 16 B part written back (the backup)
+  run("interleaved r80", k_rw<5, 0, 2>, 80, 1);
+  run("interleaved r112", k_rw<7, 0, 2>, 112, 1);
+  run("interleaved r112w16", k_rw<7, 1, 2>, 128, 1);
   return 0;
 }
