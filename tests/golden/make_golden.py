@@ -86,6 +86,11 @@ INTMCP_CASES = {
     "intmcp_uniform": ({"action_selection": "uniform"}, 32, [(3, 3)], "0", 50, "Driving-v1"),
     "intmcp_deep": ({"discount": 0.99, "epsilon": 0.01}, 16, [(4, 4)], "0", 20, "Driving-v1"),
     "intmcp_pe": ({}, 48, [(5, 5)], "0", 100, "PursuitEvasion-v1"),
+},
+                        16, [(2, 2)], "0", 50, "Driving-v1"),
+    "intmcp_depleted_pe": ({"extra_particles_prop": 1.0,
+                            "reinvigoration_sample_limit_factor": 0.45, "action_selection": "uniform"},
+                           16, [(5, 5)], "1", 100, "PursuitEvasion-v1"),
 }
 
 
@@ -137,13 +142,13 @@ def main(only=None):
             json.dump(data, f, separators=(",", ":"))
         n = sum(len(e["records"]) for e in data["episodes"])
         print(f"{name}: {len(data['episodes'])} episodes, {n} records")
-    for name in IPOMCP_CASES:
+    for name in IPOMCP_CASES if only in (None, "ipomcp") else ():
         data = run_case(name, IPOMCP_CASES, "IPOMCP")
         with open(os.path.join(HERE, f"{name}.json"), "w") as f:
             json.dump(data, f, separators=(",", ":"))
         n = sum(len(e["records"]) for e in data["episodes"])
         print(f"{name}: {len(data['episodes'])} episodes, {n} records")
-    for name in INTMCP_CASES if only is None else ():
+    for name in INTMCP_CASES if only is None else (only if isinstance(only, list) else ()):
         data = run_intmcp_case(name)
         with open(os.path.join(HERE, f"{name}.json"), "w") as f:
             json.dump(data, f, separators=(",", ":"))
@@ -156,5 +161,11 @@ def main(only=None):
 
 
 if __name__ == "__main__":
-    # --ipomcp: (re)generate only the IPOMCP fixtures
-    main(only="ipomcp" if "--ipomcp" in sys.argv else None)
+    # --ipomcp: (re)generate only the IPOMCP fixtures; --intmcp NAME...: only
+    # the named I-NTMCP fixtures
+    if "--ipomcp" in sys.argv:
+        main(only="ipomcp")
+    elif "--intmcp" in sys.argv:
+        main(only=sys.argv[sys.argv.index("--intmcp") + 1:])
+    else:
+        main()

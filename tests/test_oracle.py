@@ -88,3 +88,40 @@ def test_intmcp_oracle_matches_reference_goldens(case):
         for t, (got, exp) in enumerate(zip(records, ep["records"])):
             assert got == exp, f"{case} step {t}"
         assert len(records) == len(ep["records"])
+
+
+def test_intmcp_depleted_branch_unreachable_for_valid_configs():
+    """intmcp.py:421-431 reinvigorates a depleted belief at search time (root
+    below extra_particles, or an empty level-0 node).  With the reference's own
+    BeliefRejectionSampler (belief.py:85 asserts sample_limit_factor >= 1, and
+    use_rejected_samples=True fills up with rejected samples) every update leaves
+    the level-1 root with num_particles + extra_particles >= extra_particles and
+    every non-absorbing level-0 support node with ceil(p * target) >= 1
+    particles, and an absorbing node always holds the particle of the visit
+    that marked it -- so the branch cannot fire (the GPU engine
+    reports POMCP_E_UNSUPPORTED if it ever did).  Checked here on the extreme
+    valid settings (every particle an extra one, the minimum try budget)."""
+    import math
+    import oracle.intmcp as OI
+    from oracle.run import oracle_intmcp_episode
+    hits = []
+    orig = OI._Planner._nested_sim
+
+    def spy(self, n, search_level, top_level):
+        size = len(self.tree.belief[n])
+        if size == 0 or (top_level and size < self.cfg.extra_particles):
+            hits.append((self.level, size))
+        return orig(self, n, search_level, top_level)
+
+    OI._Planner._nested_sim = spy
+    try:
+        cfg = dict(discount=0.95, search_time_limit=0.2, c=math.sqrt(2), truncated=False,
+                   action_selection="ucb", pucb_exploration_fraction=0.25, known_bounds=None,
+                   step_limit=None, epsilon=0.92, seed=2, state_belief_only=False,
+                   extra_particles_prop=1.0, reinvigoration_sample_limit_factor=1.0)
+        oracle_intmcp_episode(cfg, 16, 2, ego="0", max_steps=50)
+        oracle_intmcp_episode(dict(cfg, action_selection="uniform", seed=5), 16, 5, ego="1",
+                              max_steps=40, env="PursuitEvasion-v1")
+    finally:
+        OI._Planner._nested_sim = orig
+    assert hits == []
