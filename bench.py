@@ -191,7 +191,8 @@ def main_intmcp(args):
     if world > 1:
         raise SystemExit("--planner intmcp is a single-GPU configuration (BASELINE config 5)")
     from posggym_baselines_amd import build as nb
-    nb.build()
+    if not os.environ.get("POMCP_LIB_PATH"):   # a prebuilt variant library is used as it is
+        nb.build()
     from posggym_baselines_amd.envs import DrivingModel, PursuitEvasionModel
     from posggym_baselines_amd.planning import BatchedINTMCP, MCTSConfig
     from posggym_baselines_amd.planning.intmcp import plan_intmcp_capacities
@@ -327,7 +328,7 @@ def main():
     dev = torch.cuda.current_device()
 
     from posggym_baselines_amd import build as nb
-    if rank == 0:
+    if rank == 0 and not os.environ.get("POMCP_LIB_PATH"):   # prebuilt variants as they are
         nb.build()
     if world > 1:
         dist.barrier()

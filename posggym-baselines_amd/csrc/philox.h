@@ -28,9 +28,14 @@ enum Stream : uint32_t {
   S_ENV_POLICY_BASE = 40,
 };
 
+// PB_PHILOX_ROUNDS: ablation builds only (tools/ablate.sh measures the RNG's
+// share of k_search); any other value breaks parity.
+#ifndef PB_PHILOX_ROUNDS
+#define PB_PHILOX_ROUNDS 10
+#endif
 PB_HD void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
+  for (int r = 0; r < PB_PHILOX_ROUNDS; ++r) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
     const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;

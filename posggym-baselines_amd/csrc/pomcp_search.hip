@@ -226,9 +226,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
 #pragma unroll
         for (int q = 0; q < A; ++q) {
           const double v = hilo_d(st[q].z, st[q].w);
+#ifdef POMCP_ABLATE_SELECT   // ablation build only (tools/ablate.sh): no FP64 div / sqrt, breaks parity
+          sc[q] = v + p.c * log_n * (double)(int)st[q].x;
+#else
           const double nvq = nz ? (v - mm_min) / range : v;
           const int n = (int)st[q].x > 0 ? (int)st[q].x : 1;
           sc[q] = nvq + p.c * sqrt(log_n / (double)n);
+#endif
         }
       } else {                             // PUCB, mcts.py:502-527
         const double noise = 1.0 / (double)A;
@@ -274,6 +278,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   uint32_t r0_a = 0, r0_vis = 0;
   double r0_r = 0.0, r0_val = 0.0;
   uint4 r0_s1 = make_uint4(0, 0, 0, 0);
+  // the root's {total, agg} per action: in registers for the whole launch
+  // (only the backup reads or writes them), written back at the end -- a root
+  // level then touches no HBM line at all
+  uint4 r1[kMaxA];
+#pragma unroll
+  for (int q = 0; q < kMaxA; ++q) r1[q] = make_uint4(0, 0, 0, 0);
   PathEntry rpath[kRegPath];     // levels 1..kRegPath
   uint4 pre[kMaxA];              // statistics line of the next LEVEL pass's node
 #pragma unroll
@@ -306,6 +316,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
 #pragma unroll
           for (int q = 0; q < kSlots; ++q) rc[rc_slot(a, q)][lid] = rb[part_slot(a, q)];
         }
+        r1[a] = rb[part_stats1(a)];
       }
     }
     pf = rbel[d_belief((uint32_t)bsize)];   // the first simulation's particle
@@ -455,7 +466,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
 #pragma unroll
           for (int q = 0; q < kSlots; ++q)
             sl[q] = kRootSlotsInLds ? rc[rc_slot(a, q)][lid] : rb[part_slot(a, q)];
-          r0_s1 = rb[part_stats1(a)];   // no wait: consumed by the backup
+          r0_s1 = r1[0];
+#pragma unroll
+          for (int q = 1; q < kMaxA; ++q)
+            if (q == a) r0_s1 = r1[q];
           uint32_t n0, n1;
           double r;
           int done;
@@ -672,9 +686,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         const double agg = hilo_d(r0_s1.z, r0_s1.w) + delta * (gr - value);
         rc[rc_stats(a)][lid] = make_uint4((uint32_t)n, 0u, (uint32_t)__double2loint(value),
                                           (uint32_t)__double2hiint(value));
-        const_cast<uint4*>(rb)[part_stats1(a)] = make_uint4(
-            (uint32_t)__double2loint(total), (uint32_t)__double2hiint(total),
-            (uint32_t)__double2loint(agg), (uint32_t)__double2hiint(agg));
+        const uint4 s1n = make_uint4((uint32_t)__double2loint(total), (uint32_t)__double2hiint(total),
+                                     (uint32_t)__double2loint(agg), (uint32_t)__double2hiint(agg));
+#pragma unroll
+        for (int q = 0; q < kMaxA; ++q)
+          if (q == a) r1[q] = s1n;
         if (value > mm_max) mm_max = value;
         if (value < mm_min) mm_min = value;
       }
@@ -704,6 +720,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
     for (int a = 0; a < kMaxA; ++a) {
       if (a < A) {
         const_cast<uint4*>(rb)[a] = rc[rc_stats(a)][lid];
+        const_cast<uint4*>(rb)[part_stats1(a)] = r1[a];
         if (kRootSlotsInLds) {
 #pragma unroll
           for (int q = 0; q < kSlots; ++q) const_cast<uint4*>(rb)[part_slot(a, q)] = rc[rc_slot(a, q)][lid];
@@ -720,7 +737,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
     if (have && a < A) {
       st[a] = cached ? rc[rc_stats(a)][lid]
                      : reinterpret_cast<const uint4*>(an + (int64_t)root_blk * blk_bytes)[a];
-      s1s[a] = reinterpret_cast<const uint4*>(an + (int64_t)root_blk * blk_bytes)[part_stats1(a)];
+      s1s[a] = cached ? r1[a]
+                      : reinterpret_cast<const uint4*>(an + (int64_t)root_blk * blk_bytes)[part_stats1(a)];
     }
   }
   // _final_action_selection (mcts.py:565-600) ends get_action; a search split

@@ -1,0 +1,32 @@
+#!/bin/bash
+# Ablation builds of k_search (measurement only; results are NOT the reference's):
+# how much of a search the Philox RNG and the FP64 UCB scoring cost.
+#   tools/ablate.sh build      (here: hipcc the variants into variants/)
+#   tools/ablate.sh run TAG    (GPU box, via gpurun)
+set -o pipefail
+if [ "$1" = build ]; then
+  mkdir -p variants
+  for v in "base:" "philox3:-DPB_PHILOX_ROUNDS=3" "nosel:-DPOMCP_ABLATE_SELECT" \
+           "both:-DPB_PHILOX_ROUNDS=3 -DPOMCP_ABLATE_SELECT"; do
+    n=${v%%:*}; f=${v#*:}
+    POMCP_LIB_PATH=$PWD/variants/lib_$n.so POMCP_EXTRA_FLAGS="$f" \
+      python -c "import sys; sys.path.insert(0,'posggym-baselines_amd'); from posggym_baselines_amd import build; build.build(force=True)" || exit 1
+  done
+  exit 0
+fi
+O=gpurun_out/ablate_$2
+mkdir -p $O
+for n in base philox3 nosel both base; do
+  echo "== $n" >> $O/exp.log
+  POMCP_LIB_PATH=$PWD/variants/lib_$n.so timeout -k 10 300 python bench.py --no-cpu-baseline --steps 2 --warmup 1 >> $O/exp.log 2>&1 || exit 1
+done
+python3 - $O/exp.log <<'PY'
+import json, sys
+name = None
+for line in open(sys.argv[1]):
+    if line.startswith("=="):
+        name = line.split()[1]
+    elif line.startswith("{"):
+        d = json.loads(line)
+        print(f"{name:8s} {d['value']/1e9:6.3f} G sims/s  kernel {d['roofline']['kernel_ms']:8.1f} ms")
+PY
