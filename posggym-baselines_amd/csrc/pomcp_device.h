@@ -60,6 +60,29 @@ struct LogRec {
   uint32_t v0, v1;
 };
 
+// A search wave's particle log in memory: structure of arrays, ids[cap] then
+// v0[cap] then v1[cap] (cap = 64 Np records), so an append of the wave's
+// records is three fully coalesced dword stores instead of one 12 B-strided
+// store (+1% measured; the log's cost is its bytes: without any log store
+// the search runs 12% faster, tools/ablate.sh).
+struct WaveLog {
+  uint32_t* id;
+  uint32_t* v0;
+  uint32_t* v1;
+  __device__ __forceinline__ WaveLog(LogRec* plog, int64_t Np, int64_t wave) {
+    const int64_t cap = (int64_t)64 * Np;
+    id = reinterpret_cast<uint32_t*>(plog) + wave * 3 * cap;
+    v0 = id + cap;
+    v1 = v0 + cap;
+  }
+  __device__ __forceinline__ LogRec load(int64_t i) const { return LogRec{id[i], v0[i], v1[i]}; }
+  __device__ __forceinline__ void store(int64_t i, const LogRec& r) const {
+    id[i] = r.id;
+    v0[i] = r.v0;
+    v1[i] = r.v1;
+  }
+};
+
 struct alignas(16) Line {   // allocation unit of the block arena
   uint4 part[kLine];
 };

@@ -400,12 +400,12 @@ __global__ __launch_bounds__(256) void k_extract(DevParams p) {
   tval[wi][lane] = (uint32_t)h.root_t + 1u;
   dst[wi][lane] = ((int64_t)tree * 2 + (h.belief_sel ^ 1)) * p.Nr;
   __builtin_amdgcn_wave_barrier();
-  const LogRec* const wl = p.plog + (int64_t)sw * kWave * p.Np;
+  const WaveLog wl(p.plog, p.Np, sw);
   const uint32_t n = p.wlog[sw];
   for (uint32_t base = 0; base < n; base += kWave) {
     const uint32_t i = base + (uint32_t)lane;
     LogRec r = {0xFFFFFFFFu, 0u, 0u};
-    if (i < n) r = wl[i];
+    if (i < n) r = wl.load(i);
     const uint32_t l = r.id >> kIdBits;
     const bool m = i < n && want[wi][l] == r.id;
     uint64_t mask = __ballot(m);
@@ -776,7 +776,7 @@ __global__ __launch_bounds__(256) void k_compact_log(DevParams p) {
   kept[wi][lane] = 0;
   act[wi][lane] = mytree < p.B ? p.cnt[mytree] : 0;
   __builtin_amdgcn_wave_barrier();
-  LogRec* const wl = p.plog + (int64_t)sw * kWave * p.Np;
+  const WaveLog wl(p.plog, p.Np, sw);
   const uint32_t n = p.wlog[sw];
   const uint32_t A = (uint32_t)p.A;
   uint32_t out = 0;
@@ -785,7 +785,7 @@ __global__ __launch_bounds__(256) void k_compact_log(DevParams p) {
     LogRec r = {0u, 0u, 0u};
     bool keep = false;
     if (i < n) {
-      r = wl[i];
+      r = wl.load(i);
       const uint32_t l = r.id >> kIdBits;
       const uint32_t id = r.id & kIdMask;
       const int tree = sw * kWave + (int)l;
@@ -806,7 +806,7 @@ __global__ __launch_bounds__(256) void k_compact_log(DevParams p) {
     }
     const uint64_t mk = __ballot(keep);
     __builtin_amdgcn_s_waitcnt(0);   // the whole chunk is loaded before any store
-    if (keep) wl[out + (uint32_t)__popcll(mk & ((1ull << lane) - 1ull))] = r;
+    if (keep) wl.store(out + (uint32_t)__popcll(mk & ((1ull << lane) - 1ull)), r);
     out += (uint32_t)__popcll(mk);
   }
   __builtin_amdgcn_wave_barrier();

@@ -106,7 +106,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   const int64_t blk_bytes = blk_stride_lines(A) * 128;   // block b at an + b * blk_bytes
   // the wave's shared particle log (pomcp_device.h LogRec); wpos is the same in
   // every lane still in the loop (advanced by ballot at convergent points)
-  LogRec* const wl = p.plog + (int64_t)wave * kWave * p.Np;
+  const WaveLog wl(p.plog, p.Np, wave);
   const uint32_t wpos0 = p.wlog[wave];
   uint32_t wpos = wpos0;
   bool app = false;          // this lane has a record to append
@@ -114,7 +114,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   auto append = [&]() {      // call where every lane still in the loop is active
     const uint64_t m = __ballot(app);
     if (m != 0ull) {
-      if (app) wl[wpos + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = rec;
+#ifndef POMCP_ABLATE_LOG   // ablation build only: no particle-log stores
+      if (app) wl.store(wpos + (uint32_t)__popcll(m & ((1ull << lane) - 1ull)), rec);
+#endif
       wpos += (uint32_t)__popcll(m);
       app = false;
     }
@@ -439,7 +441,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
       {
         const uint4 pr = pf;                                     // belief.py:55
         if (sims + 1 < num_sims) {
+#ifdef POMCP_ABLATE_BELIEF   // ablation build only (tools/ablate.sh): no belief line per simulation
+          pf.w += uniform_int(w_bel, (uint32_t)bsize) & 1u;
+#else
           pf = rbel[uniform_int(w_bel, (uint32_t)bsize)];
+#endif
           pend_b = 0;
         }
         t = (int)pr.x;
