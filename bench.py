@@ -288,7 +288,7 @@ def main_intmcp(args):
                    "pairs": B, "sims_per_level": S, "pairs_searched": searched,
                    "arena_per_pair": {"max_nodes": caps.max_nodes, "max_stats": caps.max_stats,
                                       "max_log": caps.max_log, "hash_slots": caps.hash_slots,
-                                      "bytes": caps.bytes_per_pair(),
+                                      "bytes": caps.bytes_per_pair(A),
                                       "nodes_used": max(max(s.n_nodes[0], s.n_nodes[1])
                                                         for s in st)}},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -25,6 +25,8 @@
 namespace pb {
 
 constexpr int kImPath = 128;          // tree levels per simulation
+constexpr int kImMaxA = 6;            // registration order: 6 x 3 bits (INode.info)
+constexpr int kImRegPath = 4;         // path levels held in registers (deeper ones in p.path)
 constexpr uint32_t kImNoSupport = 0xFFFFFFFFu;
 constexpr int32_t kImSkip = -2;       // intmcp_update action: leave the pair untouched
 
@@ -70,14 +72,14 @@ struct ImParams {
   int64_t Nn, Ns, Nl, H, Nr, Nsp;   // per tree: nodes, stat entries, log records, hash slots;
                                     // per pair: root belief, support particles
   IHdr* hdr;
-  INode* nodes;         // [B][2][Nn]
-  IStat* stats;         // [B][2][Ns]
+  char* nodes;          // [B][2][Nn] node blocks: the INode, then its A IStat (nstride B)
+  int64_t nstride;      // 32 * (1 + A)
   IHash* hash;          // [B][2][H]
   IRec* log;            // [B][2][Nl]
   uint4* root;          // [B][2][Nr] {v0, v1, nested, support slot}
   ISup* sup;            // [B][2][Nr]
   uint2* supp;          // [B][2][Nsp]
-  int4* path;           // [B][kImPath][2] path of the running simulation
+  int4* path;           // [B][kImPath][3] path of the running simulation (deep levels)
   double* prob;         // [B][Nr] support probabilities (update scratch)
   const double* logtab;
   int64_t logtab_n;
@@ -103,8 +105,7 @@ struct ImPair {
   const ImParams& p;
   const Model& m;
   int pair;
-  INode* nd[2];
-  IStat* st[2];
+  char* nb[2];     // node blocks of the level-1 (0) and level-0 (1) trees
   IHash* hs[2];
   IRec* lg[2];
   uint4* rootb;   // [2][Nr]
@@ -116,19 +117,42 @@ struct ImPair {
 
   __device__ ImPair(const ImParams& pp, const Model& mm, int b) : p(pp), m(mm), pair(b) {
     for (int k = 0; k < 2; ++k) {
-      nd[k] = p.nodes + ((int64_t)b * 2 + k) * p.Nn;
-      st[k] = p.stats + ((int64_t)b * 2 + k) * p.Ns;
+      nb[k] = p.nodes + ((int64_t)b * 2 + k) * p.Nn * p.nstride;
       hs[k] = p.hash + ((int64_t)b * 2 + k) * p.H;
       lg[k] = p.log + ((int64_t)b * 2 + k) * p.Nl;
     }
     rootb = p.root + (int64_t)b * 2 * p.Nr;
     sup = p.sup + (int64_t)b * 2 * p.Nr;
     supp = p.supp + (int64_t)b * 2 * p.Nsp;
-    path = p.path + (int64_t)b * kImPath * 2;
+    path = p.path + (int64_t)b * kImPath * 3;
     prob = p.prob + (int64_t)b * p.Nr;
     h = p.hdr[b];
   }
   __device__ void store() { p.hdr[pair] = h; }
+
+  // A node's block: the INode and, right after it, the statistics of its A
+  // actions (node.py:120-178), so a node and its statistics arrive in one
+  // round trip (they used to be an index apart: two dependent loads).
+  __device__ __forceinline__ INode& N(int k, int n) const {
+    return *reinterpret_cast<INode*>(nb[k] + (int64_t)n * p.nstride);
+  }
+  __device__ __forceinline__ IStat* S(int k, int n) const {
+    return reinterpret_cast<IStat*>(nb[k] + (int64_t)n * p.nstride + 32);
+  }
+  // the node and the {visits, -, value} head of every action's statistics,
+  // issued together (entries of unregistered actions are never used)
+  struct View {
+    INode x;
+    uint4 sh[kImMaxA];
+  };
+  __device__ __forceinline__ View view(int k, int n) const {
+    View v;
+    v.x = N(k, n);
+    const uint4* s = reinterpret_cast<const uint4*>(S(k, n));
+#pragma unroll
+    for (int q = 0; q < kImMaxA; ++q) v.sh[q] = q < p.A ? s[2 * q] : make_uint4(0, 0, 0, 0);
+    return v;
+  }
   __device__ void fail(int code) {
     if (h.err == 0) h.err = code;
   }
@@ -181,11 +205,11 @@ struct ImPair {
         x.parent = n;
         x.info = (uint32_t)a;
         x.visits = 0;
-        x.t = nd[k][n].t + 1;
+        x.t = N(k, n).t + 1;
         x.stats = -1;
         x.support = kImNoSupport;
         x.okey = okey;
-        nd[k][c] = x;
+        N(k, c) = x;
         IHash ne;
         ne.okey = okey;
         ne.na = na;
@@ -200,7 +224,7 @@ struct ImPair {
   }
   // ObsNode.add_child(a) (node.py:68-80) if not a child yet
   __device__ void reg(int k, int n, int a) {
-    INode& x = nd[k][n];
+    INode& x = N(k, n);
     const int nr = im_nreg(x.info);
     for (int i = 0; i < nr; ++i)
       if (im_order(x.info, i) == a) return;
@@ -223,15 +247,15 @@ struct ImPair {
         z.value = 0.0;
         z.total = 0.0;
         z.agg = 0.0;
-        st[k][x.stats + q] = z;
+        S(k, n)[q] = z;
       }
     }
   }
   __device__ void traverse(int k, int n) {   // intmcp.py:797-809
-    while (n > 0 && !im_path_ok(nd[k][n].info)) {
-      const int par = nd[k][n].parent;
-      reg(k, par, (int)im_paction(nd[k][n].info));
-      nd[k][n].info |= 1u << 4;
+    while (n > 0 && !im_path_ok(N(k, n).info)) {
+      const int par = N(k, n).parent;
+      reg(k, par, (int)im_paction(N(k, n).info));
+      N(k, n).info |= 1u << 4;
       n = par;
     }
   }
@@ -258,20 +282,26 @@ struct ImPair {
   // the agent of tree k: k = 0 the ego, k = 1 the other agent
   __device__ int agent(int k) const { return k == 0 ? p.ego : p.other; }
 
-  // {visits, -, value} of the registered children of node x, all loads issued
-  // before any is used (one memory round trip instead of one per child)
-  __device__ void child_stats(int k, const INode& x, int nr, uint4 (&q)[6]) const {
+  // {visits, -, value} of the registered children of node x, in registration
+  // order, from the node's view
+  __device__ void child_stats(const View& v, int nr, uint4 (&q)[kImMaxA]) const {
 #pragma unroll
-    for (int i = 0; i < 6; ++i)
-      q[i] = i < nr ? *reinterpret_cast<const uint4*>(&st[k][x.stats + im_order(x.info, i)])
-                    : make_uint4(0, 0, 0, 0);
+    for (int i = 0; i < kImMaxA; ++i) {
+      const int a = im_order(v.x.info, i);
+      uint4 r = v.sh[0];
+#pragma unroll
+      for (int j = 1; j < kImMaxA; ++j)
+        if (j == a) r = v.sh[j];
+      q[i] = i < nr ? r : make_uint4(0, 0, 0, 0);
+    }
   }
 
-  __device__ int select(int k, const INode& x) {   // intmcp.py:670-701
+  __device__ int select(int k, const View& v) {   // intmcp.py:670-701
+    const INode& x = v.x;
     if (x.visits == 0) return (int)d_sel((uint32_t)p.A);
     const int nr = im_nreg(x.info);
-    uint4 q[6];
-    child_stats(k, x, nr, q);
+    uint4 q[kImMaxA];
+    child_stats(v, nr, q);
     if (p.sel == POMCP_SEL_UCB) {
       const double log_n = logn(x.visits);
       double best = -__builtin_inf();
@@ -302,21 +332,25 @@ struct ImPair {
 
   // INTMCP.sample_action of the level-0 planner (intmcp.py:763-791) at node n
   __device__ int sample_action(int n) {
-    traverse(1, n);
-    const INode x = nd[1][n];
+    View v = view(1, n);   // node + statistics: one round trip
+    if (n > 0 && !im_path_ok(v.x.info)) {
+      traverse(1, n);
+      v = view(1, n);
+    }
+    const INode& x = v.x;
     const int nr = im_nreg(x.info);
     if (x.visits == 0 || nr == 0) return (int)d_act(p.other, (uint32_t)p.A);
     const double sq = sqrt((double)x.visits);
-    uint4 q[6];
-    child_stats(1, x, nr, q);
-    double pr[6];
+    uint4 q[kImMaxA];
+    child_stats(v, nr, q);
+    double pr[kImMaxA];
     double total = 0.0;
     for (int i = 0; i < nr; ++i) {
       pr[i] = host_exp((double)(int)q[i].x / sq);   // == math.exp (host_exp.h)
       total = i == 0 ? pr[i] : total + pr[i];
     }
     // random.choices(children, weights=p / sum): cum weights, x = random() * total
-    double cum[6];
+    double cum[kImMaxA];
     double acc = 0.0;
     for (int i = 0; i < nr; ++i) {
       const double w = pr[i] / total;
@@ -398,20 +432,31 @@ struct ImPair {
 
   // ----------------------------------------------------------- simulate
   // INTMCP._simulate (intmcp.py:444-517) from node n of tree k; returns the
-  // search depth.
+  // search depth.  Each level loads the child's whole block (node +
+  // statistics) once: it updates the child's visits / flags and is the next
+  // level's view.  The path keeps each level's statistics as they were before
+  // (visits, value, total, agg), so the backup writes without reading; the
+  // first kImRegPath levels stay in registers.
   __device__ int simulate(int k, uint32_t s0, uint32_t s1, uint32_t nested, int n) {
     int depth = 0, plen = 0;
     double leaf = 0.0;
-    const int me = agent(k);
+    uint4 rp[kImRegPath][3];   // {n, a, done, -}, {r, value0}, {total0, agg0} | visits0 in [0].w
+    View v = view(k, n);
     for (;;) {
-      const INode x = nd[k][n];
+      const INode& x = v.x;
       if (depth > p.depth_limit || x.t + depth > p.step_limit) break;
       if (im_nreg(x.info) < p.A) {                 // leaf: add the missing children
         expand(k, n);
         leaf = rollout(k, s0, s1, x.t, depth);
         break;
       }
-      const int a = select(k, x);
+      const int a = select(k, v);
+      // the chosen action's {total, agg}: needed by the backup only (no wait)
+      const uint4 s2 = reinterpret_cast<const uint4*>(S(k, n))[2 * a + 1];
+      uint4 sa = v.sh[0];
+#pragma unroll
+      for (int q = 1; q < kImMaxA; ++q)
+        if (q == a) sa = v.sh[q];
       const int ao = other_action(k, nested);
       uint32_t n0, n1, nn;
       double r;
@@ -419,46 +464,73 @@ struct ImPair {
       uint64_t okey;
       step(k, s0, s1, nested, a, ao, &n0, &n1, &r, &done, &okey, &nn);
       int c = find(k, n, a, okey);
-      if (c >= 0) {
-        nd[k][c].visits += 1;
-      } else {
+      const bool created = c < 0;
+      if (created) {
         c = child(k, n, a, okey);
         if (c < 0) return depth;
-        nd[k][c].visits = 1;
       }
-      uint32_t info = nd[k][c].info;
+      View cv = view(k, c);
+      cv.x.visits = created ? 1 : cv.x.visits + 1;
+      uint32_t info = cv.x.info;
       if (im_path_ok(x.info)) info |= 1u << 4;   // x: node n, unchanged since loaded
       info = done ? (info | 8u) : (info & ~8u);
-      nd[k][c].info = info;
+      cv.x.info = info;
+      *reinterpret_cast<int4*>(&N(k, c)) =          // {parent, info, visits, t}
+          make_int4(cv.x.parent, (int)cv.x.info, cv.x.visits, cv.x.t);
       log_add(k, c, n0, n1, nn);
       if (plen >= kImPath) {
         fail(POMCP_E_ARENA);
         return depth;
       }
-      path[plen * 2] = make_int4(n, a, done, x.stats);   // the backup needs no node load
-      path[plen * 2 + 1] = make_int4(__double2loint(r), __double2hiint(r), 0, 0);
+      const uint4 e0 = make_uint4((uint32_t)n, (uint32_t)a, (uint32_t)done, sa.x);
+      const uint4 e1 = make_uint4((uint32_t)__double2loint(r), (uint32_t)__double2hiint(r), sa.z, sa.w);
+      if (plen < kImRegPath) {
+#pragma unroll
+        for (int l = 0; l < kImRegPath; ++l)
+          if (l == plen) {
+            rp[l][0] = e0;
+            rp[l][1] = e1;
+            rp[l][2] = s2;
+          }
+      } else {
+        path[plen * 3] = make_int4((int)e0.x, (int)e0.y, (int)e0.z, (int)e0.w);
+        path[plen * 3 + 1] = make_int4((int)e1.x, (int)e1.y, (int)e1.z, (int)e1.w);
+        path[plen * 3 + 2] = make_int4((int)s2.x, (int)s2.y, (int)s2.z, (int)s2.w);
+      }
       ++plen;
-      (void)me;
       if (done) break;
       n = c;
+      v = cv;
       s0 = n0;
       s1 = n1;
       nested = nn;
       ++depth;
     }
     double g = leaf;
-    for (int l = plen - 1; l >= 0; --l) {            // backup, node.py:166-178
-      const int4 e = path[l * 2], f = path[l * 2 + 1];
-      const double r = __hiloint2double(f.y, f.x);
-      g = e.z ? r : r + p.discount * g;
-      IStat& s = st[k][e.w + e.y];
-      s.visits += 1;
-      s.total += g;
-      const double delta = g - s.value;
-      s.value += delta / (double)s.visits;
-      s.agg += delta * (g - s.value);
-      mm_update(k, s.value);
+    auto backup = [&](uint4 e0, uint4 e1, uint4 e2) {   // node.py:166-178
+      const double r = hilo_d(e1.x, e1.y);
+      g = e0.z ? r : r + p.discount * g;
+      const int vis = (int)e0.w + 1;
+      const double value0 = hilo_d(e1.z, e1.w);
+      const double total = hilo_d(e2.x, e2.y) + g;
+      const double delta = g - value0;
+      const double value = value0 + delta / (double)vis;
+      const double agg = hilo_d(e2.z, e2.w) + delta * (g - value);
+      uint4* sp = reinterpret_cast<uint4*>(S(k, (int)e0.x) + e0.y);
+      sp[0] = make_uint4((uint32_t)vis, 0u, (uint32_t)__double2loint(value),
+                         (uint32_t)__double2hiint(value));
+      sp[1] = make_uint4((uint32_t)__double2loint(total), (uint32_t)__double2hiint(total),
+                         (uint32_t)__double2loint(agg), (uint32_t)__double2hiint(agg));
+      mm_update(k, value);
+    };
+    for (int l = plen - 1; l >= kImRegPath; --l) {
+      const int4 a0 = path[l * 3], a1 = path[l * 3 + 1], a2 = path[l * 3 + 2];
+      backup(make_uint4(a0.x, a0.y, a0.z, a0.w), make_uint4(a1.x, a1.y, a1.z, a1.w),
+             make_uint4(a2.x, a2.y, a2.z, a2.w));
     }
+#pragma unroll
+    for (int l = kImRegPath - 1; l >= 0; --l)
+      if (l < plen) backup(rp[l][0], rp[l][1], rp[l][2]);
     return depth;
   }
 
@@ -523,7 +595,7 @@ struct ImPair {
     ISup& e = sup_tab(sel)[si];
     const int to_add = target - e.size;
     if (to_add <= 0) return;
-    const int par = nd[1][n].parent;
+    const int par = N(1, n).parent;
     const int pi = find_support(sel ^ 1, par, h.pad);   // previous support count in pad
     if (pi < 0) {
       fail(POMCP_E_UNSUPPORTED);   // parent belief not materialised
@@ -600,10 +672,10 @@ __device__ void im_support(ImPair<Env>& P, int sel, int size, int* nsup) {
 template <class Env>
 __device__ void im_extract_support(ImPair<Env>& P, int sel, int nsup) {
   ISup* tab = P.sup_tab(sel);
-  for (int q = 0; q < nsup; ++q) P.nd[1][tab[q].node].support = (uint32_t)q;
+  for (int q = 0; q < nsup; ++q) P.N(1, tab[q].node).support = (uint32_t)q;
   for (int q = 0; q < nsup; ++q) tab[q].cap = 0;
   for (int i = 0; i < P.h.n_log[1]; ++i) {
-    const uint32_t s = P.nd[1][P.lg[1][i].node].support;
+    const uint32_t s = P.N(1, P.lg[1][i].node).support;
     if (s != kImNoSupport) tab[s].cap += 1;
   }
   int off = 0;
@@ -615,16 +687,16 @@ __device__ void im_extract_support(ImPair<Env>& P, int sel, int nsup) {
   }
   if (off > P.p.Nsp) {
     P.fail(POMCP_E_ARENA);
-    for (int q = 0; q < nsup; ++q) P.nd[1][tab[q].node].support = kImNoSupport;
+    for (int q = 0; q < nsup; ++q) P.N(1, tab[q].node).support = kImNoSupport;
     return;
   }
   uint2* parts = P.sup_parts(sel);
   for (int i = 0; i < P.h.n_log[1]; ++i) {
     const IRec r = P.lg[1][i];
-    const uint32_t s = P.nd[1][r.node].support;
+    const uint32_t s = P.N(1, r.node).support;
     if (s != kImNoSupport) parts[tab[s].off + tab[s].size++] = make_uint2(r.v0, r.v1);
   }
-  for (int q = 0; q < nsup; ++q) P.nd[1][tab[q].node].support = kImNoSupport;
+  for (int q = 0; q < nsup; ++q) P.N(1, tab[q].node).support = kImNoSupport;
 }
 
 template <class Env>
@@ -649,7 +721,7 @@ __global__ __launch_bounds__(64) void k_im_reset(ImParams p) {
     r.stats = -1;
     r.support = kImNoSupport;
     r.okey = 0;
-    p.nodes[((int64_t)b * 2 + k) * p.Nn] = r;
+    *reinterpret_cast<INode*>(p.nodes + ((int64_t)b * 2 + k) * p.Nn * p.nstride) = r;
     h.n_nodes[k] = 1;
     h.n_stats[k] = 0;
     h.n_log[k] = 0;
@@ -681,17 +753,17 @@ __global__ __launch_bounds__(64) void k_im_update(ImParams p) {
   ImPair<Env> P(p, sm, b);
   const uint64_t obs = p.in_obs[b];
   if (p.in_actions[b] == kImSkip) {   // a pair whose episode has ended: untouched
-    p.out[2 * b] = im_absorbing(P.nd[0][P.h.cur].info) ? 1 : 0;
+    p.out[2 * b] = im_absorbing(P.N(0, P.h.cur).info) ? 1 : 0;
     p.out[2 * b + 1] = P.h.err;
     return;
   }
   P.h.num_sims = 0;         // the step's counters (intmcp.py:114-136 resets them first)
   P.h.search_depth = 0;
-  if (P.h.err == 0 && !im_absorbing(P.nd[0][P.h.cur].info)) {
+  if (P.h.err == 0 && !im_absorbing(P.N(0, P.h.cur).info)) {
     auto draw_model = [&](uint32_t n) { return P.d_model(n); };
     const double* prob = P.prob;
     int nsup = 0;
-    if (P.nd[0][P.h.cur].t == 0) {
+    if (P.N(0, P.h.cur).t == 0) {
       // _initial_nested_update (intmcp.py:216-268), level 1
       const int node = P.child(0, 0, p.A, obs);
       if (node >= 0) {
@@ -718,12 +790,12 @@ __global__ __launch_bounds__(64) void k_im_update(ImParams p) {
           const int sel = P.h.sup_sel ^ 1;
           im_support(P, sel, n, &nsup);
           ISup* tab = P.sup_tab(sel);
-          const uint64_t o0 = P.nd[1][tab[0].node].okey;
+          const uint64_t o0 = P.N(1, tab[0].node).okey;
           Env::sample_agent_initial(sm, p.other, o0, draw_model, &s0, &s1);   // probe
           int off = 0;
           for (int q = 0; q < nsup && P.h.err == 0; ++q) {
             P.traverse(1, tab[q].node);
-            const uint64_t oq = P.nd[1][tab[q].node].okey;
+            const uint64_t oq = P.N(1, tab[q].node).okey;
             tab[q].off = off;
             tab[q].size = 0;
             uint2* pp = P.sup_parts(sel) + off;
@@ -769,7 +841,7 @@ __global__ __launch_bounds__(64) void k_im_update(ImParams p) {
           }
         }
         P.h.pad = prev_size;
-        if (!im_absorbing(P.nd[0][node].info) && P.h.err == 0)
+        if (!im_absorbing(P.N(0, node).info) && P.h.err == 0)
           P.reinvig_top(node, action, obs, p.n_target, &n);   // ceil(1.0 * target)
         P.h.cur = node;
         P.h.root_size = n;
@@ -783,9 +855,9 @@ __global__ __launch_bounds__(64) void k_im_update(ImParams p) {
           for (int q = 0; q < nsup && P.h.err == 0; ++q) {
             const int m = tab[q].node;
             P.traverse(1, m);
-            if (im_absorbing(P.nd[1][m].info)) continue;
+            if (im_absorbing(P.N(1, m).info)) continue;
             const int tq = (int)ceil(prob[q] * (double)p.n_target);
-            P.reinvig_nested(m, (int)im_paction(P.nd[1][m].info), P.nd[1][m].okey, tq, sel, q);
+            P.reinvig_nested(m, (int)im_paction(P.N(1, m).info), P.N(1, m).okey, tq, sel, q);
           }
           int used = 0;
           for (int q = 0; q < nsup; ++q) used = max(used, tab[q].off + tab[q].cap);
@@ -802,7 +874,7 @@ __global__ __launch_bounds__(64) void k_im_update(ImParams p) {
   }
   P.h.pad = 0;
   P.store();
-  p.out[2 * b] = im_absorbing(P.nd[0][P.h.cur].info) ? 1 : 0;
+  p.out[2 * b] = im_absorbing(P.N(0, P.h.cur).info) ? 1 : 0;
   p.out[2 * b + 1] = P.h.err;
 }
 
@@ -824,14 +896,14 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
   }
   const int root = P.h.cur;
   int action = 0;
-  if (P.h.err == 0 && !im_absorbing(P.nd[0][root].info) && P.nd[0][root].t > 0) {
+  if (P.h.err == 0 && !im_absorbing(P.N(0, root).info) && P.N(0, root).t > 0) {
     uint4* rb = P.root_buf(P.h.root_sel);
     for (int level = 0; level < 2 && P.h.err == 0; ++level) {
       const int num_sims = level == 0 ? sims0 : sims1;
       for (int s = 0; s < num_sims && P.h.err == 0; ++s) {
         // _nested_sim(history, level, top_level=True) of the level-1 planner
         P.traverse(0, root);
-        if (im_nreg(P.nd[0][root].info) == 0) P.expand(0, root);
+        if (im_nreg(P.N(0, root).info) == 0) P.expand(0, root);
         if (P.h.root_size == 0 || P.h.root_size < p.extra) {
           P.fail(POMCP_E_UNSUPPORTED);   // depleted root (needs the top-level reinvigoration)
           break;
@@ -841,7 +913,7 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
           // the level-0 planner's _nested_sim at the particle's history
           const int n = (int)hp.z;
           P.traverse(1, n);
-          if (im_nreg(P.nd[1][n].info) == 0) P.expand(1, n);
+          if (im_nreg(P.N(1, n).info) == 0) P.expand(1, n);
           ISup& e = P.sup_tab(P.h.sup_sel)[hp.w];
           if (e.size == 0) {
             P.fail(POMCP_E_UNSUPPORTED);   // depleted level-0 node
@@ -849,10 +921,10 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
           }
           const uint2 q = P.sup_parts(P.h.sup_sel)[e.off + P.d_bel(0, (uint32_t)e.size)];
           P.simulate(1, q.x, q.y, 0u, n);
-          P.nd[1][n].visits += 1;
+          P.N(1, n).visits += 1;
         } else {
           const int d = P.simulate(0, hp.x, hp.y, hp.z, root);
-          P.nd[0][root].visits += 1;
+          P.N(0, root).visits += 1;
           if (d > P.h.search_depth) P.h.search_depth = d;
         }
         P.h.num_sims += 1;
@@ -864,7 +936,8 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
       return;
     }
     // max_value_action_selection (intmcp.py:718-732)
-    const INode x = P.nd[0][root];
+    const INode x = P.N(0, root);
+    const IStat* const rs = P.S(0, root);
     const int nr = im_nreg(x.info);
     if (nr == 0) {
       action = (int)P.d_sel((uint32_t)p.A);
@@ -873,7 +946,7 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
       int ties[6], nt = 0;
       for (int i = 0; i < nr; ++i) {
         const int a = im_order(x.info, i);
-        const double v = P.st[0][x.stats + a].value;
+        const double v = rs[a].value;
         if (v == mx) {
           ties[nt++] = a;
         } else if (v > mx) {

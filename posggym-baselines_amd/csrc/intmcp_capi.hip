@@ -25,7 +25,8 @@ __global__ __launch_bounds__(64) void k_im_root_stats(ImParams d, intmcp_root_st
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= d.B) return;
   const IHdr h = d.hdr[t];
-  const INode node = d.nodes[(int64_t)t * 2 * d.Nn + h.cur];
+  const char* const blk = d.nodes + ((int64_t)t * 2 * d.Nn + h.cur) * d.nstride;
+  const INode node = *reinterpret_cast<const INode*>(blk);
   intmcp_root_stats o;
   memset(&o, 0, sizeof(o));
   o.action = h.last_action;
@@ -38,7 +39,7 @@ __global__ __launch_bounds__(64) void k_im_root_stats(ImParams d, intmcp_root_st
   const int nr = im_nreg(node.info);
   o.num_children = nr;
   if (node.stats >= 0) {
-    const IStat* sv = d.stats + (int64_t)t * 2 * d.Ns + node.stats;
+    const IStat* sv = reinterpret_cast<const IStat*>(blk + 32);
     for (int i = 0; i < nr && i < POMCP_MAX_ACTIONS; ++i) {
       const int a = im_order(node.info, i);
       o.child_action[i] = a;
@@ -208,14 +209,14 @@ int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, in
     d.field = reinterpret_cast<decltype(d.field)>(p);                           \
   } while (0)
   IM_ALLOC(hdr, IHdr, B);
-  IM_ALLOC(nodes, INode, B * 2 * d.Nn);
-  IM_ALLOC(stats, IStat, B * 2 * d.Ns);
+  d.nstride = 32 * (1 + (int64_t)d.A);   // node blocks: INode + A IStat (intmcp.hip)
+  IM_ALLOC(nodes, char, B * 2 * d.Nn * d.nstride);
   IM_ALLOC(hash, IHash, B * 2 * d.H);
   IM_ALLOC(log, IRec, B * 2 * d.Nl);
   IM_ALLOC(root, uint4, B * 2 * d.Nr);
   IM_ALLOC(sup, ISup, B * 2 * d.Nr);
   IM_ALLOC(supp, uint2, B * 2 * d.Nsp);
-  IM_ALLOC(path, int4, B * kImPath * 2);
+  IM_ALLOC(path, int4, B * kImPath * 3);
   IM_ALLOC(prob, double, B * d.Nr);
   IM_ALLOC(logtab, double, c.log_table_size);
   IM_ALLOC(dpow, double, c.discount_pow_size);
@@ -388,8 +389,15 @@ int intmcp_get_nodes(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int
   const int n = ctx->host_hdr[pair].n_nodes[tree];
   *count = n;
   if (!out || capacity < n) return POMCP_OK;
-  return im_copy(ctx, reinterpret_cast<INode*>(out), ctx->ip.nodes + ((int64_t)pair * 2 + tree) * ctx->ip.Nn,
-                 (size_t)n);
+  // the INode of every block (layout: intmcp.hip ImPair::N)
+  const int64_t ns = ctx->ip.nstride;
+  std::vector<char> blocks((size_t)n * (size_t)ns);
+  rc = im_copy(ctx, blocks.data(), ctx->ip.nodes + ((int64_t)pair * 2 + tree) * ctx->ip.Nn * ns,
+               blocks.size());
+  if (rc != POMCP_OK) return rc;
+  INode* o = reinterpret_cast<INode*>(out);
+  for (int i = 0; i < n; ++i) std::memcpy(&o[i], blocks.data() + (size_t)i * ns, sizeof(INode));
+  return POMCP_OK;
 }
 
 int intmcp_get_stats(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int32_t capacity,
@@ -400,8 +408,22 @@ int intmcp_get_stats(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int
   const int n = ctx->host_hdr[pair].n_stats[tree];
   *count = n;
   if (!out || capacity < n) return POMCP_OK;
-  return im_copy(ctx, reinterpret_cast<IStat*>(out), ctx->ip.stats + ((int64_t)pair * 2 + tree) * ctx->ip.Ns,
-                 (size_t)n);
+  // statistics in allocation order (INode.stats = their first index), gathered
+  // from the node blocks
+  const int nn = ctx->host_hdr[pair].n_nodes[tree];
+  const int64_t ns = ctx->ip.nstride;
+  std::vector<char> blocks((size_t)nn * (size_t)ns);
+  rc = im_copy(ctx, blocks.data(), ctx->ip.nodes + ((int64_t)pair * 2 + tree) * ctx->ip.Nn * ns,
+               blocks.size());
+  if (rc != POMCP_OK) return rc;
+  IStat* o = reinterpret_cast<IStat*>(out);
+  for (int i = 0; i < nn; ++i) {
+    const INode* x = reinterpret_cast<const INode*>(blocks.data() + (size_t)i * ns);
+    if (x->stats < 0) continue;
+    for (int a = 0; a < ctx->ip.A && x->stats + a < n; ++a)
+      std::memcpy(&o[x->stats + a], blocks.data() + (size_t)i * ns + 32 + 32 * (size_t)a, sizeof(IStat));
+  }
+  return POMCP_OK;
 }
 
 int intmcp_get_support(intmcp_ctx* ctx, int32_t pair, int32_t* entries, int32_t capacity_entries,

@@ -42,8 +42,8 @@ INT32_MAX = 2**31 - 1
 
 @dataclass
 class IntmcpCapacities:
-    max_nodes: int              # obs nodes per tree (32 B)
-    max_stats: int              # action statistics per tree (32 B)
+    max_nodes: int              # obs nodes per tree (32 B + A x 32 B statistics block each)
+    max_stats: int              # action statistics per tree (allocation counter limit)
     max_log: int                # particle log records per tree (16 B)
     hash_slots: int             # obs-child map slots per tree (16 B)
     max_root_belief: int        # level-1 root particles (16 B, x2) and support entries (16 B, x2)
@@ -51,8 +51,8 @@ class IntmcpCapacities:
     log_table_size: int
     discount_pow_size: int
 
-    def bytes_per_pair(self) -> int:
-        return (2 * (self.max_nodes * 32 + self.max_stats * 32 + self.max_log * 16
+    def bytes_per_pair(self, num_actions: int = 5) -> int:
+        return (2 * (self.max_nodes * 32 * (1 + num_actions) + self.max_log * 16
                      + self.hash_slots * 16) + 4 * self.max_root_belief * 16
                 + 2 * self.max_support_particles * 8 + self.max_root_belief * 8)
 
