@@ -27,6 +27,11 @@ namespace pb {
 constexpr int kImPath = 128;          // tree levels per simulation
 constexpr int kImMaxA = 6;            // registration order: 6 x 3 bits (INode.info)
 constexpr int kImRegPath = 4;         // path levels held in registers (deeper ones in p.path)
+// A node's block, two 128 B lines: line 0 = the INode (32 B) + the head
+// {visits, -, value} of each action's statistics (16 B each); line 1 = their
+// {total, agg} tails.  A node view (selection, the other agent's softmax)
+// is one line; the chosen action's tail is read for the backup only.
+constexpr int64_t kImBlock = 256;
 constexpr uint32_t kImNoSupport = 0xFFFFFFFFu;
 constexpr int32_t kImSkip = -2;       // intmcp_update action: leave the pair untouched
 
@@ -72,8 +77,8 @@ struct ImParams {
   int64_t Nn, Ns, Nl, H, Nr, Nsp;   // per tree: nodes, stat entries, log records, hash slots;
                                     // per pair: root belief, support particles
   IHdr* hdr;
-  char* nodes;          // [B][2][Nn] node blocks: the INode, then its A IStat (nstride B)
-  int64_t nstride;      // 32 * (1 + A)
+  char* nodes;          // [B][2][Nn] node blocks (kImBlock B, see ImPair::N)
+  int64_t nstride;      // kImBlock
   IHash* hash;          // [B][2][H]
   IRec* log;            // [B][2][Nl]
   uint4* root;          // [B][2][Nr] {v0, v1, nested, support slot}
@@ -130,14 +135,17 @@ struct ImPair {
   }
   __device__ void store() { p.hdr[pair] = h; }
 
-  // A node's block: the INode and, right after it, the statistics of its A
-  // actions (node.py:120-178), so a node and its statistics arrive in one
-  // round trip (they used to be an index apart: two dependent loads).
+  // A node's block (kImBlock): the INode with the heads of its actions'
+  // statistics (node.py:120-178) in one line, so a node and its statistics
+  // arrive together (they used to be an index apart: two dependent loads).
   __device__ __forceinline__ INode& N(int k, int n) const {
-    return *reinterpret_cast<INode*>(nb[k] + (int64_t)n * p.nstride);
+    return *reinterpret_cast<INode*>(nb[k] + (int64_t)n * kImBlock);
   }
-  __device__ __forceinline__ IStat* S(int k, int n) const {
-    return reinterpret_cast<IStat*>(nb[k] + (int64_t)n * p.nstride + 32);
+  __device__ __forceinline__ uint4* H(int k, int n) const {   // {visits, -, value} per action
+    return reinterpret_cast<uint4*>(nb[k] + (int64_t)n * kImBlock + 32);
+  }
+  __device__ __forceinline__ uint4* T(int k, int n) const {   // {total, agg} per action
+    return reinterpret_cast<uint4*>(nb[k] + (int64_t)n * kImBlock + 128);
   }
   // the node and the {visits, -, value} head of every action's statistics,
   // issued together (entries of unregistered actions are never used)
@@ -148,9 +156,9 @@ struct ImPair {
   __device__ __forceinline__ View view(int k, int n) const {
     View v;
     v.x = N(k, n);
-    const uint4* s = reinterpret_cast<const uint4*>(S(k, n));
+    const uint4* s = H(k, n);
 #pragma unroll
-    for (int q = 0; q < kImMaxA; ++q) v.sh[q] = q < p.A ? s[2 * q] : make_uint4(0, 0, 0, 0);
+    for (int q = 0; q < kImMaxA; ++q) v.sh[q] = q < p.A ? s[q] : make_uint4(0, 0, 0, 0);
     return v;
   }
   __device__ void fail(int code) {
@@ -189,13 +197,18 @@ struct ImPair {
   }
   // The obs child (n, a, okey); created (visits 0) if missing (INTMCP.traverse /
   // history extension, intmcp.py:797-809, 466).
-  __device__ int child(int k, int n, int a, uint64_t okey) {
+  // created (optional): whether it was missing; parent_t >= 0: node n's t,
+  // known to the caller (saves reloading the parent).
+  __device__ int child(int k, int n, int a, uint64_t okey, bool* created = nullptr,
+                       int parent_t = -1) {
     const uint32_t na = ((uint32_t)n << 3) | (uint32_t)a;
     uint32_t s = hkey(na, okey);
+    if (created) *created = false;
     for (int64_t probe = 0; probe < p.H; ++probe) {
       const IHash e = hs[k][s];
       if (e.child >= 0 && e.na == na && e.okey == okey) return e.child;
       if (e.child < 0) {
+        if (created) *created = true;
         if (h.n_nodes[k] >= p.Nn) {
           fail(POMCP_E_ARENA);
           return -1;
@@ -205,7 +218,7 @@ struct ImPair {
         x.parent = n;
         x.info = (uint32_t)a;
         x.visits = 0;
-        x.t = N(k, n).t + 1;
+        x.t = (parent_t >= 0 ? parent_t : N(k, n).t) + 1;
         x.stats = -1;
         x.support = kImNoSupport;
         x.okey = okey;
@@ -247,7 +260,8 @@ struct ImPair {
         z.value = 0.0;
         z.total = 0.0;
         z.agg = 0.0;
-        S(k, n)[q] = z;
+        H(k, n)[q] = make_uint4(0, 0, 0, 0);
+        T(k, n)[q] = make_uint4(0, 0, 0, 0);
       }
     }
   }
@@ -437,11 +451,10 @@ struct ImPair {
   // level's view.  The path keeps each level's statistics as they were before
   // (visits, value, total, agg), so the backup writes without reading; the
   // first kImRegPath levels stay in registers.
-  __device__ int simulate(int k, uint32_t s0, uint32_t s1, uint32_t nested, int n) {
+  __device__ int simulate(int k, uint32_t s0, uint32_t s1, uint32_t nested, int n, View v) {
     int depth = 0, plen = 0;
     double leaf = 0.0;
     uint4 rp[kImRegPath][3];   // {n, a, done, -}, {r, value0}, {total0, agg0} | visits0 in [0].w
-    View v = view(k, n);
     for (;;) {
       const INode& x = v.x;
       if (depth > p.depth_limit || x.t + depth > p.step_limit) break;
@@ -452,7 +465,7 @@ struct ImPair {
       }
       const int a = select(k, v);
       // the chosen action's {total, agg}: needed by the backup only (no wait)
-      const uint4 s2 = reinterpret_cast<const uint4*>(S(k, n))[2 * a + 1];
+      const uint4 s2 = T(k, n)[a];
       uint4 sa = v.sh[0];
 #pragma unroll
       for (int q = 1; q < kImMaxA; ++q)
@@ -463,12 +476,9 @@ struct ImPair {
       int done;
       uint64_t okey;
       step(k, s0, s1, nested, a, ao, &n0, &n1, &r, &done, &okey, &nn);
-      int c = find(k, n, a, okey);
-      const bool created = c < 0;
-      if (created) {
-        c = child(k, n, a, okey);
-        if (c < 0) return depth;
-      }
+      bool created;   // one probe chain: found, or created where the probe ended
+      const int c = child(k, n, a, okey, &created, x.t);
+      if (c < 0) return depth;
       View cv = view(k, c);
       cv.x.visits = created ? 1 : cv.x.visits + 1;
       uint32_t info = cv.x.info;
@@ -516,11 +526,10 @@ struct ImPair {
       const double delta = g - value0;
       const double value = value0 + delta / (double)vis;
       const double agg = hilo_d(e2.z, e2.w) + delta * (g - value);
-      uint4* sp = reinterpret_cast<uint4*>(S(k, (int)e0.x) + e0.y);
-      sp[0] = make_uint4((uint32_t)vis, 0u, (uint32_t)__double2loint(value),
-                         (uint32_t)__double2hiint(value));
-      sp[1] = make_uint4((uint32_t)__double2loint(total), (uint32_t)__double2hiint(total),
-                         (uint32_t)__double2loint(agg), (uint32_t)__double2hiint(agg));
+      H(k, (int)e0.x)[e0.y] = make_uint4((uint32_t)vis, 0u, (uint32_t)__double2loint(value),
+                                         (uint32_t)__double2hiint(value));
+      T(k, (int)e0.x)[e0.y] = make_uint4((uint32_t)__double2loint(total), (uint32_t)__double2hiint(total),
+                                         (uint32_t)__double2loint(agg), (uint32_t)__double2hiint(agg));
       mm_update(k, value);
     };
     for (int l = plen - 1; l >= kImRegPath; --l) {
@@ -898,32 +907,57 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
   int action = 0;
   if (P.h.err == 0 && !im_absorbing(P.N(0, root).info) && P.N(0, root).t > 0) {
     uint4* rb = P.root_buf(P.h.root_sel);
+    // _nested_sim(history, level, top_level=True) of the level-1 planner
+    // (intmcp.py:410-442) starts with traverse + expand of the root: no draws,
+    // and no-ops once done, so they run once per launch.  The depleted-root
+    // branch cannot be reached with a valid configuration.
+    if (sims0 + sims1 > 0) {
+      P.traverse(0, root);
+      if (im_nreg(P.N(0, root).info) == 0) P.expand(0, root);
+      if (P.h.root_size == 0 || P.h.root_size < p.extra) P.fail(POMCP_E_UNSUPPORTED);
+    }
+    const ISup* const stab = P.sup_tab(P.h.sup_sel);
+    const uint2* const sparts = P.sup_parts(P.h.sup_sel);
     for (int level = 0; level < 2 && P.h.err == 0; ++level) {
       const int num_sims = level == 0 ? sims0 : sims1;
+      // the root particle of the next simulation (belief.py:55; the level-1
+      // planner's own stream, which nothing else draws during a search) and,
+      // at level 0, its history's support entry: loaded one simulation ahead
+      uint4 hp_next = make_uint4(0, 0, 0, 0);
+      ISup e_next = {0, 0, 0, 0};
+      if (num_sims > 0) {
+        hp_next = rb[P.d_bel(1, (uint32_t)P.h.root_size)];
+        if (level == 0) e_next = stab[hp_next.w];
+      }
       for (int s = 0; s < num_sims && P.h.err == 0; ++s) {
-        // _nested_sim(history, level, top_level=True) of the level-1 planner
-        P.traverse(0, root);
-        if (im_nreg(P.N(0, root).info) == 0) P.expand(0, root);
-        if (P.h.root_size == 0 || P.h.root_size < p.extra) {
-          P.fail(POMCP_E_UNSUPPORTED);   // depleted root (needs the top-level reinvigoration)
-          break;
+        const uint4 hp = hp_next;
+        const ISup e = e_next;
+        if (s + 1 < num_sims) {
+          hp_next = rb[P.d_bel(1, (uint32_t)P.h.root_size)];
+          if (level == 0) e_next = stab[hp_next.w];
         }
-        const uint4 hp = rb[P.d_bel(1, (uint32_t)P.h.root_size)];
         if (level == 0) {
-          // the level-0 planner's _nested_sim at the particle's history
+          // the level-0 planner's _nested_sim at the particle's history: its
+          // node + statistics and the support particle in one round trip
           const int n = (int)hp.z;
-          P.traverse(1, n);
-          if (im_nreg(P.N(1, n).info) == 0) P.expand(1, n);
-          ISup& e = P.sup_tab(P.h.sup_sel)[hp.w];
           if (e.size == 0) {
-            P.fail(POMCP_E_UNSUPPORTED);   // depleted level-0 node
+            P.fail(POMCP_E_UNSUPPORTED);   // depleted level-0 node (unreachable)
             break;
           }
-          const uint2 q = P.sup_parts(P.h.sup_sel)[e.off + P.d_bel(0, (uint32_t)e.size)];
-          P.simulate(1, q.x, q.y, 0u, n);
+          const uint2 q = sparts[e.off + P.d_bel(0, (uint32_t)e.size)];
+          auto v = P.view(1, n);
+          if (n > 0 && !im_path_ok(v.x.info)) {
+            P.traverse(1, n);
+            v = P.view(1, n);
+          }
+          if (im_nreg(v.x.info) == 0) {
+            P.expand(1, n);
+            v = P.view(1, n);
+          }
+          P.simulate(1, q.x, q.y, 0u, n, v);
           P.N(1, n).visits += 1;
         } else {
-          const int d = P.simulate(0, hp.x, hp.y, hp.z, root);
+          const int d = P.simulate(0, hp.x, hp.y, hp.z, root, P.view(0, root));
           P.N(0, root).visits += 1;
           if (d > P.h.search_depth) P.h.search_depth = d;
         }
@@ -937,7 +971,7 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
     }
     // max_value_action_selection (intmcp.py:718-732)
     const INode x = P.N(0, root);
-    const IStat* const rs = P.S(0, root);
+    const uint4* const rs = P.H(0, root);
     const int nr = im_nreg(x.info);
     if (nr == 0) {
       action = (int)P.d_sel((uint32_t)p.A);
@@ -946,7 +980,7 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
       int ties[6], nt = 0;
       for (int i = 0; i < nr; ++i) {
         const int a = im_order(x.info, i);
-        const double v = rs[a].value;
+        const double v = hilo_d(rs[a].z, rs[a].w);
         if (v == mx) {
           ties[nt++] = a;
         } else if (v > mx) {

@@ -25,7 +25,7 @@ __global__ __launch_bounds__(64) void k_im_root_stats(ImParams d, intmcp_root_st
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= d.B) return;
   const IHdr h = d.hdr[t];
-  const char* const blk = d.nodes + ((int64_t)t * 2 * d.Nn + h.cur) * d.nstride;
+  const char* const blk = d.nodes + ((int64_t)t * 2 * d.Nn + h.cur) * kImBlock;
   const INode node = *reinterpret_cast<const INode*>(blk);
   intmcp_root_stats o;
   memset(&o, 0, sizeof(o));
@@ -39,14 +39,15 @@ __global__ __launch_bounds__(64) void k_im_root_stats(ImParams d, intmcp_root_st
   const int nr = im_nreg(node.info);
   o.num_children = nr;
   if (node.stats >= 0) {
-    const IStat* sv = reinterpret_cast<const IStat*>(blk + 32);
+    const uint4* hv = reinterpret_cast<const uint4*>(blk + 32);    // node block: intmcp.hip
+    const uint4* tv = reinterpret_cast<const uint4*>(blk + 128);
     for (int i = 0; i < nr && i < POMCP_MAX_ACTIONS; ++i) {
       const int a = im_order(node.info, i);
       o.child_action[i] = a;
       if (a < d.A) {
-        o.child_visits[i] = sv[a].visits;
-        o.child_values[i] = sv[a].value;
-        o.child_totals[i] = sv[a].total;
+        o.child_visits[i] = (int)hv[a].x;
+        o.child_values[i] = hilo_d(hv[a].z, hv[a].w);
+        o.child_totals[i] = hilo_d(tv[a].x, tv[a].y);
       }
     }
   }
@@ -209,7 +210,7 @@ int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, in
     d.field = reinterpret_cast<decltype(d.field)>(p);                           \
   } while (0)
   IM_ALLOC(hdr, IHdr, B);
-  d.nstride = 32 * (1 + (int64_t)d.A);   // node blocks: INode + A IStat (intmcp.hip)
+  d.nstride = kImBlock;   // node blocks (intmcp.hip)
   IM_ALLOC(nodes, char, B * 2 * d.Nn * d.nstride);
   IM_ALLOC(hash, IHash, B * 2 * d.H);
   IM_ALLOC(log, IRec, B * 2 * d.Nl);
@@ -421,7 +422,16 @@ int intmcp_get_stats(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int
     const INode* x = reinterpret_cast<const INode*>(blocks.data() + (size_t)i * ns);
     if (x->stats < 0) continue;
     for (int a = 0; a < ctx->ip.A && x->stats + a < n; ++a)
-      std::memcpy(&o[x->stats + a], blocks.data() + (size_t)i * ns + 32 + 32 * (size_t)a, sizeof(IStat));
+    {
+      const char* bk = blocks.data() + (size_t)i * ns;   // head {visits, -, value}, tail {total, agg}
+      IStat st;
+      std::memcpy(&st.visits, bk + 32 + 16 * (size_t)a, 4);
+      st.pad = 0;
+      std::memcpy(&st.value, bk + 32 + 16 * (size_t)a + 8, 8);
+      std::memcpy(&st.total, bk + 128 + 16 * (size_t)a, 8);
+      std::memcpy(&st.agg, bk + 128 + 16 * (size_t)a + 8, 8);
+      o[x->stats + a] = st;
+    }
   }
   return POMCP_OK;
 }

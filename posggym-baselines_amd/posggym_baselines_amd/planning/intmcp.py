@@ -52,7 +52,7 @@ class IntmcpCapacities:
     discount_pow_size: int
 
     def bytes_per_pair(self, num_actions: int = 5) -> int:
-        return (2 * (self.max_nodes * 32 * (1 + num_actions) + self.max_log * 16
+        return (2 * (self.max_nodes * 256 + self.max_log * 16
                      + self.hash_slots * 16) + 4 * self.max_root_belief * 16
                 + 2 * self.max_support_particles * 8 + self.max_root_belief * 8)
 

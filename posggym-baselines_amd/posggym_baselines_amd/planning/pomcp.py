@@ -162,8 +162,16 @@ class POMCP:
         absorbing = self._engine.update([a], [key])   # broadcast to every replica
         # a replica whose root is absorbing stops searching and merges as zeros;
         # the planner is absorbing once all of them are (oracle/root_parallel.py)
-        self.root = dataclasses.replace(self.root, t=self.root.t + 1,
-                                        is_absorbing=bool(np.all(absorbing)))
+        # -- on every rank, or the ranks would stop calling the collective apart
+        done = bool(np.all(absorbing))
+        if self._world > 1:
+            import torch
+            import torch.distributed as dist
+            flag = torch.tensor([0 if done else 1], dtype=torch.int32,
+                                device=f"cuda:{self.config.device}")
+            dist.all_reduce(flag, group=self._pg)
+            done = int(flag.item()) == 0
+        self.root = dataclasses.replace(self.root, t=self.root.t + 1, is_absorbing=done)
         self.step_statistics["update_time"] = time.time() - start
 
     # -------------------------------------------------------------- search
