@@ -202,10 +202,16 @@ struct ImPair {
   __device__ int child(int k, int n, int a, uint64_t okey, bool* created = nullptr,
                        int parent_t = -1) {
     const uint32_t na = ((uint32_t)n << 3) | (uint32_t)a;
-    uint32_t s = hkey(na, okey);
+    const uint32_t s = hkey(na, okey);
+    return child_from(k, n, a, okey, s, hs[k][s], created, parent_t);
+  }
+  // child(), with the first probe (slot s, entry e) already loaded
+  __device__ int child_from(int k, int n, int a, uint64_t okey, uint32_t s, IHash e,
+                            bool* created, int parent_t) {
+    const uint32_t na = ((uint32_t)n << 3) | (uint32_t)a;
     if (created) *created = false;
     for (int64_t probe = 0; probe < p.H; ++probe) {
-      const IHash e = hs[k][s];
+      if (probe > 0) e = hs[k][s];
       if (e.child >= 0 && e.na == na && e.okey == okey) return e.child;
       if (e.child < 0) {
         if (created) *created = true;
@@ -345,8 +351,8 @@ struct ImPair {
   }
 
   // INTMCP.sample_action of the level-0 planner (intmcp.py:763-791) at node n
-  __device__ int sample_action(int n) {
-    View v = view(1, n);   // node + statistics: one round trip
+  __device__ int sample_action(int n, const View* pre = nullptr) {
+    View v = pre ? *pre : view(1, n);   // node + statistics: one round trip
     if (n > 0 && !im_path_ok(v.x.info)) {
       traverse(1, n);
       v = view(1, n);
@@ -455,6 +461,8 @@ struct ImPair {
     int depth = 0, plen = 0;
     double leaf = 0.0;
     uint4 rp[kImRegPath][3];   // {n, a, done, -}, {r, value0}, {total0, agg0} | visits0 in [0].w
+    View nv;                   // the other agent's history node (level 1), prefetched
+    bool have_nv = false;
     for (;;) {
       const INode& x = v.x;
       if (depth > p.depth_limit || x.t + depth > p.step_limit) break;
@@ -470,15 +478,38 @@ struct ImPair {
 #pragma unroll
       for (int q = 1; q < kImMaxA; ++q)
         if (q == a) sa = v.sh[q];
-      const int ao = other_action(k, nested);
-      uint32_t n0, n1, nn;
+      // the other agent's action (intmcp.py:602-615): at level 1 its
+      // history node's view was loaded when the previous level created it
+      const bool nested_k = k == 0 && !p.state_belief_only;
+      const int ao = nested_k ? sample_action((int)nested, have_nv ? &nv : nullptr)
+                              : other_action(k, nested);
+      uint32_t n0, n1, nn = 0u;
       double r;
       int done;
-      uint64_t okey;
-      step(k, s0, s1, nested, a, ao, &n0, &n1, &r, &done, &okey, &nn);
+      const int me = agent(k);
+      const uint32_t j = Env::kStepDraws ? d_model(2) : 0u;
+      Env::step(m, me, s0, s1, (uint32_t)a, (uint32_t)ao, j, &n0, &n1, &r, &done);
+      const uint64_t okey = Env::obs_key(m, me, n0, n1);
+      // the child (a, obs) here and, at level 1, the other agent's history
+      // extension: both first probes in flight together, one probe chain each
+      const uint32_t na = ((uint32_t)n << 3) | (uint32_t)a;
+      const uint32_t hsl = hkey(na, okey);
+      const IHash he = hs[k][hsl];
+      if (k == 0) {
+        const uint64_t ok = Env::obs_key(m, p.other, n0, n1);
+        const uint32_t nna = ((uint32_t)nested << 3) | (uint32_t)ao;
+        const uint32_t nsl = hkey(nna, ok);
+        const IHash ne = hs[1][nsl];
+        const int cn = child_from(1, (int)nested, ao, ok, nsl, ne, nullptr, -1);
+        nn = cn < 0 ? 0u : (uint32_t)cn;
+      }
       bool created;   // one probe chain: found, or created where the probe ended
-      const int c = child(k, n, a, okey, &created, x.t);
+      const int c = child_from(k, n, a, okey, hsl, he, &created, x.t);
       if (c < 0) return depth;
+      if (nested_k) {   // the next level's other-agent view (no wait)
+        nv = view(1, (int)nn);
+        have_nv = true;
+      }
       View cv = view(k, c);
       cv.x.visits = created ? 1 : cv.x.visits + 1;
       uint32_t info = cv.x.info;
