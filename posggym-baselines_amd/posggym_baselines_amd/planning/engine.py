@@ -93,6 +93,21 @@ def plan_wallclock_capacities(config, step_limit: int, num_trees: int = 1, num_a
     return caps, sims
 
 
+_LOG_TABLE = np.zeros(1, dtype=np.float64)
+
+
+def log_table(n: int) -> np.ndarray:
+    """[0.0, log(1), .., log(n-1)] with the host's math.log (the reference's
+    UCB term, mcts.py:534), bit for bit; one cached table per process, grown on
+    demand (wall-clock arenas ask for tens of millions of entries)."""
+    global _LOG_TABLE
+    if len(_LOG_TABLE) < n:
+        m = len(_LOG_TABLE)
+        ext = np.fromiter(map(math.log, range(m, n)), dtype=np.float64, count=n - m)
+        _LOG_TABLE = np.concatenate([_LOG_TABLE, ext])
+    return _LOG_TABLE[:n]
+
+
 class PomcpEngine:
     SELECTION = {"pucb": N.SEL_PUCB, "ucb": N.SEL_UCB, "uniform": N.SEL_UNIFORM}
 
@@ -157,8 +172,7 @@ class PomcpEngine:
         c.overflow_slots = capacities.overflow_slots
         # FP64 tables from Python's own math.log and float ** int (bit-exact with
         # mcts.py:534 and mcts.py:421)
-        self._logtab = np.array([0.0] + [math.log(n) for n in range(1, capacities.log_table_size)],
-                                dtype=np.float64)
+        self._logtab = log_table(capacities.log_table_size)
         self._dpow = np.array([config.discount ** k for k in range(capacities.discount_pow_size)],
                               dtype=np.float64)
         c.log_table = self._logtab.ctypes.data_as(C.POINTER(C.c_double))

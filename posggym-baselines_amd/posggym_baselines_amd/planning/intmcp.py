@@ -17,7 +17,15 @@ Scope (DESIGN.md "I-NTMCP"): nesting level 1, random search policies
 (``search_policies=None``), ``ucb`` / ``uniform`` selection (the reference's
 ``pucb_action_selection`` reads ``self.action_space``, which INTMCP does not
 define, ``intmcp.py:645``).  The reinvigoration of a depleted root during the
-search (``intmcp.py:426-431``) reports POMCP_E_UNSUPPORTED instead of running.
+search (``intmcp.py:426-431``) cannot run under a valid configuration (the
+reference asserts ``reinvigoration_sample_limit_factor >= 1``, ``belief.py:85``;
+DESIGN.md §10); the kernel reports POMCP_E_UNSUPPORTED should it ever be reached.
+
+Wall-clock mode (``num_sims=None``, the reference's default): the arenas are
+sized from ``search_time_limit`` and an HBM budget
+(:func:`plan_intmcp_wallclock_capacities`), and ``get_action`` stops launching
+chunks before one could overflow them, so a time-limited episode never fails
+with POMCP_E_ARENA (``step_statistics["arena_full"]`` records an early stop).
 """
 import ctypes as C
 import dataclasses
@@ -34,6 +42,7 @@ from posggym_baselines_amd.envs import engine_model
 
 from posggym_baselines_amd import _native as N
 from posggym_baselines_amd.planning.config import MCTSConfig
+from posggym_baselines_amd.planning.engine import log_table
 from posggym_baselines_amd.planning.search_policy import RandomSearchPolicy
 from posggym_baselines_amd.planning.utils import PlanningStatTracker
 
@@ -42,7 +51,7 @@ INT32_MAX = 2**31 - 1
 
 @dataclass
 class IntmcpCapacities:
-    max_nodes: int              # obs nodes per tree (32 B + A x 32 B statistics block each)
+    max_nodes: int              # obs nodes per tree (256 B node block each: node + statistics)
     max_stats: int              # action statistics per tree (allocation counter limit)
     max_log: int                # particle log records per tree (16 B)
     hash_slots: int             # obs-child map slots per tree (16 B)
@@ -88,13 +97,47 @@ def plan_intmcp_capacities(config, step_limit: int, num_sims: int, searches: int
         log_table_size=total_sims + 2, discount_pow_size=min(L, 4096) + 2)
 
 
+# Wall-clock sizing.  One pair's simulation rate alone on the GPU (one lane,
+# chunked launches) is bounded by INTMCP_WALL_CLOCK_SIMS_PER_S per level
+# (measured 65-100 k/s per level on MI355X, tests/test_gpu_intmcp.py
+# test_wall_clock_episode_half_second; >= 2.5x margin): a search runs at
+# most that many simulations per level per second of its share of
+# search_time_limit.  The node arena is the smaller of the worst case for that
+# rate and the HBM budget; get_action's headroom check keeps a chunk inside it.
+INTMCP_WALL_CLOCK_SIMS_PER_S = 250_000
+INTMCP_WALL_CLOCK_HBM_BUDGET = 16 << 30
+_INTMCP_ID_LIMIT = (1 << 28) - 1
+
+
+def plan_intmcp_wallclock_capacities(config, step_limit: int, num_actions: int,
+                                     nesting_level: int = 1):
+    """Capacities of a wall-clock (``num_sims=None``) I-NTMCP engine; returns
+    (capacities, per-level simulation ceiling of one search)."""
+    per_level = config.search_time_limit / (nesting_level + 1)
+    sims = max(64, math.ceil(per_level * INTMCP_WALL_CLOCK_SIMS_PER_S))
+    searches = (step_limit if step_limit < INT32_MAX else 100) + 1
+    caps = plan_intmcp_capacities(config, step_limit, sims, searches, num_actions)
+    # per node and pair: two trees x (256 B block + 16 B log record + <=64 B of
+    # hash slots); per-search arrays (root belief, support) keep their worst case
+    per_node = 2 * (256 + 16 + 64)
+    fixed = caps.bytes_per_pair(num_actions) - caps.max_nodes * 2 * 256 \
+        - caps.max_log * 2 * 16 - caps.hash_slots * 2 * 16
+    nodes = (INTMCP_WALL_CLOCK_HBM_BUDGET - fixed) // per_node
+    nodes = max(1 << 16, min(caps.max_nodes, nodes, _INTMCP_ID_LIMIT))
+    caps.max_nodes = caps.max_log = nodes
+    caps.max_stats = num_actions * nodes
+    caps.hash_slots = _next_pow2(2 * nodes)
+    return caps, sims
+
+
 class IntmcpEngine:
     """Python handle on one ``intmcp_ctx`` (``num_pairs`` planner pairs)."""
 
     SELECTION = {"ucb": N.SEL_UCB, "uniform": N.SEL_UNIFORM}
 
     def __init__(self, model, agent_id, config, num_pairs=1, capacities=None, num_sims=None,
-                 searches=None, device=None, stream=None, tree_key_base=0, seed=None):
+                 searches=None, device=None, stream=None, tree_key_base=0, seed=None,
+                 wall_clock=False):
         lib = N.load()
         model = engine_model(model)   # posggym-style models by spec.id + kwargs
         if len(model.possible_agents) != 2:
@@ -119,6 +162,10 @@ class IntmcpEngine:
         else:
             step_limit = INT32_MAX
         self.step_limit = step_limit
+        self.wall_clock_sims = None
+        if capacities is None and wall_clock:
+            capacities, self.wall_clock_sims = plan_intmcp_wallclock_capacities(
+                config, step_limit, self.A)
         if capacities is None:
             sims = num_sims if num_sims is not None else (config.num_sims or 1024)
             budget = searches if searches is not None else (
@@ -150,8 +197,7 @@ class IntmcpEngine:
             s = int(np.random.SeedSequence().entropy) & (2**63 - 1)
         c.seed = int(s) & (2**64 - 1)
         c.tree_key_base = int(tree_key_base)
-        self._logtab = np.array([0.0] + [math.log(n) for n in range(1, capacities.log_table_size)],
-                                dtype=np.float64)
+        self._logtab = log_table(capacities.log_table_size)
         self._dpow = np.array([config.discount ** k for k in range(capacities.discount_pow_size)],
                               dtype=np.float64)
         c.log_table = self._logtab.ctypes.data_as(C.POINTER(C.c_double))
@@ -225,6 +271,26 @@ class IntmcpEngine:
     def root_stats(self):
         self._check(self._lib.intmcp_get_root_stats(self._ctx, self._stats), "get_root_stats")
         return self._stats
+
+    def headroom(self, stats=None):
+        """Simulations (of either level) that can still run in every pair
+        before the next update without overflowing a tree's arenas: each one
+        adds at most ``L`` nodes, statistics blocks and log records to each
+        tree, and the next update's reinvigoration is kept in reserve.  Uses
+        the counters of ``stats`` (``root_stats()``'s last result)."""
+        cfg, caps = self.config, self.capacities
+        L = min(cfg.depth_limit, self.step_limit) + 1
+        target = cfg.num_particles + cfg.extra_particles
+        reinv = int(math.ceil(cfg.reinvigoration_sample_limit_factor * target)) + target
+        reserve = 2 * reinv + 2 * target + 8        # plan_intmcp_capacities' per-update share
+        st = self._stats if stats is None else stats
+        room = INT32_MAX
+        for p in range(self.num_pairs):
+            for t in range(2):
+                left = min(caps.max_nodes - st[p].n_nodes[t], caps.max_log - st[p].n_log[t],
+                           (caps.max_stats - st[p].n_stats[t]) // self.A) - reserve
+                room = min(room, left // L)
+        return max(0, room)
 
     def root_belief(self, pair=0):
         """Level-1 root particles as (v0, v1, level-0 node) u32 rows."""
@@ -348,7 +414,8 @@ class INTMCP:
         self.other_agent_policies = {other: _NestedPlanner(self, other)}
         self._num_sims = num_sims if num_sims is not None else config.num_sims
         self._engine = IntmcpEngine(model, agent_id, config, num_pairs=1,
-                                    num_sims=self._num_sims or 1024)
+                                    num_sims=self._num_sims,
+                                    wall_clock=self._num_sims is None)
         self.step_limit = self._engine.step_limit
         self._logger = logging.getLogger()
         self._last_action = None
@@ -438,15 +505,26 @@ class INTMCP:
         if self._num_sims is not None:
             self._engine.search(self._num_sims, fetch=False)
         else:
+            # the reference's per-level time split (intmcp.py:383-397) as
+            # launches of growing chunks, each within the arena headroom and the
+            # per-level ceiling the arenas were sized for; a full arena ends the
+            # search early (step_statistics "arena_full"), it does not fail
             per_level = self.config.search_time_limit / (self.nesting_level + 1)
+            ceiling = self._engine.wall_clock_sims
             flags = N.INTMCP_BEGIN
+            room = self._engine.headroom(self._engine.root_stats())
             for level in range(self.nesting_level + 1):
-                t0, chunk = time.time(), 16
-                while time.time() - t0 < per_level:
-                    sims = (chunk, 0) if level == 0 else (0, chunk)
+                t0, chunk, done = time.time(), 16, 0
+                while time.time() - t0 < per_level and done < ceiling:
+                    n = min(chunk, room, ceiling - done)
+                    if n <= 0:
+                        self.step_statistics["arena_full"] = True
+                        break
+                    sims = (n, 0) if level == 0 else (0, n)
                     self._engine.search_levels(sims[0], sims[1], flags)
                     flags = 0
-                    self._engine.root_stats()          # synchronises
+                    room = self._engine.headroom(self._engine.root_stats())   # synchronises
+                    done += n
                     chunk = min(chunk * 2, 4096)
             self._engine.search_levels(0, 0, flags | N.INTMCP_FINAL)
         st = self._engine.root_stats()[0]

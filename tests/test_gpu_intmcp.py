@@ -88,3 +88,52 @@ def test_device_softmax_exp_equals_math_exp():
     ref = _py_exp(x)
     bad = np.nonzero(~_same(out, ref))[0]
     assert len(bad) == 0, [(x[i].hex(), out[i].hex(), ref[i].hex()) for i in bad[:5]]
+
+
+def _wall_clock_episode(time_limit, env_seed, max_steps):
+    from gpu_util import product_model
+    from oracle.episode import run_episode
+    from posggym_baselines_amd.planning import INTMCP, MCTSConfig
+    model = product_model("Driving-v1")
+    cfg = MCTSConfig(**dict(TEST_CFG, search_time_limit=time_limit))   # num_sims=None
+    planner = INTMCP.initialize(model, "0", cfg, 1, None)
+    planner.reset()
+    steps = []
+
+    def step(obs):
+        a = planner.step(obs)
+        if not planner.root.is_absorbing:
+            steps.append(dict(planner.step_statistics, visits=planner.root.visits,
+                              child_visits=sum(c[1] for c in planner.root.children)))
+        return a
+
+    trace = run_episode(step, env_seed, max_steps=max_steps)
+    planner.close()
+    return trace, steps, planner._engine.wall_clock_sims
+
+
+def test_wall_clock_episode_half_second():
+    """The reference's default mode (num_sims=None, intmcp.py:383-397: the time
+    limit split over the levels) over a whole Driving-v1 episode at
+    search_time_limit=0.5: arenas sized from the time limit, every chunk within
+    the headroom, no POMCP_E_ARENA and no early stop."""
+    trace, steps, ceiling = _wall_clock_episode(0.5, 41, 50)
+    assert trace["len"] >= 3 and len(steps) >= 2
+    for st in steps:
+        assert not st.get("arena_full")
+        assert 0.45 <= st["search_time"] < 2.0
+        assert 64 < st["num_sims"] <= 2 * ceiling
+        assert 0 < st["child_visits"] <= st["visits"]
+    print("I-NTMCP wall-clock sims per step:", [st["num_sims"] for st in steps])
+
+
+def test_wall_clock_small_arena_stops_early(monkeypatch):
+    """A 64 K-node arena (the floor) cannot hold a 1 s episode: the chunk loop
+    stops at the headroom (step_statistics["arena_full"]) instead of failing,
+    the update's reinvigoration still fits, and every step returns an action."""
+    from posggym_baselines_amd.planning import intmcp as M
+    monkeypatch.setattr(M, "INTMCP_WALL_CLOCK_HBM_BUDGET", 1)
+    trace, steps, _ = _wall_clock_episode(1.0, 41, 12)
+    assert len(steps) >= 3
+    assert any(st.get("arena_full") for st in steps)
+    assert all(st["child_visits"] <= st["visits"] for st in steps)

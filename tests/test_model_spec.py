@@ -45,3 +45,31 @@ def test_pursuit_evasion_spec_maps_to_restatement():
 def test_unsupported_models_raise(bad):
     with pytest.raises(NotImplementedError):
         engine_model(bad)
+
+
+def test_intmcp_wallclock_capacities_within_budget():
+    """Wall-clock I-NTMCP arenas: the per-level simulation ceiling follows the
+    time limit, the node arena stays inside the HBM budget, and the headroom
+    keeps the next update's reinvigoration in reserve."""
+    from types import SimpleNamespace
+    from posggym_baselines_amd.planning import MCTSConfig
+    from posggym_baselines_amd.planning import intmcp as M
+    for tl in (0.1, 1.0, 10.0):
+        cfg = MCTSConfig(discount=0.95, c=1.4, truncated=False, search_time_limit=tl)
+        caps, sims = M.plan_intmcp_wallclock_capacities(cfg, 50, 5)
+        assert sims == max(64, int(tl / 2 * M.INTMCP_WALL_CLOCK_SIMS_PER_S + 0.999))
+        assert caps.bytes_per_pair(5) <= M.INTMCP_WALL_CLOCK_HBM_BUDGET * 1.1
+        assert caps.max_nodes < 1 << 28 and caps.hash_slots >= 2 * caps.max_nodes
+        assert caps.log_table_size >= 2 * sims * 51
+    cfg = MCTSConfig(discount=0.95, c=1.4, truncated=False, search_time_limit=1.0)
+    caps, _ = M.plan_intmcp_wallclock_capacities(cfg, 50, 5)
+    eng = object.__new__(M.IntmcpEngine)
+    eng.config, eng.capacities, eng.step_limit, eng.A, eng.num_pairs = cfg, caps, 50, 5, 1
+    L = min(cfg.depth_limit, 50) + 1
+    target = cfg.num_particles + cfg.extra_particles
+    reserve = 2 * (int(-(-cfg.reinvigoration_sample_limit_factor * target // 1)) + target) \
+        + 2 * target + 8
+    st = [SimpleNamespace(n_nodes=[10, 20], n_log=[5, 5], n_stats=[50, 100])]
+    assert eng.headroom(st) == (caps.max_nodes - 20 - reserve) // L
+    st = [SimpleNamespace(n_nodes=[caps.max_nodes - reserve, 0], n_log=[0, 0], n_stats=[0, 0])]
+    assert eng.headroom(st) == 0
