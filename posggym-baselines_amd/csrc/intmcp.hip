@@ -326,7 +326,11 @@ struct ImPair {
       const double log_n = logn(x.visits);
       double best = -__builtin_inf();
       int ba = 0;
-      for (int i = 0; i < nr; ++i) {
+      // unrolled with a bound check: the arrays stay in registers (a loop to
+      // nr indexes them dynamically, which puts them in scratch memory)
+#pragma unroll
+      for (int i = 0; i < kImMaxA; ++i) {
+        if (i >= nr) break;
         const int a = im_order(x.info, i);
         const int sv = (int)q[i].x;
         if (sv == 0) return a;
@@ -339,7 +343,9 @@ struct ImPair {
       return ba;
     }
     int min_n = x.visits + 1, nxt = 0;            // min_visit_action_selection
-    for (int i = 0; i < nr; ++i) {
+#pragma unroll
+    for (int i = 0; i < kImMaxA; ++i) {
+      if (i >= nr) break;
       const int a = im_order(x.info, i);
       const int v = (int)q[i].x;
       if (v < min_n) {
@@ -351,8 +357,11 @@ struct ImPair {
   }
 
   // INTMCP.sample_action of the level-0 planner (intmcp.py:763-791) at node n
-  __device__ int sample_action(int n, const View* pre = nullptr) {
-    View v = pre ? *pre : view(1, n);   // node + statistics: one round trip
+  __device__ int sample_action(int n) {
+    View v = view(1, n);                // node + statistics: one round trip
+    return sample_action(n, v);
+  }
+  __device__ int sample_action(int n, View v) {
     if (n > 0 && !im_path_ok(v.x.info)) {
       traverse(1, n);
       v = view(1, n);
@@ -365,25 +374,33 @@ struct ImPair {
     child_stats(v, nr, q);
     double pr[kImMaxA];
     double total = 0.0;
-    for (int i = 0; i < nr; ++i) {
+#pragma unroll
+    for (int i = 0; i < kImMaxA; ++i) {
+      if (i >= nr) break;
       pr[i] = host_exp((double)(int)q[i].x / sq);   // == math.exp (host_exp.h)
       total = i == 0 ? pr[i] : total + pr[i];
     }
     // random.choices(children, weights=p / sum): cum weights, x = random() * total
     double cum[kImMaxA];
     double acc = 0.0;
-    for (int i = 0; i < nr; ++i) {
+#pragma unroll
+    for (int i = 0; i < kImMaxA; ++i) {
+      if (i >= nr) break;
       const double w = pr[i] / total;
       acc = i == 0 ? w : acc + w;
       cum[i] = acc;
     }
-    const double u = d_sel_float() * (cum[nr - 1] + 0.0);
-    int lo = 0, hi = nr - 1;   // bisect_right(cum, u, 0, n - 1)
-    while (lo < hi) {
-      const int mid = (lo + hi) / 2;
-      if (u < cum[mid]) hi = mid;
-      else lo = mid + 1;
-    }
+    double last = cum[0];
+#pragma unroll
+    for (int i = 1; i < kImMaxA; ++i)
+      if (i == nr - 1) last = cum[i];
+    const double u = d_sel_float() * (last + 0.0);
+    // bisect_right(cum, u, 0, nr - 1) over the non-decreasing cum: the first
+    // i < nr - 1 with u < cum[i], else nr - 1 (a scan keeps cum in registers)
+    int lo = nr - 1;
+#pragma unroll
+    for (int i = kImMaxA - 2; i >= 0; --i)
+      if (i < nr - 1 && u < cum[i]) lo = i;
     return im_order(x.info, lo);
   }
 
@@ -481,7 +498,8 @@ struct ImPair {
       // the other agent's action (intmcp.py:602-615): at level 1 its
       // history node's view was loaded when the previous level created it
       const bool nested_k = k == 0 && !p.state_belief_only;
-      const int ao = nested_k ? sample_action((int)nested, have_nv ? &nv : nullptr)
+      const int ao = nested_k ? (have_nv ? sample_action((int)nested, nv)
+                                         : sample_action((int)nested))
                               : other_action(k, nested);
       uint32_t n0, n1, nn = 0u;
       double r;
