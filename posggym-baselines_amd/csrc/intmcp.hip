@@ -311,7 +311,7 @@ struct ImPair {
       uint4 r = v.sh[0];
 #pragma unroll
       for (int j = 1; j < kImMaxA; ++j)
-        if (j == a) r = v.sh[j];
+        r = sel4(j == a, v.sh[j], r);
       q[i] = i < nr ? r : make_uint4(0, 0, 0, 0);
     }
   }
@@ -494,7 +494,7 @@ struct ImPair {
       uint4 sa = v.sh[0];
 #pragma unroll
       for (int q = 1; q < kImMaxA; ++q)
-        if (q == a) sa = v.sh[q];
+        sa = sel4(q == a, v.sh[q], sa);
       // the other agent's action (intmcp.py:602-615): at level 1 its
       // history node's view was loaded when the previous level created it
       const bool nested_k = k == 0 && !p.state_belief_only;

@@ -184,6 +184,14 @@ __device__ __forceinline__ double rl_d(double v, int l) {
   return __hiloint2double(hi, lo);
 }
 
+// c ? a : b for uint4, component by component.  A conditional operator or a
+// conditional assignment on the vector struct is an aggregate copy whose
+// source clang picks by address (a select of pointers): an array read that way
+// ("if (q == a) x = arr[q]") stays in scratch memory instead of registers.
+__device__ __forceinline__ uint4 sel4(bool c, uint4 a, uint4 b) {
+  return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+}
+
 __device__ __forceinline__ double hilo_d(uint32_t lo, uint32_t hi) {
   return __hiloint2double((int)hi, (int)lo);
 }

@@ -327,8 +327,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   }
 
   // Overflow children (beyond the kSlots inline ones) of action node ani.
-  auto ovf_child = [&](uint32_t ani, uint64_t okey, int done, uint32_t* cid, int* cblk, int* cvis,
-                       int32_t** cptr) {
+  // Returns its results by value: out-parameters would keep the caller's
+  // locals in scratch memory.
+  struct OvfChild {
+    uint32_t cid;
+    int cblk, cvis;
+    int32_t* cptr;
+  };
+  auto ovf_child = [&](uint32_t ani, uint64_t okey, int done, int cblk, int cvis) -> OvfChild {
+    OvfChild o{0u, cblk, cvis, nullptr};
     const uint64_t key = okey | ((uint64_t)epoch << kEpochShift);
     uint32_t b = ovf_hash(ani, okey) & p.bucket_mask;
     bool found = false;
@@ -342,16 +349,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         if (!live || (skey == key && w0.z == ani)) {
           if (live) {
             const uint4 w1 = reinterpret_cast<const uint4*>(ep)[1];
-            *cblk = (int)w1.x;
-            *cvis = (int)w1.y + 1;
+            o.cblk = (int)w1.x;
+            o.cvis = (int)w1.y + 1;
           } else {
             ++n_nodes;
           }
           reinterpret_cast<uint4*>(ep)[0] =
               make_uint4((uint32_t)key, (uint32_t)(key >> 32), ani, (uint32_t)done);
-          reinterpret_cast<uint4*>(ep)[1] = make_uint4((uint32_t)*cblk, (uint32_t)*cvis, 0u, 0u);
-          *cid = p.ovf_base + b * kBucket + (uint32_t)e;
-          *cptr = &ep->block;
+          reinterpret_cast<uint4*>(ep)[1] = make_uint4((uint32_t)o.cblk, (uint32_t)o.cvis, 0u, 0u);
+          o.cid = p.ovf_base + b * kBucket + (uint32_t)e;
+          o.cptr = &ep->block;
           found = true;
           break;
         }
@@ -359,6 +366,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
       b = (b + 1) & p.bucket_mask;
     }
     if (!found) err = POMCP_E_ARENA;
+    return o;
   };
 
   // The generative step of one tree level (mcts.py:331-352) for ego action a.
@@ -468,14 +476,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
           uint4 sl[kSlots];
 #pragma unroll
           for (int q = 1; q < kMaxA; ++q)
-            if (q == a) sa = st[q];
+            sa = sel4(q == a, st[q], sa);
 #pragma unroll
           for (int q = 0; q < kSlots; ++q)
             sl[q] = kRootSlotsInLds ? rc[rc_slot(a, q)][lid] : rb[part_slot(a, q)];
           r0_s1 = r1[0];
 #pragma unroll
-          for (int q = 1; q < kMaxA; ++q)
-            if (q == a) r0_s1 = r1[q];
+          for (int q = 1; q < kMaxA; ++q) r0_s1 = sel4(q == a, r1[q], r0_s1);   // (sel4: registers)
           uint32_t n0, n1;
           double r;
           int done;
@@ -490,13 +497,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
             uint4 sk = sl[0];
 #pragma unroll
             for (int q = 1; q < kSlots; ++q)
-              if (q == ks) sk = sl[q];
-            if (match) {
-              cblk = (int)sk.z;
-              cvis = (int)sk.w + 1;
-            } else {
-              ++n_nodes;
-            }
+              sk = sel4(q == ks, sl[q], sk);
+            // selects, not if / else: stores to different locals in the two
+            // branches get merged into one store through a pointer
+            cblk = match ? (int)sk.z : cblk;
+            cvis = match ? (int)sk.w + 1 : cvis;
+            n_nodes += match ? 0 : 1;
             const uint64_t nk = okey | kValidBit | ((uint64_t)done << 63);
             const uint4 nsl = make_uint4((uint32_t)nk, (uint32_t)(nk >> 32), (uint32_t)cblk, (uint32_t)cvis);
             cid = ani * kSlots + (uint32_t)ks + 1u;
@@ -510,7 +516,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
               leaf_rc = -1;
             }
           } else {
-            ovf_child(ani, okey, done, &cid, &cblk, &cvis, &leaf_ptr);
+            const OvfChild o = ovf_child(ani, okey, done, cblk, cvis);
+            cid = o.cid;
+            cblk = o.cblk;
+            cvis = o.cvis;
+            leaf_ptr = o.cptr;
             leaf_rc = -1;
           }
           if (err != 0 || n_log >= p.Np) {
@@ -555,7 +565,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         uint4 sa = st[0];
   #pragma unroll
         for (int q = 1; q < kMaxA; ++q)
-          if (q == a) sa = st[q];
+          sa = sel4(q == a, st[q], sa);
         // the chosen action's stats1 and child slots (second round trip)
         const uint4 s1a = ap[part_stats1(a)];
         uint4 sl[kSlots];
@@ -579,20 +589,21 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
           uint4 sk = sl[0];
   #pragma unroll
           for (int q = 1; q < kSlots; ++q)
-            if (q == ks) sk = sl[q];
-          if (match) {
-            cblk = (int)sk.z;
-            cvis = (int)sk.w + 1;
-          } else {
-            ++n_nodes;
-          }
+            sk = sel4(q == ks, sl[q], sk);
+          cblk = match ? (int)sk.z : cblk;   // (selects, as at the root level)
+          cvis = match ? (int)sk.w + 1 : cvis;
+          n_nodes += match ? 0 : 1;
           const uint64_t nk = okey | kValidBit | ((uint64_t)done << 63);
           uint4* slot = const_cast<uint4*>(ap) + part_slot(a, ks);
           *slot = make_uint4((uint32_t)nk, (uint32_t)(nk >> 32), (uint32_t)cblk, (uint32_t)cvis);
           cid = ani * kSlots + (uint32_t)ks + 1u;
           leaf_ptr = reinterpret_cast<int32_t*>(slot) + 2;
         } else {
-          ovf_child(ani, okey, done, &cid, &cblk, &cvis, &leaf_ptr);
+          const OvfChild o = ovf_child(ani, okey, done, cblk, cvis);
+          cid = o.cid;
+          cblk = o.cblk;
+          cvis = o.cvis;
+          leaf_ptr = o.cptr;
         }
         PT_MARK(13);
         if (err != 0 || n_log >= p.Np || plen >= kMaxPath) {
@@ -695,8 +706,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         const uint4 s1n = make_uint4((uint32_t)__double2loint(total), (uint32_t)__double2hiint(total),
                                      (uint32_t)__double2loint(agg), (uint32_t)__double2hiint(agg));
 #pragma unroll
-        for (int q = 0; q < kMaxA; ++q)
-          if (q == a) r1[q] = s1n;
+        for (int q = 0; q < kMaxA; ++q) r1[q] = sel4(q == a, s1n, r1[q]);
         if (value > mm_max) mm_max = value;
         if (value < mm_min) mm_min = value;
       }

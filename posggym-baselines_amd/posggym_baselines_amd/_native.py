@@ -286,6 +286,13 @@ def load():
         raise ImportError(
             f"{LIB_PATH} is missing: build it with `python -m posggym_baselines_amd.build` "
             "(or __graft_entry__.build()); there is no CPU fallback for the planner")
+    # One HIP runtime per process: PyTorch ships its own libamdhip64.so.7 (same
+    # soname as /opt/rocm's).  Whichever loads first serves both; torch only
+    # initialises on its own copy, so it is loaded before this library.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(LIB_PATH)
     for name, res, args in SIGNATURES + DEBUG_SIGNATURES + INTMCP_SIGNATURES:
         fn = getattr(lib, name)
