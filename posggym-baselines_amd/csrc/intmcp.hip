@@ -34,6 +34,8 @@ constexpr int kImRegPath = 4;         // path levels held in registers (deeper o
 constexpr int64_t kImBlock = 256;
 constexpr uint32_t kImNoSupport = 0xFFFFFFFFu;
 constexpr int32_t kImSkip = -2;       // intmcp_update action: leave the pair untouched
+constexpr int kImLogLds = 2048;       // math.log(N) entries staged in LDS by k_im_search
+constexpr int kImRootWords = 8;       // the level-1 root's view (INode + 6 heads) in LDS, uint4s
 
 struct INode {          // 32 B
   int32_t parent;
@@ -119,6 +121,13 @@ struct ImPair {
   int4* path;
   double* prob;   // [Nr]
   IHdr h;
+  // k_im_search only: math.log(N) for N < lt_n staged in LDS, and the level-1
+  // root's view (this lane's column of an [kImRootWords][64] uint4 array),
+  // which only this lane's backups at the root change during a search
+  const double* lt_lds = nullptr;
+  int lt_n = 0;
+  uint4* rv = nullptr;
+  int rv_root = -1;
 
   __device__ ImPair(const ImParams& pp, const Model& mm, int b) : p(pp), m(mm), pair(b) {
     for (int k = 0; k < 2; ++k) {
@@ -159,6 +168,22 @@ struct ImPair {
     const uint4* s = H(k, n);
 #pragma unroll
     for (int q = 0; q < kImMaxA; ++q) v.sh[q] = q < p.A ? s[q] : make_uint4(0, 0, 0, 0);
+    return v;
+  }
+  __device__ void rv_put(const View& v) {
+    uint4 w[2];
+    __builtin_memcpy(w, &v.x, sizeof(INode));
+    rv[0] = w[0];
+    rv[kWave] = w[1];
+#pragma unroll
+    for (int q = 0; q < kImMaxA; ++q) rv[(2 + q) * kWave] = v.sh[q];
+  }
+  __device__ View rv_get() const {
+    View v;
+    uint4 w[2] = {rv[0], rv[kWave]};
+    __builtin_memcpy(&v.x, w, sizeof(INode));
+#pragma unroll
+    for (int q = 0; q < kImMaxA; ++q) v.sh[q] = rv[(2 + q) * kWave];
     return v;
   }
   __device__ void fail(int code) {
@@ -291,6 +316,7 @@ struct ImPair {
     return h.mm_max[k] > h.mm_min[k] ? (v - h.mm_min[k]) / (h.mm_max[k] - h.mm_min[k]) : v;
   }
   __device__ double logn(int n) {
+    if (n < lt_n) return lt_lds[n];
     if (n >= p.logtab_n) {
       fail(POMCP_E_ARENA);
       return 0.0;
@@ -431,6 +457,9 @@ struct ImPair {
       fail(POMCP_E_ARENA);
       return;
     }
+#ifdef IM_ABLATE_LOG   // ablation build only (measurement): no particle log stores
+    if (node >= 0) return;
+#endif
     IRec r;
     r.node = (uint32_t)node;
     r.v0 = v0;
@@ -441,6 +470,9 @@ struct ImPair {
 
   // ------------------------------------------------------------ rollout
   __device__ double rollout(int k, uint32_t s0, uint32_t s1, int t, int depth) {   // intmcp.py:547-593
+#ifdef IM_ABLATE_ROLLOUT   // ablation build only (measurement): no rollout
+    return 0.0;
+#endif
     double ret = 0.0;
     int kk = 0;
     const int me = agent(k);
@@ -575,8 +607,10 @@ struct ImPair {
       const double delta = g - value0;
       const double value = value0 + delta / (double)vis;
       const double agg = hilo_d(e2.z, e2.w) + delta * (g - value);
-      H(k, (int)e0.x)[e0.y] = make_uint4((uint32_t)vis, 0u, (uint32_t)__double2loint(value),
-                                         (uint32_t)__double2hiint(value));
+      const uint4 head = make_uint4((uint32_t)vis, 0u, (uint32_t)__double2loint(value),
+                                    (uint32_t)__double2hiint(value));
+      H(k, (int)e0.x)[e0.y] = head;
+      if (k == 0 && (int)e0.x == rv_root) rv[(2 + e0.y) * kWave] = head;   // the cached root view
       T(k, (int)e0.x)[e0.y] = make_uint4((uint32_t)__double2loint(total), (uint32_t)__double2hiint(total),
                                          (uint32_t)__double2loint(agg), (uint32_t)__double2hiint(agg));
       mm_update(k, value);
@@ -944,10 +978,17 @@ constexpr int kImBegin = 1, kImFinal = 2;
 template <class Env>
 __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sims1, int flags) {
   __shared__ typename Env::Model sm;
-  stage_model(p.model, sm);
+  __shared__ double slog[kImLogLds];                  // math.log(N): no global load per selection
+  __shared__ uint4 srv[kImRootWords * kWave];         // level-1 root views, one column per lane
+  const int ltn = p.logtab_n < kImLogLds ? (int)p.logtab_n : kImLogLds;
+  for (int i = threadIdx.x; i < ltn; i += blockDim.x) slog[i] = p.logtab[i];
+  stage_model(p.model, sm);                           // (synchronises)
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= p.B) return;
   ImPair<Env> P(p, sm, b);
+  P.lt_lds = slog;
+  P.lt_n = ltn;
+  P.rv = srv + threadIdx.x;
   if (flags & kImBegin) {
     P.h.num_sims = 0;
     P.h.search_depth = 0;
@@ -977,6 +1018,10 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
       if (num_sims > 0) {
         hp_next = rb[P.d_bel(1, (uint32_t)P.h.root_size)];
         if (level == 0) e_next = stab[hp_next.w];
+        if (level == 1) {   // the root's view, kept current by the backups (ImPair::rv)
+          P.rv_put(P.view(0, root));
+          P.rv_root = root;
+        }
       }
       for (int s = 0; s < num_sims && P.h.err == 0; ++s) {
         const uint4 hp = hp_next;
@@ -1004,10 +1049,12 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
             v = P.view(1, n);
           }
           P.simulate(1, q.x, q.y, 0u, n, v);
-          P.N(1, n).visits += 1;
+          P.N(1, n).visits = v.x.visits + 1;   // (simulate writes no INode of its start)
         } else {
-          const int d = P.simulate(0, hp.x, hp.y, hp.z, root, P.view(0, root));
-          P.N(0, root).visits += 1;
+          const auto v = P.rv_get();
+          const int d = P.simulate(0, hp.x, hp.y, hp.z, root, v);
+          P.N(0, root).visits = v.x.visits + 1;
+          P.rv[0].z = (uint32_t)(v.x.visits + 1);   // INode.visits: bytes 8-11
           if (d > P.h.search_depth) P.h.search_depth = d;
         }
         P.h.num_sims += 1;
