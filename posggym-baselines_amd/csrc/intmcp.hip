@@ -32,6 +32,14 @@ constexpr int kImRegPath = 4;         // path levels held in registers (deeper o
 // {total, agg} tails.  A node view (selection, the other agent's softmax)
 // is one line; the chosen action's tail is read for the backup only.
 constexpr int64_t kImBlock = 256;
+// Node blocks are interleaved by wavefront: [B / 64][2 trees][Nn][64 lanes]
+// blocks, so the 64 pairs of a wave keep node n of their trees side by side
+// and a wave's loads spread over the blocks in use, not over 64 separate
+// per-pair slabs (fewer pages per load instruction to translate).
+constexpr int64_t kImNodeStride = kWave * kImBlock;   // node n -> n + 1 of one tree
+__host__ __device__ __forceinline__ int64_t im_node_off(int64_t Nn, int b, int k, int64_t n) {
+  return ((((int64_t)(b / kWave) * 2 + k) * Nn + n) * kWave + (b % kWave)) * kImBlock;
+}
 constexpr uint32_t kImNoSupport = 0xFFFFFFFFu;
 constexpr int32_t kImSkip = -2;       // intmcp_update action: leave the pair untouched
 constexpr int kImLogLds = 2048;       // math.log(N) entries staged in LDS by k_im_search
@@ -79,8 +87,8 @@ struct ImParams {
   int64_t Nn, Ns, Nl, H, Nr, Nsp;   // per tree: nodes, stat entries, log records, hash slots;
                                     // per pair: root belief, support particles
   IHdr* hdr;
-  char* nodes;          // [B][2][Nn] node blocks (kImBlock B, see ImPair::N)
-  int64_t nstride;      // kImBlock
+  char* nodes;          // [B / 64][2][Nn][64] node blocks (kImBlock B, im_node_off)
+  int64_t nstride;      // kImNodeStride
   IHash* hash;          // [B][2][H]
   IRec* log;            // [B][2][Nl]
   uint4* root;          // [B][2][Nr] {v0, v1, nested, support slot}
@@ -131,7 +139,7 @@ struct ImPair {
 
   __device__ ImPair(const ImParams& pp, const Model& mm, int b) : p(pp), m(mm), pair(b) {
     for (int k = 0; k < 2; ++k) {
-      nb[k] = p.nodes + ((int64_t)b * 2 + k) * p.Nn * p.nstride;
+      nb[k] = p.nodes + im_node_off(p.Nn, b, k, 0);
       hs[k] = p.hash + ((int64_t)b * 2 + k) * p.H;
       lg[k] = p.log + ((int64_t)b * 2 + k) * p.Nl;
     }
@@ -148,13 +156,13 @@ struct ImPair {
   // statistics (node.py:120-178) in one line, so a node and its statistics
   // arrive together (they used to be an index apart: two dependent loads).
   __device__ __forceinline__ INode& N(int k, int n) const {
-    return *reinterpret_cast<INode*>(nb[k] + (int64_t)n * kImBlock);
+    return *reinterpret_cast<INode*>(nb[k] + (int64_t)n * kImNodeStride);
   }
   __device__ __forceinline__ uint4* H(int k, int n) const {   // {visits, -, value} per action
-    return reinterpret_cast<uint4*>(nb[k] + (int64_t)n * kImBlock + 32);
+    return reinterpret_cast<uint4*>(nb[k] + (int64_t)n * kImNodeStride + 32);
   }
   __device__ __forceinline__ uint4* T(int k, int n) const {   // {total, agg} per action
-    return reinterpret_cast<uint4*>(nb[k] + (int64_t)n * kImBlock + 128);
+    return reinterpret_cast<uint4*>(nb[k] + (int64_t)n * kImNodeStride + 128);
   }
   // the node and the {visits, -, value} head of every action's statistics,
   // issued together (entries of unregistered actions are never used)
@@ -307,6 +315,41 @@ struct ImPair {
   __device__ void expand(int k, int n) {
     for (int a = 0; a < p.A; ++a) reg(k, n, a);
   }
+  // expand() of node n whose INode the caller holds current (x, updated):
+  // the same registrations in action order, no reads -- reg() re-reads the
+  // node for every action, a dependent round trip each
+  __device__ void expand_known(int k, int n, INode& x) {
+    uint32_t info = x.info;
+    int nr = im_nreg(info);
+    bool alloc = false;
+    for (int a = 0; a < p.A; ++a) {
+      bool have = false;
+      for (int i = 0; i < nr; ++i) have |= im_order(info, i) == a;
+      if (have) continue;
+      if (nr >= 6) {
+        fail(POMCP_E_INVALID);
+        break;
+      }
+      info = (info & ~(7u << 5)) | ((uint32_t)(nr + 1) << 5) | ((uint32_t)a << (8 + 3 * nr));
+      ++nr;
+      alloc |= x.stats < 0;
+    }
+    if (alloc) {
+      if (h.n_stats[k] + p.A > p.Ns) {
+        fail(POMCP_E_ARENA);
+        return;
+      }
+      x.stats = h.n_stats[k];
+      h.n_stats[k] += p.A;
+      for (int q = 0; q < p.A; ++q) {
+        H(k, n)[q] = make_uint4(0, 0, 0, 0);
+        T(k, n)[q] = make_uint4(0, 0, 0, 0);
+      }
+      N(k, n).stats = x.stats;
+    }
+    x.info = info;
+    N(k, n).info = info;
+  }
 
   __device__ void mm_update(int k, double v) {
     if (v > h.mm_max[k]) h.mm_max[k] = v;
@@ -389,8 +432,8 @@ struct ImPair {
   }
   __device__ int sample_action(int n, View v) {
     if (n > 0 && !im_path_ok(v.x.info)) {
-      traverse(1, n);
-      v = view(1, n);
+      traverse(1, n);           // registers n's path at its ancestors; n itself
+      v.x.info |= 1u << 4;      // only gains the path_ok bit (no reload)
     }
     const INode& x = v.x;
     const int nr = im_nreg(x.info);
@@ -516,7 +559,8 @@ struct ImPair {
       const INode& x = v.x;
       if (depth > p.depth_limit || x.t + depth > p.step_limit) break;
       if (im_nreg(x.info) < p.A) {                 // leaf: add the missing children
-        expand(k, n);
+        INode xe = x;
+        expand_known(k, n, xe);
         leaf = rollout(k, s0, s1, x.t, depth);
         break;
       }
@@ -813,7 +857,7 @@ __global__ __launch_bounds__(64) void k_im_reset(ImParams p) {
     r.stats = -1;
     r.support = kImNoSupport;
     r.okey = 0;
-    *reinterpret_cast<INode*>(p.nodes + ((int64_t)b * 2 + k) * p.Nn * p.nstride) = r;
+    *reinterpret_cast<INode*>(p.nodes + im_node_off(p.Nn, b, k, 0)) = r;
     h.n_nodes[k] = 1;
     h.n_stats[k] = 0;
     h.n_log[k] = 0;
@@ -1041,12 +1085,13 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
           const uint2 q = sparts[e.off + P.d_bel(0, (uint32_t)e.size)];
           auto v = P.view(1, n);
           if (n > 0 && !im_path_ok(v.x.info)) {
-            P.traverse(1, n);
-            v = P.view(1, n);
+            P.traverse(1, n);         // (n itself only gains the path_ok bit)
+            v.x.info |= 1u << 4;
           }
           if (im_nreg(v.x.info) == 0) {
-            P.expand(1, n);
-            v = P.view(1, n);
+            P.expand_known(1, n, v.x);   // nothing registered: fresh, zero statistics
+#pragma unroll
+            for (int q = 0; q < kImMaxA; ++q) v.sh[q] = make_uint4(0, 0, 0, 0);
           }
           P.simulate(1, q.x, q.y, 0u, n, v);
           P.N(1, n).visits = v.x.visits + 1;   // (simulate writes no INode of its start)

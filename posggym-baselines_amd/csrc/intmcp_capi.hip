@@ -25,7 +25,7 @@ __global__ __launch_bounds__(64) void k_im_root_stats(ImParams d, intmcp_root_st
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= d.B) return;
   const IHdr h = d.hdr[t];
-  const char* const blk = d.nodes + ((int64_t)t * 2 * d.Nn + h.cur) * kImBlock;
+  const char* const blk = d.nodes + im_node_off(d.Nn, t, 0, h.cur);
   const INode node = *reinterpret_cast<const INode*>(blk);
   intmcp_root_stats o;
   memset(&o, 0, sizeof(o));
@@ -97,6 +97,17 @@ template <class T>
 static int im_copy(intmcp_ctx* ctx, T* dst, const T* src, size_t n) {
   if (n == 0) return POMCP_OK;
   IM_TRY(ctx, hipMemcpyAsync(dst, src, sizeof(T) * n, hipMemcpyDeviceToHost, ctx->stream));
+  IM_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return POMCP_OK;
+}
+
+// blocks 0..n-1 of one tree of one pair, packed (the device layout interleaves
+// them by wave: im_node_off)
+static int im_copy_blocks(intmcp_ctx* ctx, std::vector<char>& out, int pair, int tree, int n) {
+  out.resize((size_t)n * kImBlock);
+  if (n == 0) return POMCP_OK;
+  IM_TRY(ctx, hipMemcpy2DAsync(out.data(), kImBlock, ctx->ip.nodes + im_node_off(ctx->ip.Nn, pair, tree, 0),
+                               kImNodeStride, kImBlock, n, hipMemcpyDeviceToHost, ctx->stream));
   IM_TRY(ctx, hipStreamSynchronize(ctx->stream));
   return POMCP_OK;
 }
@@ -210,8 +221,8 @@ int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, in
     d.field = reinterpret_cast<decltype(d.field)>(p);                           \
   } while (0)
   IM_ALLOC(hdr, IHdr, B);
-  d.nstride = kImBlock;   // node blocks (intmcp.hip)
-  IM_ALLOC(nodes, char, B * 2 * d.Nn * d.nstride);
+  d.nstride = kImNodeStride;   // node blocks (intmcp.hip), interleaved by wave
+  IM_ALLOC(nodes, char, (B + kWave - 1) / kWave * kWave * 2 * d.Nn * kImBlock);
   IM_ALLOC(hash, IHash, B * 2 * d.H);
   IM_ALLOC(log, IRec, B * 2 * d.Nl);
   IM_ALLOC(root, uint4, B * 2 * d.Nr);
@@ -391,10 +402,9 @@ int intmcp_get_nodes(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int
   *count = n;
   if (!out || capacity < n) return POMCP_OK;
   // the INode of every block (layout: intmcp.hip ImPair::N)
-  const int64_t ns = ctx->ip.nstride;
-  std::vector<char> blocks((size_t)n * (size_t)ns);
-  rc = im_copy(ctx, blocks.data(), ctx->ip.nodes + ((int64_t)pair * 2 + tree) * ctx->ip.Nn * ns,
-               blocks.size());
+  const int64_t ns = kImBlock;
+  std::vector<char> blocks;
+  rc = im_copy_blocks(ctx, blocks, pair, tree, n);
   if (rc != POMCP_OK) return rc;
   INode* o = reinterpret_cast<INode*>(out);
   for (int i = 0; i < n; ++i) std::memcpy(&o[i], blocks.data() + (size_t)i * ns, sizeof(INode));
@@ -412,10 +422,9 @@ int intmcp_get_stats(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int
   // statistics in allocation order (INode.stats = their first index), gathered
   // from the node blocks
   const int nn = ctx->host_hdr[pair].n_nodes[tree];
-  const int64_t ns = ctx->ip.nstride;
-  std::vector<char> blocks((size_t)nn * (size_t)ns);
-  rc = im_copy(ctx, blocks.data(), ctx->ip.nodes + ((int64_t)pair * 2 + tree) * ctx->ip.Nn * ns,
-               blocks.size());
+  const int64_t ns = kImBlock;
+  std::vector<char> blocks;
+  rc = im_copy_blocks(ctx, blocks, pair, tree, nn);
   if (rc != POMCP_OK) return rc;
   IStat* o = reinterpret_cast<IStat*>(out);
   for (int i = 0; i < nn; ++i) {
