@@ -304,6 +304,31 @@ struct ImPair {
       }
     }
   }
+  // reg() of node n whose INode the caller holds current (x, updated): no reads
+  __device__ void reg_known(int k, int n, int a, INode& x) {
+    const int nr = im_nreg(x.info);
+    for (int i = 0; i < nr; ++i)
+      if (im_order(x.info, i) == a) return;
+    if (nr >= 6) {
+      fail(POMCP_E_INVALID);
+      return;
+    }
+    x.info = (x.info & ~(7u << 5)) | ((uint32_t)(nr + 1) << 5) | ((uint32_t)a << (8 + 3 * nr));
+    if (a < p.A && x.stats < 0) {
+      if (h.n_stats[k] + p.A > p.Ns) {
+        fail(POMCP_E_ARENA);
+        return;
+      }
+      x.stats = h.n_stats[k];
+      h.n_stats[k] += p.A;
+      for (int q = 0; q < p.A; ++q) {
+        H(k, n)[q] = make_uint4(0, 0, 0, 0);
+        T(k, n)[q] = make_uint4(0, 0, 0, 0);
+      }
+      N(k, n).stats = x.stats;
+    }
+    N(k, n).info = x.info;
+  }
   __device__ void traverse(int k, int n) {   // intmcp.py:797-809
     while (n > 0 && !im_path_ok(N(k, n).info)) {
       const int par = N(k, n).parent;
@@ -428,11 +453,20 @@ struct ImPair {
   // INTMCP.sample_action of the level-0 planner (intmcp.py:763-791) at node n
   __device__ int sample_action(int n) {
     View v = view(1, n);                // node + statistics: one round trip
-    return sample_action(n, v);
+    return sample_action(n, v, -1, nullptr);
   }
-  __device__ int sample_action(int n, View v) {
+  // pn / pnx: a node the caller holds current (the previous level's history
+  // node: usually n's parent), so the traverse of a fresh history node
+  // registers it at its parent without reading either
+  __device__ int sample_action(int n, View& v, int pn = -1, INode* pnx = nullptr) {
     if (n > 0 && !im_path_ok(v.x.info)) {
-      traverse(1, n);           // registers n's path at its ancestors; n itself
+      if (pnx != nullptr && v.x.parent == pn) {   // traverse(1, n), first step known
+        reg_known(1, pn, (int)im_paction(v.x.info), *pnx);
+        N(1, n).info = v.x.info | (1u << 4);
+        if (pn > 0 && !im_path_ok(pnx->info)) traverse(1, pn);
+      } else {
+        traverse(1, n);         // registers n's path at its ancestors; n itself
+      }
       v.x.info |= 1u << 4;      // only gains the path_ok bit (no reload)
     }
     const INode& x = v.x;
@@ -555,6 +589,8 @@ struct ImPair {
     uint4 rp[kImRegPath][3];   // {n, a, done, -}, {r, value0}, {total0, agg0} | visits0 in [0].w
     View nv;                   // the other agent's history node (level 1), prefetched
     bool have_nv = false;
+    INode pnx;                 // the previous level's history node, as it is now
+    int pn = -1;
     for (;;) {
       const INode& x = v.x;
       if (depth > p.depth_limit || x.t + depth > p.step_limit) break;
@@ -574,9 +610,15 @@ struct ImPair {
       // the other agent's action (intmcp.py:602-615): at level 1 its
       // history node's view was loaded when the previous level created it
       const bool nested_k = k == 0 && !p.state_belief_only;
-      const int ao = nested_k ? (have_nv ? sample_action((int)nested, nv)
-                                         : sample_action((int)nested))
-                              : other_action(k, nested);
+      int ao;
+      if (nested_k) {
+        if (!have_nv) nv = view(1, (int)nested);
+        ao = sample_action((int)nested, nv, pn, pn >= 0 ? &pnx : nullptr);
+        pn = (int)nested;   // the next level's history node is a child of this one
+        pnx = nv.x;
+      } else {
+        ao = other_action(k, nested);
+      }
       uint32_t n0, n1, nn = 0u;
       double r;
       int done;
