@@ -32,13 +32,21 @@ constexpr int kImRegPath = 4;         // path levels held in registers (deeper o
 // {total, agg} tails.  A node view (selection, the other agent's softmax)
 // is one line; the chosen action's tail is read for the backup only.
 constexpr int64_t kImBlock = 256;
-// Node blocks are interleaved by wavefront: [B / 64][2 trees][Nn][64 lanes]
-// blocks, so the 64 pairs of a wave keep node n of their trees side by side
-// and a wave's loads spread over the blocks in use, not over 64 separate
-// per-pair slabs (fewer pages per load instruction to translate).
-constexpr int64_t kImNodeStride = kWave * kImBlock;   // node n -> n + 1 of one tree
-__host__ __device__ __forceinline__ int64_t im_node_off(int64_t Nn, int b, int k, int64_t n) {
-  return ((((int64_t)(b / kWave) * 2 + k) * Nn + n) * kWave + (b % kWave)) * kImBlock;
+// Node blocks are interleaved by wavefront: per wave [2 trees][Nn][W lanes]
+// blocks (W = 64, fewer in a last partial wave), so the pairs of a wave keep
+// node n of their trees side by side and a wave's loads spread over the blocks
+// in use, not over 64 separate per-pair slabs (fewer pages per load
+// instruction to translate).  B x 2 x Nn blocks in all.
+__host__ __device__ __forceinline__ int im_wave_width(int B, int b) {
+  const int w0 = b - b % kWave;
+  return B - w0 < kWave ? B - w0 : kWave;
+}
+__host__ __device__ __forceinline__ int64_t im_node_stride(int B, int b) {   // node n -> n + 1
+  return (int64_t)im_wave_width(B, b) * kImBlock;
+}
+__host__ __device__ __forceinline__ int64_t im_node_off(int64_t Nn, int B, int b, int k, int64_t n) {
+  const int64_t w0 = b - b % kWave;
+  return (w0 * 2 * Nn + ((int64_t)k * Nn + n) * im_wave_width(B, b) + (b - w0)) * kImBlock;
 }
 constexpr uint32_t kImNoSupport = 0xFFFFFFFFu;
 constexpr int32_t kImSkip = -2;       // intmcp_update action: leave the pair untouched
@@ -87,8 +95,8 @@ struct ImParams {
   int64_t Nn, Ns, Nl, H, Nr, Nsp;   // per tree: nodes, stat entries, log records, hash slots;
                                     // per pair: root belief, support particles
   IHdr* hdr;
-  char* nodes;          // [B / 64][2][Nn][64] node blocks (kImBlock B, im_node_off)
-  int64_t nstride;      // kImNodeStride
+  char* nodes;          // node blocks (kImBlock B), wave-interleaved: im_node_off
+  int64_t nstride;      // kImBlock (the packed block size of the extraction ABI)
   IHash* hash;          // [B][2][H]
   IRec* log;            // [B][2][Nl]
   uint4* root;          // [B][2][Nr] {v0, v1, nested, support slot}
@@ -121,6 +129,7 @@ struct ImPair {
   const Model& m;
   int pair;
   char* nb[2];     // node blocks of the level-1 (0) and level-0 (1) trees
+  int64_t ns;      // node n -> n + 1 (im_node_stride)
   IHash* hs[2];
   IRec* lg[2];
   uint4* rootb;   // [2][Nr]
@@ -139,10 +148,11 @@ struct ImPair {
 
   __device__ ImPair(const ImParams& pp, const Model& mm, int b) : p(pp), m(mm), pair(b) {
     for (int k = 0; k < 2; ++k) {
-      nb[k] = p.nodes + im_node_off(p.Nn, b, k, 0);
+      nb[k] = p.nodes + im_node_off(p.Nn, p.B, b, k, 0);
       hs[k] = p.hash + ((int64_t)b * 2 + k) * p.H;
       lg[k] = p.log + ((int64_t)b * 2 + k) * p.Nl;
     }
+    ns = im_node_stride(p.B, b);
     rootb = p.root + (int64_t)b * 2 * p.Nr;
     sup = p.sup + (int64_t)b * 2 * p.Nr;
     supp = p.supp + (int64_t)b * 2 * p.Nsp;
@@ -156,13 +166,13 @@ struct ImPair {
   // statistics (node.py:120-178) in one line, so a node and its statistics
   // arrive together (they used to be an index apart: two dependent loads).
   __device__ __forceinline__ INode& N(int k, int n) const {
-    return *reinterpret_cast<INode*>(nb[k] + (int64_t)n * kImNodeStride);
+    return *reinterpret_cast<INode*>(nb[k] + (int64_t)n * ns);
   }
   __device__ __forceinline__ uint4* H(int k, int n) const {   // {visits, -, value} per action
-    return reinterpret_cast<uint4*>(nb[k] + (int64_t)n * kImNodeStride + 32);
+    return reinterpret_cast<uint4*>(nb[k] + (int64_t)n * ns + 32);
   }
   __device__ __forceinline__ uint4* T(int k, int n) const {   // {total, agg} per action
-    return reinterpret_cast<uint4*>(nb[k] + (int64_t)n * kImNodeStride + 128);
+    return reinterpret_cast<uint4*>(nb[k] + (int64_t)n * ns + 128);
   }
   // the node and the {visits, -, value} head of every action's statistics,
   // issued together (entries of unregistered actions are never used)
@@ -899,7 +909,7 @@ __global__ __launch_bounds__(64) void k_im_reset(ImParams p) {
     r.stats = -1;
     r.support = kImNoSupport;
     r.okey = 0;
-    *reinterpret_cast<INode*>(p.nodes + im_node_off(p.Nn, b, k, 0)) = r;
+    *reinterpret_cast<INode*>(p.nodes + im_node_off(p.Nn, p.B, b, k, 0)) = r;
     h.n_nodes[k] = 1;
     h.n_stats[k] = 0;
     h.n_log[k] = 0;

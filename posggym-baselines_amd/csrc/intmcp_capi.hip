@@ -25,7 +25,7 @@ __global__ __launch_bounds__(64) void k_im_root_stats(ImParams d, intmcp_root_st
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= d.B) return;
   const IHdr h = d.hdr[t];
-  const char* const blk = d.nodes + im_node_off(d.Nn, t, 0, h.cur);
+  const char* const blk = d.nodes + im_node_off(d.Nn, d.B, t, 0, h.cur);
   const INode node = *reinterpret_cast<const INode*>(blk);
   intmcp_root_stats o;
   memset(&o, 0, sizeof(o));
@@ -106,8 +106,10 @@ static int im_copy(intmcp_ctx* ctx, T* dst, const T* src, size_t n) {
 static int im_copy_blocks(intmcp_ctx* ctx, std::vector<char>& out, int pair, int tree, int n) {
   out.resize((size_t)n * kImBlock);
   if (n == 0) return POMCP_OK;
-  IM_TRY(ctx, hipMemcpy2DAsync(out.data(), kImBlock, ctx->ip.nodes + im_node_off(ctx->ip.Nn, pair, tree, 0),
-                               kImNodeStride, kImBlock, n, hipMemcpyDeviceToHost, ctx->stream));
+  IM_TRY(ctx, hipMemcpy2DAsync(out.data(), kImBlock,
+                               ctx->ip.nodes + im_node_off(ctx->ip.Nn, ctx->ip.B, pair, tree, 0),
+                               im_node_stride(ctx->ip.B, pair), kImBlock, n, hipMemcpyDeviceToHost,
+                               ctx->stream));
   IM_TRY(ctx, hipStreamSynchronize(ctx->stream));
   return POMCP_OK;
 }
@@ -221,8 +223,8 @@ int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, in
     d.field = reinterpret_cast<decltype(d.field)>(p);                           \
   } while (0)
   IM_ALLOC(hdr, IHdr, B);
-  d.nstride = kImNodeStride;   // node blocks (intmcp.hip), interleaved by wave
-  IM_ALLOC(nodes, char, (B + kWave - 1) / kWave * kWave * 2 * d.Nn * kImBlock);
+  d.nstride = kImBlock;   // node blocks (intmcp.hip), interleaved by wave: im_node_off
+  IM_ALLOC(nodes, char, B * 2 * d.Nn * d.nstride);
   IM_ALLOC(hash, IHash, B * 2 * d.H);
   IM_ALLOC(log, IRec, B * 2 * d.Nl);
   IM_ALLOC(root, uint4, B * 2 * d.Nr);
