@@ -41,6 +41,112 @@ __global__ __launch_bounds__(256) void k_rw(uint4* buf, int lg, int lg_region, i
   if (acc == 0x12345678u) sink[0] = acc;
 }
 
+// Reads PARTS x 16 B and writes back 16 B to each of NW different 32 B
+// sectors (parts 0, 2, 4, ..): partial-sector writes.
+template <int PARTS, int NW>
+__global__ __launch_bounds__(256) void k_rw_split(uint4* buf, int lg, int lg_region, int iters, uint32_t* sink) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = gid & 63u, wave = gid >> 6;
+  uint32_t x = gid * 0x9E3779B9u + 0x7F4A7C15u;
+  uint32_t acc = 0;
+  const uint64_t rmask = (1ull << lg_region) - 1;
+  for (int i = 0; i < iters; ++i) {
+    x ^= x << 13; x ^= x >> 17; x ^= x << 5;
+    const uint64_t line = ((((uint64_t)wave << lg_region) | (x & rmask)) << 6) | lane;
+    uint4* p = buf + line * 8;
+    uint4 v[PARTS];
+#pragma unroll
+    for (int q = 0; q < PARTS; ++q) v[q] = p[q];
+#pragma unroll
+    for (int q = 0; q < PARTS; ++q) { v[q].x += 1; acc += v[q].y; }
+#pragma unroll
+    for (int q = 0; q < NW; ++q) p[2 * q] = v[q];
+    x += acc & 1;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+// As k_rw, but each access's write-back is issued after the NEXT access's
+// loads: on gfx9 (CDNA) stores count in vmcnt, so a wait for a load issued
+// after a store also waits for the store's acknowledgement; deferring the
+// store keeps it off the dependent chain.
+template <int PARTS, int WPARTS, int MODE>
+__global__ __launch_bounds__(256) void k_rw_defer(uint4* buf, int lg, int lg_region, int iters, uint32_t* sink) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = gid & 63u, wave = gid >> 6;
+  uint32_t x = gid * 0x9E3779B9u + 0x7F4A7C15u;
+  uint32_t acc = 0;
+  const uint64_t rmask = (1ull << lg_region) - 1;
+  auto addr = [&]() {
+    x ^= x << 13; x ^= x >> 17; x ^= x << 5;
+    uint64_t line;
+    if (MODE == 0) line = ((uint64_t)x * 0x9E3779B1u) >> (64 - lg);
+    else if (MODE == 1) line = ((uint64_t)gid << lg_region) | (x & rmask);
+    else line = ((((uint64_t)wave << lg_region) | (x & rmask)) << 6) | lane;
+    return buf + line * 8;
+  };
+  uint4* p = addr();
+  uint4 v[PARTS];
+#pragma unroll
+  for (int q = 0; q < PARTS; ++q) v[q] = p[q];
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int q = 0; q < PARTS; ++q) { v[q].x += 1; acc += v[q].y; }
+    x += acc & 1;
+    uint4* const pn = addr();
+    uint4 vn[PARTS];
+#pragma unroll
+    for (int q = 0; q < PARTS; ++q) vn[q] = pn[q];
+#pragma unroll
+    for (int q = 0; q < WPARTS; ++q) p[q] = v[q];   // the previous access's write-back
+#pragma unroll
+    for (int q = 0; q < PARTS; ++q) v[q] = vn[q];
+    p = pn;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+// Cooperative line load: the 64 lanes of a wave fetch the 64 lanes' 128 B
+// lines 8 at a time -- in load j lane l reads 16 B part (l % 8) of the line of
+// lane 8 j + l / 8 -- so each load instruction touches 8 lines instead of 64;
+// the parts are regrouped per lane through LDS.  Same bytes, 8x fewer lines per
+// instruction (address processing, translation).
+template <int MODE>
+__global__ __launch_bounds__(256) void k_coop(uint4* buf, int lg, int lg_region, int iters, uint32_t* sink) {
+  __shared__ uint4 lds[4][64][9];   // [wave in block][lane][part] (+1: bank spread)
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = gid & 63u, wave = gid >> 6, wib = threadIdx.x >> 6;
+  uint32_t x = gid * 0x9E3779B9u + 0x7F4A7C15u;
+  uint32_t acc = 0;
+  const uint64_t rmask = (1ull << lg_region) - 1;
+  for (int i = 0; i < iters; ++i) {
+    x ^= x << 13; x ^= x >> 17; x ^= x << 5;
+    uint64_t line;
+    if (MODE == 0) line = ((uint64_t)x * 0x9E3779B1u) >> (64 - lg);
+    else if (MODE == 1) line = ((uint64_t)gid << lg_region) | (x & rmask);
+    else line = ((((uint64_t)wave << lg_region) | (x & rmask)) << 6) | lane;
+    const int lo = (int)(uint32_t)line, hi = (int)(uint32_t)(line >> 32);
+    uint4 got[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int src = 8 * j + (int)(lane >> 3);
+      const uint64_t l2 = (uint64_t)(uint32_t)__shfl(lo, src) | ((uint64_t)(uint32_t)__shfl(hi, src) << 32);
+      got[j] = buf[l2 * 8 + (lane & 7u)];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lds[wib][8 * j + (lane >> 3)][lane & 7u] = got[j];
+    __builtin_amdgcn_wave_barrier();
+    uint4 v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = lds[wib][lane][q];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { v[q].x += 1; acc += v[q].y; }
+    x += acc & 1;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
 int main(int argc, char** argv) {
   const int lg_region = argc > 1 ? atoi(argv[1]) : 10;   // lines per lane region (log2)
   uint4* buf; uint32_t* sink;
@@ -80,5 +186,13 @@ int main(int argc, char** argv) {
   run("interleaved r80", k_rw<5, 0, 2>, 80, 1);
   run("interleaved r112", k_rw<7, 0, 2>, 112, 1);
   run("interleaved r112w16", k_rw<7, 1, 2>, 128, 1);
+  run("interleaved r112w16 defer", k_rw_defer<7, 1, 2>, 128, 1);
+  run("interleaved r112w32", k_rw<7, 2, 2>, 144, 1);       // one full 32 B sector
+  run("interleaved r112w16x2", k_rw_split<7, 2>, 144, 1);  // two half sectors
+  run("interleaved r112w64", k_rw<7, 4, 2>, 176, 1);
+  run("interleaved rw112 defer", k_rw_defer<7, 7, 2>, 112, 2);
+  run("global r128 coop", k_coop<0>, 128, 1);
+  run("per-lane r128 coop", k_coop<1>, 128, 1);
+  run("interleaved r128 coop", k_coop<2>, 128, 1);
   return 0;
 }
