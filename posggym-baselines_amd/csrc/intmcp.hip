@@ -727,11 +727,20 @@ struct ImPair {
   __device__ ISup* sup_tab(int sel) { return sup + (int64_t)sel * p.Nr; }
   __device__ uint2* sup_parts(int sel) { return supp + (int64_t)sel * p.Nsp; }
 
+  // the slot of level-0 node n in support table `sel` (count entries): the
+  // node's `support` field while the caller has that table's slots marked
+  // (mark_support), else a scan
   __device__ int find_support(int sel, int n, int count) {
+    const uint32_t s = N(1, n).support;
+    if (s != kImNoSupport) return (int)s < count && sup_tab(sel)[s].node == n ? (int)s : -1;
     const ISup* t = sup_tab(sel);
     for (int i = 0; i < count; ++i)
       if (t[i].node == n) return i;
     return -1;
+  }
+  __device__ void mark_support(int sel, int count, bool on) {
+    const ISup* t = sup_tab(sel);
+    for (int i = 0; i < count; ++i) N(1, t[i].node).support = on ? (uint32_t)i : kImNoSupport;
   }
 
   // BeliefRejectionSampler (belief.py:145-194, use_rejected_samples=True) for a
@@ -835,19 +844,22 @@ __device__ void im_support(ImPair<Env>& P, int sel, int size, int* nsup) {
   uint4* rb = P.root_buf(P.h.root_sel);
   ISup* tab = P.sup_tab(sel);
   int n = 0;
+  // node -> slot through the nodes' `support` field (kImNoSupport outside a
+  // materialisation), not a scan of the table per particle: O(size), not
+  // O(size x distinct nodes)
   for (int i = 0; i < size; ++i) {
     const int nodeid = (int)rb[i].z;
-    int s = -1;
-    for (int q = 0; q < n; ++q)
-      if (tab[q].node == nodeid) s = q;
-    if (s < 0) {
+    int s = (int)P.N(1, nodeid).support;
+    if (P.N(1, nodeid).support == kImNoSupport) {
       s = n++;
       tab[s].node = nodeid;
       tab[s].size = 0;   // count for now
+      P.N(1, nodeid).support = (uint32_t)s;
     }
     tab[s].size += 1;
     rb[i].w = (uint32_t)s;
   }
+  for (int q = 0; q < n; ++q) P.N(1, tab[q].node).support = kImNoSupport;
   for (int q = 0; q < n; ++q) {
     prob[q] = 0.0 + 1.0 * ((double)tab[q].size / (double)size);
     tab[q].size = 0;
@@ -887,20 +899,24 @@ __device__ void im_extract_support(ImPair<Env>& P, int sel, int nsup) {
   for (int q = 0; q < nsup; ++q) P.N(1, tab[q].node).support = kImNoSupport;
 }
 
+// Every obs-child map slot empty ({0, 0, -1}), grid-stride over all pairs'
+// tables (a lane per pair would clear a wall-clock arena's 2 x 2^26 slots alone).
+__global__ __launch_bounds__(256) void k_im_clear_hash(IHash* hs, int64_t n) {
+  IHash e;
+  e.okey = 0;
+  e.na = 0;
+  e.child = -1;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    hs[i] = e;
+}
+
 template <class Env>
 __global__ __launch_bounds__(64) void k_im_reset(ImParams p) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= p.B) return;
   IHdr h = p.hdr[b];
-  for (int k = 0; k < 2; ++k) {
-    IHash* hs = p.hash + ((int64_t)b * 2 + k) * p.H;
-    for (int64_t i = 0; i < p.H; ++i) {
-      IHash e;
-      e.okey = 0;
-      e.na = 0;
-      e.child = -1;
-      hs[i] = e;
-    }
+  for (int k = 0; k < 2; ++k) {   // (the hash tables: k_im_clear_hash, all lanes)
     INode r;
     r.parent = -1;
     r.info = 1u << 4;   // path_ok
@@ -1040,6 +1056,7 @@ __global__ __launch_bounds__(64) void k_im_update(ImParams p) {
           im_extract_support(P, sel, nsup);
           ISup* tab = P.sup_tab(sel);
           P.h.pad = P.h.n_sup;   // previous support count (parents)
+          P.mark_support(sel ^ 1, P.h.pad, true);   // parents found by node, not by scan
           for (int q = 0; q < nsup && P.h.err == 0; ++q) {
             const int m = tab[q].node;
             P.traverse(1, m);
@@ -1047,6 +1064,7 @@ __global__ __launch_bounds__(64) void k_im_update(ImParams p) {
             const int tq = (int)ceil(prob[q] * (double)p.n_target);
             P.reinvig_nested(m, (int)im_paction(P.N(1, m).info), P.N(1, m).okey, tq, sel, q);
           }
+          P.mark_support(sel ^ 1, P.h.pad, false);
           int used = 0;
           for (int q = 0; q < nsup; ++q) used = max(used, tab[q].off + tab[q].cap);
           P.h.sup_sel = sel;

@@ -277,6 +277,10 @@ int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, in
 int intmcp_reset(intmcp_ctx* ctx) {
   if (!ctx) return POMCP_E_INVALID;
   IM_TRY(ctx, hipSetDevice(ctx->device));
+  const int64_t slots = (int64_t)ctx->ip.B * 2 * ctx->ip.H;
+  const int64_t cblocks = std::min<int64_t>((slots + 255) / 256, 256 * 64);
+  hipLaunchKernelGGL(k_im_clear_hash, dim3((unsigned)cblocks), dim3(256), 0, ctx->stream, ctx->ip.hash,
+                     slots);
   IM_LAUNCH(ctx, k_im_reset, dim3(im_blocks(ctx->ip.B)), dim3(64), ctx->ip);
   IM_TRY(ctx, hipGetLastError());
   IM_TRY(ctx, hipStreamSynchronize(ctx->stream));

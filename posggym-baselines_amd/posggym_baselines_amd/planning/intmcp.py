@@ -99,8 +99,8 @@ def plan_intmcp_capacities(config, step_limit: int, num_sims: int, searches: int
 
 # Wall-clock sizing.  One pair's simulation rate alone on the GPU (one lane,
 # chunked launches) is bounded by INTMCP_WALL_CLOCK_SIMS_PER_S per level
-# (measured 65-100 k/s per level on MI355X, tests/test_gpu_intmcp.py
-# test_wall_clock_episode_half_second; >= 2.5x margin): a search runs at
+# (measured 80-130 k/s per level on MI355X, tests/test_gpu_intmcp.py
+# test_wall_clock_episode_half_second; ~2x margin): a search runs at
 # most that many simulations per level per second of its share of
 # search_time_limit.  The node arena is the smaller of the worst case for that
 # rate and the HBM budget; get_action's headroom check keeps a chunk inside it.
