@@ -51,11 +51,63 @@ HBM_PEAK_GBS = 8000.0
 def _device_info(dev):
     """Name and compute-unit count of the GPU (the same code measures 3.75-4.73 G
     sims/s across boxes of the pool, DESIGN.md §6: recorded to tell boxes apart)."""
+    import subprocess
     import torch
     p = torch.cuda.get_device_properties(dev)
-    return {"name": p.name, "gcn_arch": getattr(p, "gcnArchName", ""),
+    info = {"name": p.name, "gcn_arch": getattr(p, "gcnArchName", ""),
             "compute_units": p.multi_processor_count,
             "hbm_gib": round(p.total_memory / 2**30, 1)}
+    try:   # static facts that may differ between boxes (rocm-smi; optional)
+        out = subprocess.run(["rocm-smi", "-d", os.environ.get("LOCAL_RANK", "0"), "--showmemvendor",
+                              "--showcomputepartition", "--showmemorypartition", "--json"],
+                             capture_output=True, text=True, timeout=10).stdout
+        d = next(iter(json.loads(out[out.index("{"):]).values()))
+        info["smi"] = {k: v for k, v in d.items() if "artition" in k or "vendor" in k}
+    except Exception:
+        pass
+    return info
+
+
+class _ClockSampler:
+    """`rocm-smi` readings of this rank's GPU taken during the timed region
+    (graphics clock, package power): recorded beside the result, because the
+    same code measures differently on different boxes of the pool (DESIGN.md
+    §6).  A child process per reading; a failure only leaves the list empty."""
+
+    def __init__(self, card: int, every_s: float = 0.4):
+        import threading
+        self.card, self.every, self.samples = card, every_s, []
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        import re
+        import subprocess
+        while not self._stop.is_set() and len(self.samples) < 8:
+            try:
+                out = subprocess.run(["rocm-smi", "-d", str(self.card), "--showclocks",
+                                      "--showpower", "--json"], capture_output=True, text=True,
+                                     timeout=5).stdout
+                d = next(iter(json.loads(out[out.index("{"):]).values()))
+                mhz = {}
+                for c in ("sclk", "mclk", "fclk"):
+                    m = re.search(r"(\d+)", d.get(f"{c} clock speed:", ""))
+                    mhz[f"{c}_mhz"] = int(m.group(1)) if m else None
+                pw = d.get("Current Socket Graphics Package Power (W)")
+                self.samples.append(dict(mhz, power_w=float(pw) if pw else None))
+            except Exception:
+                return
+            self._stop.wait(self.every)
+
+    def __enter__(self):
+        if not os.environ.get("BENCH_NO_CLOCKS"):
+            self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        if self._t.is_alive():
+            self._t.join(timeout=10)
 
 
 def parse():
@@ -381,13 +433,14 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(ev[k])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    with _ClockSampler(int(os.environ.get("LOCAL_RANK", "0"))) as clocks:
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            step(ev[k])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
     kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
     if world > 1:
         t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=f"cuda:{dev}")
@@ -442,7 +495,7 @@ def main():
                    "sims_per_planner_step": S * K,
                    "rollout_steps_per_sim": sum(s.n_rollout_steps for s in st) / max(sims, 1),
                    "parallelism": f"root-parallel x{world}",
-                   "device": _device_info(dev),
+                   "device": dict(_device_info(dev), during_run=clocks.samples),
                    "arena": {"max_blocks": caps.max_blocks,
                              "max_blocks_used": max(s.n_blocks for s in st),
                              "max_particles": caps.max_particles,
