@@ -227,6 +227,7 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
   d.H = c.overflow_slots;
   d.bucket_mask = (uint32_t)(c.overflow_slots / kBucket - 1);
   d.ovf_base = (uint32_t)(c.max_blocks * c.num_actions * kSlots + 1);
+  d.islots = kSlots;
   const int64_t B = c.num_trees;
   void* p;
 #define ALLOC(field, type, count)                                               \
@@ -760,6 +761,15 @@ int pomcp_debug_exp(const double* x, int32_t n, double* out) {
 int pomcp_debug_host_exp(const double* x, int32_t n, double* out) {
   if (!x || !out || n < 0) return POMCP_E_INVALID;
   for (int32_t i = 0; i < n; ++i) out[i] = host_exp(x[i]);
+  return POMCP_OK;
+}
+
+// Debug: use only the first n (1..6) inline obs slots of every action node, so
+// the overflow map serves the rest (tests of that path: the models here rarely
+// give an action node more than 6 obs children).  Before the first search.
+int pomcp_debug_set_inline_slots(pomcp_ctx* ctx, int32_t n) {
+  if (!ctx || n < 1 || n > kSlots) return POMCP_E_INVALID;
+  ctx->dp.islots = n;
   return POMCP_OK;
 }
 

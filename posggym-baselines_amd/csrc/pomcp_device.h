@@ -139,6 +139,8 @@ struct DevParams {
   int64_t Nb, Np, Nr, H;
   uint32_t bucket_mask;
   uint32_t ovf_base;    // node ids >= ovf_base are overflow entries
+  int32_t islots;       // inline obs slots in use per action node (kSlots; fewer only in
+                        // tests of the overflow map: pomcp_debug_set_inline_slots)
   TreeHdr* hdr;
   Line* an;             // [B][Nb][A + 1] action blocks
   OvfSlot* ovf;         // [B][H]

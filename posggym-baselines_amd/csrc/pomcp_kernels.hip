@@ -254,7 +254,7 @@ struct Tree {
                             ChildRef* c) {
     const uint32_t ani = (uint32_t)(blk * p.A + a);
     const int lo = part_slot(a, 0);   // block layout: pomcp_device.h
-    const bool cl = lane >= lo && lane < lo + kSlots;
+    const bool cl = lane >= lo && lane < lo + p.islots;
     const uint64_t skey = (uint64_t)q.x | ((uint64_t)q.y << 32);
     const bool valid = cl && (skey & kValidBit) != 0;
     const uint64_t m = __ballot(valid && (skey & kObsMask) == okey);

@@ -107,6 +107,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   // the wave's shared particle log (pomcp_device.h LogRec); wpos is the same in
   // every lane still in the loop (advanced by ballot at convergent points)
   const WaveLog wl(p.plog, p.Np, wave);
+  const int islots = p.islots;   // kSlots (fewer: overflow-map tests)
   const uint32_t wpos0 = p.wlog[wave];
   uint32_t wpos = wpos0;
   bool app = false;          // this lane has a record to append
@@ -391,7 +392,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
     for (int q = kSlots - 1; q >= 0; --q) {
       const uint64_t sk = (uint64_t)sl[q].x | ((uint64_t)sl[q].y << 32);
       const bool vb = (sk & kValidBit) != 0;
-      if (!vb || (sk & kObsMask) == okey) {
+      if (q < islots && (!vb || (sk & kObsMask) == okey)) {
         ks = q;
         *match = vb;
       }

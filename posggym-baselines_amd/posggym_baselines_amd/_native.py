@@ -197,6 +197,7 @@ DEBUG_SIGNATURES = [
     ("pomcp_debug_host_exp", C.c_int, [_PD, C.c_int32, _PD]),
     ("pomcp_debug_phase_timing", C.c_int,
      [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32, C.POINTER(C.c_int32)]),
+    ("pomcp_debug_set_inline_slots", C.c_int, [C.c_void_p, C.c_int32]),
 ]
 
 
@@ -295,6 +296,8 @@ def load():
         pass
     lib = C.CDLL(LIB_PATH)
     for name, res, args in SIGNATURES + DEBUG_SIGNATURES + INTMCP_SIGNATURES:
+        if (name, res, args) in DEBUG_SIGNATURES and not hasattr(lib, name):
+            continue   # diagnostics: optional in libraries built from older sources
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

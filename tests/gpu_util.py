@@ -88,10 +88,13 @@ def _arena_usage(engine):
     return nb.value, nl.value
 
 
-def batched_episodes(cfg_kwargs, num_sims, env_seeds, steps, capacities=None, usage=None):
+def batched_episodes(cfg_kwargs, num_sims, env_seeds, steps, capacities=None, usage=None,
+                     inline_slots=None, probes=None):
     """Lockstep episodes of len(env_seeds) independent planners in ONE engine
     (tree b = planner b, env seed env_seeds[b]), `steps` real steps each.
-    Returns per-tree record lists in the oracle format."""
+    Returns per-tree record lists in the oracle format.  inline_slots: use only
+    that many inline obs slots per action node (pomcp_debug_set_inline_slots);
+    probes: a list that receives each search's overflow-map probes."""
     import numpy as np
     from oracle.driving import DrivingModel as EnvModel
     from oracle.driving import pack_obs
@@ -103,6 +106,9 @@ def batched_episodes(cfg_kwargs, num_sims, env_seeds, steps, capacities=None, us
     B = len(env_seeds)
     bp = BatchedPOMCP(model, "0", product_config(cfg_kwargs, num_sims), B, num_sims,
                       searches=steps, reroot=True, capacities=capacities)
+    if inline_slots is not None:
+        from posggym_baselines_amd import _native as N
+        assert N.load().pomcp_debug_set_inline_slots(bp.engine._ctx, int(inline_slots)) == 0
     envs = []
     for s in env_seeds:
         es = Streams(s, ENV_TREE_BASE)
@@ -120,6 +126,8 @@ def batched_episodes(cfg_kwargs, num_sims, env_seeds, steps, capacities=None, us
             usage.append(("after_update", _arena_usage(bp.engine)))
         actions = bp.search()
         stats = bp.engine.root_stats()
+        if probes is not None:
+            probes.append(sum(int(st.n_probes) for st in stats))
         for b in range(B):
             records[b].append(stats_record(stats[b], 5, True, actions[b], bp.engine.root_belief(b)))
             es, env, st, obs = envs[b]

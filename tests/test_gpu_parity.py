@@ -100,6 +100,33 @@ def _batched_vs_oracle(cfg, num_trees, num_sims, check_trees, rekey=None, env="D
     return stats
 
 
+@pytest.mark.parametrize("islots", [1, 2])
+def test_overflow_map_bit_exact(islots):
+    """The overflow map of obs children (beyond an action node's inline slots:
+    k_search's ovf_child, k_reroot_child's lookup, k_compact's rebuild).  The
+    models here rarely give an action node more than 6 obs children (none in
+    4,096-simulation searches from 2,125-particle roots on either model), so
+    the engine uses only `islots` inline slots (pomcp_debug_set_inline_slots)
+    and the rest go to the map: 40 planners over 5 real steps with re-roots,
+    bit-exact against the oracle, the map probed every search."""
+    from gpu_util import batched_episodes
+    from oracle.run import oracle_episode
+    S, K = 128, 5
+    seeds, exp = [], []
+    s = 4400
+    while len(seeds) < 40:
+        trace, recs = oracle_episode(TEST_CFG, S, s, tree=len(seeds), max_steps=K)
+        if trace["len"] >= K and all(r["searched"] for r in recs):
+            seeds.append(s)
+            exp.append(recs)
+        s += 1
+    probes = []
+    got = batched_episodes(TEST_CFG, S, seeds, K, inline_slots=islots, probes=probes)
+    for b in range(len(seeds)):
+        assert got[b] == exp[b], f"tree {b} (env seed {seeds[b]})"
+    assert all(n > 0 for n in probes), probes
+
+
 def test_batched_synthetic_roots_ucb():
     _batched_vs_oracle(TEST_CFG, 37, 256, range(37))
 
