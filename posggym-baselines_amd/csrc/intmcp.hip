@@ -601,6 +601,10 @@ struct ImPair {
     bool have_nv = false;
     INode pnx;                 // the previous level's history node, as it is now
     int pn = -1;
+    if (k == 0 && !p.state_belief_only) {   // the first level's history view, in flight
+      nv = view(1, (int)nested);            // while the root selection runs
+      have_nv = true;
+    }
     for (;;) {
       const INode& x = v.x;
       if (depth > p.depth_limit || x.t + depth > p.step_limit) break;
