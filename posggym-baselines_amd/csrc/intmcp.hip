@@ -50,6 +50,7 @@ __host__ __device__ __forceinline__ int64_t im_node_off(int64_t Nn, int B, int b
 }
 constexpr uint32_t kImNoSupport = 0xFFFFFFFFu;
 constexpr int32_t kImSkip = -2;       // intmcp_update action: leave the pair untouched
+constexpr int kWave64 = 64;           // lanes of a wave (k_im_update's wave mode)
 constexpr int kImLogLds = 2048;       // math.log(N) entries staged in LDS by k_im_search
 constexpr int kImRootWords = 8;       // the level-1 root's view (INode + 6 heads) in LDS, uint4s
 
@@ -842,7 +843,13 @@ struct ImPair {
 // Level-0 support of the root belief: distinct other-agent nodes in
 // first-occurrence order with probability count / size (intmcp.py:334-362);
 // writes support slots into the root buffer's .w.
-template <class Env>
+// kWave: the 64 lanes of the wave run the same pair (k_im_update's wave mode,
+// every lane holding the same state) and share the scans: 64 records per
+// step, grouped per node / slot in lane order, so the result (first-occurrence
+// order, insertion order per slot) is the serial loop's.
+__device__ __forceinline__ uint64_t im_lanes_below() { return (1ull << (threadIdx.x & 63)) - 1ull; }
+
+template <class Env, bool kWave = false>
 __device__ void im_support(ImPair<Env>& P, int sel, int size, int* nsup) {
   double* prob = P.prob;
   uint4* rb = P.root_buf(P.h.root_sel);
@@ -851,17 +858,41 @@ __device__ void im_support(ImPair<Env>& P, int sel, int size, int* nsup) {
   // node -> slot through the nodes' `support` field (kImNoSupport outside a
   // materialisation), not a scan of the table per particle: O(size), not
   // O(size x distinct nodes)
-  for (int i = 0; i < size; ++i) {
-    const int nodeid = (int)rb[i].z;
-    int s = (int)P.N(1, nodeid).support;
-    if (P.N(1, nodeid).support == kImNoSupport) {
-      s = n++;
-      tab[s].node = nodeid;
-      tab[s].size = 0;   // count for now
-      P.N(1, nodeid).support = (uint32_t)s;
+  if constexpr (kWave) {
+    for (int base = 0; base < size; base += kWave64) {
+      const int i = base + (int)(threadIdx.x & 63);
+      const bool on = i < size;
+      const int nodeid = on ? (int)rb[i].z : -1;
+      uint64_t todo = __ballot(on);
+      while (todo) {   // each distinct node of the batch, in the order of its first lane
+        const int lead = __ffsll((long long)todo) - 1;
+        const int ln = __shfl(nodeid, lead);
+        const uint64_t peers = __ballot(on && nodeid == ln);
+        int s = (int)P.N(1, ln).support;
+        if (P.N(1, ln).support == kImNoSupport) {
+          s = n++;
+          tab[s].node = ln;
+          tab[s].size = 0;
+          P.N(1, ln).support = (uint32_t)s;
+        }
+        tab[s].size += __popcll(peers);
+        if (on && nodeid == ln) rb[i].w = (uint32_t)s;
+        todo &= ~peers;
+      }
     }
-    tab[s].size += 1;
-    rb[i].w = (uint32_t)s;
+  } else {
+    for (int i = 0; i < size; ++i) {
+      const int nodeid = (int)rb[i].z;
+      int s = (int)P.N(1, nodeid).support;
+      if (P.N(1, nodeid).support == kImNoSupport) {
+        s = n++;
+        tab[s].node = nodeid;
+        tab[s].size = 0;   // count for now
+        P.N(1, nodeid).support = (uint32_t)s;
+      }
+      tab[s].size += 1;
+      rb[i].w = (uint32_t)s;
+    }
   }
   for (int q = 0; q < n; ++q) P.N(1, tab[q].node).support = kImNoSupport;
   for (int q = 0; q < n; ++q) {
@@ -873,14 +904,29 @@ __device__ void im_support(ImPair<Env>& P, int sel, int size, int* nsup) {
 
 // Materialise the level-0 support beliefs from the level-0 log (insertion
 // order), leaving `slack` free slots per entry for reinvigoration.
-template <class Env>
+template <class Env, bool kWave = false>
 __device__ void im_extract_support(ImPair<Env>& P, int sel, int nsup) {
   ISup* tab = P.sup_tab(sel);
   for (int q = 0; q < nsup; ++q) P.N(1, tab[q].node).support = (uint32_t)q;
   for (int q = 0; q < nsup; ++q) tab[q].cap = 0;
-  for (int i = 0; i < P.h.n_log[1]; ++i) {
-    const uint32_t s = P.N(1, P.lg[1][i].node).support;
-    if (s != kImNoSupport) tab[s].cap += 1;
+  const int nlog = P.h.n_log[1];
+  if constexpr (kWave) {
+    for (int base = 0; base < nlog; base += kWave64) {
+      const int i = base + (int)(threadIdx.x & 63);
+      const uint32_t s = i < nlog ? P.N(1, P.lg[1][i].node).support : kImNoSupport;
+      uint64_t todo = __ballot(s != kImNoSupport);
+      while (todo) {
+        const uint32_t ls = (uint32_t)__shfl((int)s, __ffsll((long long)todo) - 1);
+        const uint64_t peers = __ballot(s == ls);
+        tab[ls].cap += __popcll(peers);
+        todo &= ~peers;
+      }
+    }
+  } else {
+    for (int i = 0; i < nlog; ++i) {
+      const uint32_t s = P.N(1, P.lg[1][i].node).support;
+      if (s != kImNoSupport) tab[s].cap += 1;
+    }
   }
   int off = 0;
   for (int q = 0; q < nsup; ++q) {   // room for the reinvigoration (accepted + rejected)
@@ -895,10 +941,31 @@ __device__ void im_extract_support(ImPair<Env>& P, int sel, int nsup) {
     return;
   }
   uint2* parts = P.sup_parts(sel);
-  for (int i = 0; i < P.h.n_log[1]; ++i) {
-    const IRec r = P.lg[1][i];
-    const uint32_t s = P.N(1, r.node).support;
-    if (s != kImNoSupport) parts[tab[s].off + tab[s].size++] = make_uint2(r.v0, r.v1);
+  if constexpr (kWave) {
+    for (int base = 0; base < nlog; base += kWave64) {
+      const int i = base + (int)(threadIdx.x & 63);
+      IRec r{0u, 0u, 0u, 0u};
+      uint32_t s = kImNoSupport;
+      if (i < nlog) {
+        r = P.lg[1][i];
+        s = P.N(1, r.node).support;
+      }
+      uint64_t todo = __ballot(s != kImNoSupport);
+      while (todo) {   // each slot of the batch: its records in lane (= insertion) order
+        const uint32_t ls = (uint32_t)__shfl((int)s, __ffsll((long long)todo) - 1);
+        const uint64_t peers = __ballot(s == ls);
+        const int at = tab[ls].off + tab[ls].size;
+        if (s == ls) parts[at + __popcll(peers & im_lanes_below())] = make_uint2(r.v0, r.v1);
+        tab[ls].size += __popcll(peers);
+        todo &= ~peers;
+      }
+    }
+  } else {
+    for (int i = 0; i < nlog; ++i) {
+      const IRec r = P.lg[1][i];
+      const uint32_t s = P.N(1, r.node).support;
+      if (s != kImNoSupport) parts[tab[s].off + tab[s].size++] = make_uint2(r.v0, r.v1);
+    }
   }
   for (int q = 0; q < nsup; ++q) P.N(1, tab[q].node).support = kImNoSupport;
 }
@@ -952,11 +1019,15 @@ __global__ __launch_bounds__(64) void k_im_reset(ImParams p) {
 }
 
 // INTMCP.update (intmcp.py:198-300) for every pair.
-template <class Env>
+// kWave (few pairs: the drop-in's one): a wave per pair, its 64 lanes running
+// the same pair in lockstep (identical state, identical stores) and sharing
+// the scans of the episode's particle logs, which grow with every search;
+// otherwise a lane per pair.
+template <class Env, bool kWave>
 __global__ __launch_bounds__(64) void k_im_update(ImParams p) {
   __shared__ typename Env::Model sm;
   stage_model(p.model, sm);
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = kWave ? (int)blockIdx.x : (int)(blockIdx.x * blockDim.x + threadIdx.x);
   if (b >= p.B) return;
   ImPair<Env> P(p, sm, b);
   const uint64_t obs = p.in_obs[b];
@@ -996,7 +1067,7 @@ __global__ __launch_bounds__(64) void k_im_update(ImParams p) {
         if (P.h.err == 0 && n > 0) {
           // level 0: support of the histories, their initial beliefs
           const int sel = P.h.sup_sel ^ 1;
-          im_support(P, sel, n, &nsup);
+          im_support<Env, kWave>(P, sel, n, &nsup);
           ISup* tab = P.sup_tab(sel);
           const uint64_t o0 = P.N(1, tab[0].node).okey;
           Env::sample_agent_initial(sm, p.other, o0, draw_model, &s0, &s1);   // probe
@@ -1038,14 +1109,31 @@ __global__ __launch_bounds__(64) void k_im_update(ImParams p) {
         P.h.root_sel ^= 1;
         uint4* rb = P.root_buf(P.h.root_sel);
         int n = 0;
-        for (int i = 0; i < P.h.n_log[0]; ++i) {
-          const IRec r = P.lg[0][i];
-          if ((int)r.node == node) {
-            if (n >= p.Nr) {
+        const int nlog = P.h.n_log[0];
+        if constexpr (kWave) {
+          for (int base = 0; base < nlog; base += kWave64) {
+            const int i = base + (int)(threadIdx.x & 63);
+            IRec r{0u, 0u, 0u, 0u};
+            if (i < nlog) r = P.lg[0][i];
+            const bool hit = i < nlog && (int)r.node == node;
+            const uint64_t m = __ballot(hit);
+            if (n + __popcll(m) > p.Nr) {
               P.fail(POMCP_E_ARENA);
               break;
             }
-            rb[n++] = make_uint4(r.v0, r.v1, r.nested, 0u);
+            if (hit) rb[n + __popcll(m & im_lanes_below())] = make_uint4(r.v0, r.v1, r.nested, 0u);
+            n += __popcll(m);
+          }
+        } else {
+          for (int i = 0; i < nlog; ++i) {
+            const IRec r = P.lg[0][i];
+            if ((int)r.node == node) {
+              if (n >= p.Nr) {
+                P.fail(POMCP_E_ARENA);
+                break;
+              }
+              rb[n++] = make_uint4(r.v0, r.v1, r.nested, 0u);
+            }
           }
         }
         P.h.pad = prev_size;
@@ -1056,8 +1144,8 @@ __global__ __launch_bounds__(64) void k_im_update(ImParams p) {
         // level 0: support of the new root belief, materialised + reinvigorated
         if (P.h.err == 0 && n > 0) {
           const int sel = P.h.sup_sel ^ 1;
-          im_support(P, sel, n, &nsup);
-          im_extract_support(P, sel, nsup);
+          im_support<Env, kWave>(P, sel, n, &nsup);
+          im_extract_support<Env, kWave>(P, sel, nsup);
           ISup* tab = P.sup_tab(sel);
           P.h.pad = P.h.n_sup;   // previous support count (parents)
           P.mark_support(sel ^ 1, P.h.pad, true);   // parents found by node, not by scan

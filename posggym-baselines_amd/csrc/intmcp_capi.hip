@@ -309,7 +309,17 @@ int intmcp_update(intmcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_k
                              hipMemcpyHostToDevice, ctx->stream));
   IM_TRY(ctx, hipMemcpyAsync((void*)ctx->ip.in_obs, obs_keys, sizeof(uint64_t) * B,
                              hipMemcpyHostToDevice, ctx->stream));
-  IM_LAUNCH(ctx, k_im_update, dim3(im_blocks(B)), dim3(64), ctx->ip);
+  // a wave per pair for few pairs (the drop-in): the update's log scans are
+  // shared by the wave's lanes (k_im_update kWave); a lane per pair otherwise
+  const bool wave = B <= 1024;
+  const dim3 ugrid(wave ? (unsigned)B : (unsigned)im_blocks(B));
+  if (ctx->cfg.base.env_id == POMCP_ENV_PURSUIT_EVASION) {
+    if (wave) hipLaunchKernelGGL((k_im_update<EnvPursuitEvasion, true>), ugrid, dim3(64), 0, ctx->stream, ctx->ip);
+    else hipLaunchKernelGGL((k_im_update<EnvPursuitEvasion, false>), ugrid, dim3(64), 0, ctx->stream, ctx->ip);
+  } else {
+    if (wave) hipLaunchKernelGGL((k_im_update<EnvDriving, true>), ugrid, dim3(64), 0, ctx->stream, ctx->ip);
+    else hipLaunchKernelGGL((k_im_update<EnvDriving, false>), ugrid, dim3(64), 0, ctx->stream, ctx->ip);
+  }
   IM_TRY(ctx, hipGetLastError());
   IM_TRY(ctx, hipMemcpyAsync(ctx->host_out.data(), ctx->ip.out, sizeof(int32_t) * 2 * B,
                              hipMemcpyDeviceToHost, ctx->stream));

@@ -29,18 +29,20 @@ TEST_CFG = dict(discount=0.95, search_time_limit=0.1, c=2 ** 0.5, truncated=Fals
                 step_limit=None, epsilon=0.92, seed=3, state_belief_only=False)
 
 
-@pytest.mark.parametrize("env,ego,sel", [("Driving-v1", "0", "ucb"),
-                                         ("PursuitEvasion-v1", "1", "uniform")])
-def test_batched_pairs_match_oracle(env, ego, sel):
-    """150 planner pairs (3 launch blocks) in one engine, lockstep episodes:
-    pair b equals the oracle planner with tree key b."""
+@pytest.mark.parametrize("env,ego,sel,B", [("Driving-v1", "0", "ucb", 150),
+                                           ("PursuitEvasion-v1", "1", "uniform", 150),
+                                           ("Driving-v1", "0", "ucb", 1100)])
+def test_batched_pairs_match_oracle(env, ego, sel, B):
+    """Planner pairs in one engine, lockstep episodes: pair b equals the oracle
+    planner with tree key b.  150 pairs: the update runs a wave per pair
+    (shared log scans); 1,100 pairs: a lane per pair."""
     from gpu_util import batched_intmcp_episodes
     from oracle.run import oracle_intmcp_episode
     cfg = dict(TEST_CFG, action_selection=sel)
-    seeds = [500 + b for b in range(150)]
+    seeds = [500 + b for b in range(B)]
     steps, sims = 4, 48
     got = batched_intmcp_episodes(cfg, sims, seeds, steps, env=env, ego=ego)
-    for b in (0, 1, 63, 64, 100, 127, 128, 149):
+    for b in (0, 1, 63, 64, 100, 127, 128, 149, B - 1):
         _, exp = oracle_intmcp_episode(cfg, sims, seeds[b], ego=ego, tree=b, max_steps=steps,
                                        env=env)
         assert got[b] == exp, f"pair {b}"
