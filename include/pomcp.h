@@ -186,6 +186,15 @@ int pomcp_rekey(pomcp_ctx* ctx, uint64_t seed);
  * the operand of the RCCL all-reduce at action-selection time. */
 int pomcp_root_merge_buffer(pomcp_ctx* ctx, void** device_ptr);
 
+/* The root-parallel exchange of SURVEY §8(b)/(e) (mcts.py:269-306 run as
+ * root-parallel trees on several GPUs): sums the merge buffer over an RCCL
+ * communicator, in place, on the context's stream -- ncclAllReduce(buf, buf,
+ * num_trees * num_actions * 2, ncclFloat64, ncclSum, comm, stream) -- before
+ * pomcp_merge_roots.  rccl_comm: an ncclComm_t of the caller (one rank per
+ * GPU).  RCCL is resolved at the first call (the process's librccl if one is
+ * loaded, e.g. PyTorch's, else librccl.so.1); POMCP_E_UNSUPPORTED without it. */
+int pomcp_allreduce_root(pomcp_ctx* ctx, void* rccl_comm);
+
 /* Root-parallel decision of one planner. */
 typedef struct pomcp_merged_root {
   int32_t action;               /* merged final action (see pomcp_merge_roots) */

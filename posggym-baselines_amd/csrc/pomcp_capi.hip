@@ -3,6 +3,7 @@
 // Owns every device allocation of a planner batch, validates the
 // MCTSConfig-derived parameters (config.py:33-55 asserts) and launches the
 // kernels of pomcp_kernels.hip on one HIP stream.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -549,6 +550,35 @@ int pomcp_rekey(pomcp_ctx* ctx, uint64_t seed) {
 int pomcp_root_merge_buffer(pomcp_ctx* ctx, void** device_ptr) {
   if (!ctx || !device_ptr) return POMCP_E_INVALID;
   *device_ptr = ctx->dp.merge;
+  return POMCP_OK;
+}
+
+// ncclAllReduce, resolved at run time (no link-time RCCL dependency): the copy
+// already in the process if any (PyTorch's), else the system's
+typedef int (*pb_nccl_allreduce_fn)(const void*, void*, size_t, int, int, void*, hipStream_t);
+static pb_nccl_allreduce_fn pb_rccl_allreduce() {
+  static pb_nccl_allreduce_fn fn = nullptr;
+  static bool tried = false;
+  if (!tried) {
+    tried = true;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+    if (h) fn = reinterpret_cast<pb_nccl_allreduce_fn>(dlsym(h, "ncclAllReduce"));
+  }
+  return fn;
+}
+
+int pomcp_allreduce_root(pomcp_ctx* ctx, void* rccl_comm) {
+  if (!ctx || !rccl_comm) return POMCP_E_INVALID;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  const pb_nccl_allreduce_fn allreduce = pb_rccl_allreduce();
+  if (!allreduce) return fail(ctx, POMCP_E_UNSUPPORTED, "allreduce_root: librccl not found");
+  constexpr int kNcclFloat64 = 8, kNcclSum = 0;   // rccl.h ncclDataType_t / ncclRedOp_t
+  const size_t n = (size_t)ctx->dp.B * (size_t)ctx->dp.A * 2;
+  const int rc = allreduce(ctx->dp.merge, ctx->dp.merge, n, kNcclFloat64, kNcclSum, rccl_comm,
+                           ctx->stream);
+  if (rc != 0) return fail(ctx, POMCP_E_HIP, "allreduce_root: ncclAllReduce error " + std::to_string(rc));
   return POMCP_OK;
 }
 

@@ -175,6 +175,7 @@ SIGNATURES = [
     ("pomcp_arena_usage", C.c_int, [_CTX, _P32, _P32]),
     ("pomcp_rekey", C.c_int, [_CTX, C.c_uint64]),
     ("pomcp_root_merge_buffer", C.c_int, [_CTX, C.POINTER(C.c_void_p)]),
+    ("pomcp_allreduce_root", C.c_int, [_CTX, C.c_void_p]),
     ("pomcp_merge_roots", C.c_int, [_CTX, C.c_int32, C.POINTER(PomcpMergedRoot)]),
     ("pomcp_synthetic_obs", C.c_int, [_CTX, C.c_uint64, _PU64]),
     ("pomcp_snapshot", C.c_int, [_CTX]),

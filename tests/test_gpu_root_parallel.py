@@ -171,3 +171,37 @@ def test_root_parallel_wall_clock_episode():
     planner.close()
     assert trace["len"] >= 3 and len(steps) >= 2
     assert all(0 <= a < 5 and n >= 16 * 16 and n % 16 == 0 for a, n in steps), steps
+
+
+def test_allreduce_root_c_abi_single_rank():
+    """pomcp_allreduce_root (the C-ABI exchange of SURVEY §8(b)) over a one-rank
+    RCCL communicator made with the process's librccl (ncclCommInitAll): the
+    sum over one rank leaves the merge buffer as it was, and the device merge
+    after it is the merge without it."""
+    import ctypes as C
+    import torch
+    from posggym_baselines_amd import _native as N
+    from posggym_baselines_amd.planning import BatchedPOMCP
+    from posggym_baselines_amd.planning.parallel import merge_buffer_tensor
+    model = product_model("Driving-v1")
+    bp = BatchedPOMCP(model, "0", product_config(CFG, 64), 16, 64)
+    bp.init_synthetic(1000)
+    bp.search()
+    bp.engine.root_stats()   # synchronises the engine
+    dev = torch.device("cuda:0")
+    before = merge_buffer_tensor(bp.engine, dev).cpu().clone()
+    key = lambda ms: [(m.action, list(m.visits), [float(x).hex() for x in m.totals]) for m in ms]
+    m0 = key(bp.engine.merge_roots(4))
+    rccl = C.CDLL("librccl.so.1")
+    comm = C.c_void_p()
+    devs = (C.c_int * 1)(0)
+    assert rccl.ncclCommInitAll(C.byref(comm), 1, devs) == 0
+    try:
+        assert N.load().pomcp_allreduce_root(bp.engine._ctx, comm) == 0
+        bp.engine.root_stats()
+        after = merge_buffer_tensor(bp.engine, dev).cpu()
+        assert torch.equal(before, after)
+        assert key(bp.engine.merge_roots(4)) == m0
+    finally:
+        rccl.ncclCommDestroy(comm)
+        bp.close()
