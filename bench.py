@@ -51,52 +51,79 @@ HBM_PEAK_GBS = 8000.0
 def _device_info(dev):
     """Name and compute-unit count of the GPU (the same code measures 3.75-4.73 G
     sims/s across boxes of the pool, DESIGN.md §6: recorded to tell boxes apart)."""
-    import subprocess
     import torch
     p = torch.cuda.get_device_properties(dev)
     info = {"name": p.name, "gcn_arch": getattr(p, "gcnArchName", ""),
             "compute_units": p.multi_processor_count,
             "hbm_gib": round(p.total_memory / 2**30, 1)}
-    try:   # static facts that may differ between boxes (rocm-smi; optional)
+    if _SMI_STATIC:
+        info["smi"] = dict(_SMI_STATIC)
+    return info
+
+
+_SMI_STATIC = {}
+
+
+def _smi_static():
+    """Facts that may differ between boxes (memory vendor, partition modes),
+    read with rocm-smi BEFORE this process touches the GPU: a child process
+    started after the GPU is initialised may not exec (it inherits the
+    device), so nothing later in the run starts one."""
+    import subprocess
+    try:
         out = subprocess.run(["rocm-smi", "-d", os.environ.get("LOCAL_RANK", "0"), "--showmemvendor",
                               "--showcomputepartition", "--showmemorypartition", "--json"],
                              capture_output=True, text=True, timeout=10).stdout
         d = next(iter(json.loads(out[out.index("{"):]).values()))
-        info["smi"] = {k: v for k, v in d.items() if "artition" in k or "vendor" in k}
+        _SMI_STATIC.update({k: v for k, v in d.items() if "artition" in k or "vendor" in k})
     except Exception:
         pass
-    return info
 
 
 class _ClockSampler:
-    """`rocm-smi` readings of this rank's GPU taken during the timed region
-    (graphics clock, package power): recorded beside the result, because the
-    same code measures differently on different boxes of the pool (DESIGN.md
-    §6).  A child process per reading; a failure only leaves the list empty."""
+    """Graphics clock and package power read from sysfs (no child process)
+    during the timed region, recorded beside the result because the same code
+    measures differently on different boxes of the pool.  The
+    GPU drawing the most power is reported (this run's, on a one-GPU box).  A
+    failure only leaves the list empty."""
 
-    def __init__(self, card: int, every_s: float = 0.4):
+    def __init__(self, every_s: float = 0.3):
         import threading
-        self.card, self.every, self.samples = card, every_s, []
+        self.every, self.samples = every_s, []
         self._stop = threading.Event()
         self._t = threading.Thread(target=self._run, daemon=True)
 
-    def _run(self):
-        import re
-        import subprocess
-        while not self._stop.is_set() and len(self.samples) < 8:
+    @staticmethod
+    def _read():
+        import glob
+        best = None
+        for dev in glob.glob("/sys/class/drm/card*/device"):
             try:
-                out = subprocess.run(["rocm-smi", "-d", str(self.card), "--showclocks",
-                                      "--showpower", "--json"], capture_output=True, text=True,
-                                     timeout=5).stdout
-                d = next(iter(json.loads(out[out.index("{"):]).values()))
-                mhz = {}
-                for c in ("sclk", "mclk", "fclk"):
-                    m = re.search(r"(\d+)", d.get(f"{c} clock speed:", ""))
-                    mhz[f"{c}_mhz"] = int(m.group(1)) if m else None
-                pw = d.get("Current Socket Graphics Package Power (W)")
-                self.samples.append(dict(mhz, power_w=float(pw) if pw else None))
+                with open(os.path.join(dev, "pp_dpm_sclk")) as f:
+                    cur = [ln for ln in f.read().splitlines() if ln.strip().endswith("*")]
+                sclk = int("".join(ch for ch in cur[0].split(":")[1] if ch.isdigit())) if cur else None
+                pw = None
+                for h in glob.glob(os.path.join(dev, "hwmon", "hwmon*")):
+                    for name in ("power1_average", "power1_input"):
+                        fp = os.path.join(h, name)
+                        if os.path.exists(fp):
+                            with open(fp) as f:
+                                pw = int(f.read().strip()) / 1e6
+                            break
+                    if pw is not None:
+                        break
+                if best is None or (pw or 0.0) > (best["power_w"] or 0.0):
+                    best = {"sclk_mhz": sclk, "power_w": pw}
             except Exception:
+                continue
+        return best
+
+    def _run(self):
+        while not self._stop.is_set() and len(self.samples) < 16:
+            r = self._read()
+            if r is None:
                 return
+            self.samples.append(r)
             self._stop.wait(self.every)
 
     def __enter__(self):
@@ -243,14 +270,14 @@ def cpu_baseline_intmcp(sims, pairs, seed, env="Driving-v1"):
 
 def main_intmcp(args):
     import torch
-    torch.cuda.set_device(0)
-    dev = torch.cuda.current_device()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
         raise SystemExit("--planner intmcp is a single-GPU configuration (BASELINE config 5)")
     from posggym_baselines_amd import build as nb
     if not os.environ.get("POMCP_LIB_PATH"):   # a prebuilt variant library is used as it is
-        nb.build()
+        nb.build()   # (before the GPU is touched: hipcc runs as a child process)
+    torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
     from posggym_baselines_amd.envs import DrivingModel, PursuitEvasionModel
     from posggym_baselines_amd.planning import BatchedINTMCP, MCTSConfig
     from posggym_baselines_amd.planning.intmcp import plan_intmcp_capacities
@@ -344,6 +371,7 @@ def main_intmcp(args):
                                "level x 2 levels per step (one batched launch), ucb c=sqrt2 "
                                "gamma=0.95 depth_limit=2",
                    "pairs": B, "sims_per_level": S, "pairs_searched": searched,
+                   "device": _device_info(dev),
                    "arena_per_pair": {"max_nodes": caps.max_nodes, "max_stats": caps.max_stats,
                                       "max_log": caps.max_log, "hash_slots": caps.hash_slots,
                                       "bytes": caps.bytes_per_pair(A),
@@ -362,6 +390,7 @@ def main_intmcp(args):
 
 def main():
     args = parse()
+    _smi_static()   # before anything touches the GPU
     if args.planner == "intmcp":
         return main_intmcp(args)
     import torch
@@ -377,6 +406,9 @@ def main():
         procs = max(1, min(args.cpu_procs, os.cpu_count() or 1))
         sample = args.cpu_sample_sims if not args.deep else max(64, args.cpu_sample_sims // 8)
         cpu = cpu_baseline_parallel(sample, procs, args.seed, args.env, base_cfg)
+    from posggym_baselines_amd import build as nb
+    if rank == 0 and not os.environ.get("POMCP_LIB_PATH"):   # prebuilt variants as they are
+        nb.build()   # before the GPU is touched (hipcc runs as a child process)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
@@ -384,12 +416,8 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
-
-    from posggym_baselines_amd import build as nb
-    if rank == 0 and not os.environ.get("POMCP_LIB_PATH"):   # prebuilt variants as they are
-        nb.build()
     if world > 1:
-        dist.barrier()
+        dist.barrier()   # rank 0's build is complete
     from posggym_baselines_amd.envs import DrivingModel, PursuitEvasionModel
     from posggym_baselines_amd.planning import BatchedPOMCP, MCTSConfig
     from posggym_baselines_amd.planning.engine import plan_capacities
@@ -433,7 +461,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    with _ClockSampler(int(os.environ.get("LOCAL_RANK", "0"))) as clocks:
+    with _ClockSampler() as clocks:
         t0 = time.perf_counter()
         for k in range(args.steps):
             step(ev[k])
