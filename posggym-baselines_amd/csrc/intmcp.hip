@@ -26,7 +26,7 @@ namespace pb {
 
 constexpr int kImPath = 128;          // tree levels per simulation
 constexpr int kImMaxA = 6;            // registration order: 6 x 3 bits (INode.info)
-constexpr int kImRegPath = 4;         // path levels held in registers (deeper ones in p.path)
+constexpr int kImRegPath = 3;         // path levels held in registers (deeper ones in p.path)
 // A node's block, two 128 B lines: line 0 = the INode (32 B) + the head
 // {visits, -, value} of each action's statistics (16 B each); line 1 = their
 // {total, agg} tails.  A node view (selection, the other agent's softmax)
