@@ -162,6 +162,25 @@ struct ImPair {
     h = p.hdr[b];
   }
   __device__ void store() { p.hdr[pair] = h; }
+  // what a search changes (k_im_search): the other fields need not stay live
+  // in registers for the launch
+  __device__ void store_search() {
+    IHdr& o = p.hdr[pair];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      o.n_nodes[k] = h.n_nodes[k];
+      o.n_stats[k] = h.n_stats[k];
+      o.n_log[k] = h.n_log[k];
+      o.mm_min[k] = h.mm_min[k];
+      o.mm_max[k] = h.mm_max[k];
+    }
+#pragma unroll
+    for (int q = 0; q < 6; ++q) o.ctr[q] = h.ctr[q];
+    o.err = h.err;
+    o.last_action = h.last_action;
+    o.num_sims = h.num_sims;
+    o.search_depth = h.search_depth;
+  }
 
   // A node's block (kImBlock): the INode with the heads of its actions'
   // statistics (node.py:120-178) in one line, so a node and its statistics
@@ -1269,7 +1288,7 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
     }
     if (!(flags & kImFinal) || P.h.err != 0) {   // no action from a failed search
       if (P.h.err != 0 && (flags & kImFinal)) P.h.last_action = -1;
-      P.store();
+      P.store_search();
       return;
     }
     // max_value_action_selection (intmcp.py:718-732)
@@ -1296,7 +1315,7 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
     }
   }
   if (flags & kImFinal) P.h.last_action = action;
-  P.store();
+  P.store_search();
 }
 
 template <class Env>
