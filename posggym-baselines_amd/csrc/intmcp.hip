@@ -52,6 +52,7 @@ constexpr uint32_t kImNoSupport = 0xFFFFFFFFu;
 constexpr int32_t kImSkip = -2;       // intmcp_update action: leave the pair untouched
 constexpr int kWave64 = 64;           // lanes of a wave (k_im_update's wave mode)
 constexpr int kImLogLds = 2048;       // math.log(N) entries staged in LDS by k_im_search
+constexpr int kImDpowLds = 64;        // discount powers staged in LDS by k_im_search
 constexpr int kImRootWords = 8;       // the level-1 root's view (INode + 6 heads) in LDS, uint4s
 
 struct INode {          // 32 B
@@ -146,6 +147,15 @@ struct ImPair {
   int lt_n = 0;
   uint4* rv = nullptr;
   int rv_root = -1;
+  // the rollout's discount powers (k_im_search: staged in LDS)
+  const double* dp = nullptr;
+  // k_im_search only: one-word lookahead per RNG stream.  la_fill computes the
+  // next word of every stream whose last word was consumed, at points where the
+  // wave waits on a load anyway; draw() consumes it.  Each stream is consumed
+  // in order, so results are unchanged; stored counters exclude a computed but
+  // unconsumed word (la_pend).
+  uint32_t la_w[6];
+  uint32_t la_pend = 0u;
 
   __device__ ImPair(const ImParams& pp, const Model& mm, int b) : p(pp), m(mm), pair(b) {
     for (int k = 0; k < 2; ++k) {
@@ -160,8 +170,15 @@ struct ImPair {
     path = p.path + (int64_t)b * kImPath * 3;
     prob = p.prob + (int64_t)b * p.Nr;
     h = p.hdr[b];
+    dp = p.dpow;
   }
-  __device__ void store() { p.hdr[pair] = h; }
+  __device__ __forceinline__ uint32_t ctr_stored(int q) const { return h.ctr[q] - ((la_pend >> q) & 1u); }
+  __device__ void store() {
+    IHdr o = h;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) o.ctr[q] = ctr_stored(q);
+    p.hdr[pair] = o;
+  }
   // what a search changes (k_im_search): the other fields need not stay live
   // in registers for the launch
   __device__ void store_search() {
@@ -175,7 +192,7 @@ struct ImPair {
       o.mm_max[k] = h.mm_max[k];
     }
 #pragma unroll
-    for (int q = 0; q < 6; ++q) o.ctr[q] = h.ctr[q];
+    for (int q = 0; q < 6; ++q) o.ctr[q] = ctr_stored(q);
     o.err = h.err;
     o.last_action = h.last_action;
     o.num_sims = h.num_sims;
@@ -229,16 +246,32 @@ struct ImPair {
   }
 
   // ------------------------------------------------------------------ RNG
-  __device__ uint32_t draw(int slot, uint32_t stream) {
+  __device__ __forceinline__ uint32_t draw(int slot, uint32_t stream) {
+    if ((la_pend >> slot) & 1u) {
+      la_pend &= ~(1u << slot);
+      return la_w[slot];
+    }
     return philox_word(h.seed, h.tree_key, stream, h.ctr[slot]++);
   }
-  __device__ uint32_t d_bel(int level, uint32_t n) {   // planner random.Random(seed)
+  __device__ __forceinline__ void la_fill() {
+    constexpr uint32_t st[6] = {S_BELIEF, S_SELECT, S_MODEL, S_ACT_BASE, S_ACT_BASE + 1,
+                                S_BELIEF_NESTED};
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      if (q == 2 && !Env::kStepDraws) continue;
+      if (!((la_pend >> q) & 1u)) {
+        la_w[q] = philox_word(h.seed, h.tree_key, st[q], h.ctr[q]++);
+        la_pend |= 1u << q;
+      }
+    }
+  }
+  __device__ __forceinline__ uint32_t d_bel(int level, uint32_t n) {   // planner random.Random(seed)
     return level == 1 ? uniform_int(draw(0, S_BELIEF), n) : uniform_int(draw(5, S_BELIEF_NESTED), n);
   }
-  __device__ uint32_t d_sel(uint32_t n) { return uniform_int(draw(1, S_SELECT), n); }
-  __device__ double d_sel_float() { return uniform_float(draw(1, S_SELECT)); }
-  __device__ uint32_t d_model(uint32_t n) { return uniform_int(draw(2, S_MODEL), n); }
-  __device__ uint32_t d_act(int agent, uint32_t n) {   // model.action_spaces[agent].sample()
+  __device__ __forceinline__ uint32_t d_sel(uint32_t n) { return uniform_int(draw(1, S_SELECT), n); }
+  __device__ __forceinline__ double d_sel_float() { return uniform_float(draw(1, S_SELECT)); }
+  __device__ __forceinline__ uint32_t d_model(uint32_t n) { return uniform_int(draw(2, S_MODEL), n); }
+  __device__ __forceinline__ uint32_t d_act(int agent, uint32_t n) {   // model.action_spaces[agent].sample()
     return agent == 0 ? uniform_int(draw(3, S_ACT_BASE), n) : uniform_int(draw(4, S_ACT_BASE + 1), n);
   }
 
@@ -595,7 +628,7 @@ struct ImPair {
         fail(POMCP_E_ARENA);
         return ret;
       }
-      ret += p.dpow[kk] * r;
+      ret += dp[kk] * r;
       if (done) break;
       s0 = n0;
       s1 = n1;
@@ -621,9 +654,11 @@ struct ImPair {
     bool have_nv = false;
     INode pnx;                 // the previous level's history node, as it is now
     int pn = -1;
+    int roll_t = -1;           // >= 0: the descent ended at a leaf of this t
     if (k == 0 && !p.state_belief_only) {   // the first level's history view, in flight
       nv = view(1, (int)nested);            // while the root selection runs
       have_nv = true;
+      la_fill();                            // (the RNG words, while it is in flight)
     }
     for (;;) {
       const INode& x = v.x;
@@ -631,8 +666,8 @@ struct ImPair {
       if (im_nreg(x.info) < p.A) {                 // leaf: add the missing children
         INode xe = x;
         expand_known(k, n, xe);
-        leaf = rollout(k, s0, s1, x.t, depth);
-        break;
+        roll_t = x.t;   // the rollout runs after the loop: once for the whole wave,
+        break;          // not once per depth at which some lane reached a leaf
       }
       const int a = select(k, v);
       // the chosen action's {total, agg}: needed by the backup only (no wait)
@@ -681,6 +716,7 @@ struct ImPair {
         have_nv = true;
       }
       View cv = view(k, c);
+      la_fill();   // the next level's RNG words, while the child's view is in flight
       cv.x.visits = created ? 1 : cv.x.visits + 1;
       uint32_t info = cv.x.info;
       if (im_path_ok(x.info)) info |= 1u << 4;   // x: node n, unchanged since loaded
@@ -717,6 +753,7 @@ struct ImPair {
       nested = nn;
       ++depth;
     }
+    if (roll_t >= 0) leaf = rollout(k, s0, s1, roll_t, depth);
     double g = leaf;
     auto backup = [&](uint4 e0, uint4 e1, uint4 e2) {   // node.py:166-178
       const double r = hilo_d(e1.x, e1.y);
@@ -1205,8 +1242,12 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
   __shared__ typename Env::Model sm;
   __shared__ double slog[kImLogLds];                  // math.log(N): no global load per selection
   __shared__ uint4 srv[kImRootWords * kWave];         // level-1 root views, one column per lane
+  __shared__ double sdp[kImDpowLds];                  // discount powers (rollout)
   const int ltn = p.logtab_n < kImLogLds ? (int)p.logtab_n : kImLogLds;
   for (int i = threadIdx.x; i < ltn; i += blockDim.x) slog[i] = p.logtab[i];
+  const bool dp_lds = p.dpow_n <= kImDpowLds;
+  if (dp_lds)
+    for (int i = threadIdx.x; i < p.dpow_n; i += blockDim.x) sdp[i] = p.dpow[i];
   stage_model(p.model, sm);                           // (synchronises)
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= p.B) return;
@@ -1214,6 +1255,7 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
   P.lt_lds = slog;
   P.lt_n = ltn;
   P.rv = srv + threadIdx.x;
+  if (dp_lds) P.dp = sdp;
   if (flags & kImBegin) {
     P.h.num_sims = 0;
     P.h.search_depth = 0;
@@ -1265,6 +1307,7 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
           }
           const uint2 q = sparts[e.off + P.d_bel(0, (uint32_t)e.size)];
           auto v = P.view(1, n);
+          P.la_fill();   // the RNG words, while the start node's view is in flight
           if (n > 0 && !im_path_ok(v.x.info)) {
             P.traverse(1, n);         // (n itself only gains the path_ok bit)
             v.x.info |= 1u << 4;

@@ -139,3 +139,40 @@ def test_wall_clock_small_arena_stops_early(monkeypatch):
     assert len(steps) >= 3
     assert any(st.get("arena_full") for st in steps)
     assert all(st["child_visits"] <= st["visits"] for st in steps)
+
+
+def test_search_split_over_launches_equals_one_launch():
+    """The wall-clock loop's chunked launches (search_levels, several per level,
+    then the final selection alone) are bit-identical to one launch of the same
+    totals, and so is the next step (update + search) after them: the RNG
+    words k_im_search computes ahead and does not consume are not counted as
+    drawn (ImPair::la_pend)."""
+    import numpy as np
+    from gpu_util import intmcp_state_record, product_config, product_model
+    from posggym_baselines_amd import _native as N
+    from posggym_baselines_amd.planning import BatchedINTMCP
+    model = product_model("Driving-v1")
+    B, S = 130, 96
+    one = BatchedINTMCP(model, "0", product_config(TEST_CFG, S), B, S, searches=2)
+    split = BatchedINTMCP(model, "0", product_config(TEST_CFG, S), B, S, searches=2)
+    keys = one.init_synthetic(1000)
+    split.init_synthetic(1000)
+    for step in range(2):
+        a1 = one.search()
+        e = split.engine
+        e.search_levels(40, 0, N.INTMCP_BEGIN)
+        e.search_levels(S - 40, 0, 0)
+        e.search_levels(0, 7, 0)
+        e.search_levels(0, S - 7, 0)
+        e.search_levels(0, 0, N.INTMCP_FINAL)
+        a2 = np.array([s.action for s in e.root_stats()], dtype=a1.dtype)
+        assert np.array_equal(a1, a2), step
+        for b in (0, 1, 63, 64, 129):
+            r1 = intmcp_state_record(one.engine, b, True, int(a1[b]))
+            r2 = intmcp_state_record(e, b, True, int(a2[b]))
+            assert r1 == r2, (step, b)
+        acts = np.asarray(a1, dtype=np.int32)
+        one.engine.update(acts, keys)
+        e.update(acts, keys)
+    one.close()
+    split.close()
