@@ -309,6 +309,13 @@ def main_intmcp(args):
                              int(1.5 * mx(lambda s: max(s.n_stats[0], s.n_stats[1]))) + 64 * A)
         caps.hash_slots = min(caps.hash_slots, 1 << max(4, (2 * nodes - 1).bit_length()))
         probe.close()
+    # every timed step searches the same trees again (no restore), so the arenas
+    # grow with warmup + steps: say so instead of failing inside hipMalloc
+    need, free = caps.bytes_per_pair(A) * B, torch.cuda.mem_get_info(dev)[0]
+    if need > 0.95 * free:
+        raise SystemExit(f"I-NTMCP arenas for {B} pairs x {searches} searches need "
+                         f"{need / 2**30:.0f} GiB, {free / 2**30:.0f} GiB free: "
+                         "use fewer --steps/--warmup or --trees")
     stream = torch.cuda.Stream(device=dev)
     bp = BatchedINTMCP(model, "0", cfg, B, S, capacities=caps, stream=stream.cuda_stream,
                        device=dev)
