@@ -86,11 +86,6 @@ INTMCP_CASES = {
     "intmcp_uniform": ({"action_selection": "uniform"}, 32, [(3, 3)], "0", 50, "Driving-v1"),
     "intmcp_deep": ({"discount": 0.99, "epsilon": 0.01}, 16, [(4, 4)], "0", 20, "Driving-v1"),
     "intmcp_pe": ({}, 48, [(5, 5)], "0", 100, "PursuitEvasion-v1"),
-},
-                        16, [(2, 2)], "0", 50, "Driving-v1"),
-    "intmcp_depleted_pe": ({"extra_particles_prop": 1.0,
-                            "reinvigoration_sample_limit_factor": 0.45, "action_selection": "uniform"},
-                           16, [(5, 5)], "1", 100, "PursuitEvasion-v1"),
 }
 
 
@@ -133,39 +128,156 @@ def config_kats():
     return rows
 
 
-def main(only=None):
+def tracker_sequences():
+    """Scripted ``step_statistics`` sequences for ``PlanningStatTracker``
+    (utils.py:45-144): NaN steps (an absorbing root reports NaN search
+    statistics), keys missing from a step (``.get(k, np.nan)``, utils.py:82),
+    ``mem_usage`` reduced by max, an empty episode (``reset_episode`` with no
+    steps is a no-op, utils.py:98-99) and ``track_overall=False``."""
+    nan = float("nan")
+    keys = ["search_time", "update_time", "reinvigoration_time", "evaluation_time",
+            "policy_calls", "inference_time", "search_depth", "num_sims", "mem_usage",
+            "min_value", "max_value"]
+
+    def full(i, j):
+        return {k: 0.125 * (i + 1) + 0.01 * j * (n + 1) - (0.3 if k == "min_value" else 0.0)
+                for n, k in enumerate(keys)}
+
+    eps = []
+    # 1: plain steps
+    eps.append([full(0, j) for j in range(4)])
+    # 2: a NaN step in the middle (absorbing root) and one with missing keys
+    e = [full(1, j) for j in range(5)]
+    e[2] = dict(e[2], search_time=nan, num_sims=nan, min_value=nan, max_value=nan)
+    e[3] = {"search_time": 0.5, "mem_usage": 7.0, "num_sims": 33.0}
+    eps.append(e)
+    # 3: empty episode (reset with no steps)
+    eps.append([])
+    # 4: every step NaN for some keys, mem_usage falling then rising
+    e = [dict(full(2, j), mem_usage=m, search_depth=nan) for j, m in enumerate((9.0, 3.0, 12.5))]
+    eps.append(e)
+    # 5: a single step with only mem_usage
+    eps.append([{"mem_usage": 2.0}])
+    return eps
+
+
+def _enc(v):
+    """JSON form of a tracker value: hex float, 'nan' or a list of them."""
+    import numpy as np
+    if isinstance(v, (list, tuple, np.ndarray)):
+        return [_enc(x) for x in v]
+    v = float(v)
+    return "nan" if math.isnan(v) else v.hex()
+
+
+def planning_stat_tracker():
+    """Run the reference ``PlanningStatTracker`` over tracker_sequences():
+    get_episode() after every step, get() after every reset_episode()."""
+    import_reference()
+    from posggym_baselines.planning.utils import PlanningStatTracker
+
+    class _Planner:
+        step_statistics = {}
+
+    out = []
+    for track_overall in (True, False):
+        pl = _Planner()
+        tr = PlanningStatTracker(pl, track_overall=track_overall)
+        log = {"track_overall": track_overall, "episodes": []}
+        for ep in tracker_sequences():
+            rec = {"steps": [{k: _enc(v) for k, v in st.items()} for st in ep],
+                   "get_episode": [], "get": None}
+            for st in ep:
+                pl.step_statistics = dict(st)
+                tr.step()
+                rec["get_episode"].append({k: _enc(v) for k, v in tr.get_episode().items()})
+            tr.reset_episode()
+            rec["get"] = {k: _enc(v) for k, v in tr.get().items()}
+            rec["num_episodes"] = tr._num_episodes
+            rec["all_steps"] = list(tr._all_steps)
+            log["episodes"].append(rec)
+        out.append(log)
+    return out
+
+
+def config_checks():
+    """MCTSConfig.__post_init__ assertions and normalisation (config.py:33-45)
+    from the reference: which argument sets raise, and the lower-cased
+    ``action_selection``."""
+    P = import_reference()
+    base = dict(discount=0.95, search_time_limit=0.1, c=1.0, truncated=False)
+    cases = [
+        {}, {"discount": -0.01}, {"discount": 1.01}, {"discount": 0.0}, {"search_time_limit": 0.0},
+        {"search_time_limit": -1.0}, {"c": 0.0}, {"c": -1.0}, {"pucb_exploration_fraction": -0.1},
+        {"pucb_exploration_fraction": 1.0}, {"pucb_exploration_fraction": 1.1},
+        {"extra_particles_prop": 1.5}, {"extra_particles_prop": -0.5}, {"epsilon": 0.0},
+        {"epsilon": 1.0}, {"epsilon": 0.999}, {"action_selection": "UCB"},
+        {"action_selection": "Uniform"}, {"action_selection": "PUCB"}, {"action_selection": "greedy"},
+        {"search_time_limit": 0.001}, {"search_time_limit": 0.015, "extra_particles_prop": 1.0},
+    ]
+    rows = []
+    for over in cases:
+        kw = dict(base, **over)
+        row = {"kwargs": kw}
+        try:
+            c = P.MCTSConfig(**kw)
+            row.update(action_selection=c.action_selection, num_particles=c.num_particles,
+                       extra_particles=c.extra_particles, depth_limit=c.depth_limit)
+        except Exception as ex:
+            row["raises"] = type(ex).__name__
+        rows.append(row)
+    return rows
+
+
+def _write(out_dir, name, data):
+    with open(os.path.join(out_dir, f"{name}.json"), "w") as f:
+        json.dump(data, f, separators=(",", ":"))
+
+
+def main(only=None, out_dir=HERE):
+    """only: None (every fixture), "ipomcp", "meta" (config + tracker
+    fixtures only) or a list of I-NTMCP case names."""
     if not reference_available():
         raise SystemExit("reference not available (container-only script)")
+    os.makedirs(out_dir, exist_ok=True)
     for name in CASES if only is None else ():
         data = run_case(name)
-        with open(os.path.join(HERE, f"{name}.json"), "w") as f:
-            json.dump(data, f, separators=(",", ":"))
+        _write(out_dir, name, data)
         n = sum(len(e["records"]) for e in data["episodes"])
         print(f"{name}: {len(data['episodes'])} episodes, {n} records")
     for name in IPOMCP_CASES if only in (None, "ipomcp") else ():
         data = run_case(name, IPOMCP_CASES, "IPOMCP")
-        with open(os.path.join(HERE, f"{name}.json"), "w") as f:
-            json.dump(data, f, separators=(",", ":"))
+        _write(out_dir, name, data)
         n = sum(len(e["records"]) for e in data["episodes"])
         print(f"{name}: {len(data['episodes'])} episodes, {n} records")
     for name in INTMCP_CASES if only is None else (only if isinstance(only, list) else ()):
         data = run_intmcp_case(name)
-        with open(os.path.join(HERE, f"{name}.json"), "w") as f:
-            json.dump(data, f, separators=(",", ":"))
+        _write(out_dir, name, data)
         n = sum(len(e["records"]) for e in data["episodes"])
         print(f"{name}: {len(data['episodes'])} episodes, {n} records")
-    if only is None:
-        with open(os.path.join(HERE, "config_kats.json"), "w") as f:
-            json.dump(config_kats(), f, separators=(",", ":"))
-        print("config_kats written")
+    if only in (None, "meta"):
+        _write(out_dir, "config_kats", config_kats())
+        _write(out_dir, "config_checks", config_checks())
+        _write(out_dir, "planning_stat_tracker", planning_stat_tracker())
+        print("config_kats, config_checks, planning_stat_tracker written")
 
 
 if __name__ == "__main__":
-    # --ipomcp: (re)generate only the IPOMCP fixtures; --intmcp NAME...: only
-    # the named I-NTMCP fixtures
-    if "--ipomcp" in sys.argv:
-        main(only="ipomcp")
-    elif "--intmcp" in sys.argv:
-        main(only=sys.argv[sys.argv.index("--intmcp") + 1:])
+    # --out DIR: write there instead of tests/golden/ (the CPU test regenerates
+    # into a temporary directory and compares byte for byte);
+    # --ipomcp: only the IPOMCP fixtures; --meta: only the config / tracker
+    # fixtures; --intmcp NAME...: only the named I-NTMCP fixtures
+    argv = list(sys.argv[1:])
+    out = HERE
+    if "--out" in argv:
+        i = argv.index("--out")
+        out = argv[i + 1]
+        del argv[i:i + 2]
+    if "--ipomcp" in argv:
+        main(only="ipomcp", out_dir=out)
+    elif "--meta" in argv:
+        main(only="meta", out_dir=out)
+    elif "--intmcp" in argv:
+        main(only=argv[argv.index("--intmcp") + 1:], out_dir=out)
     else:
-        main()
+        main(out_dir=out)

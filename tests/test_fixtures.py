@@ -1,0 +1,115 @@
+"""The fixture generator and the host-side contracts it pins (no GPU).
+
+* ``tests/golden/make_golden.py`` compiles, and -- where ``/root/reference``
+  exists (this container; never the GPU box) -- regenerates every committed
+  fixture byte for byte from the real reference.
+* The product ``PlanningStatTracker`` equals the reference tracker
+  (``posggym_baselines/planning/utils.py:45-144``) on scripted step sequences
+  (``planning_stat_tracker.json``).
+* The product ``MCTSConfig`` equals the reference's derived fields and
+  assertions (``config.py:33-55``; ``config_kats.json``, ``config_checks.json``).
+"""
+import filecmp
+import math
+import os
+import py_compile
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from golden_util import GOLDEN, load
+from posggym_baselines_amd.planning import MCTSConfig
+from posggym_baselines_amd.planning.utils import PlanningStatTracker
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MAKE = os.path.join(GOLDEN, "make_golden.py")
+
+
+def test_make_golden_compiles(tmp_path):
+    py_compile.compile(MAKE, cfile=str(tmp_path / "make_golden.pyc"), doraise=True)
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/posggym_baselines"),
+                    reason="the reference exists only in the build container")
+def test_make_golden_regenerates_committed_fixtures(tmp_path):
+    out = tmp_path / "golden"
+    r = subprocess.run([sys.executable, MAKE, "--out", str(out)], cwd=ROOT, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    committed = sorted(f for f in os.listdir(GOLDEN) if f.endswith(".json"))
+    made = sorted(f for f in os.listdir(out) if f.endswith(".json"))
+    assert made == committed
+    _, mismatch, errors = filecmp.cmpfiles(GOLDEN, str(out), committed, shallow=False)
+    assert mismatch == [] and errors == []
+
+
+def _dec(v):
+    if isinstance(v, list):
+        return [_dec(x) for x in v]
+    return float("nan") if v == "nan" else float.fromhex(v)
+
+
+def _enc(v):
+    v = float(v)
+    return "nan" if math.isnan(v) else v.hex()
+
+
+@pytest.mark.filterwarnings("ignore::RuntimeWarning")
+def test_planning_stat_tracker_matches_reference():
+    class _Planner:
+        step_statistics = {}
+
+    for log in load("planning_stat_tracker"):
+        pl = _Planner()
+        tr = PlanningStatTracker(pl, track_overall=log["track_overall"])
+        for ep in log["episodes"]:
+            for st, exp in zip(ep["steps"], ep["get_episode"]):
+                pl.step_statistics = {k: _dec(v) for k, v in st.items()}
+                tr.step()
+                assert {k: _enc(v) for k, v in tr.get_episode().items()} == exp
+            tr.reset_episode()
+            assert {k: _enc(v) for k, v in tr.get().items()} == ep["get"]
+            assert tr._num_episodes == ep["num_episodes"]
+            assert list(tr._all_steps) == ep["all_steps"]
+
+
+def test_product_config_kats():
+    for row in load("config_kats"):
+        kw = dict(discount=row["discount"], search_time_limit=row["search_time_limit"], c=1.0,
+                  truncated=False, epsilon=row["epsilon"],
+                  extra_particles_prop=row["extra_particles_prop"])
+        if "raises" in row:
+            with pytest.raises(ZeroDivisionError):
+                MCTSConfig(**kw)
+            continue
+        c = MCTSConfig(**kw)
+        assert (c.num_particles, c.extra_particles, c.depth_limit) == (
+            row["num_particles"], row["extra_particles"], row["depth_limit"])
+
+
+def test_product_config_checks():
+    for row in load("config_checks"):
+        if "raises" in row:
+            exc = {"AssertionError": AssertionError, "ZeroDivisionError": ZeroDivisionError,
+                   "ValueError": ValueError}[row["raises"]]
+            with pytest.raises(exc):
+                MCTSConfig(**row["kwargs"])
+            continue
+        c = MCTSConfig(**row["kwargs"])
+        assert c.action_selection == row["action_selection"]
+        assert (c.num_particles, c.extra_particles, c.depth_limit) == (
+            row["num_particles"], row["extra_particles"], row["depth_limit"])
+
+
+def test_tracker_fixture_covers_nan_and_max_reductions():
+    """The fixture exercises what the verdict asked for: NaN steps, missing keys,
+    mem_usage max, an empty episode."""
+    log = load("planning_stat_tracker")[0]
+    steps = [st for ep in log["episodes"] for st in ep["steps"]]
+    assert any(v == "nan" for st in steps for v in st.values())
+    assert any(len(st) < 11 for st in steps)
+    assert any(len(ep["steps"]) == 0 for ep in log["episodes"])
+    mem = [_dec(ep["get"]["mem_usage_mean"]) for ep in log["episodes"]]
+    assert not all(np.isnan(mem))
