@@ -4,8 +4,9 @@ One step = one exact-mode POMCP search (``get_action``, mcts.py:269-306) of
 ``--sims`` simulations on each of ``--trees`` synthetic Driving-v1 roots
 (tree b's root is the ego's belief after the initial update for
 an environment sampled under seed 1000 + b), followed by the root-parallel
-exchange: one all-reduce (RCCL over xGMI) of every tree's (visit count, total
-value) per root action and the merged action choice.  Ranks search the same
+exchange: one all-gather (RCCL over xGMI) of every tree's exchange record
+((visit count, total value) per root action + step statistics) and the device
+merge of every planner's replicas in one fixed order.  Ranks search the same
 roots with different RNG keys (seed ^ rank << 32); per-GPU work is fixed as N
 grows (weak scaling).  Inputs are resident in HBM before timing starts; each
 timed step restores the post-update root state (a few KB per tree) and
@@ -37,6 +38,7 @@ for _p in (ROOT, os.path.join(ROOT, "posggym-baselines_amd")):
 # tree level stepped (node 8 + A x 12 child statistics + 100), per leaf expansion
 # (A x 28 + 4), per obs node created
 B_SIM, B_NEW_NODE = 16, 28
+B_LOG_APPEND = 16   # of b_level: the particle-log record (the root level's only HBM term)
 
 
 def b_level(A):
@@ -66,18 +68,58 @@ _SMI_STATIC = {}
 
 def _smi_static():
     """Facts that may differ between boxes (memory vendor, partition modes),
-    read with rocm-smi BEFORE this process touches the GPU: a child process
-    started after the GPU is initialised may not exec (it inherits the
-    device), so nothing later in the run starts one."""
-    import subprocess
+    read from sysfs: no child process is started (under rocprofv3 the GPU is
+    initialised before this program runs, and a process that has initialised
+    the GPU must not exec another program)."""
+    import glob
+    for dev in sorted(glob.glob("/sys/class/drm/card*/device")):
+        vals = {}
+        for key, name in (("GPU memory vendor", "mem_info_vram_vendor"),
+                          ("Compute Partition", "current_compute_partition"),
+                          ("Memory Partition", "current_memory_partition")):
+            try:
+                with open(os.path.join(dev, name)) as f:
+                    vals[key] = f.read().strip()
+            except OSError:
+                pass
+        if vals:
+            _SMI_STATIC.update(vals)
+            return
+
+
+def _lib_sha16():
+    """sha256 prefix of the engine library this process loads: PMC traffic in
+    profiles/ is reported only when it was measured on this same library."""
+    import hashlib
+    from posggym_baselines_amd import _native
+    with open(_native.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def _pmc_traffic(name, lib_sha, **match):
+    """HBM bytes per launch from profiles/<name> (tools/summarize_profile.py
+    --current) if it was measured on this library and workload, else None."""
+    prof = os.path.join(ROOT, "profiles", name)
     try:
-        out = subprocess.run(["rocm-smi", "-d", os.environ.get("LOCAL_RANK", "0"), "--showmemvendor",
-                              "--showcomputepartition", "--showmemorypartition", "--json"],
-                             capture_output=True, text=True, timeout=10).stdout
-        d = next(iter(json.loads(out[out.index("{"):]).values()))
-        _SMI_STATIC.update({k: v for k, v in d.items() if "artition" in k or "vendor" in k})
+        pm = json.load(open(prof))
     except Exception:
-        pass
+        return None
+    if pm.get("lib_sha16") != lib_sha:
+        return None
+    if any(pm.get(k, "Driving-v1" if k == "env" else None) != v for k, v in match.items()):
+        return None
+    return pm.get("hbm_bytes_per_launch")
+
+
+def _build_if_missing():
+    """The in-tree library is built by __graft_entry__.build() (or here when it
+    is missing, before the GPU is touched: hipcc runs as a child process); a
+    present library is used as it is -- never rebuilt from inside a profiled
+    run."""
+    from posggym_baselines_amd import _native
+    from posggym_baselines_amd import build as nb
+    if not os.path.exists(_native.LIB_PATH):
+        nb.build()
 
 
 class _ClockSampler:
@@ -273,9 +315,8 @@ def main_intmcp(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
         raise SystemExit("--planner intmcp is a single-GPU configuration (BASELINE config 5)")
-    from posggym_baselines_amd import build as nb
-    if not os.environ.get("POMCP_LIB_PATH"):   # a prebuilt variant library is used as it is
-        nb.build()   # (before the GPU is touched: hipcc runs as a child process)
+    _build_if_missing()
+    lib_sha = _lib_sha16()
     torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
     from posggym_baselines_amd.envs import DrivingModel, PursuitEvasionModel
@@ -352,15 +393,7 @@ def main_intmcp(args):
     alg_bytes = (B_SIM * sims_timed + b_level(A) * (lv0 + lv1) + b_other(A) * lv1
                  + B_STAT * stats + B_NODE_HASH * nodes) / args.steps
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    traffic = None
-    prof = os.path.join(ROOT, "profiles", "pmc_intmcp.json")
-    if os.path.exists(prof):
-        try:
-            pm = json.load(open(prof))
-            if pm.get("trees") == B and pm.get("sims") == S and pm.get("env") == args.env:
-                traffic = pm.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic = _pmc_traffic("pmc_intmcp.json", lib_sha, trees=B, sims=S, env=args.env)
     out = {
         "metric": f"I-NTMCP simulations/sec on {args.env} (nesting level 1, exact search)",
         "value": sims_timed / elapsed,
@@ -378,7 +411,7 @@ def main_intmcp(args):
                                "level x 2 levels per step (one batched launch), ucb c=sqrt2 "
                                "gamma=0.95 depth_limit=2",
                    "pairs": B, "sims_per_level": S, "pairs_searched": searched,
-                   "device": _device_info(dev),
+                   "device": _device_info(dev), "lib_sha16": lib_sha,
                    "arena_per_pair": {"max_nodes": caps.max_nodes, "max_stats": caps.max_stats,
                                       "max_log": caps.max_log, "hash_slots": caps.hash_slots,
                                       "bytes": caps.bytes_per_pair(A),
@@ -413,9 +446,8 @@ def main():
         procs = max(1, min(args.cpu_procs, os.cpu_count() or 1))
         sample = args.cpu_sample_sims if not args.deep else max(64, args.cpu_sample_sims // 8)
         cpu = cpu_baseline_parallel(sample, procs, args.seed, args.env, base_cfg)
-    from posggym_baselines_amd import build as nb
-    if rank == 0 and not os.environ.get("POMCP_LIB_PATH"):   # prebuilt variants as they are
-        nb.build()   # before the GPU is touched (hipcc runs as a child process)
+    if rank == 0:
+        _build_if_missing()
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
@@ -425,10 +457,11 @@ def main():
     dev = torch.cuda.current_device()
     if world > 1:
         dist.barrier()   # rank 0's build is complete
+    lib_sha = _lib_sha16()
     from posggym_baselines_amd.envs import DrivingModel, PursuitEvasionModel
     from posggym_baselines_amd.planning import BatchedPOMCP, MCTSConfig
     from posggym_baselines_amd.planning.engine import plan_capacities
-    from posggym_baselines_amd.planning.parallel import merge_buffer_tensor
+    from posggym_baselines_amd.planning.parallel import gather_buffer_tensor, merge_buffer_tensor
 
     B, S, K = args.trees, args.sims, args.root_parallel
     cfg = MCTSConfig(seed=args.seed, num_sims=S, **base_cfg)
@@ -443,6 +476,7 @@ def main():
     bp.engine.rekey(args.seed ^ (rank << 32))
     A = bp.engine.A
     merge = merge_buffer_tensor(bp.engine, f"cuda:{dev}")
+    gather = gather_buffer_tensor(bp.engine, world, f"cuda:{dev}") if world > 1 else None
 
     def step(events=None):
         with torch.cuda.stream(stream):
@@ -452,12 +486,13 @@ def main():
             bp.search(fetch=False)
             if events is not None:
                 events[1].record(stream)
-            # the root-parallel decision: one all-reduce of (visits, total) per
-            # root action (RCCL, same stream), then the device merge of each
-            # planner's K replicas (pomcp_merge_roots) -- the same on every rank
+            # the root-parallel decision: one all-gather of every rank's exchange
+            # records (RCCL, same stream), then the device merge of each planner's
+            # world x K replicas in replica order (pomcp_merge_roots) -- the same
+            # FP64 sums and action on every rank
             if world > 1:
-                dist.all_reduce(merge)
-            bp.engine.merge_roots(K, fetch=False)
+                dist.all_gather_into_tensor(gather, merge)
+            bp.engine.merge_roots(K, fetch=False, world=world if world > 1 else 0)
 
     for _ in range(args.warmup):
         step()
@@ -482,27 +517,29 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms = float(t[0]), float(t[1])
     st = bp.engine.root_stats()
-    sims = sum(s.num_sims for s in st)
+    sims = sum(s.num_sims for s in st)          # counted by the kernel, last timed launch
     levels = sum(s.n_levels for s in st)
     expands = sum(s.n_expansions for s in st)
     new_nodes = sum(s.n_new_nodes for s in st)
     alg_bytes = B_SIM * sims + b_level(A) * levels + b_expand(A) * expands + B_NEW_NODE * new_nodes
+    # the root level of every simulation is served from LDS / registers except
+    # its particle-log append: its other bytes never reach HBM
+    root_levels = min(sims, levels)
+    alg_bytes_hbm = alg_bytes - (b_level(A) - B_LOG_APPEND) * root_levels
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    total_sims = world * B * S * args.steps
+    achieved_hbm = alg_bytes_hbm / (kernel_ms * 1e-3) / 1e9
+    counted = sims
+    if world > 1:
+        t = torch.tensor([counted], dtype=torch.float64, device=f"cuda:{dev}")
+        dist.all_reduce(t)   # every rank's counted simulations
+        counted = int(t.item())
+    # every timed step re-searches the same restored roots: the same count each step
+    total_sims = counted * args.steps
     value = total_sims / elapsed
-    merged = bp.engine.merge_roots(K)   # the last step's decisions (checks replica errors)
+    merged = bp.engine.merge_roots(K, world=world if world > 1 else 0)   # checks replica errors
     if not all(0 <= m.action < A for m in merged):
         raise SystemExit("merged action out of range")
-    traffic = None
-    prof = os.path.join(ROOT, "profiles", "pmc_search.json")
-    if os.path.exists(prof):
-        try:
-            pm = json.load(open(prof))
-            if (pm.get("trees") == B and pm.get("sims") == S
-                    and pm.get("env", "Driving-v1") == args.env):
-                traffic = pm.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic = _pmc_traffic("pmc_search.json", lib_sha, trees=B, sims=S, env=args.env)
     env_desc = ("PursuitEvasion-v1 16x16 max_obs_distance=12" if args.env == "PursuitEvasion-v1"
                 else "Driving-v1 14x14RoundAbout")
     out = {
@@ -531,6 +568,7 @@ def main():
                    "rollout_steps_per_sim": sum(s.n_rollout_steps for s in st) / max(sims, 1),
                    "parallelism": f"root-parallel x{world}",
                    "device": dict(_device_info(dev), during_run=clocks.samples),
+                   "lib_sha16": lib_sha, "counted_sims_per_step": counted,
                    "arena": {"max_blocks": caps.max_blocks,
                              "max_blocks_used": max(s.n_blocks for s in st),
                              "max_particles": caps.max_particles,
@@ -538,7 +576,10 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "k_search", "kernel_ms": kernel_ms,
-                     "alg_bytes_per_launch": alg_bytes},
+                     "alg_bytes_per_launch": alg_bytes,
+                     # the same without the root level's LDS-served bytes
+                     "alg_bytes_hbm_per_launch": alg_bytes_hbm,
+                     "achieved_hbm": achieved_hbm, "frac_hbm": achieved_hbm / HBM_PEAK_GBS},
     }
     if cpu is not None:
         out["cpu_baseline"] = cpu

@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define POMCP_ABI_VERSION 2
+#define POMCP_ABI_VERSION 3
 #define POMCP_MAX_ACTIONS 8
 
 typedef enum pomcp_status {
@@ -181,26 +181,44 @@ int pomcp_arena_usage(pomcp_ctx* ctx, int32_t* max_blocks_used, int32_t* max_log
  * keeping counters (rank g uses seed ^ (g << 32)). */
 int pomcp_rekey(pomcp_ctx* ctx, uint64_t seed);
 
-/* Device pointer of the merge buffer written by pomcp_search:
- * double[num_trees][num_actions][2] = (child visits, child total value),
- * the operand of the RCCL all-reduce at action-selection time. */
+/* Exchange record of one tree, written by pomcp_search (the operand of the
+ * root-parallel exchange at action-selection time): POMCP_XREC(A) doubles =
+ *   [2a] child visits, [2a + 1] child total value    (a < num_actions)
+ *   [2A + 0] num_sims, [2A + 1] root visits, [2A + 2] search depth,
+ *   [2A + 3] error (pomcp_status), [2A + 4] min value, [2A + 5] max value
+ * (integers are exact in a double). */
+#define POMCP_XREC_STATS 6
+#define POMCP_XREC(num_actions) (2 * (num_actions) + POMCP_XREC_STATS)
+
+/* Device pointer of the merge buffer: double[num_trees][POMCP_XREC(A)], this
+ * GPU's exchange records. */
 int pomcp_root_merge_buffer(pomcp_ctx* ctx, void** device_ptr);
 
+/* Device pointer of the gather buffer: double[world][num_trees][POMCP_XREC(A)],
+ * every rank's merge buffer in rank order (allocated on the first call for a
+ * given world size; a larger world re-allocates).  The caller may fill it with
+ * its own all-gather (e.g. torch.distributed.all_gather_into_tensor) instead
+ * of pomcp_allgather_root. */
+int pomcp_root_gather_buffer(pomcp_ctx* ctx, int32_t world, void** device_ptr);
+
 /* The root-parallel exchange of SURVEY §8(b)/(e) (mcts.py:269-306 run as
- * root-parallel trees on several GPUs): sums the merge buffer over an RCCL
- * communicator, in place, on the context's stream -- ncclAllReduce(buf, buf,
- * num_trees * num_actions * 2, ncclFloat64, ncclSum, comm, stream) -- before
- * pomcp_merge_roots.  rccl_comm: an ncclComm_t of the caller (one rank per
- * GPU).  RCCL is resolved at the first call (the process's librccl if one is
- * loaded, e.g. PyTorch's, else librccl.so.1); POMCP_E_UNSUPPORTED without it. */
-int pomcp_allreduce_root(pomcp_ctx* ctx, void* rccl_comm);
+ * root-parallel trees on several GPUs): ncclAllGather(merge buffer -> gather
+ * buffer, num_trees * POMCP_XREC(A) doubles per rank, comm, context stream),
+ * before pomcp_merge_roots(..., world, ...).  An all-gather, not an
+ * all-reduce: the merge then sums the replicas in one fixed order on every
+ * rank (a ring all-reduce's summation order depends on the algorithm and the
+ * rank count, so its FP64 sums could not be restated).  rccl_comm: an
+ * ncclComm_t of `world` ranks, one per GPU, created by the RCCL library that
+ * is already loaded in this process (PyTorch's, or one the caller loaded): the
+ * library never loads a second RCCL copy; POMCP_E_UNSUPPORTED if none is loaded. */
+int pomcp_allgather_root(pomcp_ctx* ctx, void* rccl_comm, int32_t world);
 
 /* Root-parallel decision of one planner. */
 typedef struct pomcp_merged_root {
   int32_t action;               /* merged final action (see pomcp_merge_roots) */
   int32_t num_trees;            /* replicas merged */
   int32_t search_depth;         /* max over the replicas */
-  int32_t error;                /* first non-zero replica error, in tree order */
+  int32_t error;                /* first non-zero replica error, in replica order */
   int64_t num_sims;             /* summed over the replicas */
   int64_t root_visits;          /* summed */
   double min_value, max_value;  /* min / max over the replicas' MinMaxStats */
@@ -209,16 +227,22 @@ typedef struct pomcp_merged_root {
 } pomcp_merged_root;
 
 /* Root-parallel merge on the device: trees [g*group, (g+1)*group) are the
- * replicas of planner g (num_trees % group == 0); their entries of the merge
- * buffer (as last written by pomcp_search, or after an all-reduce of it across
- * GPUs) are summed in a fixed order and the merged action is
+ * replicas of planner g on every rank (num_trees % group == 0).
+ *   world == 0: this GPU's merge buffer alone (replicas k = 0..group-1);
+ *   world >= 1: the gather buffer of `world` ranks (pomcp_allgather_root):
+ *               replica j = r * group + k is tree g*group + k of rank r.
+ * Replica records are summed in one fixed order -- lane l of a 64-lane wave
+ * sums replicas [l*c, (l+1)*c), c = ceil(N / 64), N = max(world,1) * group, in
+ * replica order from 0.0, then the 64 partials in lane order from 0.0
+ * (restated by oracle/root_parallel.py) -- so every rank takes the same
+ * decision, bit-identical to one GPU merging all N replicas:
  *   PUCB: argmax summed visits (the merged max_visit_action_selection,
  *         mcts.py:565-581);  UCB / uniform: argmax summed total / summed visits
  *         over visited actions (max_value_action_selection, mcts.py:583-600);
  * lowest action on ties, 0 if nothing was visited.  Replaces the reference's
  * single-tree _final_action_selection when one planner runs many trees.
  * out (host, [num_trees / group]) may be NULL: the result stays on device. */
-int pomcp_merge_roots(pomcp_ctx* ctx, int32_t group, pomcp_merged_root* out);
+int pomcp_merge_roots(pomcp_ctx* ctx, int32_t group, int32_t world, pomcp_merged_root* out);
 
 /* Bench / batch helpers: synthetic roots (the configured environment).  Tree b samples s0 from
  * the model's b0 under env key (env_seed_base + b, 0x40000000) and the ego's

@@ -17,10 +17,12 @@ INF = float("inf")
 
 
 def merge_roots(visits, totals, sel):
-    """Merge K replicas' root children: ``visits[k][a]``, ``totals[k][a]``.
+    """Merge N replicas' root children: ``visits[j][a]``, ``totals[j][a]``.
 
+    Across ranks (``pomcp_merge_roots`` after the all-gather) replica j = r * K
+    + k is replica k of rank r, so the list is rank-major.
     Fixed summation order: lane l of 64 sums replicas [l*c, (l+1)*c), c =
-    ceil(K / 64), in order from 0.0; the 64 partials are summed in lane order
+    ceil(N / 64), in order from 0.0; the 64 partials are summed in lane order
     from 0.0.  PUCB: argmax of summed visits (``max_visit_action_selection``,
     ``mcts.py:565-581``); UCB / uniform: argmax of summed total / summed visits
     over visited actions (``max_value_action_selection``, ``mcts.py:583-600``);

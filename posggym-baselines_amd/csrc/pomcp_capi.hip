@@ -43,6 +43,8 @@ struct pomcp_ctx {
   const void* host_model = nullptr;
   size_t model_bytes = 0;
   pomcp_merged_root* merged = nullptr;   // [B] device results of pomcp_merge_roots
+  double* gather = nullptr;              // [gather_world][B][R] pomcp_root_gather_buffer
+  int gather_world = 0;
 };
 
 static void make_model(const pomcp_grid* g, DrvModel* m) {
@@ -252,7 +254,7 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
   ALLOC(dpow, double, c.discount_pow_size);
   ALLOC(model, uint8_t, ctx->model_bytes);
   ALLOC(stats, pomcp_root_stats, B);
-  ALLOC(merge, double, B * d.A * 2);
+  ALLOC(merge, double, B * POMCP_XREC(d.A));
   ALLOC(upd_out, int32_t, B * 2);
   ALLOC(in_actions, int32_t, B);
   ALLOC(in_obs, uint64_t, B);
@@ -553,42 +555,75 @@ int pomcp_root_merge_buffer(pomcp_ctx* ctx, void** device_ptr) {
   return POMCP_OK;
 }
 
-// ncclAllReduce, resolved at run time (no link-time RCCL dependency): the copy
-// already in the process if any (PyTorch's), else the system's
-typedef int (*pb_nccl_allreduce_fn)(const void*, void*, size_t, int, int, void*, hipStream_t);
-static pb_nccl_allreduce_fn pb_rccl_allreduce() {
-  static pb_nccl_allreduce_fn fn = nullptr;
-  static bool tried = false;
-  if (!tried) {
-    tried = true;
+int pomcp_root_gather_buffer(pomcp_ctx* ctx, int32_t world, void** device_ptr) {
+  if (!ctx || !device_ptr || world < 1) return POMCP_E_INVALID;
+  if (world > ctx->gather_world) {
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->gather) {
+      for (auto& q : ctx->allocs)
+        if (q == ctx->gather) q = nullptr;
+      (void)hipFree(ctx->gather);
+      ctx->gather = nullptr;
+      ctx->gather_world = 0;
+    }
+    void* q = nullptr;
+    const size_t bytes = sizeof(double) * (size_t)world * (size_t)ctx->dp.B * POMCP_XREC(ctx->dp.A);
+    int rc = dev_alloc(ctx, &q, bytes);
+    if (rc != POMCP_OK) return rc;
+    HIP_TRY(ctx, hipMemsetAsync(q, 0, bytes, ctx->stream));
+    ctx->gather = reinterpret_cast<double*>(q);
+    ctx->gather_world = world;
+  }
+  *device_ptr = ctx->gather;
+  return POMCP_OK;
+}
+
+// ncclAllGather of the RCCL copy already in this process (PyTorch's, or one
+// the caller loaded; its soname is librccl.so.1): never a second copy, whose
+// functions would be handed a communicator created by the first one.
+typedef int (*pb_nccl_allgather_fn)(const void*, void*, size_t, int, void*, hipStream_t);
+static pb_nccl_allgather_fn pb_rccl_allgather() {
+  static pb_nccl_allgather_fn fn = nullptr;
+  if (!fn) {
     void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
-    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
-    if (h) fn = reinterpret_cast<pb_nccl_allreduce_fn>(dlsym(h, "ncclAllReduce"));
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);
+    if (h) fn = reinterpret_cast<pb_nccl_allgather_fn>(dlsym(h, "ncclAllGather"));
   }
   return fn;
 }
 
-int pomcp_allreduce_root(pomcp_ctx* ctx, void* rccl_comm) {
-  if (!ctx || !rccl_comm) return POMCP_E_INVALID;
+int pomcp_allgather_root(pomcp_ctx* ctx, void* rccl_comm, int32_t world) {
+  if (!ctx || !rccl_comm || world < 1) return POMCP_E_INVALID;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
-  const pb_nccl_allreduce_fn allreduce = pb_rccl_allreduce();
-  if (!allreduce) return fail(ctx, POMCP_E_UNSUPPORTED, "allreduce_root: librccl not found");
-  constexpr int kNcclFloat64 = 8, kNcclSum = 0;   // rccl.h ncclDataType_t / ncclRedOp_t
-  const size_t n = (size_t)ctx->dp.B * (size_t)ctx->dp.A * 2;
-  const int rc = allreduce(ctx->dp.merge, ctx->dp.merge, n, kNcclFloat64, kNcclSum, rccl_comm,
-                           ctx->stream);
-  if (rc != 0) return fail(ctx, POMCP_E_HIP, "allreduce_root: ncclAllReduce error " + std::to_string(rc));
+  const pb_nccl_allgather_fn allgather = pb_rccl_allgather();
+  if (!allgather)
+    return fail(ctx, POMCP_E_UNSUPPORTED,
+                "allgather_root: no RCCL library is loaded in this process (load the one the "
+                "communicator was created with first)");
+  void* gbuf = nullptr;
+  int rc = pomcp_root_gather_buffer(ctx, world, &gbuf);
+  if (rc != POMCP_OK) return rc;
+  constexpr int kNcclFloat64 = 8;   // rccl.h ncclDataType_t
+  const size_t n = (size_t)ctx->dp.B * POMCP_XREC(ctx->dp.A);
+  rc = allgather(ctx->dp.merge, gbuf, n, kNcclFloat64, rccl_comm, ctx->stream);
+  if (rc != 0) return fail(ctx, POMCP_E_HIP, "allgather_root: ncclAllGather error " + std::to_string(rc));
   return POMCP_OK;
 }
 
-int pomcp_merge_roots(pomcp_ctx* ctx, int32_t group, pomcp_merged_root* out) {
+int pomcp_merge_roots(pomcp_ctx* ctx, int32_t group, int32_t world, pomcp_merged_root* out) {
   if (!ctx || group < 1 || ctx->dp.B % group != 0)
     return fail(ctx, POMCP_E_INVALID, "merge_roots: group must divide num_trees");
+  if (world < 0 || (world > 0 && world > ctx->gather_world))
+    return fail(ctx, POMCP_E_INVALID, "merge_roots: no gather buffer for that many ranks");
+  if ((int64_t)(world > 0 ? world : 1) * group > INT32_MAX / 2)
+    return fail(ctx, POMCP_E_INVALID, "merge_roots: too many replicas");
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   const int G = ctx->dp.B / group;
-  hipLaunchKernelGGL(k_merge_roots, dim3((unsigned)G), dim3(kWave), 0, ctx->stream, ctx->dp,
-                     (int)group, ctx->merged);
+  const double* src = world > 0 ? ctx->gather : ctx->dp.merge;
+  hipLaunchKernelGGL(k_merge_roots, dim3((unsigned)G), dim3(kWave), 0, ctx->stream, src,
+                     (int)ctx->dp.B, (int)ctx->dp.A, (int)ctx->dp.sel, (int)group,
+                     world > 0 ? (int)world : 1, ctx->merged);
   HIP_TRY(ctx, hipGetLastError());
   if (!out) return POMCP_OK;
   HIP_TRY(ctx, hipMemcpyAsync(out, ctx->merged, sizeof(pomcp_merged_root) * (size_t)G,

@@ -157,7 +157,7 @@ struct DevParams {
   const void* model;    // Env::Model (envs.h), staged in LDS by every kernel
   int32_t env;          // pomcp_env
   pomcp_root_stats* stats;
-  double* merge;        // [B][A][2]
+  double* merge;        // [B][POMCP_XREC(A)] exchange records (pomcp.h)
   int32_t* upd_out;     // [B][2] {root_abs, error}
   const int32_t* in_actions;
   const uint64_t* in_obs;

@@ -855,51 +855,58 @@ __global__ __launch_bounds__(256) void k_restore(DevParams p, const TreeHdr* sna
 }
 
 // Root-parallel merge: trees [g * group, (g + 1) * group) are
-// the root-parallel replicas of planner g; their root statistics in the merge
-// buffer ([B][A][2] = (visits, total), written by k_search and possibly
-// all-reduced across GPUs since) are summed and the merged action chosen:
+// the root-parallel replicas of planner g on every rank; their exchange
+// records (pomcp.h POMCP_XREC: (visits, total) per root action + step
+// statistics, written by k_search) are read from `src` = [world][B][R] (one
+// rank's merge buffer, or the all-gathered buffers of `world` ranks in rank
+// order), replica j = r * group + k being tree g * group + k of rank r, and the
+// merged action chosen:
 //   * PUCB  (max_visit_action_selection, mcts.py:565-581): argmax of summed visits;
 //   * UCB / uniform (max_value_action_selection, mcts.py:583-600): argmax of
 //     summed total / summed visits over the visited actions;
 // lowest action on ties (the replicas' choice must be the same everywhere, so
 // the reference's random tie-break is not drawn); 0 when nothing was visited
 // (action_space[0], mcts.py:270-272).  Summation order is fixed: lane l of the
-// group's wave sums trees [l * c, (l + 1) * c), c = ceil(group / 64), in tree
+// group's wave sums replicas [l * c, (l + 1) * c), c = ceil(N / 64), in replica
 // order from 0.0, then lane 0 sums the 64 partials in lane order from 0.0
-// (restated by oracle/root_parallel.py, bit-exact).  The step statistics of
-// the replicas (search depth, simulations, root visits, MinMaxStats, errors)
-// are reduced alongside.
-__global__ __launch_bounds__(64) void k_merge_roots(DevParams p, int group,
+// (restated by oracle/root_parallel.py, bit-exact), so every rank takes the
+// same decision and it does not depend on how the records were exchanged.
+// The step statistics of the replicas (search depth, simulations, root visits,
+// MinMaxStats, errors) are reduced alongside.
+__global__ __launch_bounds__(64) void k_merge_roots(const double* src, int B, int A, int sel,
+                                                    int group, int world,
                                                     pomcp_merged_root* out) {
   __shared__ double part[2][POMCP_MAX_ACTIONS][kWave];
   __shared__ double pmm[2][kWave];
   __shared__ int64_t pn[2][kWave];
   __shared__ int32_t pi[2][kWave];
-  const int g = blockIdx.x, lane = lane_id(), A = p.A;
-  const int c = (group + kWave - 1) / kWave;
-  const int k0 = min(lane * c, group), k1 = min(k0 + c, group);
-  const int64_t t0 = (int64_t)g * group;
-  const double* m = p.merge + t0 * A * 2;
+  const int g = blockIdx.x, lane = lane_id();
+  const int R = POMCP_XREC(A);
+  const int n = world * group;
+  const int c = (n + kWave - 1) / kWave;
+  const int j0 = min(lane * c, n), j1 = min(j0 + c, n);
   double v[POMCP_MAX_ACTIONS], t[POMCP_MAX_ACTIONS];
 #pragma unroll
   for (int a = 0; a < POMCP_MAX_ACTIONS; ++a) v[a] = t[a] = 0.0;
   double mn = __builtin_inf(), mx = -__builtin_inf();
   int64_t sims = 0, rv = 0;
   int depth = 0, err = 0;
-  for (int k = k0; k < k1; ++k) {
+  for (int j = j0; j < j1; ++j) {
+    const int r = j / group, k = j - r * group;
+    const double* m = src + ((int64_t)r * B + (int64_t)g * group + k) * R;
 #pragma unroll
     for (int a = 0; a < POMCP_MAX_ACTIONS; ++a)
       if (a < A) {
-        v[a] = v[a] + m[((int64_t)k * A + a) * 2];
-        t[a] = t[a] + m[((int64_t)k * A + a) * 2 + 1];
+        v[a] = v[a] + m[2 * a];
+        t[a] = t[a] + m[2 * a + 1];
       }
-    const pomcp_root_stats& s = p.stats[t0 + k];
-    depth = max(depth, s.search_depth);
-    sims += s.num_sims;
-    rv += s.root_visits;
-    if (s.min_value < mn) mn = s.min_value;
-    if (s.max_value > mx) mx = s.max_value;
-    if (err == 0) err = s.error;
+    const double* s = m + 2 * A;
+    sims += (int64_t)s[0];
+    rv += (int64_t)s[1];
+    depth = max(depth, (int)s[2]);
+    if (err == 0) err = (int)s[3];
+    if (s[4] < mn) mn = s[4];
+    if (s[5] > mx) mx = s[5];
   }
 #pragma unroll
   for (int a = 0; a < POMCP_MAX_ACTIONS; ++a) {
@@ -916,7 +923,7 @@ __global__ __launch_bounds__(64) void k_merge_roots(DevParams p, int group,
   if (lane != 0) return;
   pomcp_merged_root r;
   r.action = 0;
-  r.num_trees = group;
+  r.num_trees = n;
   r.search_depth = 0;
   r.error = 0;
   r.num_sims = 0;
@@ -943,7 +950,7 @@ __global__ __launch_bounds__(64) void k_merge_roots(DevParams p, int group,
     r.visits[a] = sv;
     r.totals[a] = st;
     if (a >= A || !(sv > 0.0)) continue;
-    const double score = p.sel == POMCP_SEL_PUCB ? sv : st / sv;
+    const double score = sel == POMCP_SEL_PUCB ? sv : st / sv;
     if (!any || score > best) {
       best = score;
       r.action = a;

@@ -819,6 +819,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   hw->ctr[3] = c_a0 - (p.other == 0 ? (uint32_t)pend_s : 0u);
   hw->ctr[4] = c_a1 - (p.other == 1 ? (uint32_t)pend_s : 0u);
   pomcp_root_stats* const so = p.stats + tree;
+  double* const xr = p.merge + (int64_t)tree * POMCP_XREC(A);   // exchange record (pomcp.h)
 #pragma unroll
   for (int a = 0; a < kMaxA; ++a) {
     if (a >= A) continue;
@@ -826,9 +827,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
     so->child_visits[a] = (int)st[a].x;
     so->child_values[a] = va;
     so->child_totals[a] = tot;
-    p.merge[((int64_t)tree * A + a) * 2] = (double)st[a].x;
-    p.merge[((int64_t)tree * A + a) * 2 + 1] = tot;
+    xr[2 * a] = (double)st[a].x;
+    xr[2 * a + 1] = tot;
   }
+  xr[2 * A + 0] = (double)sims;
+  xr[2 * A + 1] = (double)root_visits;
+  xr[2 * A + 2] = (double)max_depth;
+  xr[2 * A + 3] = (double)err;
+  xr[2 * A + 4] = mm_min;
+  xr[2 * A + 5] = mm_max;
   so->action = action;
   so->num_sims = sims;
   so->search_depth = max_depth;

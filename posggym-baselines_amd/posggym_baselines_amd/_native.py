@@ -11,8 +11,14 @@ import os
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.environ.get("POMCP_LIB_PATH") or os.path.join(LIB_DIR, "libpomcp_hip.so")
 
-POMCP_ABI_VERSION = 2
+POMCP_ABI_VERSION = 3
 POMCP_MAX_ACTIONS = 8
+POMCP_XREC_STATS = 6
+
+
+def xrec(num_actions: int) -> int:
+    """Doubles per tree in the exchange record (include/pomcp.h POMCP_XREC)."""
+    return 2 * num_actions + POMCP_XREC_STATS
 
 POMCP_OK = 0
 POMCP_E_INVALID = -1
@@ -175,8 +181,9 @@ SIGNATURES = [
     ("pomcp_arena_usage", C.c_int, [_CTX, _P32, _P32]),
     ("pomcp_rekey", C.c_int, [_CTX, C.c_uint64]),
     ("pomcp_root_merge_buffer", C.c_int, [_CTX, C.POINTER(C.c_void_p)]),
-    ("pomcp_allreduce_root", C.c_int, [_CTX, C.c_void_p]),
-    ("pomcp_merge_roots", C.c_int, [_CTX, C.c_int32, C.POINTER(PomcpMergedRoot)]),
+    ("pomcp_root_gather_buffer", C.c_int, [_CTX, C.c_int32, C.POINTER(C.c_void_p)]),
+    ("pomcp_allgather_root", C.c_int, [_CTX, C.c_void_p, C.c_int32]),
+    ("pomcp_merge_roots", C.c_int, [_CTX, C.c_int32, C.c_int32, C.POINTER(PomcpMergedRoot)]),
     ("pomcp_synthetic_obs", C.c_int, [_CTX, C.c_uint64, _PU64]),
     ("pomcp_snapshot", C.c_int, [_CTX]),
     ("pomcp_restore", C.c_int, [_CTX]),

@@ -18,7 +18,12 @@ _SUPPORTED = {
                                                 "use_progress_reward": True}),
 }
 # posggym env kwargs that do not change the generative model
-_IGNORED_KWARGS = {"render_mode", "normalize_reward", "max_episode_steps"}
+_IGNORED_KWARGS = {"render_mode", "max_episode_steps"}
+# kwargs the restatements implement at one value only: accepted at that value,
+# anything else raises (PursuitEvasion-v1 always divides its rewards by the
+# normaliser, pursuit_evasion.py reward_norm; a planner built for
+# normalize_reward=False would silently plan with other rewards)
+_FIXED_KWARGS = {"normalize_reward": True}
 
 
 def engine_model(model):
@@ -39,6 +44,10 @@ def engine_model(model):
     kwargs = dict(getattr(spec, "kwargs", None) or {})
     for k in _IGNORED_KWARGS:
         kwargs.pop(k, None)
+    for k, v in _FIXED_KWARGS.items():
+        if k in kwargs:
+            if kwargs.pop(k) != v:
+                raise NotImplementedError(f"{env_id}: {k}={not v} is not restated (only {v})")
     unknown = set(kwargs) - set(defaults)
     if unknown:
         raise NotImplementedError(f"{env_id}: unsupported env kwargs {sorted(unknown)}")

@@ -273,16 +273,27 @@ class PomcpEngine:
         levels = min(self.config.depth_limit, self.step_limit) + 1
         return max(0, min(cap.max_blocks - nb - 1, (cap.max_particles - nl - 1) // min(levels, 64)))
 
-    def merge_roots(self, group, fetch=True):
+    def gather_buffer_ptr(self, world: int) -> int:
+        """Device pointer of the [world][trees][xrec(A)] gather buffer."""
+        p = C.c_void_p()
+        self._check(self._lib.pomcp_root_gather_buffer(self._ctx, int(world), C.byref(p)),
+                    "gather_buffer")
+        return p.value
+
+    def merge_roots(self, group, fetch=True, world=0):
         """Device merge of root-parallel replicas (``pomcp_merge_roots``): trees
-        [g * group, (g + 1) * group) are planner g.  Returns the
-        ``PomcpMergedRoot`` array (or None with ``fetch=False``)."""
+        [g * group, (g + 1) * group) are planner g; ``world`` = 0 merges this
+        GPU's records, ``world`` >= 1 the gather buffer of that many ranks.
+        Returns the ``PomcpMergedRoot`` array (or None with ``fetch=False``);
+        raises if any merged replica reported an error."""
         G = self.num_trees // group
         if not fetch:
-            self._check(self._lib.pomcp_merge_roots(self._ctx, int(group), None), "merge_roots")
+            self._check(self._lib.pomcp_merge_roots(self._ctx, int(group), int(world), None),
+                        "merge_roots")
             return None
         out = (N.PomcpMergedRoot * G)()
-        self._check(self._lib.pomcp_merge_roots(self._ctx, int(group), out), "merge_roots")
+        self._check(self._lib.pomcp_merge_roots(self._ctx, int(group), int(world), out),
+                    "merge_roots")
         return out
 
     def synthetic_obs(self, env_seed_base):

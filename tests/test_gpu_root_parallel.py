@@ -4,8 +4,9 @@ planner): K replica trees of ONE planner, merged on the device.
 * every replica is the exact oracle planner with RNG key (seed, k), fed the
   merged action and the real observation (oracle/root_parallel.py);
 * the device merge (pomcp_merge_roots) equals the CPU restatement bit for bit;
-* the merge buffer (the operand of the cross-GPU all-reduce) equals the root
-  statistics it is built from.
+* the merge buffer (the operand of the cross-GPU all-gather) equals the root
+  statistics it is built from, and the merge over a gathered buffer of any
+  rank count follows the replica order.
 """
 import math
 
@@ -82,24 +83,35 @@ def test_root_parallel_planner_matches_oracle_replicas(env, sel, K, sims, ego):
     planner.close()
 
 
+def _records(bp, A):
+    """The merge buffer as [trees][xrec(A)] and the root stats it must equal."""
+    import torch
+    from posggym_baselines_amd.planning.parallel import merge_buffer_tensor
+    B = bp.num_trees
+    st = bp.engine.root_stats()   # synchronises the engine's stream first
+    buf = merge_buffer_tensor(bp.engine, torch.device("cuda:0")).cpu().numpy().reshape(B, -1)
+    return buf, st
+
+
 @pytest.mark.parametrize("sel", ["ucb", "pucb"])
 def test_device_merge_equals_cpu_merge_and_merge_buffer_equals_root_stats(sel):
-    import torch
     from oracle.root_parallel import merge_roots
     from posggym_baselines_amd.planning import BatchedPOMCP
-    from posggym_baselines_amd.planning.parallel import merge_buffer_tensor
     model = product_model("Driving-v1")
     B, S, group = 4160, 64, 1040      # 4 planners x 1040 replicas (uneven 64-lane chunks)
     bp = BatchedPOMCP(model, "0", product_config(dict(CFG, action_selection=sel), S), B, S)
     bp.init_synthetic(77)
     bp.search(fetch=False)
-    st = bp.engine.root_stats()
     A = 5
-    buf = merge_buffer_tensor(bp.engine, torch.device("cuda:0")).cpu().numpy().reshape(B, A, 2)
+    buf, st = _records(bp, A)
+    assert buf.shape == (B, 2 * A + 6)
     vis = np.array([list(s.child_visits[:A]) for s in st], dtype=np.float64)
     tot = np.array([list(s.child_totals[:A]) for s in st], dtype=np.float64)
-    assert np.array_equal(buf[..., 0], vis)
-    assert np.array_equal(buf[..., 1].view(np.uint64), tot.view(np.uint64))
+    assert np.array_equal(buf[:, 0:2 * A:2], vis)
+    assert np.array_equal(buf[:, 1:2 * A:2].view(np.uint64), tot.view(np.uint64))
+    stats = np.array([[s.num_sims, s.root_visits, s.search_depth, s.error, s.min_value,
+                       s.max_value] for s in st], dtype=np.float64)
+    assert np.array_equal(buf[:, 2 * A:].view(np.uint64), stats.view(np.uint64))
     merged = bp.engine.merge_roots(group)
     for g in range(B // group):
         sl = slice(g * group, (g + 1) * group)
@@ -114,6 +126,43 @@ def test_device_merge_equals_cpu_merge_and_merge_buffer_equals_root_stats(sel):
         assert m.search_depth == max(s.search_depth for s in st[sl])
         assert m.min_value == min(s.min_value for s in st[sl])
         assert m.max_value == max(s.max_value for s in st[sl])
+    bp.close()
+
+
+@pytest.mark.parametrize("world,group", [(3, 5), (8, 1), (5, 40)])
+def test_device_merge_over_gathered_ranks(world, group):
+    """pomcp_merge_roots(world > 1) on a gather buffer: rank r's records are the
+    batch's records rolled by r * group trees (as if rank r had searched those
+    roots), so planner g's replica j = r * group + k is tree (g group + k + r
+    group) mod B.  The device merge of the world x group replicas equals the
+    CPU merge in replica order, bit for bit (the order the all-gather fixes for
+    every rank count)."""
+    import torch
+    from oracle.root_parallel import merge_roots
+    from posggym_baselines_amd.planning import BatchedPOMCP
+    from posggym_baselines_amd.planning.parallel import gather_buffer_tensor
+    model = product_model("Driving-v1")
+    A, S = 5, 48
+    B = group * 8
+    bp = BatchedPOMCP(model, "0", product_config(CFG, S), B, S)
+    bp.init_synthetic(501)
+    bp.search(fetch=False)
+    buf, st = _records(bp, A)
+    gath = gather_buffer_tensor(bp.engine, world, torch.device("cuda:0"))
+    rows = np.concatenate([np.roll(buf, -r * group, axis=0) for r in range(world)])
+    gath.copy_(torch.from_numpy(rows.reshape(-1)).to("cuda:0"))
+    torch.cuda.synchronize()
+    merged = bp.engine.merge_roots(group, world=world)
+    for g in range(B // group):
+        idx = [(g * group + k + r * group) % B for r in range(world) for k in range(group)]
+        a, sv, stt = merge_roots(buf[idx, 0:2 * A:2].tolist(), buf[idx, 1:2 * A:2].tolist(), "ucb")
+        m = merged[g]
+        assert m.num_trees == world * group
+        assert m.action == a
+        assert list(m.visits[:A]) == sv
+        assert [x.hex() for x in m.totals[:A]] == [x.hex() for x in stt]
+        assert m.num_sims == sum(int(buf[i, 2 * A]) for i in idx)
+        assert m.min_value == min(buf[i, 2 * A + 4] for i in idx)
     bp.close()
 
 
@@ -173,35 +222,37 @@ def test_root_parallel_wall_clock_episode():
     assert all(0 <= a < 5 and n >= 16 * 16 and n % 16 == 0 for a, n in steps), steps
 
 
-def test_allreduce_root_c_abi_single_rank():
-    """pomcp_allreduce_root (the C-ABI exchange of SURVEY §8(b)) over a one-rank
-    RCCL communicator made with the process's librccl (ncclCommInitAll): the
-    sum over one rank leaves the merge buffer as it was, and the device merge
-    after it is the merge without it."""
+def test_allgather_root_c_abi_single_rank():
+    """pomcp_allgather_root (the C-ABI exchange of SURVEY §8(b)) over a one-rank
+    RCCL communicator made with the process's librccl (ncclCommInitAll; the
+    library resolves ncclAllGather in the copy already loaded): the gather
+    buffer of one rank equals the merge buffer, and the merge over it equals
+    the local merge."""
     import ctypes as C
     import torch
     from posggym_baselines_amd import _native as N
     from posggym_baselines_amd.planning import BatchedPOMCP
-    from posggym_baselines_amd.planning.parallel import merge_buffer_tensor
+    from posggym_baselines_amd.planning.parallel import gather_buffer_tensor, merge_buffer_tensor
     model = product_model("Driving-v1")
     bp = BatchedPOMCP(model, "0", product_config(CFG, 64), 16, 64)
     bp.init_synthetic(1000)
     bp.search()
     bp.engine.root_stats()   # synchronises the engine
     dev = torch.device("cuda:0")
-    before = merge_buffer_tensor(bp.engine, dev).cpu().clone()
-    key = lambda ms: [(m.action, list(m.visits), [float(x).hex() for x in m.totals]) for m in ms]
+    local = merge_buffer_tensor(bp.engine, dev).cpu().clone()
+    key = lambda ms: [(m.action, list(m.visits), [float(x).hex() for x in m.totals], m.num_sims,
+                       m.root_visits, m.search_depth) for m in ms]
     m0 = key(bp.engine.merge_roots(4))
     rccl = C.CDLL("librccl.so.1")
     comm = C.c_void_p()
     devs = (C.c_int * 1)(0)
     assert rccl.ncclCommInitAll(C.byref(comm), 1, devs) == 0
     try:
-        assert N.load().pomcp_allreduce_root(bp.engine._ctx, comm) == 0
+        assert N.load().pomcp_allgather_root(bp.engine._ctx, comm, 1) == 0
         bp.engine.root_stats()
-        after = merge_buffer_tensor(bp.engine, dev).cpu()
-        assert torch.equal(before, after)
-        assert key(bp.engine.merge_roots(4)) == m0
+        gathered = gather_buffer_tensor(bp.engine, 1, dev).cpu()
+        assert torch.equal(gathered.view(torch.int64), local.view(torch.int64))
+        assert key(bp.engine.merge_roots(4, world=1)) == m0
     finally:
         rccl.ncclCommDestroy(comm)
         bp.close()

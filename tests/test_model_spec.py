@@ -35,12 +35,16 @@ def test_pursuit_evasion_spec_maps_to_restatement():
     assert isinstance(m, PursuitEvasionModel)
     assert bytes(m.pomcp_pe_grid()) == bytes(PursuitEvasionModel().pomcp_pe_grid())
     assert engine_model(posggym_like("PursuitEvasion-v1")).max_obs_distance == 12
+    # the restatement normalises rewards: the default normalize_reward=True is accepted
+    assert isinstance(engine_model(posggym_like("PursuitEvasion-v1", normalize_reward=True)),
+                      PursuitEvasionModel)
 
 
 @pytest.mark.parametrize("bad", [posggym_like("LevelBasedForaging-v3"),
                                  posggym_like("Driving-v1", grid="A0Grid"),
                                  posggym_like("Driving-v1", num_agents=3),
                                  posggym_like("Driving-v1", obstacle_density=0.1),
+                                 posggym_like("PursuitEvasion-v1", normalize_reward=False),
                                  object()])
 def test_unsupported_models_raise(bad):
     with pytest.raises(NotImplementedError):

@@ -82,6 +82,8 @@ def main():
             json.dump({"tag": tag, "trees": trees, "sims": sims,
                        "env": b["metric"].split(" on ")[1].split(" ")[0],
                        "hbm_bytes_per_launch": hbm,
+                       # bench.py reports this traffic only for the same library
+                       "lib_sha16": cfg.get("lib_sha16"),
                        "source": f"profiles/{tag}_summary.json"}, f, indent=1)
     print(json.dumps(summary["pmc"], indent=1), stats)
 
