@@ -157,6 +157,24 @@ int pomcp_search(pomcp_ctx* ctx, int32_t num_sims, int32_t* actions_out);
  * pomcp_search(n1 + ... + nk).  Root stats' action is -1 after it. */
 int pomcp_search_continue(pomcp_ctx* ctx, int32_t num_sims);
 
+/* Search kernel of pomcp_search / pomcp_search_continue (results are the same
+ * bit for bit; only the speed differs):
+ *   POMCP_SEARCH_AUTO  (default) wave-per-tree for small batches whose
+ *                      scratch fits, tree-per-lane otherwise;
+ *   POMCP_SEARCH_LANE  one tree per lane, tree in HBM (k_search: the
+ *                      throughput kernel for thousands of trees);
+ *   POMCP_SEARCH_WAVE  one wave per tree, tree blocks in LDS (k_search_lds: a
+ *                      lone planner's latency, mcts.py:285's loop as fast as one
+ *                      tree allows). */
+typedef enum pomcp_search_kernel {
+  POMCP_SEARCH_AUTO = 0,
+  POMCP_SEARCH_LANE = 1,
+  POMCP_SEARCH_WAVE = 2
+} pomcp_search_kernel;
+int pomcp_set_search_kernel(pomcp_ctx* ctx, int32_t kind);
+/* The kernel the next search will use (POMCP_SEARCH_LANE or _WAVE). */
+int32_t pomcp_search_kernel_used(const pomcp_ctx* ctx);
+
 /* Copy every tree's pomcp_root_stats of the last search to host. */
 int pomcp_get_root_stats(pomcp_ctx* ctx, pomcp_root_stats* out);
 

@@ -145,6 +145,8 @@ struct DevParams {
   Line* an;             // [B][Nb][A + 1] action blocks
   OvfSlot* ovf;         // [B][H]
   LogRec* plog;         // [waves][64 * Np] per-search-wave particle log
+  LogRec* lscr;         // [B][Np] k_search_lds: one launch's records per tree (allocated on
+                        // first use), appended to plog by k_log_merge
   uint32_t* wlog;       // [waves] records in each wave's log
   uint32_t* want;       // [B] re-root: log id of the child to extract (0xFFFFFFFF: none)
   int32_t* cnt;         // [B] re-root: particles extracted into the new root belief

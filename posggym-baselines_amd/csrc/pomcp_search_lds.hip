@@ -1,0 +1,674 @@
+// k_search_lds: the POMCP simulation loop with ONE WAVE per tree and the
+// tree in LDS -- the exact single tree (BASELINE config 2 as ONE planner, the
+// drop-in POMCP's default mode) and small batches of planners.
+//
+// Replaces posggym_baselines/planning/mcts.py:269-452 (get_action, _simulate,
+// _rollout, the selection rules, the final action choice) like k_search
+// (pomcp_search.hip), with the same results bit for bit: the same simulations
+// in the same order, the same draws of every stream, the same FP64 operations
+// in the same order.  k_search runs one tree per LANE and is the throughput
+// kernel for thousands of trees; a lone tree there is one lane waiting on
+// ~6 dependent HBM round trips per simulation (~11 us).  Here the whole wave
+// works on one simulation at a time:
+//   * the tree's blocks live in LDS for the launch (staged in from the HBM
+//     arena at the start, written back at the end), so a tree level is a few
+//     LDS reads; blocks beyond the LDS pool stay in HBM (a uniform branch per
+//     access), so any tree size runs, the overflowing part at HBM speed;
+//   * lane 8a + q holds part q of action a's 128 B line (q = 0 statistics
+//     {visits, value}, 1 {total, agg}, 2..7 the six inline child slots): one
+//     LDS read per lane gives the selection its statistics and every action's
+//     child slots at once;
+//   * lane group a (8 lanes) runs the generative step and the observation key
+//     for action a -- for EVERY action, before the selection has picked one
+//     (the step's draws come from the other agent's and the model's streams,
+//     which the selection does not touch), so the step overlaps the FP64
+//     selection instead of following it; the child lookup of all actions is
+//     one ballot; the chosen action's results are read out of its lane group;
+//   * the UCB / PUCB scores of the A actions are computed in parallel lanes
+//     (lane 8a), then scanned in action order with the reference's strict '>'
+//     (mcts.py:541-545);
+//   * RNG (philox.h): a page of 64 Philox blocks per stream in VGPRs (lane l:
+//     block page*64 + l), refilled every 256 draws; a draw is one readlane;
+//   * loads one simulation ahead: the next belief particle (belief.py:55: its
+//     index depends only on the belief stream) and math.log of the root's next
+//     visit count; math.log(N) of every candidate child is loaded as soon as
+//     the child lookup has found it, a level before the selection there uses it;
+//   * particle-log records (mcts.py:371) go to a per-tree scratch log (no
+//     atomics); k_log_merge then appends every tree's records to the search
+//     waves' shared logs (pomcp_device.h WaveLog) in tree order, so re-root,
+//     extraction and compaction read the same log as after k_search.
+// Block layout in LDS: [block][action] 128 B lines {stats0, stats1, slots 0..5};
+// in HBM the (A + 1)-line layout of pomcp_device.h (staged by part).
+#pragma clang fp contract(off)
+
+namespace pb {
+
+constexpr int kLdsPoolBytes = 140 * 1024;          // tree blocks; + model, path, discount table
+constexpr int kLdsPoolParts = kLdsPoolBytes / 16;
+constexpr int kLdsDpow = 256;                      // discount powers cached in LDS
+__host__ __device__ constexpr int lds_pool_blocks(int A) { return kLdsPoolParts / (8 * A); }
+
+// One RNG stream as a VGPR page (philox.h: word j = word j & 3 of block j >> 2).
+struct VStream {
+  uint4 w;         // lane l: Philox block (page * 64 + l)
+  uint32_t page;   // page held in w (0xFFFFFFFF: none)
+  uint32_t ctr;    // next draw
+};
+
+__device__ __forceinline__ void vs_fill(VStream& s, uint64_t seed, uint32_t tkey, uint32_t sid) {
+  const uint32_t pg = s.ctr >> 8;
+  uint32_t c[4] = {pg * 64u + (uint32_t)lane_id(), 0u, sid, (uint32_t)(seed >> 32)};
+  philox4x32_10(c, (uint32_t)seed, tkey);
+  s.w = make_uint4(c[0], c[1], c[2], c[3]);
+  s.page = pg;
+}
+
+__device__ __forceinline__ uint32_t vs_next(VStream& s, uint64_t seed, uint32_t tkey, uint32_t sid) {
+  if ((s.ctr >> 8) != s.page) vs_fill(s, seed, tkey, sid);
+  const uint32_t j = s.ctr++;
+  const uint32_t q = j & 3u;
+  const uint32_t x = q == 0u ? s.w.x : (q == 1u ? s.w.y : (q == 2u ? s.w.z : s.w.w));
+  return rlu(x, (int)((j >> 2) & 63u));
+}
+
+__device__ __forceinline__ uint4 rl4(uint4 v, int l) {
+  return make_uint4(rlu(v.x, l), rlu(v.y, l), rlu(v.z, l), rlu(v.w, l));
+}
+
+template <class Env, int SEL, int NA>
+__global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, int final_sel) {
+  static_assert(NA >= 2 && NA <= kMaxA, "action count");
+  constexpr int A = NA;   // == p.A (host dispatch)
+  constexpr int C = lds_pool_blocks(A);
+  __shared__ typename Env::Model sm;
+  __shared__ uint4 pool[C * 8 * A];
+  __shared__ uint4 path[(kMaxPath + 1) * 3];
+  __shared__ double dpw[kLdsDpow];
+  stage_model(p.model, sm);
+  const int tree = (int)blockIdx.x;   // grid = B workgroups of one wave
+  const int lane = lane_id();
+  const int al = lane >> 3 < A ? lane >> 3 : A - 1;   // this lane's action group
+  const int ql = lane & 7;                             // part of the action's line
+  char* const an = reinterpret_cast<char*>(p.an + tree_base_lines(tree, p.Nb, A));
+  const int64_t blk_bytes = blk_stride_lines(A) * 128;
+  auto hpart = [&](int b, int a, int q) -> uint4* {
+    return reinterpret_cast<uint4*>(an + (int64_t)b * blk_bytes) + (q == 0 ? a : kLine * (1 + a) + q - 1);
+  };
+  auto lpart = [&](int b, int a, int q) -> uint4* { return &pool[(b * A + a) * 8 + q]; };
+  // b is wave-uniform: the LDS / HBM choice is a scalar branch
+  auto ldp = [&](int b, int a, int q) -> uint4 { return b < C ? *lpart(b, a, q) : *hpart(b, a, q); };
+  auto stp = [&](int b, int a, int q, uint4 v) {   // call from one lane
+    if (b < C) *lpart(b, a, q) = v;
+    else *hpart(b, a, q) = v;
+  };
+
+  const TreeHdr* const h = p.hdr + tree;
+  const uint4* const rbel =
+      p.belief + (int64_t)tree * 2 * p.Nr + (int64_t)uni(h->belief_sel) * p.Nr;
+  int root_blk = uni(h->root_blk), root_visits = uni(h->root_visits);
+  int n_blocks = uni(h->n_blocks), n_log = uni(h->n_log), n_nodes = uni(h->n_nodes);
+  const int bsize = uni(h->belief_size), epoch = uni(h->epoch), root_abs = uni(h->root_abs);
+  const int root_t = uni(h->root_t);
+  int err = uni(h->error);
+  double mm_min = uni_d(h->mm_min), mm_max = uni_d(h->mm_max);
+  const uint64_t seed = uni64(h->seed);
+  const uint32_t tkey = uniu(h->tree_key);
+  VStream sb{make_uint4(0, 0, 0, 0), 0xFFFFFFFFu, uniu(h->ctr[0])};   // belief
+  VStream ss{make_uint4(0, 0, 0, 0), 0xFFFFFFFFu, uniu(h->ctr[1])};   // select
+  VStream sd{make_uint4(0, 0, 0, 0), 0xFFFFFFFFu, uniu(h->ctr[2])};   // model
+  VStream s0s{make_uint4(0, 0, 0, 0), 0xFFFFFFFFu, uniu(h->ctr[3])};  // agent 0's actions
+  VStream s1s{make_uint4(0, 0, 0, 0), 0xFFFFFFFFu, uniu(h->ctr[4])};  // agent 1's actions
+  auto d_belief = [&](uint32_t n) { return uniform_int(vs_next(sb, seed, tkey, S_BELIEF), n); };
+  auto d_select = [&](uint32_t n) { return uniform_int(vs_next(ss, seed, tkey, S_SELECT), n); };
+  auto d_model = [&](uint32_t n) {
+    return Env::kStepDraws ? uniform_int(vs_next(sd, seed, tkey, S_MODEL), n) : 0u;
+  };
+  auto d_act = [&](int agent, uint32_t n) {
+    return agent == 0 ? uniform_int(vs_next(s0s, seed, tkey, S_ACT_BASE), n)
+                      : uniform_int(vs_next(s1s, seed, tkey, S_ACT_BASE + 1), n);
+  };
+  const int log0 = n_log, blocks0 = n_blocks, nodes0 = n_nodes;
+  int c_rollout = 0, c_probes = 0;
+#ifdef POMCP_PHASE_TIMING
+  uint64_t pt[16];   // tools/phase_timing.py --kernel wave: sections of tree 0's simulations
+  for (int i = 0; i < 16; ++i) pt[i] = 0;
+  uint64_t pt_last = __builtin_amdgcn_s_memtime();
+#endif
+  LogRec* const scr = p.lscr + (int64_t)tree * p.Np;   // this launch's records, in order
+  const uint32_t ltag = (uint32_t)(tree & (kWave - 1)) << kIdBits;
+  OvfSlot* const ovf = p.ovf + (int64_t)tree * p.H;
+  const int islots = p.islots;
+
+  // ---- the blocks into LDS (part q of action a's line <- its HBM part)
+  const int nstage = n_blocks < C ? n_blocks : C;
+  if (lane < 8 * A) {
+    const int a = lane >> 3, q = lane & 7;
+    int b = 0;
+    for (; b + 4 <= nstage; b += 4) {
+      const uint4 x0 = *hpart(b, a, q), x1 = *hpart(b + 1, a, q), x2 = *hpart(b + 2, a, q),
+                  x3 = *hpart(b + 3, a, q);
+      *lpart(b, a, q) = x0;
+      *lpart(b + 1, a, q) = x1;
+      *lpart(b + 2, a, q) = x2;
+      *lpart(b + 3, a, q) = x3;
+    }
+    for (; b < nstage; ++b) *lpart(b, a, q) = *hpart(b, a, q);
+  }
+  const int ndp = p.dpow_n < kLdsDpow ? p.dpow_n : kLdsDpow;
+  for (int i = lane; i < ndp; i += kWave) dpw[i] = p.dpow[i];
+  __syncthreads();
+  auto dpow = [&](int k) { return k < kLdsDpow ? dpw[k] : p.dpow[k]; };
+  auto logtab = [&](int n) { return p.logtab[n < p.logtab_n ? n : 0]; };
+
+  // ObsNode.add_child for every action (mcts.py:279-281, 318-321): a zeroed block
+  auto alloc_block = [&]() -> int {
+    if (n_blocks >= p.Nb) {
+      err = POMCP_E_ARENA;
+      return -1;
+    }
+    const int b = n_blocks++;
+    if (b < C) {
+      if (lane < 8 * A) *lpart(b, lane >> 3, lane & 7) = make_uint4(0, 0, 0, 0);
+    } else if (lane < blk_parts(A)) {
+      reinterpret_cast<uint4*>(an + (int64_t)b * blk_bytes)[lane] = make_uint4(0, 0, 0, 0);
+    }
+    return b;
+  };
+
+  bool run = err == 0 && !root_abs;   // mcts.py:270-272
+  if (run && root_t == 0) {
+    err = POMCP_E_STATE;
+    run = false;
+  }
+  if (run) {
+    if (root_blk < 0) root_blk = alloc_block();   // mcts.py:279-281
+    if (root_blk < 0 || bsize <= 0) {
+      if (err == 0) err = POMCP_E_STATE;
+      run = false;
+    }
+  }
+  if (num_sims <= 0) run = false;
+  uint4 pf = make_uint4(0, 0, 0, 0);
+  double root_logn = 0.0;
+  if (run) {
+    pf = rbel[d_belief((uint32_t)bsize)];   // the first simulation's particle
+    root_logn = logtab(root_visits);
+  }
+
+  // Overflow children (beyond the inline slots) of action node ani: wave-uniform.
+  struct OvfChild {
+    uint32_t cid;
+    int cblk, cvis;
+    int32_t* cptr;
+  };
+  auto ovf_child = [&](uint32_t ani, uint64_t okey, int done, int cblk, int cvis) -> OvfChild {
+    OvfChild o{0u, cblk, cvis, nullptr};
+    const uint64_t key = okey | ((uint64_t)epoch << kEpochShift);
+    uint32_t b = ovf_hash(ani, okey) & p.bucket_mask;
+    bool found = false;
+    for (uint32_t probe = 0; probe <= p.bucket_mask && !found; ++probe) {
+      ++c_probes;
+      for (int e = 0; e < kBucket; ++e) {
+        OvfSlot* ep = ovf + (int64_t)b * kBucket + e;
+        const uint4 w0 = reinterpret_cast<const uint4*>(ep)[0];
+        const uint64_t skey = (uint64_t)w0.x | ((uint64_t)w0.y << 32);
+        const bool live = (uint32_t)(skey >> kEpochShift) == (uint32_t)epoch;
+        if (!live || (skey == key && w0.z == ani)) {
+          if (live) {
+            const uint4 w1 = reinterpret_cast<const uint4*>(ep)[1];
+            o.cblk = (int)w1.x;
+            o.cvis = (int)w1.y + 1;
+          } else {
+            ++n_nodes;
+          }
+          if (lane == 0) {
+            reinterpret_cast<uint4*>(ep)[0] =
+                make_uint4((uint32_t)key, (uint32_t)(key >> 32), ani, (uint32_t)done);
+            reinterpret_cast<uint4*>(ep)[1] = make_uint4((uint32_t)o.cblk, (uint32_t)o.cvis, 0u, 0u);
+          }
+          o.cid = p.ovf_base + b * kBucket + (uint32_t)e;
+          o.cptr = &ep->block;
+          found = true;
+          break;
+        }
+      }
+      b = (b + 1) & p.bucket_mask;
+    }
+    if (!found) err = POMCP_E_ARENA;
+    return o;
+  };
+
+  // particle-log records of this launch, buffered in VGPRs (lane i: record i
+  // of the batch) and flushed to the scratch log 64 at a time: no global store
+  // inside a simulation (a wait for any load would also wait for every older
+  // store to be acknowledged)
+  uint32_t rb_id = 0u, rb_v0 = 0u, rb_v1 = 0u;
+  int rb_n = 0, rb_base = 0;
+  auto flush_log = [&]() {
+    if (lane < rb_n) {
+      LogRec* const rp = scr + rb_base + lane;
+      rp->id = rb_id;
+      rp->v0 = rb_v0;
+      rp->v1 = rb_v1;
+    }
+    rb_base += rb_n;
+    rb_n = 0;
+  };
+  int sims = 0, max_depth = 0;
+  double lgv = 0.0;   // lanes 8a + 2 + k: math.log(visits + 1) of slot k's child (prefetched)
+  for (int it = 0; it < num_sims && run; ++it) {
+    // ------------------------------------------------ start (mcts.py:286-287)
+    const uint4 pr = pf;                                   // belief.py:55
+    if (sims + 1 < num_sims) pf = rbel[d_belief((uint32_t)bsize)];
+    int t = (int)pr.x;
+    uint32_t s0 = pr.y, s1 = pr.z;
+    int depth = 0, plen = 0;
+    int blk = root_blk, nv = root_visits;
+    int lg_lane = -1;                                      // -1: the root's log(N)
+    const double logn_root = root_logn;
+    root_logn = logtab(root_visits + 1);                   // the next simulation's (no wait)
+    double ret = 0.0;
+    int phase = (0 > p.depth_limit || t > p.step_limit) ? TP_BACKUP : TP_LEVEL;   // mcts.py:315
+    PT_MARK(0);
+    // leaf: where its block index goes (inline slot of block lb, or an overflow entry)
+    int lb = -1, la = 0, lk = 0;
+    int32_t* lptr = nullptr;
+    int k = 0, rdepth = 0;
+    // -------------------------------------------------- the tree levels
+    while (phase == TP_LEVEL) {
+      const uint32_t j = d_model(2);                       // drawn before the selection:
+      const uint32_t ao = d_act(p.other, (uint32_t)A);     // independent streams
+      PT_MARK(1);
+      const uint4 v = ldp(blk, al, ql);                    // part ql of action al's line
+      PT_MARK(2);
+      // every action's generative step at once (mcts.py:331-352)
+      uint32_t n0, n1;
+      double r;
+      int done;
+      Env::step(sm, p.ego, s0, s1, (uint32_t)al, ao, j, &n0, &n1, &r, &done);
+      const uint64_t okey = Env::obs_key(sm, p.ego, n0, n1);
+      PT_MARK(3);
+      // _search_action_selection (mcts.py:492-563) on lanes 8a
+      const double log_n = lg_lane < 0 ? logn_root : rl_d(lgv, lg_lane);
+      PT_MARK(4);
+      int a = 0;
+      if (SEL == POMCP_SEL_PUCB && nv == 0) {              // random.choices, uniform prior
+        const double w = 1.0 / (double)A;
+        double total = w;
+        for (int q = 1; q < A; ++q) total = total + w;
+        const double x = uniform_float(vs_next(ss, seed, tkey, S_SELECT)) * (total + 0.0);
+        double acc = w;
+        a = A - 1;
+        for (int q = 0; q < A - 1; ++q) {
+          if (x < acc) {
+            a = q;
+            break;
+          }
+          acc = acc + w;
+        }
+      } else if (nv == 0) {
+        a = (int)d_select((uint32_t)A);
+      } else if (SEL == POMCP_SEL_UNIFORM) {               // min_visit_action_selection
+        int min_n = nv + 1;
+#pragma unroll
+        for (int q = 0; q < A; ++q) {
+          const int vq = (int)rlu(v.x, 8 * q);
+          if (vq < min_n) {
+            min_n = vq;
+            a = q;
+          }
+        }
+      } else {
+        const bool nz = mm_max > mm_min;                   // utils.py:34-39
+        const double range = mm_max - mm_min;
+        const int n = (int)v.x;
+        const double val = hilo_d(v.z, v.w);
+        const double nvq = nz ? (val - mm_min) / range : val;
+        double sc;
+        if (SEL == POMCP_SEL_UCB) {                        // mcts.py:529-546
+          if (nv >= p.logtab_n) err = POMCP_E_ARENA;
+          sc = nvq + p.c * sqrt(log_n / (double)(n > 0 ? n : 1));
+        } else {                                           // PUCB, mcts.py:502-527
+          const double noise = 1.0 / (double)A;
+          const double prior = (1.0 / (double)A) * (1.0 - p.pucb_f) + p.pucb_f * noise;
+          const double sqrt_n = sqrt((double)nv);
+          sc = (n > 0 ? nvq : 0.0) + p.c * prior * (sqrt_n / (double)(1 + n));
+        }
+        double best = rl_d(sc, 0);
+#pragma unroll
+        for (int q = 1; q < A; ++q) {
+          const double sq = rl_d(sc, 8 * q);
+          if (sq > best) {
+            best = sq;
+            a = q;
+          }
+        }
+        if (SEL == POMCP_SEL_UCB) {                        // mcts.py:539-540: first unvisited
+          const uint64_t unv = __ballot(ql == 0 && lane < 8 * A && v.x == 0u);
+          if (unv != 0ull) a = (__ffsll((long long)unv) - 1) >> 3;
+        }
+      }
+      PT_MARK(5);
+      // ActionNode.children[obs] among the inline slots (mcts.py:356-370), every action
+      const uint64_t sk = (uint64_t)v.x | ((uint64_t)v.y << 32);
+      const bool slot_lane = ql >= 2 && ql - 2 < islots;
+      const bool vb = (sk & kValidBit) != 0;
+      const uint64_t hm = __ballot(slot_lane && (!vb || (sk & kObsMask) == okey));
+      const uint64_t vm = __ballot(slot_lane && vb);
+      // math.log(N) of every existing child, for the level below (no wait)
+      if (slot_lane) lgv = logtab((int)v.w + 1);
+      // the chosen action's results, out of its lane group
+      const int g = 8 * a;
+      const uint4 sa = rl4(v, g), s1a = rl4(v, g + 1);
+      const uint32_t c0 = rlu(n0, g), c1 = rlu(n1, g);
+      const double rr = rl_d(r, g);
+      const int dn = rl(done, g);
+      const uint64_t ok = (uint64_t)rlu((uint32_t)okey, g) | ((uint64_t)rlu((uint32_t)(okey >> 32), g) << 32);
+      const uint32_t gh = (uint32_t)((hm >> (g + 2)) & 0x3Fu);
+      const int ks = gh != 0u ? __ffs((int)gh) - 1 : -1;
+      const uint32_t ani = (uint32_t)(blk * A + a);
+      uint32_t cid = 0;
+      int cblk = -1, cvis = 1;
+      uint4 nsl = make_uint4(0, 0, 0, 0);
+      lptr = nullptr;
+      lb = -1;
+      if (ks >= 0) {
+        const int sl = g + 2 + ks;
+        if (((vm >> sl) & 1ull) != 0ull) {   // an existing child
+          cblk = (int)rlu(v.z, sl);
+          cvis = (int)rlu(v.w, sl) + 1;
+        } else {
+          ++n_nodes;
+        }
+        const uint64_t nk = ok | kValidBit | ((uint64_t)dn << 63);
+        nsl = make_uint4((uint32_t)nk, (uint32_t)(nk >> 32), (uint32_t)cblk, (uint32_t)cvis);
+        if (lane == 0) stp(blk, a, 2 + ks, nsl);
+        cid = ani * kSlots + (uint32_t)ks + 1u;
+        lb = blk;
+        la = a;
+        lk = ks;
+        lg_lane = sl;   // its log(N) was prefetched by that lane
+      } else {
+        const OvfChild o = ovf_child(ani, ok, dn, cblk, cvis);
+        cid = o.cid;
+        cblk = o.cblk;
+        cvis = o.cvis;
+        lptr = o.cptr;
+        lgv = logtab(cvis);   // (any lane)
+        lg_lane = 0;
+      }
+      PT_MARK(6);
+      if (err != 0 || n_log >= p.Np || plen > kMaxPath) {
+        if (err == 0) err = POMCP_E_ARENA;
+        run = false;
+        break;
+      }
+      if (rb_n == kWave) flush_log();
+      {
+        const bool mine = lane == rb_n;                      // mcts.py:371
+        rb_id = mine ? (cid | ltag) : rb_id;
+        rb_v0 = mine ? c0 : rb_v0;
+        rb_v1 = mine ? c1 : rb_v1;
+      }
+      ++rb_n;
+      if (lane == 0) {
+        const uint32_t ba = ((uint32_t)blk << 3) | (uint32_t)a;
+        path[3 * plen + 0] = make_uint4(ba | ((uint32_t)dn << 31), sa.x, (uint32_t)__double2loint(rr),
+                                        (uint32_t)__double2hiint(rr));
+        path[3 * plen + 1] = make_uint4(sa.z, sa.w, s1a.x, s1a.y);
+        path[3 * plen + 2] = make_uint4(s1a.z, s1a.w, 0u, 0u);
+      }
+      ++n_log;
+      ++plen;
+      // descend (mcts.py:371-376): arrival at the child (mcts.py:315-328)
+      if (dn) {
+        ret = 0.0;
+        phase = TP_BACKUP;
+        break;
+      }
+      s0 = c0;
+      s1 = c1;
+      ++t;
+      ++depth;
+      if (depth > p.depth_limit || t > p.step_limit) {
+        ret = 0.0;
+        phase = TP_BACKUP;
+      } else if (cblk < 0) {                               // mcts.py:318-328
+        const int b = alloc_block();
+        if (b < 0) {
+          run = false;
+          break;
+        }
+        if (lane == 0) {
+          if (lb >= 0) stp(lb, la, 2 + lk, make_uint4(nsl.x, nsl.y, (uint32_t)b, nsl.w));
+          else *lptr = b;
+        }
+        k = 0;
+        rdepth = depth;   // the rollout's own depth counter (mcts.py:449)
+        phase = TP_ROLL;
+      } else {
+        blk = cblk;   // the next level (its log(N): lane lg_lane of lgv)
+        nv = cvis;
+      }
+      PT_MARK(7);
+      __builtin_amdgcn_wave_barrier();   // keep lane 0's LDS stores before the next reads
+    }
+    if (!run) break;
+    // ------------------------------------------------------ the rollout
+    while (phase == TP_ROLL) {                             // mcts.py:414-450
+      if (!(rdepth <= p.depth_limit && t <= p.step_limit)) {
+        phase = TP_BACKUP;
+        break;
+      }
+      const uint32_t ae = d_act(p.ego, (uint32_t)A);       // search_policy.py:177
+      const uint32_t j = d_model(2);
+      const uint32_t ao = d_act(p.other, (uint32_t)A);     // other_policy.py:151
+      uint32_t n0, n1;
+      double r;
+      int dn;
+      Env::step(sm, p.ego, s0, s1, ae, ao, j, &n0, &n1, &r, &dn);
+      if (k >= p.dpow_n) {
+        err = POMCP_E_ARENA;
+        run = false;
+        break;
+      }
+      ret += dpow(k) * r;   // mcts.py:420-422
+      ++c_rollout;
+      if (dn) {
+        phase = TP_BACKUP;
+      } else {
+        s0 = n0;
+        s1 = n1;
+        ++t;
+        ++rdepth;
+        ++k;
+      }
+    }
+    if (!run) break;
+    PT_MARK(8);
+    // ------------------------------------------------------ backup (mcts.py:374-381)
+    __builtin_amdgcn_wave_barrier();
+    double gr = ret;
+    for (int l = plen - 1; l >= 0; --l) {
+      const uint4 e0 = path[3 * l], e1 = path[3 * l + 1], e2 = path[3 * l + 2];
+      const double r = hilo_d(e0.z, e0.w);
+      gr = (e0.x >> 31) ? r : r + p.discount * gr;
+      const int n = (int)e0.y + 1;
+      const double value0 = hilo_d(e1.x, e1.y);
+      const double total = hilo_d(e1.z, e1.w) + gr;
+      const double delta = gr - value0;
+      const double value = value0 + delta / (double)n;
+      const double agg = hilo_d(e2.x, e2.y) + delta * (gr - value);
+      const uint32_t ba = e0.x & 0x7FFFFFFFu;
+      if (lane == 0) {
+        stp((int)(ba >> 3), (int)(ba & 7u), 0,
+            make_uint4((uint32_t)n, 0u, (uint32_t)__double2loint(value), (uint32_t)__double2hiint(value)));
+        stp((int)(ba >> 3), (int)(ba & 7u), 1,
+            make_uint4((uint32_t)__double2loint(total), (uint32_t)__double2hiint(total),
+                       (uint32_t)__double2loint(agg), (uint32_t)__double2hiint(agg)));
+      }
+      if (value > mm_max) mm_max = value;   // utils.py:29-32
+      if (value < mm_min) mm_min = value;
+    }
+    ++root_visits;                                          // mcts.py:288
+    max_depth = depth > max_depth ? depth : max_depth;
+    ++sims;
+    PT_MARK(9);
+    __builtin_amdgcn_wave_barrier();
+  }
+#ifdef POMCP_PHASE_TIMING
+  if (p.timing != nullptr && tree == 0 && lane == 0)
+    for (int i = 0; i < 16; ++i) p.timing[i] = pt[i];
+#endif
+  flush_log();
+  __syncthreads();
+
+  // ------------------------------------------------------------------ results
+  const bool have = err == 0 && !root_abs && root_blk >= 0;
+  uint4 st_l = make_uint4(0, 0, 0, 0), s1_l = st_l;
+  if (have) {
+    st_l = ldp(root_blk, al, 0);
+    s1_l = ldp(root_blk, al, 1);
+  }
+  // the blocks back to HBM
+  {
+    const int nback = n_blocks < C ? n_blocks : C;
+    if (lane < 8 * A) {
+      const int a = lane >> 3, q = lane & 7;
+      for (int b = 0; b < nback; ++b) *hpart(b, a, q) = *lpart(b, a, q);
+    }
+  }
+  // _final_action_selection (mcts.py:565-600) ends get_action; a search split
+  // over several launches (final_sel = 0 for all but the last) draws it once
+  int action = -1;
+  if (have && final_sel) {
+    action = 0;
+    uint32_t ties = 0;
+    int nt = 0;
+    bool direct = false;
+    if (SEL == POMCP_SEL_PUCB) {
+      if (root_visits == 0) {
+        action = (int)d_select((uint32_t)A);
+        direct = true;
+      } else {
+        int mx = 0;
+        for (int a = 0; a < A; ++a) {
+          const int na = (int)rlu(st_l.x, 8 * a);
+          if (na == mx) {
+            ties |= 1u << a;
+            ++nt;
+          } else if (na > mx) {
+            mx = na;
+            ties = 1u << a;
+            nt = 1;
+          }
+        }
+      }
+    } else {
+      double mx = -__builtin_inf();
+      for (int a = 0; a < A; ++a) {
+        const double va = hilo_d(rlu(st_l.z, 8 * a), rlu(st_l.w, 8 * a));
+        if (va == mx) {
+          ties |= 1u << a;
+          ++nt;
+        } else if (va > mx) {
+          mx = va;
+          ties = 1u << a;
+          nt = 1;
+        }
+      }
+    }
+    if (!direct) action = kth_bit(ties, d_select((uint32_t)nt));
+  }
+  if (lane == 0) {
+    TreeHdr* const hw = p.hdr + tree;
+    hw->n_blocks = n_blocks;
+    hw->n_log = n_log;
+    hw->n_nodes = n_nodes;
+    hw->error = err;
+    hw->root_blk = root_blk;
+    hw->root_visits = root_visits;
+    hw->mm_min = mm_min;
+    hw->mm_max = mm_max;
+    hw->ctr[0] = sb.ctr;
+    hw->ctr[1] = ss.ctr;
+    hw->ctr[2] = sd.ctr;
+    hw->ctr[3] = s0s.ctr;
+    hw->ctr[4] = s1s.ctr;
+  }
+  pomcp_root_stats* const so = p.stats + tree;
+  double* const xr = p.merge + (int64_t)tree * POMCP_XREC(A);   // exchange record (pomcp.h)
+  if (lane < 8 * A && ql == 0) {   // lane 8a: action a's root child
+    const int a = lane >> 3;
+    const double va = hilo_d(st_l.z, st_l.w), tot = hilo_d(s1_l.x, s1_l.y);
+    so->child_visits[a] = (int)st_l.x;
+    so->child_values[a] = va;
+    so->child_totals[a] = tot;
+    xr[2 * a] = (double)st_l.x;
+    xr[2 * a + 1] = tot;
+  }
+  if (lane == 0) {
+    xr[2 * A + 0] = (double)sims;
+    xr[2 * A + 1] = (double)root_visits;
+    xr[2 * A + 2] = (double)max_depth;
+    xr[2 * A + 3] = (double)err;
+    xr[2 * A + 4] = mm_min;
+    xr[2 * A + 5] = mm_max;
+    so->action = action;
+    so->num_sims = sims;
+    so->search_depth = max_depth;
+    so->root_visits = root_visits;
+    so->root_absorbing = root_abs;
+    so->belief_size = bsize;
+    so->error = err;
+    so->num_children = have ? A : 0;
+    so->min_value = mm_min;
+    so->max_value = mm_max;
+    so->n_levels = n_log - log0;
+    so->n_expansions = n_blocks - blocks0;
+    so->n_new_nodes = n_nodes - nodes0;
+    so->n_rollout_steps = c_rollout;
+    so->n_probes = c_probes;
+    so->n_obs_nodes = n_nodes;
+    so->n_blocks = n_blocks;
+    so->n_log = n_log;
+    so->pad = 0;
+  }
+}
+
+// After k_search_lds: append every tree's scratch records of the launch
+// (stats.n_levels of them, in insertion order) to its search wave's shared
+// log, trees in lane order -- one wave per search wave.  A tree's records keep
+// their order; k_extract / k_compact_log separate the trees by lane tag.
+__global__ __launch_bounds__(64) void k_log_merge(DevParams p) {
+  const int sw = (int)blockIdx.x;
+  const int lane = lane_id();
+  const int tree = sw * kWave + lane;
+  const uint32_t cnt = tree < p.B ? (uint32_t)p.stats[tree].n_levels : 0u;
+  uint32_t incl = cnt;   // inclusive prefix over the lanes
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+    if (lane >= o) incl += y;
+  }
+  const uint32_t base = uniu(p.wlog[sw]);
+  const WaveLog wl(p.plog, p.Np, sw);
+  for (int l = 0; l < kWave; ++l) {
+    const uint32_t n = rlu(cnt, l);
+    if (n == 0u) continue;
+    const uint32_t off = base + rlu(incl, l) - n;
+    const LogRec* src = p.lscr + (int64_t)(sw * kWave + l) * p.Np;
+    for (uint32_t i = (uint32_t)lane; i < n; i += kWave) wl.store(off + i, src[i]);
+  }
+  if (lane == kWave - 1) p.wlog[sw] = base + incl;
+}
+
+#define PB_SEARCH_LDS_INST(E, NA)                                             \
+  template __global__ void k_search_lds<E, POMCP_SEL_PUCB, NA>(DevParams, int, int);  \
+  template __global__ void k_search_lds<E, POMCP_SEL_UCB, NA>(DevParams, int, int);   \
+  template __global__ void k_search_lds<E, POMCP_SEL_UNIFORM, NA>(DevParams, int, int);
+PB_SEARCH_LDS_INST(EnvDriving, 5)
+PB_SEARCH_LDS_INST(EnvPursuitEvasion, 4)
+#undef PB_SEARCH_LDS_INST
+
+}  // namespace pb

@@ -30,6 +30,7 @@ POMCP_E_NOT_FOUND = -6
 POMCP_E_NO_DEVICE = -7
 
 SEL_PUCB, SEL_UCB, SEL_UNIFORM = 0, 1, 2
+SEARCH_AUTO, SEARCH_LANE, SEARCH_WAVE = 0, 1, 2   # pomcp_search_kernel
 ENV_DRIVING = 1
 ENV_PURSUIT_EVASION = 2
 
@@ -175,6 +176,8 @@ SIGNATURES = [
     ("pomcp_update", C.c_int, [_CTX, _P32, _PU64, _P32]),
     ("pomcp_search", C.c_int, [_CTX, C.c_int32, _P32]),
     ("pomcp_search_continue", C.c_int, [_CTX, C.c_int32]),
+    ("pomcp_set_search_kernel", C.c_int, [_CTX, C.c_int32]),
+    ("pomcp_search_kernel_used", C.c_int32, [_CTX]),
     ("pomcp_get_root_stats", C.c_int, [_CTX, C.POINTER(PomcpRootStats)]),
     ("pomcp_set_root_belief", C.c_int, [_CTX, C.c_int32, _PU32, C.c_int32]),
     ("pomcp_get_root_belief", C.c_int, [_CTX, C.c_int32, _PU32, C.c_int32, _P32]),

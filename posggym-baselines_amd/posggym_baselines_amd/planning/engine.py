@@ -4,6 +4,7 @@ per-tree HBM arenas, and exposes update / search / statistics as numpy.
 """
 import ctypes as C
 import math
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -64,13 +65,16 @@ def plan_capacities(config, step_limit: int, num_sims: int, searches: int = 1,
 
 # Wall-clock mode (num_sims=None, the reference's default, mcts.py:285) sizes
 # the arenas from the time limit: an upper bound on one tree's simulation rate
-# (measured 89-110 k simulations/s for a lone tree on MI355X, DESIGN.md §6;
-# 2.5x margin) times search_time_limit per search.  The arena holds one
+# (a lone tree on the wave-per-tree kernel: 130-330 k simulations/s on MI355X
+# depending on how deep its simulations go; ~3x margin) times
+# search_time_limit per search, within the 2^26 obs-node id space (about 1.1 M
+# simulations per search for A = 5: a longer budget ends its search there,
+# step_statistics "arena_full").  The arena holds one
 # search plus the subtree kept by the re-root (subtree compaction at update,
 # pomcp_kernels.hip k_compact), and get_action stops launching chunks before
 # a chunk could overflow it (POMCP.get_action), so a time-limited episode never
 # fails with POMCP_E_ARENA.  HBM budget for all trees of one engine:
-WALL_CLOCK_SIMS_PER_S = 250_000
+WALL_CLOCK_SIMS_PER_S = 1_000_000
 WALL_CLOCK_HBM_BUDGET = 64 << 30
 
 
@@ -189,6 +193,10 @@ class PomcpEngine:
         self._ctx = ctx
         self._lib = lib
         self._stats = (N.PomcpRootStats * self.num_trees)()
+        # search kernel override (tests / benchmarks): POMCP_SEARCH_KERNEL=lane|wave
+        kind = os.environ.get("POMCP_SEARCH_KERNEL", "auto")
+        if kind != "auto":
+            self.set_search_kernel(kind)
 
     # ------------------------------------------------------------------
     def close(self):
@@ -232,6 +240,16 @@ class PomcpEngine:
         self._check(self._lib.pomcp_search(self._ctx, int(num_sims),
                                            out.ctypes.data_as(C.POINTER(C.c_int32))), "search")
         return out
+
+    def set_search_kernel(self, kind):
+        """"auto" | "lane" (k_search: a tree per lane, HBM) | "wave" (k_search_lds:
+        a wave per tree, tree in LDS); same results, different speed."""
+        k = {"auto": N.SEARCH_AUTO, "lane": N.SEARCH_LANE, "wave": N.SEARCH_WAVE}[kind]
+        self._check(self._lib.pomcp_set_search_kernel(self._ctx, k), "set_search_kernel")
+
+    def search_kernel(self):
+        """The kernel the next search uses: "lane" or "wave"."""
+        return "wave" if self._lib.pomcp_search_kernel_used(self._ctx) == N.SEARCH_WAVE else "lane"
 
     def root_stats(self):
         self._check(self._lib.pomcp_get_root_stats(self._ctx, self._stats), "get_root_stats")

@@ -12,6 +12,15 @@ from oracle.run import make_oracle, oracle_record
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True, params=["lane", "wave"])
+def search_kernel(request, monkeypatch):
+    """Every parity test runs on both search kernels: k_search (a tree per lane,
+    tree in HBM) and k_search_lds (a wave per tree, tree in LDS); they must give
+    the same bits as the reference / oracle."""
+    monkeypatch.setenv("POMCP_SEARCH_KERNEL", request.param)
+    return request.param
+
 SQRT2 = math.sqrt(2)
 TEST_CFG = dict(discount=0.95, search_time_limit=0.1, c=SQRT2, truncated=False,
                 action_selection="ucb", pucb_exploration_fraction=0.25, known_bounds=None,
@@ -455,3 +464,36 @@ def test_search_from_host_belief():
     got, exp = both_records(a2, b2)
     assert got == exp
     planner.close()
+
+
+def test_search_kernel_override_is_used(search_kernel):
+    from gpu_util import product_model
+    from posggym_baselines_amd.planning import BatchedPOMCP
+    bp = BatchedPOMCP(product_model("Driving-v1"), "0", product_config(TEST_CFG, 16), 3, 16)
+    assert bp.engine.search_kernel() == search_kernel
+    bp.close()
+
+
+def test_deep_tree_beyond_the_lds_pool():
+    """gamma 0.99 / epsilon 0.01 (depth_limit 459): a 1,500-simulation search
+    expands ~one block per simulation, far past the wave kernel's LDS pool
+    (224 blocks for A = 5): the blocks beyond it are read and written in HBM.
+    Bit-exact against the oracle either way; a second step re-roots into the
+    big tree (compaction moves blocks across the LDS / HBM boundary)."""
+    from gpu_util import batched_episodes
+    from oracle.run import oracle_episode
+    cfg = dict(TEST_CFG, discount=0.99, epsilon=0.01, seed=21)
+    S, K = 1500, 2
+    seeds, exp = [], []
+    s = 610
+    while len(seeds) < 2:
+        trace, recs = oracle_episode(cfg, S, s, tree=len(seeds), max_steps=K)
+        if trace["len"] >= K and all(r["searched"] for r in recs):
+            seeds.append(s)
+            exp.append(recs)
+        s += 1
+    usage = []
+    got = batched_episodes(cfg, S, seeds, K, usage=usage)
+    for b in range(len(seeds)):
+        assert got[b] == exp[b], f"tree {b} (env seed {seeds[b]})"
+    assert max(u[0] for k, u in usage) > 300   # blocks in use: beyond the LDS pool

@@ -22,13 +22,19 @@ NAMES = ["start+root (LDS)", "level: stats line wait", "level: selection",
          "level: child line wait", "level: rest", "rollout", "backup", "loop/other",
          "  step: philox x2", "  step: drv_step2", "  step: reward+done", "  step: obs key",
          "  find_slot", "  slot write / ovf", "  log+path entry", "  (before step)"]
+# k_search_lds (--kernel wave): tree 0's sections
+NAMES_WAVE = ["start", "level: draws", "level: LDS line", "level: step + obs key",
+              "level: log(N) wait", "level: selection", "level: slots / readout",
+              "level: log + path + descend", "rollout", "backup", "-", "-", "-", "-", "-", "-"]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--trees", type=int, default=65536)
     ap.add_argument("--sims", type=int, default=4096)
+    ap.add_argument("--kernel", default="lane", choices=["lane", "wave"])
     args = ap.parse_args()
+    os.environ["POMCP_SEARCH_KERNEL"] = args.kernel
     env = dict(os.environ, POMCP_EXTRA_FLAGS="-DPOMCP_PHASE_TIMING")
     subprocess.run([sys.executable, "-c", "from posggym_baselines_amd import build; build.build(force=True)"],
                    check=True, env=env, cwd=os.path.join(ROOT, "posggym-baselines_amd"))
@@ -53,10 +59,11 @@ def main():
     assert fn(bp.engine._ctx, buf.ctypes.data_as(C.POINTER(C.c_uint64)), cnt.value, C.byref(cnt)) == 0
     per = buf.reshape(-1, 16).astype(np.float64)
     per = per[per.sum(1) > 0]
+    names = NAMES_WAVE if args.kernel == "wave" else NAMES
     tot = per.sum(0)
     sims = args.sims
     print(f"waves {len(per)}; s_memtime ticks per wave per simulation round:")
-    for i, n in enumerate(NAMES):
+    for i, n in enumerate(names):
         print(f"  {n:26s} {tot[i] / len(per) / sims:10.1f}  {100 * tot[i] / tot.sum():5.1f}%")
     print(f"  {'total':26s} {tot.sum() / len(per) / sims:10.1f}")
     bp.close()
