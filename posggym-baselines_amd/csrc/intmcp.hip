@@ -173,6 +173,15 @@ struct ImPair {
     dp = p.dpow;
   }
   __device__ __forceinline__ uint32_t ctr_stored(int q) const { return h.ctr[q] - ((la_pend >> q) & 1u); }
+  // intmcp.py:326-330 (_prune_traverse's clear_belief at every update): the
+  // particles of nodes more than two steps behind the current one are dropped
+  // -- nothing reads them again (a search starts at the current root, a
+  // reinvigoration reads the previous step's beliefs) -- so both trees' logs
+  // keep only the records of nodes with t >= cur_t - 2, in insertion order.
+  // The reference clears only nodes that have children; the other old nodes'
+  // beliefs are as unreachable, so they go too.  The trees stay.
+  template <bool kWave>
+  __device__ void clear_old_beliefs(int cur_t);
   __device__ void store() {
     IHdr o = h;
 #pragma unroll
@@ -1074,6 +1083,35 @@ __global__ __launch_bounds__(64) void k_im_reset(ImParams p) {
   p.hdr[b] = h;
 }
 
+template <class Env>
+template <bool kWave>
+__device__ void ImPair<Env>::clear_old_beliefs(int cur_t) {
+  for (int k = 0; k < 2; ++k) {
+    const int n = h.n_log[k];
+    int out = 0;
+    if constexpr (kWave) {   // 64 records per step; the chunk is loaded before it is stored
+      for (int base = 0; base < n; base += kWave64) {
+        const int i = base + (int)(threadIdx.x & 63);
+        IRec r{0u, 0u, 0u, 0u};
+        bool keep = false;
+        if (i < n) {
+          r = lg[k][i];
+          keep = N(k, (int)r.node).t >= cur_t - 2;
+        }
+        const uint64_t m = __ballot(keep);
+        if (keep) lg[k][out + __popcll(m & im_lanes_below())] = r;
+        out += __popcll(m);
+      }
+    } else {
+      for (int i = 0; i < n; ++i) {
+        const IRec r = lg[k][i];
+        if (N(k, (int)r.node).t >= cur_t - 2) lg[k][out++] = r;
+      }
+    }
+    h.n_log[k] = out;
+  }
+}
+
 // INTMCP.update (intmcp.py:198-300) for every pair.
 // kWave (few pairs: the drop-in's one): a wave per pair, its 64 lanes running
 // the same pair in lockstep (identical state, identical stores) and sharing
@@ -1223,6 +1261,7 @@ __global__ __launch_bounds__(64) void k_im_update(ImParams p) {
           P.h.n_sup = 0;
           P.h.sup_used = 0;
         }
+        if (P.h.err == 0) P.template clear_old_beliefs<kWave>(P.N(0, node).t);
       }
     }
   }

@@ -80,6 +80,8 @@ struct PathEntry {
     pt[slot] += pt_now_ - pt_last;                             \
     pt_last = pt_now_;                                         \
   } while (0)
+#elif defined(POMCP_ASM_MARKS)   // analysis builds (-S): section markers in the assembly
+#define PT_MARK(slot) asm volatile(";@@MARK " #slot)
 #else
 #define PT_MARK(slot) \
   do {                \
@@ -596,6 +598,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
           n_nodes += match ? 0 : 1;
           const uint64_t nk = okey | kValidBit | ((uint64_t)done << 63);
           uint4* slot = const_cast<uint4*>(ap) + part_slot(a, ks);
+#ifdef POMCP_ABLATE_SLOTW   // ablation build only: an existing child's slot is not rewritten
+          if (!match)
+#endif
           *slot = make_uint4((uint32_t)nk, (uint32_t)(nk >> 32), (uint32_t)cblk, (uint32_t)cvis);
           cid = ani * kSlots + (uint32_t)ks + 1u;
           leaf_ptr = reinterpret_cast<int32_t*>(slot) + 2;
@@ -684,9 +689,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         uint4* const bp = reinterpret_cast<uint4*>(an + (int64_t)(ba >> 3) * blk_bytes);
         bp[ba & 7u] = make_uint4((uint32_t)n, 0u, (uint32_t)__double2loint(value),
                                  (uint32_t)__double2hiint(value));
+#ifndef POMCP_ABLATE_STATS1   // ablation build only: no {total, agg} write-back below the root
         bp[part_stats1((int)(ba & 7u))] = make_uint4(
             (uint32_t)__double2loint(total), (uint32_t)__double2hiint(total),
             (uint32_t)__double2loint(agg), (uint32_t)__double2hiint(agg));
+#endif
         if (value > mm_max) mm_max = value;   // utils.py:29-32
         if (value < mm_min) mm_min = value;
       };

@@ -43,32 +43,35 @@
 
 namespace pb {
 
-constexpr int kLdsPoolBytes = 140 * 1024;          // tree blocks; + model, path, discount table
+constexpr int kLdsPoolBytes = 136 * 1024;          // tree blocks; + model, path, caches below
 constexpr int kLdsPoolParts = kLdsPoolBytes / 16;
 constexpr int kLdsDpow = 256;                      // discount powers cached in LDS
+constexpr int kLdsBelief = 128;                    // root beliefs up to this size live in LDS
 __host__ __device__ constexpr int lds_pool_blocks(int A) { return kLdsPoolParts / (8 * A); }
 
-// One RNG stream as a VGPR page (philox.h: word j = word j & 3 of block j >> 2).
+// One RNG stream as a VGPR page of 64 consecutive draws (philox.h: draw j =
+// word j & 3 of block j >> 2): lane i holds draw base + i; a draw is one
+// readlane, a refill (every 64 draws) one Philox block per lane.
 struct VStream {
-  uint4 w;         // lane l: Philox block (page * 64 + l)
-  uint32_t page;   // page held in w (0xFFFFFFFF: none)
+  uint32_t w;      // lane i: draw base + i
+  uint32_t base;   // first draw in w (ctr - 64 initially: nothing held)
   uint32_t ctr;    // next draw
 };
 
 __device__ __forceinline__ void vs_fill(VStream& s, uint64_t seed, uint32_t tkey, uint32_t sid) {
-  const uint32_t pg = s.ctr >> 8;
-  uint32_t c[4] = {pg * 64u + (uint32_t)lane_id(), 0u, sid, (uint32_t)(seed >> 32)};
+  const uint32_t base = s.ctr & ~63u;
+  const uint32_t i = (uint32_t)lane_id();
+  uint32_t c[4] = {(base >> 2) + (i >> 2), 0u, sid, (uint32_t)(seed >> 32)};
   philox4x32_10(c, (uint32_t)seed, tkey);
-  s.w = make_uint4(c[0], c[1], c[2], c[3]);
-  s.page = pg;
+  const uint32_t q = i & 3u;
+  s.w = q == 0u ? c[0] : (q == 1u ? c[1] : (q == 2u ? c[2] : c[3]));
+  s.base = base;
 }
 
 __device__ __forceinline__ uint32_t vs_next(VStream& s, uint64_t seed, uint32_t tkey, uint32_t sid) {
-  if ((s.ctr >> 8) != s.page) vs_fill(s, seed, tkey, sid);
+  if (s.ctr - s.base >= 64u) vs_fill(s, seed, tkey, sid);
   const uint32_t j = s.ctr++;
-  const uint32_t q = j & 3u;
-  const uint32_t x = q == 0u ? s.w.x : (q == 1u ? s.w.y : (q == 2u ? s.w.z : s.w.w));
-  return rlu(x, (int)((j >> 2) & 63u));
+  return rlu(s.w, (int)(j - s.base));
 }
 
 __device__ __forceinline__ uint4 rl4(uint4 v, int l) {
@@ -84,6 +87,11 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
   __shared__ uint4 pool[C * 8 * A];
   __shared__ uint4 path[(kMaxPath + 1) * 3];
   __shared__ double dpw[kLdsDpow];
+  __shared__ uint4 bel[kLdsBelief];
+  // math.log(N) per LDS block, prefetched at a node's arrival for its next
+  // arrival (its visits then are N): nl_n[b] = N, nl_v[b] = math.log(N)
+  __shared__ double nl_v[C];
+  __shared__ int32_t nl_n[C];
   stage_model(p.model, sm);
   const int tree = (int)blockIdx.x;   // grid = B workgroups of one wave
   const int lane = lane_id();
@@ -113,11 +121,11 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
   double mm_min = uni_d(h->mm_min), mm_max = uni_d(h->mm_max);
   const uint64_t seed = uni64(h->seed);
   const uint32_t tkey = uniu(h->tree_key);
-  VStream sb{make_uint4(0, 0, 0, 0), 0xFFFFFFFFu, uniu(h->ctr[0])};   // belief
-  VStream ss{make_uint4(0, 0, 0, 0), 0xFFFFFFFFu, uniu(h->ctr[1])};   // select
-  VStream sd{make_uint4(0, 0, 0, 0), 0xFFFFFFFFu, uniu(h->ctr[2])};   // model
-  VStream s0s{make_uint4(0, 0, 0, 0), 0xFFFFFFFFu, uniu(h->ctr[3])};  // agent 0's actions
-  VStream s1s{make_uint4(0, 0, 0, 0), 0xFFFFFFFFu, uniu(h->ctr[4])};  // agent 1's actions
+  VStream sb{0u, uniu(h->ctr[0]) - 64u, uniu(h->ctr[0])};   // belief
+  VStream ss{0u, uniu(h->ctr[1]) - 64u, uniu(h->ctr[1])};   // select
+  VStream sd{0u, uniu(h->ctr[2]) - 64u, uniu(h->ctr[2])};   // model
+  VStream s0s{0u, uniu(h->ctr[3]) - 64u, uniu(h->ctr[3])};  // agent 0's actions
+  VStream s1s{0u, uniu(h->ctr[4]) - 64u, uniu(h->ctr[4])};  // agent 1's actions
   auto d_belief = [&](uint32_t n) { return uniform_int(vs_next(sb, seed, tkey, S_BELIEF), n); };
   auto d_select = [&](uint32_t n) { return uniform_int(vs_next(ss, seed, tkey, S_SELECT), n); };
   auto d_model = [&](uint32_t n) {
@@ -156,9 +164,23 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
   }
   const int ndp = p.dpow_n < kLdsDpow ? p.dpow_n : kLdsDpow;
   for (int i = lane; i < ndp; i += kWave) dpw[i] = p.dpow[i];
+  const bool bel_lds = bsize <= kLdsBelief;
+  if (bel_lds)
+    for (int i = lane; i < bsize; i += kWave) bel[i] = rbel[i];
+  for (int i = lane; i < C; i += kWave) nl_n[i] = -1;
   __syncthreads();
   auto dpow = [&](int k) { return k < kLdsDpow ? dpw[k] : p.dpow[k]; };
   auto logtab = [&](int n) { return p.logtab[n < p.logtab_n ? n : 0]; };
+  auto particle = [&](uint32_t i) { return bel_lds ? bel[i] : rbel[i]; };
+  // math.log(n) of node block b: the LDS cache, else the host table (a wait;
+  // volatile so that the compiler does not issue the load on a cache hit too)
+  auto node_log = [&](int b, int n) {
+    const int bc = b < C ? b : 0;
+    double x = nl_v[bc];
+    if (!(b < C && nl_n[bc] == n))
+      x = *reinterpret_cast<const volatile double*>(p.logtab + (n < p.logtab_n ? n : 0));
+    return x;
+  };
 
   // ObsNode.add_child for every action (mcts.py:279-281, 318-321): a zeroed block
   auto alloc_block = [&]() -> int {
@@ -189,11 +211,18 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
   }
   if (num_sims <= 0) run = false;
   uint4 pf = make_uint4(0, 0, 0, 0);
-  double root_logn = 0.0;
-  if (run) {
-    pf = rbel[d_belief((uint32_t)bsize)];   // the first simulation's particle
-    root_logn = logtab(root_visits);
-  }
+  if (run) pf = particle(d_belief((uint32_t)bsize));   // the first simulation's particle
+  // the pending log(N) prefetch of the previous level's node (written to the
+  // cache one level later, when the load has landed)
+  int pend_b = -1, pend_n = 0;
+  double pend_v = 0.0;
+  auto pend_flush = [&]() {
+    if (pend_b >= 0 && pend_b < C && lane == 0) {
+      nl_v[pend_b] = pend_v;
+      nl_n[pend_b] = pend_n;
+    }
+    pend_b = -1;
+  };
 
   // Overflow children (beyond the inline slots) of action node ani: wave-uniform.
   struct OvfChild {
@@ -255,18 +284,14 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
     rb_n = 0;
   };
   int sims = 0, max_depth = 0;
-  double lgv = 0.0;   // lanes 8a + 2 + k: math.log(visits + 1) of slot k's child (prefetched)
   for (int it = 0; it < num_sims && run; ++it) {
     // ------------------------------------------------ start (mcts.py:286-287)
     const uint4 pr = pf;                                   // belief.py:55
-    if (sims + 1 < num_sims) pf = rbel[d_belief((uint32_t)bsize)];
+    if (sims + 1 < num_sims) pf = particle(d_belief((uint32_t)bsize));
     int t = (int)pr.x;
     uint32_t s0 = pr.y, s1 = pr.z;
     int depth = 0, plen = 0;
     int blk = root_blk, nv = root_visits;
-    int lg_lane = -1;                                      // -1: the root's log(N)
-    const double logn_root = root_logn;
-    root_logn = logtab(root_visits + 1);                   // the next simulation's (no wait)
     double ret = 0.0;
     int phase = (0 > p.depth_limit || t > p.step_limit) ? TP_BACKUP : TP_LEVEL;   // mcts.py:315
     PT_MARK(0);
@@ -276,6 +301,7 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
     int k = 0, rdepth = 0;
     // -------------------------------------------------- the tree levels
     while (phase == TP_LEVEL) {
+      const double log_n = node_log(blk, nv);              // math.log(visits), mcts.py:534
       const uint32_t j = d_model(2);                       // drawn before the selection:
       const uint32_t ao = d_act(p.other, (uint32_t)A);     // independent streams
       PT_MARK(1);
@@ -289,7 +315,6 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
       const uint64_t okey = Env::obs_key(sm, p.ego, n0, n1);
       PT_MARK(3);
       // _search_action_selection (mcts.py:492-563) on lanes 8a
-      const double log_n = lg_lane < 0 ? logn_root : rl_d(lgv, lg_lane);
       PT_MARK(4);
       int a = 0;
       if (SEL == POMCP_SEL_PUCB && nv == 0) {              // random.choices, uniform prior
@@ -355,47 +380,50 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
       const bool vb = (sk & kValidBit) != 0;
       const uint64_t hm = __ballot(slot_lane && (!vb || (sk & kObsMask) == okey));
       const uint64_t vm = __ballot(slot_lane && vb);
-      // math.log(N) of every existing child, for the level below (no wait)
-      if (slot_lane) lgv = logtab((int)v.w + 1);
-      // the chosen action's results, out of its lane group
+      // this node's next arrival (visits nv + 1): its log(N) into the cache
+      pend_flush();
+      pend_v = logtab(nv + 1);
+      pend_b = blk;
+      pend_n = nv + 1;
+      // the chosen action's results, out of its lane group (lane g: action a's
+      // step and statistics, g + 1 its {total, agg}, g + 2 + k its child slot k)
+      a = uni(a);   // wave-uniform (selects of uniform values end up in VGPRs)
       const int g = 8 * a;
-      const uint4 sa = rl4(v, g), s1a = rl4(v, g + 1);
       const uint32_t c0 = rlu(n0, g), c1 = rlu(n1, g);
-      const double rr = rl_d(r, g);
       const int dn = rl(done, g);
-      const uint64_t ok = (uint64_t)rlu((uint32_t)okey, g) | ((uint64_t)rlu((uint32_t)(okey >> 32), g) << 32);
       const uint32_t gh = (uint32_t)((hm >> (g + 2)) & 0x3Fu);
-      const int ks = gh != 0u ? __ffs((int)gh) - 1 : -1;
+      const int ks = uni(gh != 0u ? __ffs((int)gh) - 1 : -1);
+      const int sl = g + 2 + ks;
       const uint32_t ani = (uint32_t)(blk * A + a);
       uint32_t cid = 0;
       int cblk = -1, cvis = 1;
-      uint4 nsl = make_uint4(0, 0, 0, 0);
+      uint4 nsl = make_uint4(0, 0, 0, 0);   // lane sl: the child slot as written
       lptr = nullptr;
       lb = -1;
       if (ks >= 0) {
-        const int sl = g + 2 + ks;
-        if (((vm >> sl) & 1ull) != 0ull) {   // an existing child
+        const bool match = ((vm >> sl) & 1ull) != 0ull;   // an existing child
+        if (match) {
           cblk = (int)rlu(v.z, sl);
           cvis = (int)rlu(v.w, sl) + 1;
         } else {
           ++n_nodes;
         }
-        const uint64_t nk = ok | kValidBit | ((uint64_t)dn << 63);
-        nsl = make_uint4((uint32_t)nk, (uint32_t)(nk >> 32), (uint32_t)cblk, (uint32_t)cvis);
-        if (lane == 0) stp(blk, a, 2 + ks, nsl);
+        const uint64_t nk = okey | kValidBit | ((uint64_t)done << 63);
+        nsl = make_uint4((uint32_t)nk, (uint32_t)(nk >> 32), match ? v.z : 0xFFFFFFFFu,
+                         match ? v.w + 1u : 1u);
+        if (lane == sl) stp(blk, a, 2 + ks, nsl);
         cid = ani * kSlots + (uint32_t)ks + 1u;
         lb = blk;
         la = a;
         lk = ks;
-        lg_lane = sl;   // its log(N) was prefetched by that lane
       } else {
+        const uint64_t ok =
+            (uint64_t)rlu((uint32_t)okey, g) | ((uint64_t)rlu((uint32_t)(okey >> 32), g) << 32);
         const OvfChild o = ovf_child(ani, ok, dn, cblk, cvis);
         cid = o.cid;
         cblk = o.cblk;
         cvis = o.cvis;
         lptr = o.cptr;
-        lgv = logtab(cvis);   // (any lane)
-        lg_lane = 0;
       }
       PT_MARK(6);
       if (err != 0 || n_log >= p.Np || plen > kMaxPath) {
@@ -411,12 +439,13 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
         rb_v1 = mine ? c1 : rb_v1;
       }
       ++rb_n;
-      if (lane == 0) {
-        const uint32_t ba = ((uint32_t)blk << 3) | (uint32_t)a;
-        path[3 * plen + 0] = make_uint4(ba | ((uint32_t)dn << 31), sa.x, (uint32_t)__double2loint(rr),
-                                        (uint32_t)__double2hiint(rr));
-        path[3 * plen + 1] = make_uint4(sa.z, sa.w, s1a.x, s1a.y);
-        path[3 * plen + 2] = make_uint4(s1a.z, s1a.w, 0u, 0u);
+      // the path entry, written by the lanes that hold it: {stats0, stats1} of
+      // action a as they were, {block << 3 | a | done << 31, r}
+      if (lane == g || lane == g + 1) {
+        path[3 * plen + (lane - g)] = v;
+        if (lane == g)
+          path[3 * plen + 2] = make_uint4(((uint32_t)blk << 3) | (uint32_t)a | ((uint32_t)done << 31),
+                                          (uint32_t)__double2loint(r), (uint32_t)__double2hiint(r), 0u);
       }
       ++n_log;
       ++plen;
@@ -439,15 +468,16 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
           run = false;
           break;
         }
-        if (lane == 0) {
-          if (lb >= 0) stp(lb, la, 2 + lk, make_uint4(nsl.x, nsl.y, (uint32_t)b, nsl.w));
-          else *lptr = b;
+        if (lb >= 0) {
+          if (lane == 8 * la + 2 + lk) stp(lb, la, 2 + lk, make_uint4(nsl.x, nsl.y, (uint32_t)b, nsl.w));
+        } else if (lane == 0) {
+          *lptr = b;
         }
         k = 0;
         rdepth = depth;   // the rollout's own depth counter (mcts.py:449)
         phase = TP_ROLL;
       } else {
-        blk = cblk;   // the next level (its log(N): lane lg_lane of lgv)
+        blk = cblk;   // the next level
         nv = cvis;
       }
       PT_MARK(7);
@@ -490,16 +520,17 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
     __builtin_amdgcn_wave_barrier();
     double gr = ret;
     for (int l = plen - 1; l >= 0; --l) {
+      // {visits, -, value} and {total, agg} before, {block << 3 | a | done << 31, r}
       const uint4 e0 = path[3 * l], e1 = path[3 * l + 1], e2 = path[3 * l + 2];
-      const double r = hilo_d(e0.z, e0.w);
-      gr = (e0.x >> 31) ? r : r + p.discount * gr;
-      const int n = (int)e0.y + 1;
-      const double value0 = hilo_d(e1.x, e1.y);
-      const double total = hilo_d(e1.z, e1.w) + gr;
+      const double r = hilo_d(e2.y, e2.z);
+      gr = (e2.x >> 31) ? r : r + p.discount * gr;
+      const int n = (int)e0.x + 1;
+      const double value0 = hilo_d(e0.z, e0.w);
+      const double total = hilo_d(e1.x, e1.y) + gr;
       const double delta = gr - value0;
       const double value = value0 + delta / (double)n;
-      const double agg = hilo_d(e2.x, e2.y) + delta * (gr - value);
-      const uint32_t ba = e0.x & 0x7FFFFFFFu;
+      const double agg = hilo_d(e1.z, e1.w) + delta * (gr - value);
+      const uint32_t ba = e2.x & 0x7FFFFFFFu;
       if (lane == 0) {
         stp((int)(ba >> 3), (int)(ba & 7u), 0,
             make_uint4((uint32_t)n, 0u, (uint32_t)__double2loint(value), (uint32_t)__double2hiint(value)));
@@ -510,6 +541,7 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
       if (value > mm_max) mm_max = value;   // utils.py:29-32
       if (value < mm_min) mm_min = value;
     }
+    pend_flush();
     ++root_visits;                                          // mcts.py:288
     max_depth = depth > max_depth ? depth : max_depth;
     ++sims;

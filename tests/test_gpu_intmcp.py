@@ -105,8 +105,11 @@ def _wall_clock_episode(time_limit, env_seed, max_steps):
     def step(obs):
         a = planner.step(obs)
         if not planner.root.is_absorbing:
+            st = planner._engine.root_stats()[0]
             steps.append(dict(planner.step_statistics, visits=planner.root.visits,
-                              child_visits=sum(c[1] for c in planner.root.children)))
+                              child_visits=sum(c[1] for c in planner.root.children),
+                              n_log=(int(st.n_log[0]), int(st.n_log[1])),
+                              n_nodes=(int(st.n_nodes[0]), int(st.n_nodes[1]))))
         return a
 
     trace = run_episode(step, env_seed, max_steps=max_steps)
@@ -139,6 +142,25 @@ def test_wall_clock_small_arena_stops_early(monkeypatch):
     assert len(steps) >= 3
     assert any(st.get("arena_full") for st in steps)
     assert all(st["child_visits"] <= st["visits"] for st in steps)
+
+
+def test_wall_clock_old_beliefs_cleared(monkeypatch):
+    """intmcp.py:326-330: at every update the particles of nodes more than two
+    steps behind are dropped, so the particle logs hold about three searches'
+    records (a search's records sit at depths t+1..t+3 and are dropped five
+    steps later), not the episode's.  With a node / log arena of ~3 M entries
+    (a 2 GiB budget) a 1 s episode appending ~150-300 k records per tree per
+    step never stops early, and the log stays bounded while the trees grow."""
+    from posggym_baselines_amd.planning import intmcp as M
+    monkeypatch.setattr(M, "INTMCP_WALL_CLOCK_HBM_BUDGET", 2 << 30)
+    trace, steps, ceiling = _wall_clock_episode(1.0, 41, 12)
+    assert len(steps) >= 6, len(steps)
+    for st in steps:
+        assert not st.get("arena_full"), [(x["n_log"], x["num_sims"]) for x in steps]
+    appended = sum(x["num_sims"] for x in steps) * 3   # <= 3 records per simulation (depth 2)
+    peak = max(max(x["n_log"]) for x in steps)
+    assert peak < appended // 2, (peak, appended)
+    print("I-NTMCP 1 s episode, n_log per step:", [x["n_log"] for x in steps])
 
 
 def test_search_split_over_launches_equals_one_launch():
