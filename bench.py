@@ -35,18 +35,20 @@ for _p in (ROOT, os.path.join(ROOT, "posggym-baselines_amd")):
         sys.path.insert(0, _p)
 
 # algorithmic HBM bytes (DESIGN.md "Algorithmic bytes"): per simulation, per
-# tree level stepped (node 8 + A x 12 child statistics + 100), per leaf expansion
-# (A x 28 + 4), per obs node created
+# tree level stepped (node 8 + A x 12 child statistics + 84), per leaf expansion
+# (A x 20 + 4), per obs node created.  The per-action record is {visits,
+# value, total}: ActionNode.agg is not kept, so it is not counted.
 B_SIM, B_NEW_NODE = 16, 28
 B_LOG_APPEND = 16   # of b_level: the particle-log record (the root level's only HBM term)
 
 
-def b_level(A):
-    return 8 + 12 * A + 100
+def b_level(A, agg=False):
+    """agg: the engine keeps ActionNode.agg (I-NTMCP: +8 B read, +8 B written)."""
+    return 8 + 12 * A + 84 + (16 if agg else 0)
 
 
 def b_expand(A):
-    return 28 * A + 4
+    return 20 * A + 4
 HBM_PEAK_GBS = 8000.0
 
 
@@ -390,7 +392,7 @@ def main_intmcp(args):
         nodes += s.n_nodes[0] + s.n_nodes[1] - s0[2]
         stats += s.n_stats[0] + s.n_stats[1] - s0[3]
     sims_timed = 2 * S * searched * args.steps
-    alg_bytes = (B_SIM * sims_timed + b_level(A) * (lv0 + lv1) + b_other(A) * lv1
+    alg_bytes = (B_SIM * sims_timed + b_level(A, agg=True) * (lv0 + lv1) + b_other(A) * lv1
                  + B_STAT * stats + B_NODE_HASH * nodes) / args.steps
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     traffic = _pmc_traffic("pmc_intmcp.json", lib_sha, trees=B, sims=S, env=args.env)

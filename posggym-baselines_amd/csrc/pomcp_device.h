@@ -34,16 +34,31 @@ constexpr uint32_t kRootId = 0;        // obs node id of a root created by the i
 
 // Action nodes (node.py:120-178) with their obs children inline (node.py:144-160).
 // An expanded obs node owns a block of (A + 1) x 128 B lines, in 16 B parts:
-//   line 0     : part a = stats0 of action a {visits, pad, value}     (A <= 6)
-//   line 1 + a : part 0 = stats1 of action a {total, agg},
-//                parts 1..6 = child slots k of action a (ChildSlot)
-// so one tree level of a simulation touches two lines: the node's action
-// statistics (selection) and the chosen action's line (obs child lookup).
+//   line 0 (the node line), A <= 5:
+//     bytes   0..19  visits of action a (u32 at 4a)             ActionNode.visits
+//     bytes  20..23  the node's own visits                       ObsNode.visits
+//     bytes  24..31  math.log(node visits + 1): log(N) of the next arrival
+//     bytes 32 + 16a {value, total} of action a (f64, f64)       value / total_value
+//   line 1 + a : parts 1..6 = child slots k of action a (ChildSlot), part 0 unused
+// A tree level reads the node line (selection, with the node's N and log(N) in
+// it: no host-table load on the path) and the chosen action's slot line; its
+// backup writes the node line only (bytes 0..31 and the action's 16 B).
+// ActionNode.agg (node.py:141-178, the running variance) is not kept: only
+// ActionNode.variance reads it and only __str__ reads that.
+// ObsNode.visits of an EXPANDED child is its block's bytes 20..23; the slot's
+// visits field is authoritative only while the child has no block, and only
+// while it is within the depth / step limits: an arrival cut off there
+// (mcts.py:315) does not rewrite its slot (k_search), so k_compact /
+// k_compact_log recount every slot's visits from the particle log (one record
+// per arrival) at each re-root.
 struct ChildSlot {
   uint64_t key;     // obs key | valid << 62 | is_absorbing << 63
   int32_t block;    // action block of the child obs node (-1 = leaf)
-  int32_t visits;   // ObsNode.visits
+  int32_t visits;   // ObsNode.visits while block == -1 (see above)
 };
+constexpr int kNodeVisByte = 20;   // node line: the node's visits (u32)
+constexpr int kNodeLogByte = 24;   // node line: math.log(visits + 1) (f64)
+__host__ __device__ constexpr int part_vt(int a) { return 2 + a; }   // {value, total} of a
 // Particle log record (ObsNode.belief.add_particle, mcts.py:371): the particle
 // (v0, v1) entered obs node `id` of the tree in lane `lane` of the search wave.
 // Its time step is not stored: every particle of a node has the same t (the
@@ -88,7 +103,6 @@ struct alignas(16) Line {   // allocation unit of the block arena
 };
 __host__ __device__ constexpr int blk_lines(int A) { return A + 1; }
 __host__ __device__ constexpr int blk_parts(int A) { return kLine * (A + 1); }
-__host__ __device__ constexpr int part_stats1(int a) { return kLine * (1 + a); }
 __host__ __device__ constexpr int part_slot(int a, int k) { return kLine * (1 + a) + 1 + k; }
 
 // The block arena is interleaved by search wave ([wave][block][lane] of

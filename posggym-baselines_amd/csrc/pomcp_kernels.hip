@@ -474,6 +474,10 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
           // already gathered into the other belief buffer by k_extract
           uint4* nb = T.other_belief();
           int n = uni(p.cnt[tree]);
+          // ObsNode.visits of the new root = its particle records (one per
+          // arrival, mcts.py:358-371); the slot's count may be stale
+          // (pomcp_device.h: cut-off arrivals, children with a block)
+          const int visits = n;
           if (n > p.Nr) T.err = POMCP_E_ARENA;
           // _reinvigorate (mcts.py:651-700) -> BeliefRejectionSampler (belief.py:145-194)
           const int need = p.n_target - n;
@@ -549,7 +553,7 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
           if (T.err == 0) {
             T.root_id = c.id;
             T.root_blk = c.blk;
-            T.root_visits = c.visits;
+            T.root_visits = visits;
             T.root_t += 1;
             T.root_abs = c.absorbing;
             T.bsel ^= 1;
@@ -683,8 +687,9 @@ __global__ __launch_bounds__(256) void k_compact(DevParams p) {
     for (int q = 0; q < kPer; ++q) {
       const int pp = prt[q];
       const bool slot = pp >= kLine && (pp % kLine) >= 1 && (pp % kLine) <= kSlots;
-      if (dst[q] >= 0 && slot && (v[q].y & (uint32_t)(kValidBit >> 32)) != 0u && (int)v[q].z >= 0)
-        v[q].z = (uint32_t)ld_agent(cmap + (int)v[q].z);
+      const bool vs = dst[q] >= 0 && slot && (v[q].y & (uint32_t)(kValidBit >> 32)) != 0u;
+      if (vs && (int)v[q].z >= 0) v[q].z = (uint32_t)ld_agent(cmap + (int)v[q].z);
+      if (vs) v[q].w = 0u;   // visits: recounted from the log by k_compact_log
     }
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
@@ -711,6 +716,7 @@ __global__ __launch_bounds__(256) void k_compact(DevParams p) {
           keep = true;
           w0.z = (uint32_t)pb * (uint32_t)A + w0.z % (uint32_t)A;
           if ((int)w1.x >= 0) w1.x = (uint32_t)ld_agent(cmap + (int)w1.x);
+          w1.y = 0u;            // visits: recounted by k_compact_log
           w1.z = (uint32_t)s;   // the old slot (pad word)
         }
       }
@@ -792,14 +798,22 @@ __global__ __launch_bounds__(256) void k_compact_log(DevParams p) {
       keep = true;
       if (act[wi][l]) {
         int32_t nid = -1;
+        int32_t* vis = nullptr;   // the node's visits (zeroed by k_compact): + 1 per record
         if (id >= p.ovf_base) {
           nid = ld_agent(p.ovf_new + (int64_t)tree * p.H + (id - p.ovf_base));
+          if (nid >= 0) vis = &p.ovf[(int64_t)tree * p.H + ((uint32_t)nid - p.ovf_base)].visits;
         } else if (id >= 1u) {
           const uint32_t ani = (id - 1u) / kSlots, k = (id - 1u) % kSlots;
           const int nb = ld_agent(p.cmap + (int64_t)tree * p.Nb + (int)(ani / A));
-          if (nb >= 0) nid = (int32_t)(((uint32_t)nb * A + ani % A) * kSlots + k + 1u);
+          if (nb >= 0) {
+            nid = (int32_t)(((uint32_t)nb * A + ani % A) * kSlots + k + 1u);
+            uint4* const bp = reinterpret_cast<uint4*>(p.an + tree_base_lines(tree, p.Nb, (int)A) +
+                                                       (int64_t)nb * blk_stride_lines((int)A));
+            vis = reinterpret_cast<int32_t*>(bp + part_slot((int)(ani % A), (int)k)) + 3;
+          }
         }
         keep = nid >= 0;
+        if (vis != nullptr) atomicAdd(vis, 1);
         r.id = (uint32_t)nid | (l << kIdBits);
       }
       if (keep) atomicAdd(&kept[wi][l], 1);

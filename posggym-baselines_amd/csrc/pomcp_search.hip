@@ -15,20 +15,30 @@
 // dependent memory access, so the cost of an iteration of the phase loop is
 // the number of memory waits in it, whatever the lanes' phases are.  Hence:
 //   * the ROOT's action statistics and inline child slots live in LDS for the
-//     whole launch (35 x 16 B per tree, lane-interleaved: conflict-free), so
-//     the root level of every simulation costs no HBM round trip; the root's
-//     {total, agg} stay in HBM and are loaded without waiting (they are only
-//     needed by the backup);
+//     whole launch (35 x 16 B per tree, lane-interleaved: conflict-free), its
+//     action totals in registers, so the root level of every simulation costs
+//     no HBM round trip;
 //   * the belief particle of the NEXT simulation is prefetched when a
 //     simulation starts (belief.py:55: its index only depends on the belief
 //     stream's counter);
 //   * one loop iteration = one level below the root + a whole rollout + the
 //     backup + the start of the next simulation with its root level (LDS);
-//     whenever a lane descends into an expanded node, the node's statistics
-//     line is loaded right away and consumed by the NEXT iteration, so its
-//     latency hides behind the rest of this iteration; only the chosen
-//     action's child line is waited for.  A depth-2 simulation takes two
-//     iterations.
+//     whenever a lane descends into an expanded node, the node line (its
+//     action statistics, its own visit count and log(N)) is loaded right away
+//     and consumed by the NEXT iteration, so its latency hides behind the rest
+//     of this iteration; only the chosen action's child line is waited for.
+//     A depth-2 simulation takes two iterations.
+//   * a level's backup writes the node line only: the chosen action's visits
+//     and {value, total}, the node's visits and the log(N) of its next
+//     arrival (loaded during the level).  A child slot is written only when it
+//     changes beyond its visit count: a new child, its block at expansion, an
+//     absorbing flag flip, and the visits of a child that has no block yet and
+//     lies within the depth / step limits (the next arrival there expands it
+//     and needs them); a cut-off arrival writes nothing (pomcp_device.h).
+//     Against the (A + 1)-line layout with {total, agg} in the action's slot
+//     line (round 2) this is 2 written sectors in one line per level instead
+//     of 3 in two: -11% wave memory-wait cycles and -10% L2 misses (PMC), 0 to
+//     +10% simulations/s depending on the box.
 // The root block is written back to HBM at the end of the launch.
 //
 // Block layout: pomcp_device.h ((A + 1) x 128 B lines).
@@ -46,9 +56,9 @@ constexpr int kTPB = 256;    // lanes per workgroup of a full launch (one workgr
 // one-wave workgroups so their waves spread over the CUs instead of filling
 // a few of them (pomcp_capi.hip search_tpb).
 constexpr int kTPBSmall = 64;
-// Root cache layout: the root's stats0[a] (always) and, when kRootSlotsInLds,
-// its inline child slots[a][k].  Without the slots a tree needs 80 B of LDS,
-// which leaves room for more than one workgroup per CU.
+// Root cache layout: the root's {visits, -, value} of action a (always) and,
+// when kRootSlotsInLds, its inline child slots[a][k].  Without the slots a tree
+// needs 80 B of LDS, which leaves room for more than one workgroup per CU.
 #ifndef POMCP_ROOT_SLOTS_LDS
 #define POMCP_ROOT_SLOTS_LDS 1
 #endif
@@ -61,13 +71,20 @@ __host__ __device__ constexpr int rc_stats(int a) { return a; }
 __host__ __device__ constexpr int rc_slot(int a, int k) { return kMaxA + a * kSlots + k; }
 
 constexpr int kRegPath = 3;  // levels 1..kRegPath held in registers (deeper ones in p.path)
+constexpr int kPre = 2 + kMaxA;   // node line parts read by a level: visits, node, {value, total}
 
 // One level (depth >= 1) of the running simulation's path: {block << 3 |
-// action | done << 31, visits before, r}, {value before, total before},
-// {agg before, -, -}.
+// action | done << 31, the action's visits before, r}, {value before, total
+// before}, {node line bytes 16..31 as the backup writes them: visits of action
+// 4, the node's visits (this arrival counted), log(visits + 1)}.
 struct PathEntry {
   uint4 e0, e1, e2;
 };
+
+// Action a's visits out of node line parts 0 and 1 (a compile-time index).
+__device__ __forceinline__ uint32_t line_visits(const uint4& p0, const uint4& p1, int a) {
+  return a == 0 ? p0.x : a == 1 ? p0.y : a == 2 ? p0.z : a == 3 ? p0.w : p1.x;
+}
 
 // Phase timing (diagnostics build, -DPOMCP_PHASE_TIMING): per-wave s_memtime
 // deltas per loop section into p.timing[wave][16]; each mark first drains every
@@ -278,22 +295,26 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   double ret = 0.0;
   uint4 pf = make_uint4(0, 0, 0, 0);   // belief particle of the next simulation
   // the root level of the running simulation: {a | done << 31, visits before},
-  // r, value before; {total, agg} before (HBM load, consumed by the backup)
+  // r, value before, total before
   int r0_on = 0;
   uint32_t r0_a = 0, r0_vis = 0;
-  double r0_r = 0.0, r0_val = 0.0;
-  uint4 r0_s1 = make_uint4(0, 0, 0, 0);
-  // the root's {total, agg} per action: in registers for the whole launch
-  // (only the backup reads or writes them), written back at the end -- a root
-  // level then touches no HBM line at all
-  uint4 r1[kMaxA];
+  double r0_r = 0.0, r0_val = 0.0, r0_tot = 0.0;
+  // the root's action totals: in registers for the whole launch (only the
+  // backup reads or writes them), written back at the end -- a root level then
+  // touches no HBM line at all
+  double rt[kMaxA];
 #pragma unroll
-  for (int q = 0; q < kMaxA; ++q) r1[q] = make_uint4(0, 0, 0, 0);
+  for (int q = 0; q < kMaxA; ++q) rt[q] = 0.0;
   PathEntry rpath[kRegPath];     // levels 1..kRegPath
-  uint4 pre[kMaxA];              // statistics line of the next LEVEL pass's node
+  uint4 pre[kPre];               // node line of the next LEVEL pass's node (parts 0 .. A + 1)
 #pragma unroll
-  for (int q = 0; q < kMaxA; ++q) pre[q] = make_uint4(0, 0, 0, 0);
-  double pre_logn = 0.0;         // math.log(visits) of that node
+  for (int q = 0; q < kPre; ++q) pre[q] = make_uint4(0, 0, 0, 0);
+  // the leaf expanded by the running simulation: its node line's bytes 16..31
+  // ({0, visits, log(visits + 1)}) are written by the backup, when the log(N)
+  // load issued at the expansion has long landed
+  int lf_b = -1;
+  uint32_t lf_nv = 0;
+  double lf_ln = 0.0;
   auto logtab = [&](int n) { return p.logtab[n < p.logtab_n ? n : 0]; };
 
   if (!valid || err != 0 || root_abs) phase = TP_DONE;   // mcts.py:270-272
@@ -313,15 +334,17 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   double root_logn = logtab(root_visits); // math.log(root visits) of the next simulation
   const uint4* const rb = reinterpret_cast<const uint4*>(an + (int64_t)(cached ? root_blk : 0) * blk_bytes);
   if (cached) {
+    const uint4 p0 = rb[0], p1 = rb[1];
 #pragma unroll
     for (int a = 0; a < kMaxA; ++a) {
       if (a < A) {
-        rc[rc_stats(a)][lid] = rb[a];
+        const uint4 vt = rb[part_vt(a)];
+        rc[rc_stats(a)][lid] = make_uint4(line_visits(p0, p1, a), 0u, vt.x, vt.y);
         if (kRootSlotsInLds) {
 #pragma unroll
           for (int q = 0; q < kSlots; ++q) rc[rc_slot(a, q)][lid] = rb[part_slot(a, q)];
         }
-        r1[a] = rb[part_stats1(a)];
+        rt[a] = hilo_d(vt.z, vt.w);
       }
     }
     pf = rbel[d_belief((uint32_t)bsize)];   // the first simulation's particle
@@ -404,7 +427,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
 
   // Descend into the child (mcts.py:371-376): arrival at an obs node (start of
   // _simulate, mcts.py:315-328): depth/step cutoff -> back up 0; unexpanded ->
-  // expand and roll out; else select there (next LEVEL).
+  // expand and roll out; else select there (next LEVEL).  cvis: the child's
+  // visits with this arrival when it has no block (its slot's count).
   auto descend = [&](int done, int cblk, int cvis, uint32_t n0, uint32_t n1) {
     if (done) {
       ret = 0.0;
@@ -412,7 +436,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
       return;
     }
     blk = cblk;
-    nvis = cvis;
     s0 = n0;
     s1 = n1;
     ++t;
@@ -427,18 +450,38 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
       } else {
         if (leaf_rc >= 0) rc[leaf_rc][lid].z = (uint32_t)b;
         else *leaf_ptr = b;
+        lf_b = b;
+        lf_nv = (uint32_t)cvis;
+        lf_ln = logtab(cvis + 1);
         ret = 0.0;
         k = 0;
         rdepth = depth;   // the rollout's own depth counter (mcts.py:449)
         phase = TP_ROLL;
       }
-    } else {   // next LEVEL pass: issue its statistics line now (no wait)
+    } else {   // next LEVEL pass: issue its node line now (no wait)
       phase = TP_LEVEL;
       const uint4* const cp = reinterpret_cast<const uint4*>(an + (int64_t)blk * blk_bytes);
 #pragma unroll
-      for (int q = 0; q < kMaxA; ++q) pre[q] = q < A ? cp[q] : make_uint4(0, 0, 0, 0);
-      pre_logn = logtab(nvis);
+      for (int q = 0; q < kPre; ++q) pre[q] = q < 2 + A ? cp[q] : make_uint4(0, 0, 0, 0);
     }
+  };
+  // A done arrival at a child that has a block (rare: it was expanded by an
+  // earlier, non-terminal arrival): ObsNode.visits += 1 in its node line.
+  auto bump_node = [&](int cb) {
+    uint4* const c1 = reinterpret_cast<uint4*>(an + (int64_t)cb * blk_bytes) + 1;
+    const uint4 x = *c1;
+    const double ln = logtab((int)x.y + 2);
+    *c1 = make_uint4(x.x, x.y + 1u, (uint32_t)__double2loint(ln), (uint32_t)__double2hiint(ln));
+  };
+  auto push_path = [&](PathEntry pe) {
+    if (plen < kRegPath) {
+#pragma unroll
+      for (int l = 0; l < kRegPath; ++l)
+        if (plen == l) rpath[l] = pe;
+    } else {
+      path[plen] = pe;
+    }
+    ++plen;
   };
 
   // One iteration of this uniform loop = one simulation of every lane's tree,
@@ -483,9 +526,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
 #pragma unroll
           for (int q = 0; q < kSlots; ++q)
             sl[q] = kRootSlotsInLds ? rc[rc_slot(a, q)][lid] : rb[part_slot(a, q)];
-          r0_s1 = r1[0];
+          r0_tot = rt[0];
 #pragma unroll
-          for (int q = 1; q < kMaxA; ++q) r0_s1 = sel4(q == a, r1[q], r0_s1);   // (sel4: registers)
+          for (int q = 1; q < kMaxA; ++q) r0_tot = q == a ? rt[q] : r0_tot;   // (selects: registers)
           uint32_t n0, n1;
           double r;
           int done;
@@ -506,6 +549,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
             cblk = match ? (int)sk.z : cblk;
             cvis = match ? (int)sk.w + 1 : cvis;
             n_nodes += match ? 0 : 1;
+            if (match && cblk >= 0 && done) bump_node(cblk);
+            // (LDS: the slot is rewritten on every arrival; its visits are
+            // meaningful while the child has no block)
             const uint64_t nk = okey | kValidBit | ((uint64_t)done << 63);
             const uint4 nsl = make_uint4((uint32_t)nk, (uint32_t)(nk >> 32), (uint32_t)cblk, (uint32_t)cvis);
             cid = ani * kSlots + (uint32_t)ks + 1u;
@@ -525,6 +571,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
             cvis = o.cvis;
             leaf_ptr = o.cptr;
             leaf_rc = -1;
+            if (cblk >= 0 && done) bump_node(cblk);
           }
           if (err != 0 || n_log >= p.Np) {
             if (err == 0) err = POMCP_E_ARENA;
@@ -559,18 +606,27 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         const uint32_t j = take_mod(2);
         const uint32_t ao = take_oth((uint32_t)A);
         PT_MARK(8);
-        uint4 st[kMaxA];   // prefetched by descend()
+        // the node line, prefetched by descend(): this arrival's N (its visits
+        // + 1) and math.log(N) are in it
+        nvis = (int)pre[1].y + 1;
+        const double log_n = hilo_d(pre[1].z, pre[1].w);
+        const double lnx = logtab(nvis + 1);   // written back by the backup (no wait here)
+        uint4 st[kMaxA];   // {visits, -, value} per action, as select_action reads them
   #pragma unroll
-        for (int q = 0; q < kMaxA; ++q) st[q] = pre[q];
+        for (int q = 0; q < kMaxA; ++q)
+          st[q] = q < A ? make_uint4(line_visits(pre[0], pre[1], q), 0u, pre[part_vt(q)].x,
+                                     pre[part_vt(q)].y)
+                        : make_uint4(0, 0, 0, 0);
         PT_MARK(1);
-        const int a = select_action(st, nvis, pre_logn);
+        const int a = select_action(st, nvis, log_n);
         PT_MARK(2);
-        uint4 sa = st[0];
+        uint4 sa = st[0], va = pre[part_vt(0)];
   #pragma unroll
-        for (int q = 1; q < kMaxA; ++q)
+        for (int q = 1; q < kMaxA; ++q) {
           sa = sel4(q == a, st[q], sa);
-        // the chosen action's stats1 and child slots (second round trip)
-        const uint4 s1a = ap[part_stats1(a)];
+          va = sel4(q == a, pre[part_vt(q < A ? q : 0)], va);
+        }
+        // the chosen action's child slots (second round trip)
         uint4 sl[kSlots];
   #pragma unroll
         for (int q = 0; q < kSlots; ++q) sl[q] = ap[part_slot(a, q)];
@@ -598,10 +654,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
           n_nodes += match ? 0 : 1;
           const uint64_t nk = okey | kValidBit | ((uint64_t)done << 63);
           uint4* slot = const_cast<uint4*>(ap) + part_slot(a, ks);
-#ifdef POMCP_ABLATE_SLOTW   // ablation build only: an existing child's slot is not rewritten
-          if (!match)
-#endif
-          *slot = make_uint4((uint32_t)nk, (uint32_t)(nk >> 32), (uint32_t)cblk, (uint32_t)cvis);
+          // the slot changes beyond its visit count, or its count is needed
+          // (no block yet, within the limits): pomcp_device.h
+          const bool cut = depth + 1 > p.depth_limit || t + 1 > p.step_limit;   // mcts.py:315
+          const bool flip = (sk.y >> 31) != (uint32_t)done;
+          if (!match || flip || (cblk < 0 && (done || !cut)))
+            *slot = make_uint4((uint32_t)nk, (uint32_t)(nk >> 32), (uint32_t)cblk, (uint32_t)cvis);
+          if (match && cblk >= 0 && done) bump_node(cblk);
           cid = ani * kSlots + (uint32_t)ks + 1u;
           leaf_ptr = reinterpret_cast<int32_t*>(slot) + 2;
         } else {
@@ -610,6 +669,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
           cblk = o.cblk;
           cvis = o.cvis;
           leaf_ptr = o.cptr;
+          if (cblk >= 0 && done) bump_node(cblk);
         }
         PT_MARK(13);
         if (err != 0 || n_log >= p.Np || plen >= kMaxPath) {
@@ -620,19 +680,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
           app = true;
           ++n_log;
           const uint32_t ba = ((uint32_t)blk << 3) | (uint32_t)a;   // blk < 2^26 / 30
-          const PathEntry pe = {
+          push_path(PathEntry{
               make_uint4(ba | ((uint32_t)done << 31), sa.x, (uint32_t)__double2loint(r),
                          (uint32_t)__double2hiint(r)),
-              make_uint4(sa.z, sa.w, s1a.x, s1a.y),
-              make_uint4(s1a.z, s1a.w, 0u, 0u)};
-          if (plen < kRegPath) {
-  #pragma unroll
-            for (int l = 0; l < kRegPath; ++l)
-              if (plen == l) rpath[l] = pe;
-          } else {
-            path[plen] = pe;
-          }
-          ++plen;
+              va,
+              make_uint4(pre[1].x, (uint32_t)nvis, (uint32_t)__double2loint(lnx),
+                         (uint32_t)__double2hiint(lnx))});
           PT_MARK(14);
           descend(done, cblk, cvis, n0, n1);
         }
@@ -684,16 +737,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         const double total = hilo_d(e1.z, e1.w) + gr;
         const double delta = gr - value0;
         const double value = value0 + delta / (double)n;
-        const double agg = hilo_d(e2.x, e2.y) + delta * (gr - value);
         const uint32_t ba = e0.x & 0x7FFFFFFFu;
-        uint4* const bp = reinterpret_cast<uint4*>(an + (int64_t)(ba >> 3) * blk_bytes);
-        bp[ba & 7u] = make_uint4((uint32_t)n, 0u, (uint32_t)__double2loint(value),
-                                 (uint32_t)__double2hiint(value));
-#ifndef POMCP_ABLATE_STATS1   // ablation build only: no {total, agg} write-back below the root
-        bp[part_stats1((int)(ba & 7u))] = make_uint4(
-            (uint32_t)__double2loint(total), (uint32_t)__double2hiint(total),
-            (uint32_t)__double2loint(agg), (uint32_t)__double2hiint(agg));
-#endif
+        const uint32_t a = ba & 7u;
+        char* const lp = an + (int64_t)(ba >> 3) * blk_bytes;   // the node line
+        if (a < 4u) reinterpret_cast<uint32_t*>(lp)[a] = (uint32_t)n;
+        reinterpret_cast<uint4*>(lp)[1] = make_uint4(a == 4u ? (uint32_t)n : e2.x, e2.y, e2.z, e2.w);
+        reinterpret_cast<uint4*>(lp)[part_vt((int)a)] =
+            make_uint4((uint32_t)__double2loint(value), (uint32_t)__double2hiint(value),
+                       (uint32_t)__double2loint(total), (uint32_t)__double2hiint(total));
         if (value > mm_max) mm_max = value;   // utils.py:29-32
         if (value < mm_min) mm_min = value;
       };
@@ -701,20 +752,22 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
 #pragma unroll
       for (int l = kRegPath - 1; l >= 0; --l)
         if (l < plen) level(rpath[l]);
-      if (r0_on) {   // the root level: stats0 in LDS, stats1 in HBM
+      if (lf_b >= 0) {   // the expanded leaf's own visits and log(N)
+        reinterpret_cast<uint4*>(an + (int64_t)lf_b * blk_bytes)[1] =
+            make_uint4(0u, lf_nv, (uint32_t)__double2loint(lf_ln), (uint32_t)__double2hiint(lf_ln));
+        lf_b = -1;
+      }
+      if (r0_on) {   // the root level: statistics in LDS, totals in registers
         const int a = (int)(r0_a & 0x7FFFFFFFu);
         gr = (r0_a >> 31) ? r0_r : r0_r + p.discount * gr;
         const int n = (int)r0_vis + 1;
-        const double total = hilo_d(r0_s1.x, r0_s1.y) + gr;
+        const double total = r0_tot + gr;
         const double delta = gr - r0_val;
         const double value = r0_val + delta / (double)n;
-        const double agg = hilo_d(r0_s1.z, r0_s1.w) + delta * (gr - value);
         rc[rc_stats(a)][lid] = make_uint4((uint32_t)n, 0u, (uint32_t)__double2loint(value),
                                           (uint32_t)__double2hiint(value));
-        const uint4 s1n = make_uint4((uint32_t)__double2loint(total), (uint32_t)__double2hiint(total),
-                                     (uint32_t)__double2loint(agg), (uint32_t)__double2hiint(agg));
 #pragma unroll
-        for (int q = 0; q < kMaxA; ++q) r1[q] = sel4(q == a, s1n, r1[q]);
+        for (int q = 0; q < kMaxA; ++q) rt[q] = q == a ? total : rt[q];
         if (value > mm_max) mm_max = value;
         if (value < mm_min) mm_min = value;
       }
@@ -739,30 +792,49 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
     if (lane == 0) p.wlog[wave] = wpos0 + mine;
   }
   if (!valid) return;
-  if (cached) {   // write the root block back
+  if (cached) {   // write the root block back (its node line's bytes 16..31 are unused)
+    uint4* const wb = const_cast<uint4*>(rb);
+    uint32_t vw[kMaxA];
 #pragma unroll
     for (int a = 0; a < kMaxA; ++a) {
+      vw[a] = 0u;
       if (a < A) {
-        const_cast<uint4*>(rb)[a] = rc[rc_stats(a)][lid];
-        const_cast<uint4*>(rb)[part_stats1(a)] = r1[a];
+        const uint4 s = rc[rc_stats(a)][lid];
+        vw[a] = s.x;
+        wb[part_vt(a)] = make_uint4(s.z, s.w, (uint32_t)__double2loint(rt[a]), (uint32_t)__double2hiint(rt[a]));
         if (kRootSlotsInLds) {
 #pragma unroll
-          for (int q = 0; q < kSlots; ++q) const_cast<uint4*>(rb)[part_slot(a, q)] = rc[rc_slot(a, q)][lid];
+          for (int q = 0; q < kSlots; ++q) wb[part_slot(a, q)] = rc[rc_slot(a, q)][lid];
         }
       }
     }
+    wb[0] = make_uint4(vw[0], vw[1], vw[2], vw[3]);
+    reinterpret_cast<uint32_t*>(wb)[4] = vw[4];
   }
   const bool have = err == 0 && !root_abs && root_blk >= 0;
-  uint4 st[kMaxA], s1s[kMaxA];
+  uint4 st[kMaxA];   // {visits, -, value}
+  double tot[kMaxA];
+  {
+    const uint4* const hb = reinterpret_cast<const uint4*>(an + (int64_t)(have ? root_blk : 0) * blk_bytes);
+    uint4 p0 = make_uint4(0, 0, 0, 0), p1 = p0;
+    if (have && !cached) {
+      p0 = hb[0];
+      p1 = hb[1];
+    }
 #pragma unroll
-  for (int a = 0; a < kMaxA; ++a) {
-    st[a] = make_uint4(0, 0, 0, 0);
-    s1s[a] = st[a];
-    if (have && a < A) {
-      st[a] = cached ? rc[rc_stats(a)][lid]
-                     : reinterpret_cast<const uint4*>(an + (int64_t)root_blk * blk_bytes)[a];
-      s1s[a] = cached ? r1[a]
-                      : reinterpret_cast<const uint4*>(an + (int64_t)root_blk * blk_bytes)[part_stats1(a)];
+    for (int a = 0; a < kMaxA; ++a) {
+      st[a] = make_uint4(0, 0, 0, 0);
+      tot[a] = 0.0;
+      if (have && a < A) {
+        if (cached) {
+          st[a] = rc[rc_stats(a)][lid];
+          tot[a] = rt[a];
+        } else {
+          const uint4 vt = hb[part_vt(a)];
+          st[a] = make_uint4(line_visits(p0, p1, a), 0u, vt.x, vt.y);
+          tot[a] = hilo_d(vt.z, vt.w);
+        }
+      }
     }
   }
   // _final_action_selection (mcts.py:565-600) ends get_action; a search split
@@ -830,12 +902,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
 #pragma unroll
   for (int a = 0; a < kMaxA; ++a) {
     if (a >= A) continue;
-    const double va = hilo_d(st[a].z, st[a].w), tot = hilo_d(s1s[a].x, s1s[a].y);
+    const double va = hilo_d(st[a].z, st[a].w);
     so->child_visits[a] = (int)st[a].x;
     so->child_values[a] = va;
-    so->child_totals[a] = tot;
+    so->child_totals[a] = tot[a];
     xr[2 * a] = (double)st[a].x;
-    xr[2 * a + 1] = tot;
+    xr[2 * a + 1] = tot[a];
   }
   xr[2 * A + 0] = (double)sims;
   xr[2 * A + 1] = (double)root_visits;

@@ -14,8 +14,8 @@
 //     arena at the start, written back at the end), so a tree level is a few
 //     LDS reads; blocks beyond the LDS pool stay in HBM (a uniform branch per
 //     access), so any tree size runs, the overflowing part at HBM speed;
-//   * lane 8a + q holds part q of action a's 128 B line (q = 0 statistics
-//     {visits, value}, 1 {total, agg}, 2..7 the six inline child slots): one
+//   * lane 8a + q holds part q of action a's 128 B LDS line (q = 0 statistics
+//     {visits, -, value}, 1 {total, -}, 2..7 the six inline child slots): one
 //     LDS read per lane gives the selection its statistics and every action's
 //     child slots at once;
 //   * lane group a (8 lanes) runs the generative step and the observation key
@@ -30,15 +30,19 @@
 //   * RNG (philox.h): a page of 64 Philox blocks per stream in VGPRs (lane l:
 //     block page*64 + l), refilled every 256 draws; a draw is one readlane;
 //   * loads one simulation ahead: the next belief particle (belief.py:55: its
-//     index depends only on the belief stream) and math.log of the root's next
-//     visit count; math.log(N) of every candidate child is loaded as soon as
-//     the child lookup has found it, a level before the selection there uses it;
+//     index depends only on the belief stream); a node's visits and the
+//     math.log(N) of its next arrival sit beside its LDS block (nl_n, nl_v;
+//     the node line's bytes 20..31 in HBM), the log loaded during a level and
+//     stored one level later;
 //   * particle-log records (mcts.py:371) go to a per-tree scratch log (no
 //     atomics); k_log_merge then appends every tree's records to the search
 //     waves' shared logs (pomcp_device.h WaveLog) in tree order, so re-root,
 //     extraction and compaction read the same log as after k_search.
-// Block layout in LDS: [block][action] 128 B lines {stats0, stats1, slots 0..5};
-// in HBM the (A + 1)-line layout of pomcp_device.h (staged by part).
+// Block layout in LDS: [block][action] 128 B lines {stats, total, slots 0..5}
+// plus the node's {N, log N}; in HBM the (A + 1)-line layout of
+// pomcp_device.h, converted part by part when staged in and written back.
+// Child slots are rewritten on every arrival here (their visits are used only
+// while the child has no block, as in k_search).
 #pragma clang fp contract(off)
 
 namespace pb {
@@ -88,8 +92,8 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
   __shared__ uint4 path[(kMaxPath + 1) * 3];
   __shared__ double dpw[kLdsDpow];
   __shared__ uint4 bel[kLdsBelief];
-  // math.log(N) per LDS block, prefetched at a node's arrival for its next
-  // arrival (its visits then are N): nl_n[b] = N, nl_v[b] = math.log(N)
+  // the node of LDS block b: nl_n[b] = N of its next arrival (its visits + 1),
+  // nl_v[b] = math.log(N) (pomcp_device.h node line bytes 20..31)
   __shared__ double nl_v[C];
   __shared__ int32_t nl_n[C];
   stage_model(p.model, sm);
@@ -99,15 +103,37 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
   const int ql = lane & 7;                             // part of the action's line
   char* const an = reinterpret_cast<char*>(p.an + tree_base_lines(tree, p.Nb, A));
   const int64_t blk_bytes = blk_stride_lines(A) * 128;
-  auto hpart = [&](int b, int a, int q) -> uint4* {
-    return reinterpret_cast<uint4*>(an + (int64_t)b * blk_bytes) + (q == 0 ? a : kLine * (1 + a) + q - 1);
+  auto hblk = [&](int b) -> uint4* { return reinterpret_cast<uint4*>(an + (int64_t)b * blk_bytes); };
+  // part q of action a's LDS line <-> the HBM block (pomcp_device.h)
+  auto hld = [&](int b, int a, int q) -> uint4 {
+    uint4* const x = hblk(b);
+    if (q >= 2) return x[part_slot(a, q - 2)];
+    const uint4 vt = x[part_vt(a)];
+    return q == 0 ? make_uint4(reinterpret_cast<const uint32_t*>(x)[a], 0u, vt.x, vt.y)
+                  : make_uint4(vt.z, vt.w, 0u, 0u);
+  };
+  auto hst = [&](int b, int a, int q, uint4 v) {
+    uint4* const x = hblk(b);
+    if (q >= 2) {
+      x[part_slot(a, q - 2)] = v;
+    } else if (q == 0) {
+      reinterpret_cast<uint32_t*>(x)[a] = v.x;
+      reinterpret_cast<uint2*>(x + part_vt(a))[0] = make_uint2(v.z, v.w);
+    } else {
+      reinterpret_cast<uint2*>(x + part_vt(a))[1] = make_uint2(v.x, v.y);
+    }
+  };
+  auto hnode_st = [&](int b, int n, double lg) {   // the node's {visits, log(visits + 1)}
+    uint32_t* const w = reinterpret_cast<uint32_t*>(hblk(b));
+    w[kNodeVisByte / 4] = (uint32_t)n;
+    reinterpret_cast<double*>(w)[kNodeLogByte / 8] = lg;
   };
   auto lpart = [&](int b, int a, int q) -> uint4* { return &pool[(b * A + a) * 8 + q]; };
   // b is wave-uniform: the LDS / HBM choice is a scalar branch
-  auto ldp = [&](int b, int a, int q) -> uint4 { return b < C ? *lpart(b, a, q) : *hpart(b, a, q); };
+  auto ldp = [&](int b, int a, int q) -> uint4 { return b < C ? *lpart(b, a, q) : hld(b, a, q); };
   auto stp = [&](int b, int a, int q, uint4 v) {   // call from one lane
     if (b < C) *lpart(b, a, q) = v;
-    else *hpart(b, a, q) = v;
+    else hst(b, a, q, v);
   };
 
   const TreeHdr* const h = p.hdr + tree;
@@ -153,32 +179,39 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
     const int a = lane >> 3, q = lane & 7;
     int b = 0;
     for (; b + 4 <= nstage; b += 4) {
-      const uint4 x0 = *hpart(b, a, q), x1 = *hpart(b + 1, a, q), x2 = *hpart(b + 2, a, q),
-                  x3 = *hpart(b + 3, a, q);
+      const uint4 x0 = hld(b, a, q), x1 = hld(b + 1, a, q), x2 = hld(b + 2, a, q),
+                  x3 = hld(b + 3, a, q);
       *lpart(b, a, q) = x0;
       *lpart(b + 1, a, q) = x1;
       *lpart(b + 2, a, q) = x2;
       *lpart(b + 3, a, q) = x3;
     }
-    for (; b < nstage; ++b) *lpart(b, a, q) = *hpart(b, a, q);
+    for (; b < nstage; ++b) *lpart(b, a, q) = hld(b, a, q);
+  }
+  for (int b = lane; b < nstage; b += kWave) {
+    const uint4 x = hblk(b)[1];
+    nl_n[b] = (int)x.y + 1;
+    nl_v[b] = hilo_d(x.z, x.w);
   }
   const int ndp = p.dpow_n < kLdsDpow ? p.dpow_n : kLdsDpow;
   for (int i = lane; i < ndp; i += kWave) dpw[i] = p.dpow[i];
   const bool bel_lds = bsize <= kLdsBelief;
   if (bel_lds)
     for (int i = lane; i < bsize; i += kWave) bel[i] = rbel[i];
-  for (int i = lane; i < C; i += kWave) nl_n[i] = -1;
   __syncthreads();
   auto dpow = [&](int k) { return k < kLdsDpow ? dpw[k] : p.dpow[k]; };
   auto logtab = [&](int n) { return p.logtab[n < p.logtab_n ? n : 0]; };
+  // math.log(n) from the host table, waited for (volatile: not speculated)
+  auto logtab_now = [&](int n) {
+    return *reinterpret_cast<const volatile double*>(p.logtab + (n < p.logtab_n ? n : 0));
+  };
   auto particle = [&](uint32_t i) { return bel_lds ? bel[i] : rbel[i]; };
-  // math.log(n) of node block b: the LDS cache, else the host table (a wait;
-  // volatile so that the compiler does not issue the load on a cache hit too)
-  auto node_log = [&](int b, int n) {
+  // the root's math.log(n): block b's entry when it holds n (the previous
+  // simulation left it there), else the host table
+  auto root_log = [&](int b, int n) {
     const int bc = b < C ? b : 0;
     double x = nl_v[bc];
-    if (!(b < C && nl_n[bc] == n))
-      x = *reinterpret_cast<const volatile double*>(p.logtab + (n < p.logtab_n ? n : 0));
+    if (!(b < C && nl_n[bc] == n)) x = logtab_now(n);
     return x;
   };
 
@@ -191,6 +224,10 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
     const int b = n_blocks++;
     if (b < C) {
       if (lane < 8 * A) *lpart(b, lane >> 3, lane & 7) = make_uint4(0, 0, 0, 0);
+      if (lane == 0) {   // a node with no visits: N = 1, log(1) = 0
+        nl_n[b] = 1;
+        nl_v[b] = 0.0;
+      }
     } else if (lane < blk_parts(A)) {
       reinterpret_cast<uint4*>(an + (int64_t)b * blk_bytes)[lane] = make_uint4(0, 0, 0, 0);
     }
@@ -212,16 +249,32 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
   if (num_sims <= 0) run = false;
   uint4 pf = make_uint4(0, 0, 0, 0);
   if (run) pf = particle(d_belief((uint32_t)bsize));   // the first simulation's particle
-  // the pending log(N) prefetch of the previous level's node (written to the
-  // cache one level later, when the load has landed)
+  // the pending node update of the previous level's node, or of the leaf just
+  // expanded: N of its next arrival and math.log(N), stored one level later,
+  // when the log load has landed
   int pend_b = -1, pend_n = 0;
   double pend_v = 0.0;
   auto pend_flush = [&]() {
-    if (pend_b >= 0 && pend_b < C && lane == 0) {
-      nl_v[pend_b] = pend_v;
-      nl_n[pend_b] = pend_n;
+    if (pend_b >= 0 && lane == 0) {
+      if (pend_b < C) {
+        nl_v[pend_b] = pend_v;
+        nl_n[pend_b] = pend_n;
+      } else {
+        hnode_st(pend_b, pend_n - 1, pend_v);
+      }
     }
     pend_b = -1;
+  };
+  // the N of a node's arrival and math.log(N) (wave-uniform block)
+  auto node_n = [&](int b, int* n, double* lg) {
+    if (b < C) {
+      *n = nl_n[b];
+      *lg = nl_v[b];
+    } else {
+      const uint4 x = hblk(b)[1];
+      *n = (int)x.y + 1;
+      *lg = hilo_d(x.z, x.w);
+    }
   };
 
   // Overflow children (beyond the inline slots) of action node ani: wave-uniform.
@@ -292,6 +345,7 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
     uint32_t s0 = pr.y, s1 = pr.z;
     int depth = 0, plen = 0;
     int blk = root_blk, nv = root_visits;
+    double lg = root_log(root_blk, root_visits);   // math.log(nv), mcts.py:534
     double ret = 0.0;
     int phase = (0 > p.depth_limit || t > p.step_limit) ? TP_BACKUP : TP_LEVEL;   // mcts.py:315
     PT_MARK(0);
@@ -301,8 +355,8 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
     int k = 0, rdepth = 0;
     // -------------------------------------------------- the tree levels
     while (phase == TP_LEVEL) {
-      const double log_n = node_log(blk, nv);              // math.log(visits), mcts.py:534
-      const uint32_t j = d_model(2);                       // drawn before the selection:
+      const double log_n = lg;
+      const uint32_t j = d_model(2);                     // drawn before the selection:
       const uint32_t ao = d_act(p.other, (uint32_t)A);     // independent streams
       PT_MARK(1);
       const uint4 v = ldp(blk, al, ql);                    // part ql of action al's line
@@ -386,7 +440,7 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
       pend_b = blk;
       pend_n = nv + 1;
       // the chosen action's results, out of its lane group (lane g: action a's
-      // step and statistics, g + 1 its {total, agg}, g + 2 + k its child slot k)
+      // step and statistics, g + 1 its total, g + 2 + k its child slot k)
       a = uni(a);   // wave-uniform (selects of uniform values end up in VGPRs)
       const int g = 8 * a;
       const uint32_t c0 = rlu(n0, g), c1 = rlu(n1, g);
@@ -425,6 +479,16 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
         cvis = o.cvis;
         lptr = o.cptr;
       }
+      if (cblk >= 0 && dn && lane == 0) {   // a done arrival at a child with a block (rare)
+        if (cblk < C) {
+          const int n2 = nl_n[cblk] + 1;
+          nl_n[cblk] = n2;
+          nl_v[cblk] = logtab_now(n2);
+        } else {
+          const uint4 x = hblk(cblk)[1];
+          hnode_st(cblk, (int)x.y + 1, logtab_now((int)x.y + 2));
+        }
+      }
       PT_MARK(6);
       if (err != 0 || n_log >= p.Np || plen > kMaxPath) {
         if (err == 0) err = POMCP_E_ARENA;
@@ -439,8 +503,8 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
         rb_v1 = mine ? c1 : rb_v1;
       }
       ++rb_n;
-      // the path entry, written by the lanes that hold it: {stats0, stats1} of
-      // action a as they were, {block << 3 | a | done << 31, r}
+      // the path entry, written by the lanes that hold it: {visits, -, value}
+      // and {total, -} of action a as they were, {block << 3 | a | done << 31, r}
       if (lane == g || lane == g + 1) {
         path[3 * plen + (lane - g)] = v;
         if (lane == g)
@@ -473,12 +537,16 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
         } else if (lane == 0) {
           *lptr = b;
         }
+        pend_flush();   // the leaf's own visits (cvis) and log(cvis + 1)
+        pend_v = logtab(cvis + 1);
+        pend_b = b;
+        pend_n = cvis + 1;
         k = 0;
         rdepth = depth;   // the rollout's own depth counter (mcts.py:449)
         phase = TP_ROLL;
       } else {
         blk = cblk;   // the next level
-        nv = cvis;
+        node_n(cblk, &nv, &lg);
       }
       PT_MARK(7);
       __builtin_amdgcn_wave_barrier();   // keep lane 0's LDS stores before the next reads
@@ -520,7 +588,7 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
     __builtin_amdgcn_wave_barrier();
     double gr = ret;
     for (int l = plen - 1; l >= 0; --l) {
-      // {visits, -, value} and {total, agg} before, {block << 3 | a | done << 31, r}
+      // {visits, -, value} and {total, -} before, {block << 3 | a | done << 31, r}
       const uint4 e0 = path[3 * l], e1 = path[3 * l + 1], e2 = path[3 * l + 2];
       const double r = hilo_d(e2.y, e2.z);
       gr = (e2.x >> 31) ? r : r + p.discount * gr;
@@ -529,14 +597,12 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
       const double total = hilo_d(e1.x, e1.y) + gr;
       const double delta = gr - value0;
       const double value = value0 + delta / (double)n;
-      const double agg = hilo_d(e1.z, e1.w) + delta * (gr - value);
       const uint32_t ba = e2.x & 0x7FFFFFFFu;
       if (lane == 0) {
         stp((int)(ba >> 3), (int)(ba & 7u), 0,
             make_uint4((uint32_t)n, 0u, (uint32_t)__double2loint(value), (uint32_t)__double2hiint(value)));
         stp((int)(ba >> 3), (int)(ba & 7u), 1,
-            make_uint4((uint32_t)__double2loint(total), (uint32_t)__double2hiint(total),
-                       (uint32_t)__double2loint(agg), (uint32_t)__double2hiint(agg)));
+            make_uint4((uint32_t)__double2loint(total), (uint32_t)__double2hiint(total), 0u, 0u));
       }
       if (value > mm_max) mm_max = value;   // utils.py:29-32
       if (value < mm_min) mm_min = value;
@@ -567,8 +633,9 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
     const int nback = n_blocks < C ? n_blocks : C;
     if (lane < 8 * A) {
       const int a = lane >> 3, q = lane & 7;
-      for (int b = 0; b < nback; ++b) *hpart(b, a, q) = *lpart(b, a, q);
+      for (int b = 0; b < nback; ++b) hst(b, a, q, *lpart(b, a, q));
     }
+    for (int b = lane; b < nback; b += kWave) hnode_st(b, nl_n[b] - 1, nl_v[b]);
   }
   // _final_action_selection (mcts.py:565-600) ends get_action; a search split
   // over several launches (final_sel = 0 for all but the last) draws it once

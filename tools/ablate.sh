@@ -1,15 +1,15 @@
 #!/bin/bash
 # Ablation builds of k_search (measurement only; results are NOT the reference's):
 # how much of a search the Philox RNG, the FP64 UCB scoring, the belief
-# particle line and the particle-log stores cost.
+# particle line and the particle-log stores cost.  Any other library can be
+# compared too: put it at variants/lib_NAME.so and list NAME in VARIANTS.
 #   tools/ablate.sh build      (here: hipcc the variants into variants/)
 #   tools/ablate.sh run TAG    (GPU box, via gpurun)
 set -o pipefail
 if [ "$1" = build ]; then
   mkdir -p variants
   for v in "base:" "philox3:-DPB_PHILOX_ROUNDS=3" "nosel:-DPOMCP_ABLATE_SELECT" \
-           "nobelief:-DPOMCP_ABLATE_BELIEF" "nolog:-DPOMCP_ABLATE_LOG" \
-           "nostats1:-DPOMCP_ABLATE_STATS1" "nol1w:-DPOMCP_ABLATE_STATS1 -DPOMCP_ABLATE_SLOTW"; do
+           "nobelief:-DPOMCP_ABLATE_BELIEF" "nolog:-DPOMCP_ABLATE_LOG"; do
     n=${v%%:*}; f=${v#*:}
     POMCP_LIB_PATH=$PWD/variants/lib_$n.so POMCP_EXTRA_FLAGS="$f" \
       python -c "import sys; sys.path.insert(0,'posggym-baselines_amd'); from posggym_baselines_amd import build; build.build(force=True)" || exit 1
