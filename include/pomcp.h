@@ -19,8 +19,9 @@
 extern "C" {
 #endif
 
-#define POMCP_ABI_VERSION 3
+#define POMCP_ABI_VERSION 4
 #define POMCP_MAX_ACTIONS 8
+#define POMCP_MAX_TYPE_POLICIES 8
 
 typedef enum pomcp_status {
   POMCP_OK = 0,
@@ -85,7 +86,7 @@ typedef struct pomcp_config {
   double known_min, known_max;
   uint64_t seed;                /* MCTSConfig.seed -> stream key (seed, tree) */
   uint32_t tree_key_base;       /* tree t uses key tree_key_base + t */
-  int32_t pad0;
+  int32_t type_based;           /* 1: POTMMCP's type-based search (pomcp_set_type_policies) */
   /* per-tree arena capacities */
   int64_t max_blocks;           /* expanded obs nodes: A x 128 B action nodes each */
   int64_t max_particles;        /* particle log records (16 B) */
@@ -189,6 +190,43 @@ int pomcp_set_root_belief(pomcp_ctx* ctx, int32_t tree, const uint32_t* particle
 /* Root belief particles of one tree as (t, v0, v1) u32 triples (belief.py:47-64). */
 int pomcp_get_root_belief(pomcp_ctx* ctx, int32_t tree, uint32_t* out, int32_t capacity,
                           int32_t* count);
+
+/* POTMMCP (potmmcp.py:18-301) with non-neural policies: a context created with
+ * pomcp_config.type_based = 1 searches with a meta-policy over the ego's
+ * policies and a mixture over the other agent's policies, every policy a fixed
+ * action distribution (planning/policies.py FixedDistributionPolicy):
+ *   - the root belief's particles carry the other agent's policy, drawn by
+ *     OtherAgentMixturePolicy.sample_initial_state (other_policy.py:178-183);
+ *   - every simulation draws an ego policy from the meta-policy row of its
+ *     particle's other-agent policy (POTMMCPMetaPolicy.sample_policy,
+ *     potmmcp.py:381-389); the ego rolls out with it (potmmcp.py:221-229) and
+ *     the other agent acts by its particle's policy;
+ *   - every obs node keeps ObsNode.action_probs, PUCB's prior (mcts.py:492-527):
+ *     a child created by a simulation starts with that simulation's ego policy
+ *     distribution, a root made by update with `expected_prior`
+ *     (get_expected_action_probs(None, ...), potmmcp.py:391-431), and a node's
+ *     priors move towards the simulation's policy on every arrival at an
+ *     existing child (potmmcp.py:255-264).
+ * Draws follow CPython's random.choices (cumulative weights, bisection).  Must
+ * be called after pomcp_create and before the first update. */
+typedef struct pomcp_type_policies {
+  int32_t num_ego;                 /* POTMMCPMetaPolicy.policies, 1..8 */
+  int32_t num_other;               /* OtherAgentMixturePolicy.policies, 1..8 (dict order) */
+  double ego_pi[POMCP_MAX_TYPE_POLICIES][POMCP_MAX_ACTIONS];     /* get_pi, action order */
+  double other_pi[POMCP_MAX_TYPE_POLICIES][POMCP_MAX_ACTIONS];
+  /* meta_policy[other policy j]: its keys (ego policy indices) and weights in the dict's order */
+  int32_t meta_len[POMCP_MAX_TYPE_POLICIES];
+  int32_t meta_policy[POMCP_MAX_TYPE_POLICIES][POMCP_MAX_TYPE_POLICIES];
+  double meta_weight[POMCP_MAX_TYPE_POLICIES][POMCP_MAX_TYPE_POLICIES];
+  double expected_prior[POMCP_MAX_ACTIONS];
+} pomcp_type_policies;
+int pomcp_set_type_policies(pomcp_ctx* ctx, const pomcp_type_policies* tp);
+
+/* Type-based contexts: the root's ObsNode.action_probs (num_actions doubles) and
+ * its particles' other-agent policy indices (belief order). */
+int pomcp_get_root_prior(pomcp_ctx* ctx, int32_t tree, double* out);
+int pomcp_get_root_policies(pomcp_ctx* ctx, int32_t tree, int32_t* out, int32_t capacity,
+                            int32_t* count);
 
 /* Arena use: the largest block count and particle-log record count over the
  * trees (after the last update's subtree compaction / the last search).  The

@@ -303,3 +303,140 @@ def reference_intmcp_episode(cfg_kwargs, num_sims, env_seed, ego="0", tree=0, ma
     trace = run_episode(step, env_seed, ego=ego, max_steps=max_steps, env=env)
     planner.close()
     return trace, records
+
+
+# ----------------------------------------------------------------- POTMMCP
+def potmmcp_policies(model, agent_id, spec, streams=None):
+    """The non-neural policy set of a POTMMCP case: ``spec`` = {"ego": {id: probs},
+    "other": {id: probs}, "meta": {other id: {ego id: weight}}}.  Returns (ego
+    policies, other-agent policies, meta_policy); a policy samples its actions
+    on its agent's action stream (8 + agent index) when ``streams`` is given."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "posggym-baselines_amd"))
+    from posggym_baselines_amd.planning.policies import FixedDistributionPolicy
+    from oracle.rng import S_ACT_BASE, StreamRandom
+    other = [i for i in model.possible_agents if i != agent_id][0]
+
+    def make(i, pid, probs):
+        rng = StreamRandom(streams, S_ACT_BASE + int(i)) if streams is not None else None
+        return FixedDistributionPolicy(model, i, pid, probs, rng)
+
+    ego_pols = {k: make(agent_id, k, v) for k, v in spec["ego"].items()}
+    oth_pols = {k: make(other, k, v) for k, v in spec["other"].items()}
+    meta = {k: dict(v) for k, v in spec["meta"].items()}
+    return ego_pols, oth_pols, meta
+
+
+def make_reference_potmmcp(model, agent_id, cfg_kwargs, num_sims, streams, spec):
+    """The reference ``POTMMCP`` (potmmcp.py:18-301) with a ``POTMMCPMetaPolicy``
+    over fixed-distribution ego policies and an ``OtherAgentMixturePolicy`` over
+    fixed-distribution other-agent policies, wired to ``streams``: mcts / potmmcp
+    ``random`` -> SELECT stream (``sample_policy``'s ``random.choices`` included),
+    other_policy ``random`` -> MIXTURE stream, planner Random -> BELIEF stream."""
+    P = import_reference()
+    import posggym_baselines.planning.belief as B
+    import posggym_baselines.planning.mcts as mcts_mod
+    import posggym_baselines.planning.other_policy as op_mod
+    import posggym_baselines.planning.potmmcp as pt_mod
+    from oracle.rng import S_BELIEF, S_MIXTURE, S_SELECT, StreamRandom
+
+    select = StreamRandom(streams, S_SELECT)
+    belief_rng = StreamRandom(streams, S_BELIEF)
+    rnd = types.ModuleType("random_shim")
+    rnd.Random = lambda seed=None: belief_rng
+    rnd.choice = select.choice
+    rnd.choices = select.choices
+    rnd.random = select.random
+    mcts_mod.random = rnd
+    pt_mod.random = rnd
+    B.random = rnd
+    mix = types.ModuleType("random_shim_mixture")
+    mix.choice = StreamRandom(streams, S_MIXTURE).choice
+    op_mod.random = mix
+    clock = _FakeClock()
+    mcts_mod.time = clock
+    pt_mod.time = clock
+    from posggym_baselines.planning.utils import KnownBounds
+    kw = dict(cfg_kwargs)
+    if kw.get("known_bounds") is not None:
+        kw["known_bounds"] = KnownBounds(*kw["known_bounds"])
+    config = P.MCTSConfig(**kw)
+    ego_pols, oth_pols, meta = potmmcp_policies(model, agent_id, spec, streams)
+    other = [i for i in model.possible_agents if i != agent_id][0]
+    others = {other: P.OtherAgentMixturePolicy(model, other, oth_pols)}
+    search = P.POTMMCPMetaPolicy(model, agent_id, ego_pols, meta)
+    planner = P.POTMMCP(model, agent_id, config, others, search)
+    inner = planner._simulate
+    count = [0]
+
+    def simulate(hps, obs_node, depth, search_policy):
+        if depth == 0:
+            count[0] += 1
+            if count[0] >= num_sims:
+                clock.now += 1e9
+                count[0] = 0
+        return inner(hps, obs_node, depth, search_policy)
+
+    planner._simulate = simulate
+    return planner
+
+
+def potmmcp_belief_digest(particles, other_ids, pack_words):
+    """sha1 over (t, v0, v1, other-agent policy index) u32 quadruples, insertion order."""
+    import hashlib
+    import struct
+    h = hashlib.sha1()
+    for st, t, pid in particles:
+        v0, v1 = pack_words(st)
+        h.update(struct.pack("<IIII", t, v0, v1, other_ids.index(pid)))
+    return h.hexdigest()
+
+
+def reference_potmmcp_record(planner, searched, action):
+    from oracle.episode import fhex
+    rec = {"searched": searched, "action": int(action)}
+    if not searched:
+        return rec
+    root = planner.root
+    other = [i for i in planner.model.possible_agents if i != planner.agent_id][0]
+    oth_ids = list(planner.other_agent_policies[other].policies)
+    parts = [(p.state, p.t, p.policy_state[other]["policy_id"]) for p in root.belief.particles]
+    st = planner.step_statistics
+    rec["belief_size"] = len(parts)
+    rec["belief_digest"] = potmmcp_belief_digest(parts, oth_ids, planner.model.pack_words)
+    rec["num_sims"] = int(st["num_sims"])
+    rec["prior"] = [fhex(root.action_probs[a]) for a in range(len(root.action_probs))]
+    if rec["num_sims"] > 0:
+        kids = root.get_child_nodes()
+        rec["search_depth"] = int(st["search_depth"])
+        rec["root_visits"] = int(root.visits)
+        rec["child_visits"] = [int(c.visits) for c in kids]
+        rec["child_values"] = [fhex(c.value) for c in kids]
+        rec["child_totals"] = [fhex(c.total_value) for c in kids]
+        rec["min_value"] = fhex(st["min_value"])
+        rec["max_value"] = fhex(st["max_value"])
+    return rec
+
+
+def reference_potmmcp_episode(cfg_kwargs, num_sims, env_seed, spec, ego="0", tree=0,
+                              max_steps=50, env="Driving-v1"):
+    """One full episode with the real reference POTMMCP. Returns (trace, records)."""
+    from oracle.envs import make_model
+    from oracle.episode import run_episode
+    from oracle.rng import Streams
+
+    streams = Streams(cfg_kwargs.get("seed") or 0, tree)
+    model = make_model(env, streams)
+    planner = make_reference_potmmcp(model, ego, cfg_kwargs, num_sims, streams, spec)
+    planner.reset()
+    records = []
+
+    def step(obs):
+        searched = not planner.root.is_absorbing
+        a = planner.step(obs)
+        records.append(reference_potmmcp_record(planner, searched, a))
+        return a
+
+    trace = run_episode(step, env_seed, ego=ego, max_steps=max_steps, env=env)
+    planner.close()
+    return trace, records

@@ -22,6 +22,7 @@ _W0, _W1 = 0x9E3779B9, 0xBB67AE85
 S_BELIEF = 0        # planner random.Random(seed): belief.sample(), rejection sampling
 S_SELECT = 1        # global `random` module: UCB/PUCB N==0 draws, final tie-breaks
 S_MODEL = 2         # generative model RNG (initial state sampling, exec-order shuffle)
+S_MIXTURE = 4       # other_policy.py `random`: OtherAgentMixturePolicy.sample_initial_state
 S_ACT_BASE = 8      # Discrete(n).sample() of agent i's action space: stream 8 + i
 S_ENV_MODEL = 32    # harness: the "real" environment's model RNG
 S_ENV_POLICY_BASE = 40  # harness: true (non-planning) agent i's random policy: 40 + i

@@ -23,6 +23,7 @@ enum Stream : uint32_t {
   S_SELECT = 1,   // global `random`: UCB/PUCB N==0, final tie-breaks
   S_MODEL = 2,    // model RNG: initial state sampling, execution-order shuffle
   S_BELIEF_NESTED = 3,  // I-NTMCP level-0 planner's random.Random(seed) (intmcp.py:66)
+  S_MIXTURE = 4,  // other_policy.py `random`: OtherAgentMixturePolicy's policy draw (POTMMCP)
   S_ACT_BASE = 8, // Discrete.sample() of agent i: 8 + i
   S_ENV_MODEL = 32,
   S_ENV_POLICY_BASE = 40,

@@ -47,6 +47,8 @@ struct pomcp_ctx {
   double* gather = nullptr;              // [gather_world][B][R] pomcp_root_gather_buffer
   int gather_world = 0;
   int search_kind = POMCP_SEARCH_AUTO;
+  TmTables host_tm{};                    // type-based contexts (pomcp_set_type_policies)
+  bool tm_set = false;
 };
 
 // Wave-per-tree search (k_search_lds) for batches up to this many trees: one
@@ -154,7 +156,9 @@ static int validate(const pomcp_config* c, std::string* why) {
   if (c->depth_limit < 0 || c->step_limit < 0) return bad("depth/step limit");
   if (c->num_particles < 1 || c->extra_particles < 0) return bad("num_particles");
   if (c->num_trees < 1) return bad("num_trees >= 1");
-  if (c->max_blocks < 1 || c->max_blocks * (c->num_actions + 1) * 128 > INT32_MAX) return bad("max_blocks");
+  if (c->type_based != 0 && c->type_based != 1) return bad("type_based is 0 or 1");
+  if (c->max_blocks < 1 || c->max_blocks * blk_lines(c->num_actions, c->type_based) * 128 > INT32_MAX)
+    return bad("max_blocks");
   if (c->num_actions < 2 || c->num_actions > kMaxA) { *why = "the search kernel supports 2 to 5 actions"; return POMCP_E_UNSUPPORTED; }
   if (c->max_particles < 1 || c->max_particles * kWave > UINT32_MAX) return bad("max_particles");
   if (c->max_blocks * c->num_actions * kSlots + 1 + c->overflow_slots >= (int64_t)kIdMask)
@@ -241,6 +245,8 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
   d.bucket_mask = (uint32_t)(c.overflow_slots / kBucket - 1);
   d.ovf_base = (uint32_t)(c.max_blocks * c.num_actions * kSlots + 1);
   d.islots = kSlots;
+  d.tm = c.type_based;
+  d.lines = blk_lines(d.A, d.tm);
   const int64_t B = c.num_trees;
   void* p;
 #define ALLOC(field, type, count)                                               \
@@ -252,9 +258,11 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
     d.field = reinterpret_cast<decltype(d.field)>(p);                           \
   } while (0)
   ALLOC(hdr, TreeHdr, B);
-  ALLOC(an, Line, arena_lines((int)B, d.Nb, d.A));   // interleaved by search wave
+  ALLOC(an, Line, arena_lines((int)B, d.Nb, d.lines));   // interleaved by search wave
   ALLOC(ovf, OvfSlot, B * d.H);
-  ALLOC(plog, LogRec, (int64_t)search_waves((int)B) * kWave * d.Np);
+  // pomcp_device.h WaveLog: 3 u32 arrays per search wave (+ aux when type-based)
+  ALLOC(plog, uint32_t, (int64_t)search_waves((int)B) * kWave * d.Np * (3 + d.tm));
+  if (d.tm) ALLOC(tmt, TmTables, 1);
   ALLOC(wlog, uint32_t, search_waves((int)B));
   ALLOC(want, uint32_t, B);
   ALLOC(cnt, int32_t, B);
@@ -382,6 +390,7 @@ static int ensure_compaction_scratch(pomcp_ctx* ctx) {
 int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_keys,
                  int32_t* root_absorbing_out) {
   if (!ctx || !obs_keys) return POMCP_E_INVALID;
+  if (ctx->dp.tm && !ctx->tm_set) return fail(ctx, POMCP_E_STATE, "update: pomcp_set_type_policies first");
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   const int B = ctx->dp.B;
   std::vector<int32_t> acts((size_t)B, -1);
@@ -425,6 +434,7 @@ static bool wave_search_fits(const pomcp_ctx* ctx) {
 }
 
 static int resolve_search_kind(const pomcp_ctx* ctx) {
+  if (ctx->dp.tm) return POMCP_SEARCH_LANE;   // the type-based search is k_search<..., TM = 1>
   if (ctx->search_kind == POMCP_SEARCH_WAVE) return POMCP_SEARCH_WAVE;
   if (ctx->search_kind == POMCP_SEARCH_LANE) return POMCP_SEARCH_LANE;
   return ctx->dp.B <= kWaveSearchMaxTrees && wave_search_fits(ctx) ? POMCP_SEARCH_WAVE
@@ -435,6 +445,8 @@ int pomcp_set_search_kernel(pomcp_ctx* ctx, int32_t kind) {
   if (!ctx || kind < POMCP_SEARCH_AUTO || kind > POMCP_SEARCH_WAVE) return POMCP_E_INVALID;
   if (kind == POMCP_SEARCH_WAVE && !wave_search_fits(ctx))
     return fail(ctx, POMCP_E_UNSUPPORTED, "set_search_kernel: wave search scratch too large");
+  if (kind == POMCP_SEARCH_WAVE && ctx->dp.tm)
+    return fail(ctx, POMCP_E_UNSUPPORTED, "set_search_kernel: the type-based search is lane-per-tree");
   ctx->search_kind = kind;
   return POMCP_OK;
 }
@@ -468,22 +480,26 @@ static int launch_search_wave(pomcp_ctx* ctx, int32_t num_sims, int final_sel) {
 
 static int launch_search(pomcp_ctx* ctx, int32_t num_sims, int final_sel) {
   if (!ctx || num_sims < 0) return POMCP_E_INVALID;
+  if (ctx->dp.tm && !ctx->tm_set) return fail(ctx, POMCP_E_STATE, "search: pomcp_set_type_policies first");
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   if (resolve_search_kind(ctx) == POMCP_SEARCH_WAVE) return launch_search_wave(ctx, num_sims, final_sel);
-  const int tpb = search_tpb(ctx->dp.B);
+  const int tpb = ctx->dp.tm ? kTPBSmall : search_tpb(ctx->dp.B);
   const dim3 grid((unsigned)((ctx->dp.B + tpb - 1) / tpb)), block((unsigned)tpb);
   // kernel per (environment, selection rule, workgroup size); the action count is the model's
   using KFn = void (*)(DevParams, int, int);
-#define PB_SEARCH_ROW(T)                                                                          \
-  {{k_search<EnvDriving, POMCP_SEL_PUCB, 5, T>, k_search<EnvDriving, POMCP_SEL_UCB, 5, T>,        \
-    k_search<EnvDriving, POMCP_SEL_UNIFORM, 5, T>},                                               \
-   {k_search<EnvPursuitEvasion, POMCP_SEL_PUCB, 4, T>, k_search<EnvPursuitEvasion, POMCP_SEL_UCB, 4, T>, \
-    k_search<EnvPursuitEvasion, POMCP_SEL_UNIFORM, 4, T>}}
-  static const KFn table[2][2][3] = {PB_SEARCH_ROW(kTPB), PB_SEARCH_ROW(kTPBSmall)};
+#define PB_SEARCH_ROW(T, TM)                                                                      \
+  {{k_search<EnvDriving, POMCP_SEL_PUCB, 5, T, TM>, k_search<EnvDriving, POMCP_SEL_UCB, 5, T, TM>, \
+    k_search<EnvDriving, POMCP_SEL_UNIFORM, 5, T, TM>},                                           \
+   {k_search<EnvPursuitEvasion, POMCP_SEL_PUCB, 4, T, TM>,                                        \
+    k_search<EnvPursuitEvasion, POMCP_SEL_UCB, 4, T, TM>,                                         \
+    k_search<EnvPursuitEvasion, POMCP_SEL_UNIFORM, 4, T, TM>}}
+  static const KFn table[3][2][3] = {PB_SEARCH_ROW(kTPB, 0), PB_SEARCH_ROW(kTPBSmall, 0),
+                                     PB_SEARCH_ROW(kTPBSmall, 1)};
 #undef PB_SEARCH_ROW
   const int e = ctx->dp.env == POMCP_ENV_PURSUIT_EVASION ? 1 : 0;
-  hipLaunchKernelGGL(table[tpb == kTPB ? 0 : 1][e][ctx->dp.sel], grid, block, 0, ctx->stream,
-                     ctx->dp, (int)num_sims, final_sel);
+  const int row = ctx->dp.tm ? 2 : (tpb == kTPB ? 0 : 1);
+  hipLaunchKernelGGL(table[row][e][ctx->dp.sel], grid, block, 0, ctx->stream, ctx->dp,
+                     (int)num_sims, final_sel);
   HIP_TRY(ctx, hipGetLastError());
   return POMCP_OK;
 }
@@ -517,6 +533,8 @@ int pomcp_get_root_stats(pomcp_ctx* ctx, pomcp_root_stats* out) {
 int pomcp_set_root_belief(pomcp_ctx* ctx, int32_t tree, const uint32_t* particles, int32_t count) {
   if (!ctx || tree < 0 || tree >= ctx->dp.B || count < 1 || !particles)
     return fail(ctx, POMCP_E_INVALID, "set_root_belief: bad arguments");
+  if (ctx->dp.tm)
+    return fail(ctx, POMCP_E_UNSUPPORTED, "set_root_belief: type-based particles carry a policy");
   if (count > ctx->dp.Nr) return fail(ctx, POMCP_E_ARENA, "set_root_belief: more particles than max_belief");
   const uint32_t t = particles[0];
   for (int32_t i = 0; i < count; ++i)
@@ -573,6 +591,102 @@ int pomcp_get_root_belief(pomcp_ctx* ctx, int32_t tree, uint32_t* out, int32_t c
     out[3 * i + 1] = tmp[i].y;
     out[3 * i + 2] = tmp[i].z;
   }
+  return POMCP_OK;
+}
+
+int pomcp_set_type_policies(pomcp_ctx* ctx, const pomcp_type_policies* tp) {
+  if (!ctx || !tp) return POMCP_E_INVALID;
+  if (!ctx->dp.tm) return fail(ctx, POMCP_E_STATE, "set_type_policies: context is not type_based");
+  const int A = ctx->dp.A, ne = tp->num_ego, no = tp->num_other;
+  if (ne < 1 || ne > kTmMax || no < 1 || no > kTmMax)
+    return fail(ctx, POMCP_E_INVALID, "set_type_policies: 1..8 ego and other-agent policies");
+  TmTables t{};
+  t.n_ego = ne;
+  t.n_other = no;
+  // random.choices' cumulative weights (itertools.accumulate) and total = cum[-1] + 0.0
+  auto cum = [](const double* w, int n, double* c, double* total) {
+    double acc = 0.0;
+    for (int i = 0; i < n; ++i) {
+      acc = i == 0 ? w[i] : acc + w[i];
+      c[i] = acc;
+    }
+    *total = acc + 0.0;
+  };
+  for (int a = 0; a < A; ++a) t.prior[0][a] = tp->expected_prior[a];
+  for (int k = 0; k < ne; ++k) {
+    for (int a = 0; a < A; ++a) {
+      if (!(tp->ego_pi[k][a] >= 0.0)) return fail(ctx, POMCP_E_INVALID, "set_type_policies: ego_pi < 0");
+      t.prior[k + 1][a] = tp->ego_pi[k][a];
+    }
+    cum(tp->ego_pi[k], A, t.ego_cum[k], &t.ego_tot[k]);
+    if (!(t.ego_tot[k] > 0.0)) return fail(ctx, POMCP_E_INVALID, "set_type_policies: ego_pi sums to 0");
+  }
+  for (int j = 0; j < no; ++j) {
+    for (int a = 0; a < A; ++a)
+      if (!(tp->other_pi[j][a] >= 0.0)) return fail(ctx, POMCP_E_INVALID, "set_type_policies: other_pi < 0");
+    cum(tp->other_pi[j], A, t.oth_cum[j], &t.oth_tot[j]);
+    if (!(t.oth_tot[j] > 0.0)) return fail(ctx, POMCP_E_INVALID, "set_type_policies: other_pi sums to 0");
+    const int m = tp->meta_len[j];
+    if (m < 1 || m > kTmMax) return fail(ctx, POMCP_E_INVALID, "set_type_policies: meta_len 1..8");
+    t.meta_len[j] = m;
+    for (int i = 0; i < m; ++i) {
+      const int k = tp->meta_policy[j][i];
+      if (k < 0 || k >= ne) return fail(ctx, POMCP_E_INVALID, "set_type_policies: meta_policy index");
+      t.meta_idx[j][i] = k;
+    }
+    cum(tp->meta_weight[j], m, t.meta_cum[j], &t.meta_tot[j]);
+  }
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  ctx->host_tm = t;
+  HIP_TRY(ctx, hipMemcpyAsync(const_cast<TmTables*>(ctx->dp.tmt), &ctx->host_tm, sizeof(TmTables),
+                              hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->tm_set = true;
+  return POMCP_OK;
+}
+
+int pomcp_get_root_prior(pomcp_ctx* ctx, int32_t tree, double* out) {
+  if (!ctx || !out || tree < 0 || tree >= ctx->dp.B) return POMCP_E_INVALID;
+  if (!ctx->dp.tm) return fail(ctx, POMCP_E_STATE, "get_root_prior: context is not type_based");
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  TreeHdr h;
+  HIP_TRY(ctx, hipMemcpyAsync(&h, ctx->dp.hdr + tree, sizeof(TreeHdr), hipMemcpyDeviceToHost,
+                              ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  const int A = ctx->dp.A;
+  if (h.root_blk < 0) {   // no block yet: the prior its code names
+    const int code = h.root_code >= 0 && h.root_code <= kTmMax ? h.root_code : 0;
+    for (int a = 0; a < A; ++a) out[a] = ctx->host_tm.prior[code][a];
+    return POMCP_OK;
+  }
+  const Line* blk = ctx->dp.an + tree_base_lines(tree, ctx->dp.Nb, ctx->dp.lines) +
+                    (int64_t)h.root_blk * blk_stride_lines(ctx->dp.lines);
+  HIP_TRY(ctx, hipMemcpyAsync(out, reinterpret_cast<const uint4*>(blk) + part_prior(A),
+                              sizeof(double) * A, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return POMCP_OK;
+}
+
+int pomcp_get_root_policies(pomcp_ctx* ctx, int32_t tree, int32_t* out, int32_t capacity,
+                            int32_t* count) {
+  if (!ctx || !count || tree < 0 || tree >= ctx->dp.B) return POMCP_E_INVALID;
+  if (!ctx->dp.tm) return fail(ctx, POMCP_E_STATE, "get_root_policies: context is not type_based");
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  TreeHdr h;
+  HIP_TRY(ctx, hipMemcpyAsync(&h, ctx->dp.hdr + tree, sizeof(TreeHdr), hipMemcpyDeviceToHost,
+                              ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  *count = h.belief_size;
+  if (!out || capacity <= 0) return POMCP_OK;
+  const int n = h.belief_size < capacity ? h.belief_size : capacity;
+  std::vector<uint4> tmp((size_t)n);
+  const uint4* src = ctx->dp.belief + (int64_t)tree * 2 * ctx->dp.Nr + (int64_t)h.belief_sel * ctx->dp.Nr;
+  if (n > 0) {
+    HIP_TRY(ctx, hipMemcpyAsync(tmp.data(), src, sizeof(uint4) * n, hipMemcpyDeviceToHost,
+                                ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  for (int i = 0; i < n; ++i) out[i] = (int32_t)tmp[i].w;
   return POMCP_OK;
 }
 

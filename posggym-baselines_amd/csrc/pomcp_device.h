@@ -79,16 +79,20 @@ struct LogRec {
 // v0[cap] then v1[cap] (cap = 64 Np records), so an append of the wave's
 // records is three fully coalesced dword stores instead of one 12 B-strided
 // store (+1% measured; the log's cost is its bytes: without any log store
-// the search runs 12% faster, tools/ablate.sh).
+// the search runs 12% faster, tools/ablate.sh).  A type-based context
+// (POTMMCP, pomcp_set_type_policies) adds aux[cap]: the particle's
+// other-agent policy index (HistoryPolicyState.policy_state, potmmcp.py:83-98).
 struct WaveLog {
   uint32_t* id;
   uint32_t* v0;
   uint32_t* v1;
-  __device__ __forceinline__ WaveLog(LogRec* plog, int64_t Np, int64_t wave) {
+  uint32_t* aux;   // null unless type-based
+  __device__ __forceinline__ WaveLog(LogRec* plog, int64_t Np, int64_t wave, int tm = 0) {
     const int64_t cap = (int64_t)64 * Np;
-    id = reinterpret_cast<uint32_t*>(plog) + wave * 3 * cap;
+    id = reinterpret_cast<uint32_t*>(plog) + wave * (3 + tm) * cap;
     v0 = id + cap;
     v1 = v0 + cap;
+    aux = tm ? v1 + cap : nullptr;
   }
   __device__ __forceinline__ LogRec load(int64_t i) const { return LogRec{id[i], v0[i], v1[i]}; }
   __device__ __forceinline__ void store(int64_t i, const LogRec& r) const {
@@ -101,26 +105,62 @@ struct WaveLog {
 struct alignas(16) Line {   // allocation unit of the block arena
   uint4 part[kLine];
 };
-__host__ __device__ constexpr int blk_lines(int A) { return A + 1; }
-__host__ __device__ constexpr int blk_parts(int A) { return kLine * (A + 1); }
+// Lines per block: the node line + one per action, + the prior line of a
+// type-based context (POTMMCP: ObsNode.action_probs, A doubles at line A + 1).
+__host__ __device__ constexpr int blk_lines(int A, int tm = 0) { return A + 1 + tm; }
+__host__ __device__ constexpr int blk_parts(int L) { return kLine * L; }   // L: lines per block
 __host__ __device__ constexpr int part_slot(int a, int k) { return kLine * (1 + a) + 1 + k; }
+__host__ __device__ constexpr int part_prior(int A) { return kLine * (A + 1); }
 
 // The block arena is interleaved by search wave ([wave][block][lane] of
-// (A + 1)-line blocks): block b of tree t starts at line
-//   ((t / 64 * Nb + b) * 64 + t % 64) * (A + 1)
+// L-line blocks, L = blk_lines): block b of tree t starts at line
+//   ((t / 64 * Nb + b) * 64 + t % 64) * L
 // so the 64 trees of a k_search wave (one per lane) keep their blocks in one
 // contiguous region whose size follows the blocks in use, not Nb.  With a
 // per-tree layout a wave's accesses spread over 64 regions of Nb blocks each
 // and the address translation caches thrash (tools/ubench).
-// A block is still one contiguous (A + 1) x 128 B piece (coalesced loads of
-// the wave-per-tree kernels are unchanged); consecutive blocks of one tree
-// are blk_stride_lines(A) apart.
-__host__ __device__ inline int64_t tree_base_lines(int t, int64_t Nb, int A) {
-  return ((int64_t)(t / kWave) * Nb * kWave + (t % kWave)) * blk_lines(A);
+// A block is still one contiguous L x 128 B piece (coalesced loads of the
+// wave-per-tree kernels are unchanged); consecutive blocks of one tree are
+// blk_stride_lines(L) apart.
+__host__ __device__ inline int64_t tree_base_lines(int t, int64_t Nb, int L) {
+  return ((int64_t)(t / kWave) * Nb * kWave + (t % kWave)) * L;
 }
-__host__ __device__ constexpr int64_t blk_stride_lines(int A) { return (int64_t)kWave * blk_lines(A); }
-__host__ __device__ inline int64_t arena_lines(int B, int64_t Nb, int A) {
-  return (int64_t)((B + kWave - 1) / kWave) * kWave * Nb * blk_lines(A);
+__host__ __device__ constexpr int64_t blk_stride_lines(int L) { return (int64_t)kWave * L; }
+__host__ __device__ inline int64_t arena_lines(int B, int64_t Nb, int L) {
+  return (int64_t)((B + kWave - 1) / kWave) * kWave * Nb * L;
+}
+
+// Type-based search (POTMMCP, potmmcp.py:18-301) with fixed-distribution
+// policies (planning/policies.py): every table holds the doubles Python's
+// random.choices bisects (cumulative weights and total = cum[-1] + 0.0).
+constexpr int kTmMax = 8;               // ego / other-agent policies
+constexpr int kCodeShift = 50;          // inline slot key bits 50..53: the child's prior code
+constexpr uint64_t kCodeMask = 15ull << kCodeShift;
+// Prior code of an obs node (its ObsNode.action_probs at creation): 0 = the
+// meta-policy's expected prior (get_expected_action_probs, potmmcp.py:391-431:
+// roots made by update), k + 1 = ego policy k's get_pi (a child created by a
+// simulation that sampled ego policy k, potmmcp.py:275-287).  Overflow
+// entries keep it in flags bits 1..4.
+struct TmTables {
+  int32_t n_ego, n_other, pad[2];
+  double prior[kTmMax + 1][kTmMax];     // [code][a]: the action_probs a node starts with
+  double ego_cum[kTmMax][kTmMax];       // ego policy k's action draw (rollouts)
+  double ego_tot[kTmMax];
+  double oth_cum[kTmMax][kTmMax];       // other-agent policy j's action draw
+  double oth_tot[kTmMax];
+  double meta_cum[kTmMax][kTmMax];      // sample_policy: meta_policy[j] in its dict order
+  double meta_tot[kTmMax];
+  int32_t meta_idx[kTmMax][kTmMax];     // ego policy of meta_policy[j]'s i-th key
+  int32_t meta_len[kTmMax];
+};
+// random.choices(population, weights): bisect_right(cum, x, 0, n - 1) for
+// x = random() * total, as CPython computes it (a linear scan: n <= 8).
+__device__ __forceinline__ int tm_choice(const double* cum, double total, int n, uint32_t w) {
+  const double x = uniform_float(w) * total;
+  int i = n - 1;
+  for (int q = n - 2; q >= 0; --q)
+    if (x < cum[q]) i = q;
+  return i;
 }
 
 // Overflow children (> kSlots per action node): open-addressing map keyed by
@@ -144,7 +184,8 @@ struct TreeHdr {
   uint64_t seed;
   uint32_t tree_key;
   uint32_t ctr[5];     // belief, select, model, act0, act1
-  int32_t pad[2];
+  int32_t root_code;   // type-based: the root's prior code while it has no block
+  uint32_t ctr_mix;    // type-based: S_MIXTURE draws (the other agent's policy per particle)
 };
 
 struct DevParams {
@@ -155,8 +196,11 @@ struct DevParams {
   uint32_t ovf_base;    // node ids >= ovf_base are overflow entries
   int32_t islots;       // inline obs slots in use per action node (kSlots; fewer only in
                         // tests of the overflow map: pomcp_debug_set_inline_slots)
+  int32_t lines;        // lines per block (blk_lines(A, tm))
+  int32_t tm;           // type-based search (POTMMCP): tmt, prior lines, log aux
+  const TmTables* tmt;
   TreeHdr* hdr;
-  Line* an;             // [B][Nb][A + 1] action blocks
+  Line* an;             // [B][Nb][lines] action blocks
   OvfSlot* ovf;         // [B][H]
   LogRec* plog;         // [waves][64 * Np] per-search-wave particle log
   LogRec* lscr;         // [B][Np] k_search_lds: one launch's records per tree (allocated on

@@ -36,6 +36,7 @@ struct ChildRef {
   int blk;            // action block of the child (-1 = leaf)
   int visits;         // ObsNode.visits after this visit
   int absorbing;
+  int code;           // type-based: the child's prior code (pomcp_device.h kCodeShift)
   int lane;           // lane holding the inline slot in the level registers (-1: overflow)
   int32_t* blk_ptr;   // where the child's block index lives (for expansion)
 };
@@ -55,13 +56,14 @@ struct Tree {
   double mm_min, mm_max;
   uint64_t seed;
   uint32_t tkey;
-  uint32_t c_belief, c_select, c_model, c_act0, c_act1;
+  uint32_t c_belief, c_select, c_model, c_act0, c_act1, c_mix;
+  int root_code;
   LdsStream r_belief, r_model, r_act0, r_act1;
   int64_t c_levels, c_expand, c_new, c_rollout, c_probes;
 
   __device__ Tree(const DevParams& pp, const Model& mm, int t) : p(pp), m(mm), tree(t) {
     lane = lane_id();
-    an = p.an + tree_base_lines(t, p.Nb, p.A);
+    an = p.an + tree_base_lines(t, p.Nb, p.lines);
     ovf = p.ovf + (int64_t)t * p.H;
     bel = p.belief + (int64_t)t * 2 * p.Nr;
     const TreeHdr h = p.hdr[t];
@@ -86,6 +88,8 @@ struct Tree {
     c_model = uniu(h.ctr[2]);
     c_act0 = uniu(h.ctr[3]);
     c_act1 = uniu(h.ctr[4]);
+    c_mix = uniu(h.ctr_mix);
+    root_code = uni(h.root_code);
     c_levels = c_expand = c_new = c_rollout = c_probes = 0;
   }
 
@@ -124,7 +128,8 @@ struct Tree {
     h.ctr[2] = c_model;
     h.ctr[3] = c_act0;
     h.ctr[4] = c_act1;
-    h.pad[0] = h.pad[1] = 0;
+    h.root_code = root_code;
+    h.ctr_mix = c_mix;
     p.hdr[tree] = h;
   }
 
@@ -152,7 +157,7 @@ struct Tree {
 
   __device__ uint4 load_block(int blk) const {
     uint4 q = make_uint4(0, 0, 0, 0);
-    if (lane < blk_parts(p.A)) q = reinterpret_cast<const uint4*>(an + (int64_t)blk * blk_stride_lines(p.A))[lane];
+    if (lane < blk_parts(p.lines)) q = reinterpret_cast<const uint4*>(an + (int64_t)blk * blk_stride_lines(p.lines))[lane];
     return q;
   }
 
@@ -163,8 +168,8 @@ struct Tree {
       return -1;
     }
     const int b = n_blocks++;
-    if (lane < blk_parts(p.A))
-      reinterpret_cast<uint4*>(an + (int64_t)b * blk_stride_lines(p.A))[lane] = make_uint4(0, 0, 0, 0);
+    if (lane < blk_parts(p.lines))
+      reinterpret_cast<uint4*>(an + (int64_t)b * blk_stride_lines(p.lines))[lane] = make_uint4(0, 0, 0, 0);
     ++c_expand;
     return b;
   }
@@ -216,6 +221,7 @@ struct Tree {
         c->blk = rl((int)s2.x, L);
         c->visits = rl((int)s2.y, L);
         c->absorbing = rl((int)s.w, L) & 1;
+        c->code = (rl((int)s.w, L) >> 1) & 15;
         c->lane = -1;
         c->blk_ptr = &(ovf + (int64_t)b * kBucket + L)->block;
         return true;
@@ -233,6 +239,7 @@ struct Tree {
         c->blk = -1;
         c->visits = init_visits;
         c->absorbing = absorbing;
+        c->code = 0;
         c->lane = -1;
         c->blk_ptr = &(ovf + (int64_t)b * kBucket + L)->block;
         *is_new = true;
@@ -258,7 +265,7 @@ struct Tree {
     const uint64_t skey = (uint64_t)q.x | ((uint64_t)q.y << 32);
     const bool valid = cl && (skey & kValidBit) != 0;
     const uint64_t m = __ballot(valid && (skey & kObsMask) == okey);
-    uint4* slots = reinterpret_cast<uint4*>(an + (int64_t)blk * blk_stride_lines(p.A)) + lo;
+    uint4* slots = reinterpret_cast<uint4*>(an + (int64_t)blk * blk_stride_lines(p.lines)) + lo;
     int L;
     bool is_new = false;
     if (m) {
@@ -266,6 +273,7 @@ struct Tree {
       c->blk = rl((int)q.z, L);
       c->visits = rl((int)q.w, L);
       c->absorbing = (int)(rlu(q.y, L) >> 31);
+      c->code = (int)((rlu(q.y, L) >> (kCodeShift - 32)) & 15u);
     } else {
       const uint64_t em = __ballot(cl && (skey & kValidBit) == 0);
       if (!em) {   // all inline slots taken: overflow map
@@ -277,7 +285,7 @@ struct Tree {
           OvfSlot* e = ovf + (int64_t)(c->id - p.ovf_base);
           if (lane == 0) {
             e->visits = c->visits;
-            e->flags = (uint32_t)done;
+            e->flags = (uint32_t)done | ((uint32_t)c->code << 1);
           }
         }
         return true;
@@ -286,6 +294,7 @@ struct Tree {
       c->blk = -1;
       c->visits = 0;
       c->absorbing = done;
+      c->code = 0;   // a root made by update: the meta-policy's expected prior
       is_new = true;
       ++n_nodes;
       ++c_new;
@@ -296,7 +305,8 @@ struct Tree {
       c->absorbing = done;
     }
     if (visit || is_new) {
-      const uint64_t nk = okey | kValidBit | ((uint64_t)c->absorbing << 63);
+      const uint64_t nk = okey | kValidBit | ((uint64_t)c->absorbing << 63) |
+                          ((uint64_t)c->code << kCodeShift);
       const uint4 ns = make_uint4((uint32_t)nk, (uint32_t)(nk >> 32), (uint32_t)c->blk,
                                   (uint32_t)c->visits);
       if (lane == L) {
@@ -400,12 +410,16 @@ __global__ __launch_bounds__(256) void k_extract(DevParams p) {
   tval[wi][lane] = (uint32_t)h.root_t + 1u;
   dst[wi][lane] = ((int64_t)tree * 2 + (h.belief_sel ^ 1)) * p.Nr;
   __builtin_amdgcn_wave_barrier();
-  const WaveLog wl(p.plog, p.Np, sw);
+  const WaveLog wl(p.plog, p.Np, sw, p.tm);
   const uint32_t n = p.wlog[sw];
   for (uint32_t base = 0; base < n; base += kWave) {
     const uint32_t i = base + (uint32_t)lane;
     LogRec r = {0xFFFFFFFFu, 0u, 0u};
-    if (i < n) r = wl.load(i);
+    uint32_t aux = 0u;   // type-based: the particle's other-agent policy
+    if (i < n) {
+      r = wl.load(i);
+      if (p.tm) aux = wl.aux[i];
+    }
     const uint32_t l = r.id >> kIdBits;
     const bool m = i < n && want[wi][l] == r.id;
     uint64_t mask = __ballot(m);
@@ -415,7 +429,7 @@ __global__ __launch_bounds__(256) void k_extract(DevParams p) {
       const int lj = __builtin_amdgcn_readlane((int)l, j);
       const int pos = cnt[wi][lj];
       if (lane == j) {
-        if (pos < p.Nr) p.belief[dst[wi][lj] + pos] = make_uint4(tval[wi][lj], r.v0, r.v1, 0u);
+        if (pos < p.Nr) p.belief[dst[wi][lj] + pos] = make_uint4(tval[wi][lj], r.v0, r.v1, aux);
         cnt[wi][lj] = pos + 1;
       }
       __builtin_amdgcn_wave_barrier();
@@ -448,10 +462,17 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
           break;
         }
         T.sample_agent_initial(obs, &s0, &s1);
-        if (lane == 0) nb[n] = make_uint4(1u, s0, s1, 0u);
+        // type-based: the other agent's policy of the particle,
+        // OtherAgentMixturePolicy.sample_initial_state (potmmcp.py:83-87)
+        uint32_t pid = 0u;
+        if (p.tm)
+          pid = uniform_int(uniu(philox_word(T.seed, T.tkey, S_MIXTURE, T.c_mix++)),
+                            (uint32_t)p.tmt->n_other);
+        if (lane == 0) nb[n] = make_uint4(1u, s0, s1, pid);
         ++n;
       }
       if (T.err == 0) {
+        T.root_code = 0;   // potmmcp.py:44-56: the meta-policy's expected prior
         T.root_id = kRootId;
         T.root_blk = -1;
         T.root_visits = 0;
@@ -506,10 +527,15 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
                                         ? philox_word(T.seed, T.tkey, S_MODEL, T.c_model + (uint32_t)lane)
                                         : 0u;
                 const uint4 hp = pbel[uniform_int(wb, (uint32_t)T.bsize)];
+                // the other agent's action: uniform, or (type-based) by the
+                // particle's policy (OtherAgentMixturePolicy.sample_action)
+                const uint32_t ao = p.tm ? (uint32_t)tm_choice(p.tmt->oth_cum[hp.w], p.tmt->oth_tot[hp.w],
+                                                               p.A, wa)
+                                         : uniform_int(wa, (uint32_t)p.A);
                 uint32_t n0, n1;
                 double r;
                 int done;
-                Env::step(sm, p.ego, hp.y, hp.z, (uint32_t)action, uniform_int(wa, (uint32_t)p.A),
+                Env::step(sm, p.ego, hp.y, hp.z, (uint32_t)action, ao,
                           Env::kStepDraws ? uniform_int(wm, 2u) : 0u, &n0, &n1, &r, &done);
                 const bool acc = valid && Env::obs_key(sm, p.ego, n0, n1) == obs;
                 const uint64_t am = __ballot(acc);
@@ -517,7 +543,7 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
                 const bool run = valid && got + pa < need;   // the loop head's test before this try
                 const uint64_t rm = __ballot(run);
                 const uint64_t jm = __ballot(run && !acc);
-                const uint4 rec = make_uint4(hp.x + 1u, n0, n1, 0u);
+                const uint4 rec = make_uint4(hp.x + 1u, n0, n1, hp.w);
                 if (run && acc) nb[n + got + pa] = rec;
                 const int rr = nrej + __popcll(jm & lt);
                 if (run && !acc && rr < need) nb[n + need + rr] = rec;
@@ -556,6 +582,7 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
             T.root_visits = visits;
             T.root_t += 1;
             T.root_abs = c.absorbing;
+            T.root_code = c.code;
             T.bsel ^= 1;
             T.bsize = n;
           }
@@ -605,8 +632,8 @@ __global__ __launch_bounds__(256) void k_compact(DevParams p) {
   const int A = p.A;
   const int nb = uni(h.n_blocks);
   const int R = uni(h.root_blk);
-  Line* const an = p.an + tree_base_lines(tree, p.Nb, A);
-  const int64_t bstride = blk_stride_lines(A);
+  Line* const an = p.an + tree_base_lines(tree, p.Nb, p.lines);
+  const int64_t bstride = blk_stride_lines(p.lines);
   int32_t* const cmap = p.cmap + (int64_t)tree * p.Nb;
   int32_t* const cpar = p.cpar + (int64_t)tree * p.Nb;
   OvfSlot* const ovf = p.ovf + (int64_t)tree * p.H;
@@ -665,9 +692,9 @@ __global__ __launch_bounds__(256) void k_compact(DevParams p) {
   //    parts are loaded before any is stored (a destination may be a source
   //    of the same pass, never of a later one).
   constexpr int kMoveBlocks = 8;
-  const int parts = blk_parts(A);   // <= 48
+  const int parts = blk_parts(p.lines);   // <= 56
   for (int i0 = 0; i0 < m; i0 += kMoveBlocks) {
-    constexpr int kPer = (kMoveBlocks * 48 + kWave - 1) / kWave;
+    constexpr int kPer = (kMoveBlocks * 56 + kWave - 1) / kWave;
     uint4 v[kPer];
     int dst[kPer], prt[kPer];
 #pragma unroll
@@ -686,7 +713,7 @@ __global__ __launch_bounds__(256) void k_compact(DevParams p) {
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
       const int pp = prt[q];
-      const bool slot = pp >= kLine && (pp % kLine) >= 1 && (pp % kLine) <= kSlots;
+      const bool slot = pp >= kLine && pp < kLine * (A + 1) && (pp % kLine) >= 1 && (pp % kLine) <= kSlots;
       const bool vs = dst[q] >= 0 && slot && (v[q].y & (uint32_t)(kValidBit >> 32)) != 0u;
       if (vs && (int)v[q].z >= 0) v[q].z = (uint32_t)ld_agent(cmap + (int)v[q].z);
       if (vs) v[q].w = 0u;   // visits: recounted from the log by k_compact_log
@@ -782,16 +809,18 @@ __global__ __launch_bounds__(256) void k_compact_log(DevParams p) {
   kept[wi][lane] = 0;
   act[wi][lane] = mytree < p.B ? p.cnt[mytree] : 0;
   __builtin_amdgcn_wave_barrier();
-  const WaveLog wl(p.plog, p.Np, sw);
+  const WaveLog wl(p.plog, p.Np, sw, p.tm);
   const uint32_t n = p.wlog[sw];
   const uint32_t A = (uint32_t)p.A;
   uint32_t out = 0;
   for (uint32_t base = 0; base < n; base += kWave) {
     const uint32_t i = base + (uint32_t)lane;
     LogRec r = {0u, 0u, 0u};
+    uint32_t aux = 0u;
     bool keep = false;
     if (i < n) {
       r = wl.load(i);
+      if (p.tm) aux = wl.aux[i];
       const uint32_t l = r.id >> kIdBits;
       const uint32_t id = r.id & kIdMask;
       const int tree = sw * kWave + (int)l;
@@ -807,8 +836,8 @@ __global__ __launch_bounds__(256) void k_compact_log(DevParams p) {
           const int nb = ld_agent(p.cmap + (int64_t)tree * p.Nb + (int)(ani / A));
           if (nb >= 0) {
             nid = (int32_t)(((uint32_t)nb * A + ani % A) * kSlots + k + 1u);
-            uint4* const bp = reinterpret_cast<uint4*>(p.an + tree_base_lines(tree, p.Nb, (int)A) +
-                                                       (int64_t)nb * blk_stride_lines((int)A));
+            uint4* const bp = reinterpret_cast<uint4*>(p.an + tree_base_lines(tree, p.Nb, p.lines) +
+                                                       (int64_t)nb * blk_stride_lines(p.lines));
             vis = reinterpret_cast<int32_t*>(bp + part_slot((int)(ani % A), (int)k)) + 3;
           }
         }
@@ -820,7 +849,11 @@ __global__ __launch_bounds__(256) void k_compact_log(DevParams p) {
     }
     const uint64_t mk = __ballot(keep);
     __builtin_amdgcn_s_waitcnt(0);   // the whole chunk is loaded before any store
-    if (keep) wl.store(out + (uint32_t)__popcll(mk & ((1ull << lane) - 1ull)), r);
+    if (keep) {
+      const uint32_t at = out + (uint32_t)__popcll(mk & ((1ull << lane) - 1ull));
+      wl.store(at, r);
+      if (p.tm) wl.aux[at] = aux;
+    }
     out += (uint32_t)__popcll(mk);
   }
   __builtin_amdgcn_wave_barrier();

@@ -107,7 +107,14 @@ __device__ __forceinline__ uint32_t line_visits(const uint4& p0, const uint4& p1
 
 enum : int { TP_LEVEL = 0, TP_ROLL = 1, TP_BACKUP = 2, TP_START = 3, TP_DONE = 4 };
 
-template <class Env, int SEL, int NA, int TPB>
+// TM = 1: the type-based search of POTMMCP (potmmcp.py:164-301) with
+// fixed-distribution policies (pomcp_device.h TmTables): per simulation an ego
+// policy drawn from the meta-policy row of the particle's other-agent policy
+// (sample_policy, potmmcp.py:381-389); the other agent acts by its particle's
+// policy, rollouts by the drawn ego policy; PUCB's prior is the node's
+// action_probs (a prior line per block), moved towards the drawn policy's
+// distribution on every arrival at an existing child (potmmcp.py:255-264).
+template <class Env, int SEL, int NA, int TPB, int TM>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES_PER_EU, POMCP_WAVES_PER_EU))) void k_search(DevParams p, int num_sims, int final_sel) {
   static_assert(NA >= 2 && NA <= kMaxA, "action count");
   __shared__ typename Env::Model sm;
@@ -120,12 +127,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   const bool valid = tree < p.B;
   const int tt = valid ? tree : 0;
   constexpr int A = NA;   // == p.A (host dispatch)
+  constexpr int L = blk_lines(NA, TM);   // == p.lines
   // this tree's blocks: interleaved with the wave's other trees (pomcp_device.h)
-  char* const an = reinterpret_cast<char*>(p.an + tree_base_lines(tt, p.Nb, A));
-  const int64_t blk_bytes = blk_stride_lines(A) * 128;   // block b at an + b * blk_bytes
+  char* const an = reinterpret_cast<char*>(p.an + tree_base_lines(tt, p.Nb, L));
+  const int64_t blk_bytes = blk_stride_lines(L) * 128;   // block b at an + b * blk_bytes
   // the wave's shared particle log (pomcp_device.h LogRec); wpos is the same in
   // every lane still in the loop (advanced by ballot at convergent points)
-  const WaveLog wl(p.plog, p.Np, wave);
+  const WaveLog wl(p.plog, p.Np, wave, TM);
+  const TmTables* const tmt = p.tmt;
+  uint32_t pid = 0;   // TM: the running simulation's other-agent policy (its particle's)
+  int epol = 0;       // TM: the ego policy drawn for it
   const int islots = p.islots;   // kSlots (fewer: overflow-map tests)
   const uint32_t wpos0 = p.wlog[wave];
   uint32_t wpos = wpos0;
@@ -135,7 +146,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
     const uint64_t m = __ballot(app);
     if (m != 0ull) {
 #ifndef POMCP_ABLATE_LOG   // ablation build only: no particle-log stores
-      if (app) wl.store(wpos + (uint32_t)__popcll(m & ((1ull << lane) - 1ull)), rec);
+      if (app) {
+        const uint32_t at = wpos + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        wl.store(at, rec);
+        if constexpr (TM != 0) wl.aux[at] = pid;
+      }
 #endif
       wpos += (uint32_t)__popcll(m);
       app = false;
@@ -167,9 +182,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   // ---- RNG streams (philox.h): one stateless Philox block per draw
   auto d_belief = [&](uint32_t n) { return uniform_int(philox_word(seed, tkey, S_BELIEF, c_bel++), n); };
   auto d_select = [&](uint32_t n) { return uniform_int(philox_word(seed, tkey, S_SELECT, c_sel++), n); };
-  auto d_act = [&](int agent, uint32_t n) {
-    return agent == 0 ? uniform_int(philox_word(seed, tkey, S_ACT_BASE, c_a0++), n)
-                      : uniform_int(philox_word(seed, tkey, S_ACT_BASE + 1, c_a1++), n);
+  auto d_act_word = [&](int agent) {
+    return agent == 0 ? philox_word(seed, tkey, S_ACT_BASE, c_a0++)
+                      : philox_word(seed, tkey, S_ACT_BASE + 1, c_a1++);
   };
   // One-draw lookahead of the streams every tree step consumes (the other
   // agent's action, the model's shuffle draw) and of the belief stream: the
@@ -194,17 +209,28 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
       pend_b = 1;
     }
   };
-  auto take_oth = [&](uint32_t n) { pend_s = 0; return uniform_int(w_oth, n); };
+  // the other agent's action (mcts.py:602-615): uniform (RandomOtherAgentPolicy)
+  // or, TM, by its particle's policy (OtherAgentMixturePolicy.sample_action)
+  auto take_oth = [&]() -> uint32_t {
+    pend_s = 0;
+    if constexpr (TM != 0) return (uint32_t)tm_choice(tmt->oth_cum[pid], tmt->oth_tot[pid], A, w_oth);
+    else return uniform_int(w_oth, (uint32_t)A);
+  };
   auto take_mod = [&](uint32_t n) { return Env::kStepDraws ? uniform_int(w_mod, n) : 0u; };
   // ObsNode.add_child for every action (mcts.py:279-281, 318-321): zeroed block
-  auto alloc_block = [&]() -> int {
+  // (TM: its prior line = the action_probs of prior code `code`)
+  auto alloc_block = [&](int code) -> int {
     if (n_blocks >= p.Nb) {
       err = POMCP_E_ARENA;
       return -1;
     }
     const int b = n_blocks++;
     uint4* d = reinterpret_cast<uint4*>(an + (int64_t)b * blk_bytes);
-    for (int q = 0; q < blk_parts(A); ++q) d[q] = make_uint4(0, 0, 0, 0);
+    for (int q = 0; q < blk_parts(A + 1); ++q) d[q] = make_uint4(0, 0, 0, 0);
+    if constexpr (TM != 0) {
+      double* const pr = reinterpret_cast<double*>(d + part_prior(A));
+      for (int q = 0; q < A; ++q) pr[q] = tmt->prior[code][q];
+    }
     return b;
   };
 
@@ -212,21 +238,25 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   // node with nv visits; log_n = math.log(nv) (host table, prefetched).  The
   // children's scores are computed branch-free (independent chains the wave
   // issues back to back); the strict '>' scan in action order is kept.
-  auto select_action = [&](const uint4 (&st)[kMaxA], int nv, double log_n) -> int {
+  // ap: the node's action_probs (TM; the uniform prior otherwise).
+  auto select_action = [&](const uint4 (&st)[kMaxA], int nv, double log_n,
+                           const double (&ap)[kMaxA]) -> int {
     int a = 0;
-    if (SEL == POMCP_SEL_PUCB && nv == 0) {   // random.choices over the uniform prior
-      const double w = 1.0 / (double)A;
-      double total = w;
-      for (int q = 1; q < A; ++q) total = total + w;
-      const double x = uniform_float(philox_word(seed, tkey, S_SELECT, c_sel++)) * (total + 0.0);
-      double acc = w;
+    if (SEL == POMCP_SEL_PUCB && nv == 0) {   // random.choices over the node's prior
+      double cum[kMaxA], acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < kMaxA; ++q) {
+        const double w = TM != 0 ? ap[q] : 1.0 / (double)A;
+        acc = q == 0 ? w : acc + w;
+        cum[q] = acc;
+      }
+      const double x = uniform_float(philox_word(seed, tkey, S_SELECT, c_sel++)) * (cum[A - 1] + 0.0);
       a = A - 1;
       for (int q = 0; q < A - 1; ++q) {
-        if (x < acc) {
+        if (x < cum[q]) {
           a = q;
           break;
         }
-        acc = acc + w;
       }
     } else if (nv == 0) {
       a = (int)d_select((uint32_t)A);
@@ -258,10 +288,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         }
       } else {                             // PUCB, mcts.py:502-527
         const double noise = 1.0 / (double)A;
-        const double prior = (1.0 / (double)A) * (1.0 - p.pucb_f) + p.pucb_f * noise;
         const double sqrt_n = sqrt((double)nv);
 #pragma unroll
         for (int q = 0; q < A; ++q) {
+          const double prior = (TM != 0 ? ap[q] : 1.0 / (double)A) * (1.0 - p.pucb_f) + p.pucb_f * noise;
           const int n = (int)st[q].x;
           const double v = hilo_d(st[q].z, st[q].w);
           const double nvq = nz ? (v - mm_min) / range : v;
@@ -305,6 +335,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   double rt[kMaxA];
 #pragma unroll
   for (int q = 0; q < kMaxA; ++q) rt[q] = 0.0;
+  // TM: the root's action_probs (registers for the launch, written back at the
+  // end) and the prior line of the next LEVEL pass's node (prefetched with it)
+  double rap[kMaxA];
+#pragma unroll
+  for (int q = 0; q < kMaxA; ++q) rap[q] = 0.0;
+  uint4 ppr[3] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
   PathEntry rpath[kRegPath];     // levels 1..kRegPath
   uint4 pre[kPre];               // node line of the next LEVEL pass's node (parts 0 .. A + 1)
 #pragma unroll
@@ -323,7 +359,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
     phase = TP_DONE;
   }
   if (phase != TP_DONE) {
-    if (root_blk < 0) root_blk = alloc_block();   // mcts.py:279-281
+    if (root_blk < 0) root_blk = alloc_block(h->root_code);   // mcts.py:279-281
     if (root_blk < 0 || bsize <= 0) {
       if (err == 0) err = POMCP_E_STATE;
       phase = TP_DONE;
@@ -345,6 +381,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
           for (int q = 0; q < kSlots; ++q) rc[rc_slot(a, q)][lid] = rb[part_slot(a, q)];
         }
         rt[a] = hilo_d(vt.z, vt.w);
+        if constexpr (TM != 0) rap[a] = reinterpret_cast<const double*>(rb + part_prior(A))[a];
       }
     }
     pf = rbel[d_belief((uint32_t)bsize)];   // the first simulation's particle
@@ -355,13 +392,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   // Overflow children (beyond the kSlots inline ones) of action node ani.
   // Returns its results by value: out-parameters would keep the caller's
   // locals in scratch memory.
+  // TM: ncode = the prior code of a child created here; o.code = the child's.
   struct OvfChild {
     uint32_t cid;
-    int cblk, cvis;
+    int cblk, cvis, code, existed;
     int32_t* cptr;
   };
-  auto ovf_child = [&](uint32_t ani, uint64_t okey, int done, int cblk, int cvis) -> OvfChild {
-    OvfChild o{0u, cblk, cvis, nullptr};
+  auto ovf_child = [&](uint32_t ani, uint64_t okey, int done, int cblk, int cvis,
+                       int ncode) -> OvfChild {
+    OvfChild o{0u, cblk, cvis, ncode, 0, nullptr};
     const uint64_t key = okey | ((uint64_t)epoch << kEpochShift);
     uint32_t b = ovf_hash(ani, okey) & p.bucket_mask;
     bool found = false;
@@ -377,11 +416,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
             const uint4 w1 = reinterpret_cast<const uint4*>(ep)[1];
             o.cblk = (int)w1.x;
             o.cvis = (int)w1.y + 1;
+            o.code = (int)((w0.w >> 1) & 15u);
+            o.existed = 1;
           } else {
             ++n_nodes;
           }
-          reinterpret_cast<uint4*>(ep)[0] =
-              make_uint4((uint32_t)key, (uint32_t)(key >> 32), ani, (uint32_t)done);
+          reinterpret_cast<uint4*>(ep)[0] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), ani,
+                                                       (uint32_t)done | ((uint32_t)o.code << 1));
           reinterpret_cast<uint4*>(ep)[1] = make_uint4((uint32_t)o.cblk, (uint32_t)o.cvis, 0u, 0u);
           o.cid = p.ovf_base + b * kBucket + (uint32_t)e;
           o.cptr = &ep->block;
@@ -428,8 +469,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   // Descend into the child (mcts.py:371-376): arrival at an obs node (start of
   // _simulate, mcts.py:315-328): depth/step cutoff -> back up 0; unexpanded ->
   // expand and roll out; else select there (next LEVEL).  cvis: the child's
-  // visits with this arrival when it has no block (its slot's count).
-  auto descend = [&](int done, int cblk, int cvis, uint32_t n0, uint32_t n1) {
+  // visits with this arrival when it has no block (its slot's count); code:
+  // its prior code (TM: the prior line of a block allocated for it).
+  auto descend = [&](int done, int cblk, int cvis, uint32_t n0, uint32_t n1, int code) {
     if (done) {
       ret = 0.0;
       phase = TP_BACKUP;
@@ -444,7 +486,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
       ret = 0.0;
       phase = TP_BACKUP;
     } else if (blk < 0) {                               // mcts.py:318-328
-      const int b = alloc_block();
+      const int b = alloc_block(code);
       if (b < 0) {
         phase = TP_DONE;
       } else {
@@ -463,7 +505,18 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
       const uint4* const cp = reinterpret_cast<const uint4*>(an + (int64_t)blk * blk_bytes);
 #pragma unroll
       for (int q = 0; q < kPre; ++q) pre[q] = q < 2 + A ? cp[q] : make_uint4(0, 0, 0, 0);
+      if constexpr (TM != 0) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) ppr[q] = cp[part_prior(A) + q];
+      }
     }
+  };
+  // TM: action_probs of a node += (the drawn policy's pi - them) / its visits
+  // (potmmcp.py:259-264), on an arrival at an existing child
+  auto prior_ema = [&](double (&ap)[kMaxA], int nv) {
+#pragma unroll
+    for (int q = 0; q < kMaxA; ++q)
+      if (q < A) ap[q] = ap[q] + (tmt->prior[epol + 1][q] - ap[q]) / (double)nv;
   };
   // A done arrival at a child that has a block (rare: it was expanded by an
   // earlier, non-terminal arrival): ObsNode.visits += 1 in its node line.
@@ -508,16 +561,22 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         depth = 0;
         plen = 0;
         r0_on = 0;
+        if constexpr (TM != 0) {   // sample_policy (potmmcp.py:381-389), select stream
+          pid = pr.w;
+          const int i = tm_choice(tmt->meta_cum[pid], tmt->meta_tot[pid], tmt->meta_len[pid],
+                                  philox_word(seed, tkey, S_SELECT, c_sel++));
+          epol = tmt->meta_idx[pid][i];
+        }
         if (0 > p.depth_limit || t > p.step_limit) {            // mcts.py:315
           ret = 0.0;
           phase = TP_BACKUP;
         } else {
           const uint32_t j = take_mod(2);
-          const uint32_t ao = take_oth((uint32_t)A);
+          const uint32_t ao = take_oth();
           uint4 st[kMaxA];
 #pragma unroll
           for (int q = 0; q < kMaxA; ++q) st[q] = q < A ? rc[rc_stats(q)][lid] : make_uint4(0, 0, 0, 0);
-          const int a = select_action(st, root_visits, root_logn);
+          const int a = select_action(st, root_visits, root_logn, rap);
           uint4 sa = st[0];
           uint4 sl[kSlots];
 #pragma unroll
@@ -538,7 +597,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
           const int ks = find_slot(sl, okey, &match);
           const uint32_t ani = (uint32_t)(root_blk * A + a);
           uint32_t cid = 0;
-          int cblk = -1, cvis = 1;
+          int cblk = -1, cvis = 1, ccode = epol + 1, existed = 0;
           if (ks >= 0) {
             uint4 sk = sl[0];
 #pragma unroll
@@ -549,10 +608,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
             cblk = match ? (int)sk.z : cblk;
             cvis = match ? (int)sk.w + 1 : cvis;
             n_nodes += match ? 0 : 1;
+            existed = match ? 1 : 0;
             if (match && cblk >= 0 && done) bump_node(cblk);
             // (LDS: the slot is rewritten on every arrival; its visits are
             // meaningful while the child has no block)
-            const uint64_t nk = okey | kValidBit | ((uint64_t)done << 63);
+            uint64_t nk = okey | kValidBit | ((uint64_t)done << 63);
+            if constexpr (TM != 0) {
+              ccode = match ? (int)((sk.y >> (kCodeShift - 32)) & 15u) : ccode;
+              nk |= (uint64_t)ccode << kCodeShift;
+            }
             const uint4 nsl = make_uint4((uint32_t)nk, (uint32_t)(nk >> 32), (uint32_t)cblk, (uint32_t)cvis);
             cid = ani * kSlots + (uint32_t)ks + 1u;
             if (kRootSlotsInLds) {
@@ -565,13 +629,18 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
               leaf_rc = -1;
             }
           } else {
-            const OvfChild o = ovf_child(ani, okey, done, cblk, cvis);
+            const OvfChild o = ovf_child(ani, okey, done, cblk, cvis, ccode);
             cid = o.cid;
             cblk = o.cblk;
             cvis = o.cvis;
+            ccode = o.code;
+            existed = o.existed;
             leaf_ptr = o.cptr;
             leaf_rc = -1;
             if (cblk >= 0 && done) bump_node(cblk);
+          }
+          if constexpr (TM != 0) {
+            if (existed) prior_ema(rap, root_visits);
           }
           if (err != 0 || n_log >= p.Np) {
             if (err == 0) err = POMCP_E_ARENA;
@@ -585,7 +654,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
             r0_vis = sa.x;
             r0_r = r;
             r0_val = hilo_d(sa.z, sa.w);
-            descend(done, cblk, cvis, n0, n1);
+            descend(done, cblk, cvis, n0, n1, ccode);
           }
         }
       }
@@ -604,7 +673,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
       if (phase == TP_LEVEL) {
         const uint4* const ap = reinterpret_cast<const uint4*>(an + (int64_t)blk * blk_bytes);
         const uint32_t j = take_mod(2);
-        const uint32_t ao = take_oth((uint32_t)A);
+        const uint32_t ao = take_oth();
         PT_MARK(8);
         // the node line, prefetched by descend(): this arrival's N (its visits
         // + 1) and math.log(N) are in it
@@ -617,8 +686,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
           st[q] = q < A ? make_uint4(line_visits(pre[0], pre[1], q), 0u, pre[part_vt(q)].x,
                                      pre[part_vt(q)].y)
                         : make_uint4(0, 0, 0, 0);
+        double lap[kMaxA];   // TM: the node's action_probs (its prior line)
+#pragma unroll
+        for (int q = 0; q < kMaxA; ++q)
+          lap[q] = TM != 0 ? hilo_d(q & 1 ? ppr[q >> 1].z : ppr[q >> 1].x, q & 1 ? ppr[q >> 1].w : ppr[q >> 1].y)
+                           : 0.0;
         PT_MARK(1);
-        const int a = select_action(st, nvis, log_n);
+        const int a = select_action(st, nvis, log_n, lap);
         PT_MARK(2);
         uint4 sa = st[0], va = pre[part_vt(0)];
   #pragma unroll
@@ -642,7 +716,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         PT_MARK(12);
         const uint32_t ani = (uint32_t)(blk * A + a);
         uint32_t cid = 0;
-        int cblk = -1, cvis = 1;
+        int cblk = -1, cvis = 1, ccode = epol + 1, existed = 0;
         leaf_rc = -1;
         if (ks >= 0) {
           uint4 sk = sl[0];
@@ -652,7 +726,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
           cblk = match ? (int)sk.z : cblk;   // (selects, as at the root level)
           cvis = match ? (int)sk.w + 1 : cvis;
           n_nodes += match ? 0 : 1;
-          const uint64_t nk = okey | kValidBit | ((uint64_t)done << 63);
+          existed = match ? 1 : 0;
+          uint64_t nk = okey | kValidBit | ((uint64_t)done << 63);
+          if constexpr (TM != 0) {
+            ccode = match ? (int)((sk.y >> (kCodeShift - 32)) & 15u) : ccode;
+            nk |= (uint64_t)ccode << kCodeShift;
+          }
           uint4* slot = const_cast<uint4*>(ap) + part_slot(a, ks);
           // the slot changes beyond its visit count, or its count is needed
           // (no block yet, within the limits): pomcp_device.h
@@ -664,12 +743,23 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
           cid = ani * kSlots + (uint32_t)ks + 1u;
           leaf_ptr = reinterpret_cast<int32_t*>(slot) + 2;
         } else {
-          const OvfChild o = ovf_child(ani, okey, done, cblk, cvis);
+          const OvfChild o = ovf_child(ani, okey, done, cblk, cvis, ccode);
           cid = o.cid;
           cblk = o.cblk;
           cvis = o.cvis;
+          ccode = o.code;
+          existed = o.existed;
           leaf_ptr = o.cptr;
           if (cblk >= 0 && done) bump_node(cblk);
+        }
+        if constexpr (TM != 0) {
+          if (existed) {   // this node's action_probs move (potmmcp.py:255-264)
+            prior_ema(lap, nvis);
+            double* const pl = reinterpret_cast<double*>(const_cast<uint4*>(ap) + part_prior(A));
+#pragma unroll
+            for (int q = 0; q < kMaxA; ++q)
+              if (q < A) pl[q] = lap[q];
+          }
         }
         PT_MARK(13);
         if (err != 0 || n_log >= p.Np || plen >= kMaxPath) {
@@ -687,7 +777,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
               make_uint4(pre[1].x, (uint32_t)nvis, (uint32_t)__double2loint(lnx),
                          (uint32_t)__double2hiint(lnx))});
           PT_MARK(14);
-          descend(done, cblk, cvis, n0, n1);
+          descend(done, cblk, cvis, n0, n1, ccode);
         }
         PT_MARK(4);
       }
@@ -698,9 +788,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
       if (!(rdepth <= p.depth_limit && t <= p.step_limit)) {
         phase = TP_BACKUP;
       } else {
-        const uint32_t ae = d_act(p.ego, (uint32_t)A);       // search_policy.py:177
+        // the ego's rollout action: RandomSearchPolicy (search_policy.py:177) or,
+        // TM, the simulation's drawn policy (potmmcp.py:221-229)
+        const uint32_t aw = d_act_word(p.ego);
+        uint32_t ae;
+        if constexpr (TM != 0) ae = (uint32_t)tm_choice(tmt->ego_cum[epol], tmt->ego_tot[epol], A, aw);
+        else ae = uniform_int(aw, (uint32_t)A);
         const uint32_t j = take_mod(2);
-        const uint32_t ao = take_oth((uint32_t)A);           // other_policy.py:151
+        const uint32_t ao = take_oth();                       // other_policy.py:151
         la_step();
         uint32_t n0, n1;
         double r;
@@ -810,6 +905,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
     }
     wb[0] = make_uint4(vw[0], vw[1], vw[2], vw[3]);
     reinterpret_cast<uint32_t*>(wb)[4] = vw[4];
+    if constexpr (TM != 0) {
+#pragma unroll
+      for (int a = 0; a < kMaxA; ++a)
+        if (a < A) reinterpret_cast<double*>(wb + part_prior(A))[a] = rap[a];
+    }
   }
   const bool have = err == 0 && !root_abs && root_blk >= 0;
   uint4 st[kMaxA];   // {visits, -, value}
@@ -936,14 +1036,17 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   so->pad = 0;
 }
 
-#define PB_SEARCH_INST(E, NA, T)                                                 \
-  template __global__ void k_search<E, POMCP_SEL_PUCB, NA, T>(DevParams, int, int);  \
-  template __global__ void k_search<E, POMCP_SEL_UCB, NA, T>(DevParams, int, int);   \
-  template __global__ void k_search<E, POMCP_SEL_UNIFORM, NA, T>(DevParams, int, int);
-PB_SEARCH_INST(EnvDriving, 5, kTPB)
-PB_SEARCH_INST(EnvPursuitEvasion, 4, kTPB)
-PB_SEARCH_INST(EnvDriving, 5, kTPBSmall)
-PB_SEARCH_INST(EnvPursuitEvasion, 4, kTPBSmall)
+#define PB_SEARCH_INST(E, NA, T, TM)                                                 \
+  template __global__ void k_search<E, POMCP_SEL_PUCB, NA, T, TM>(DevParams, int, int);  \
+  template __global__ void k_search<E, POMCP_SEL_UCB, NA, T, TM>(DevParams, int, int);   \
+  template __global__ void k_search<E, POMCP_SEL_UNIFORM, NA, T, TM>(DevParams, int, int);
+PB_SEARCH_INST(EnvDriving, 5, kTPB, 0)
+PB_SEARCH_INST(EnvPursuitEvasion, 4, kTPB, 0)
+PB_SEARCH_INST(EnvDriving, 5, kTPBSmall, 0)
+PB_SEARCH_INST(EnvPursuitEvasion, 4, kTPBSmall, 0)
+// type-based (POTMMCP) searches always launch one-wave workgroups
+PB_SEARCH_INST(EnvDriving, 5, kTPBSmall, 1)
+PB_SEARCH_INST(EnvPursuitEvasion, 4, kTPBSmall, 1)
 #undef PB_SEARCH_INST
 
 }  // namespace pb

@@ -101,8 +101,8 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
   const int lane = lane_id();
   const int al = lane >> 3 < A ? lane >> 3 : A - 1;   // this lane's action group
   const int ql = lane & 7;                             // part of the action's line
-  char* const an = reinterpret_cast<char*>(p.an + tree_base_lines(tree, p.Nb, A));
-  const int64_t blk_bytes = blk_stride_lines(A) * 128;
+  char* const an = reinterpret_cast<char*>(p.an + tree_base_lines(tree, p.Nb, blk_lines(A)));
+  const int64_t blk_bytes = blk_stride_lines(blk_lines(A)) * 128;
   auto hblk = [&](int b) -> uint4* { return reinterpret_cast<uint4*>(an + (int64_t)b * blk_bytes); };
   // part q of action a's LDS line <-> the HBM block (pomcp_device.h)
   auto hld = [&](int b, int a, int q) -> uint4 {
@@ -228,7 +228,7 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
         nl_n[b] = 1;
         nl_v[b] = 0.0;
       }
-    } else if (lane < blk_parts(A)) {
+    } else if (lane < blk_parts(blk_lines(A))) {
       reinterpret_cast<uint4*>(an + (int64_t)b * blk_bytes)[lane] = make_uint4(0, 0, 0, 0);
     }
     return b;

@@ -11,7 +11,8 @@ import os
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.environ.get("POMCP_LIB_PATH") or os.path.join(LIB_DIR, "libpomcp_hip.so")
 
-POMCP_ABI_VERSION = 3
+POMCP_ABI_VERSION = 4
+POMCP_MAX_TYPE_POLICIES = 8
 POMCP_MAX_ACTIONS = 8
 POMCP_XREC_STATS = 6
 
@@ -103,7 +104,7 @@ class PomcpConfig(C.Structure):
         ("known_max", C.c_double),
         ("seed", C.c_uint64),
         ("tree_key_base", C.c_uint32),
-        ("pad0", C.c_int32),
+        ("type_based", C.c_int32),
         ("max_blocks", C.c_int64),
         ("max_particles", C.c_int64),
         ("max_belief", C.c_int64),
@@ -162,6 +163,20 @@ class PomcpMergedRoot(C.Structure):
 
 # (name, restype, argtypes) for every symbol include/pomcp.h declares.
 _CTX = C.c_void_p
+class PomcpTypePolicies(C.Structure):
+    """``pomcp_type_policies`` (include/pomcp.h): POTMMCP's fixed-distribution policies."""
+    _fields_ = [
+        ("num_ego", C.c_int32),
+        ("num_other", C.c_int32),
+        ("ego_pi", (C.c_double * POMCP_MAX_ACTIONS) * POMCP_MAX_TYPE_POLICIES),
+        ("other_pi", (C.c_double * POMCP_MAX_ACTIONS) * POMCP_MAX_TYPE_POLICIES),
+        ("meta_len", C.c_int32 * POMCP_MAX_TYPE_POLICIES),
+        ("meta_policy", (C.c_int32 * POMCP_MAX_TYPE_POLICIES) * POMCP_MAX_TYPE_POLICIES),
+        ("meta_weight", (C.c_double * POMCP_MAX_TYPE_POLICIES) * POMCP_MAX_TYPE_POLICIES),
+        ("expected_prior", C.c_double * POMCP_MAX_ACTIONS),
+    ]
+
+
 _P32 = C.POINTER(C.c_int32)
 _PU32 = C.POINTER(C.c_uint32)
 _PU64 = C.POINTER(C.c_uint64)
@@ -181,6 +196,9 @@ SIGNATURES = [
     ("pomcp_get_root_stats", C.c_int, [_CTX, C.POINTER(PomcpRootStats)]),
     ("pomcp_set_root_belief", C.c_int, [_CTX, C.c_int32, _PU32, C.c_int32]),
     ("pomcp_get_root_belief", C.c_int, [_CTX, C.c_int32, _PU32, C.c_int32, _P32]),
+    ("pomcp_set_type_policies", C.c_int, [_CTX, C.POINTER(PomcpTypePolicies)]),
+    ("pomcp_get_root_prior", C.c_int, [_CTX, C.c_int32, _PD]),
+    ("pomcp_get_root_policies", C.c_int, [_CTX, C.c_int32, _P32, C.c_int32, _P32]),
     ("pomcp_arena_usage", C.c_int, [_CTX, _P32, _P32]),
     ("pomcp_rekey", C.c_int, [_CTX, C.c_uint64]),
     ("pomcp_root_merge_buffer", C.c_int, [_CTX, C.POINTER(C.c_void_p)]),

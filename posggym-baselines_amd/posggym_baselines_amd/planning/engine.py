@@ -117,7 +117,7 @@ class PomcpEngine:
 
     def __init__(self, model, agent_id, config, num_trees=1, capacities=None, num_sims=None,
                  searches=None, device=None, stream=None, tree_key_base=0, seed=None,
-                 wall_clock=False):
+                 wall_clock=False, type_policies=None):
         lib = N.load()
         from posggym_baselines_amd.envs import engine_model
         model = engine_model(model)   # posggym-style models by spec.id + kwargs
@@ -184,6 +184,8 @@ class PomcpEngine:
         c.discount_pow = self._dpow.ctypes.data_as(C.POINTER(C.c_double))
         c.discount_pow_size = len(self._dpow)
         model.configure_engine(c)
+        c.type_based = 1 if type_policies is not None else 0
+        self.type_based = type_policies is not None
         self._cfg = c
         dev = config.device if device is None else device
         ctx = C.c_void_p()
@@ -193,6 +195,9 @@ class PomcpEngine:
         self._ctx = ctx
         self._lib = lib
         self._stats = (N.PomcpRootStats * self.num_trees)()
+        if type_policies is not None:
+            self._check(lib.pomcp_set_type_policies(ctx, C.byref(type_policies)),
+                        "set_type_policies")
         # search kernel override (tests / benchmarks): POMCP_SEARCH_KERNEL=lane|wave
         kind = os.environ.get("POMCP_SEARCH_KERNEL", "auto")
         if kind != "auto":
@@ -215,6 +220,23 @@ class PomcpEngine:
 
     def reset(self):
         self._check(self._lib.pomcp_reset(self._ctx), "reset")
+
+    def root_prior(self, tree=0):
+        """Type-based: the root's ObsNode.action_probs (num_actions doubles)."""
+        out = (C.c_double * self.A)()
+        self._check(self._lib.pomcp_get_root_prior(self._ctx, int(tree), out), "get_root_prior")
+        return list(out)
+
+    def root_policies(self, tree=0):
+        """Type-based: the other-agent policy index of every root particle."""
+        n = C.c_int32()
+        self._check(self._lib.pomcp_get_root_policies(self._ctx, int(tree), None, 0, C.byref(n)),
+                    "get_root_policies")
+        out = np.zeros(max(n.value, 1), dtype=np.int32)
+        self._check(self._lib.pomcp_get_root_policies(
+            self._ctx, int(tree), out.ctypes.data_as(C.POINTER(C.c_int32)), n.value, C.byref(n)),
+            "get_root_policies")
+        return out[:n.value]
 
     def update(self, actions, obs_keys):
         B = self.num_trees

@@ -58,23 +58,23 @@ class RandomOtherAgentPolicy(OtherAgentPolicy):
 
 
 class OtherAgentMixturePolicy(OtherAgentPolicy):
-    """Mixture over posggym.agents policies (``other_policy.py:157-230``): the
-    policy is drawn at ``sample_initial_state`` and kept in the state.  The GPU
-    planners accept random other agents only; this class keeps the surface."""
+    """Mixture over the other agent's policies (``other_policy.py:155-216``):
+    one policy per episode, drawn uniformly by ``sample_initial_state`` and kept
+    in the state.  POTMMCP runs it on the GPU when every policy is a
+    ``FixedDistributionPolicy`` (planning/policies.py); the particle's policy
+    index is drawn on the MIXTURE stream there."""
 
-    def __init__(self, model, agent_id: str, policies: Dict[str, object],
-                 policy_distribution: Optional[Dict[str, float]] = None):
+    def __init__(self, model, agent_id: str, policies: Dict[str, object]):
         super().__init__(model, agent_id)
+        assert len(model.possible_agents) == 2, "Currently only supports 2 agents"
         self.policies = policies
-        if policy_distribution is None:
-            policy_distribution = {k: 1.0 / len(policies) for k in policies}
-        self.policy_distribution = policy_distribution
+        self.action_space = list(range(model.action_spaces[agent_id].n))
 
     def sample_initial_state(self):
         import random
-        pid = random.choices(list(self.policy_distribution),
-                             weights=list(self.policy_distribution.values()), k=1)[0]
-        return {"policy_id": pid, "policy_state": self.policies[pid].get_initial_state()}
+        policy_id = random.choice(list(self.policies))
+        return {"policy_id": policy_id,
+                "policy_state": self.policies[policy_id].get_initial_state()}
 
     def get_next_state(self, action, obs, state):
         pid = state["policy_id"]
@@ -86,7 +86,12 @@ class OtherAgentMixturePolicy(OtherAgentPolicy):
         return self.policies[state["policy_id"]].sample_action(state["policy_state"])
 
     def get_pi(self, state):
-        return self.policies[state["policy_id"]].get_pi(state["policy_state"])
+        pi = self.policies[state["policy_id"]].get_pi(state["policy_state"]).probs
+        if len(pi) != len(self.action_space):
+            for a in self.action_space:
+                if a not in pi:
+                    pi[a] = 0.0
+        return pi
 
     def close(self):
         for p in self.policies.values():

@@ -82,13 +82,17 @@ class POMCP:
             # dataclass (AttributeError in the reference); dataclasses.replace is
             # what it means.  Recorded in DESIGN.md.
             config = dataclasses.replace(config, state_belief_only=True)
+        others = {i: RandomOtherAgentPolicy(model, i) for i in model.possible_agents if i != agent_id}
+        self._init_planner(model, agent_id, config, search_policy, others, num_sims, process_group)
+
+    def _init_planner(self, model, agent_id, config, search_policy, other_agent_policies,
+                      num_sims, process_group, type_policies=None):
         self.model = model
         self._emodel = engine_model(model)
         self.agent_id = agent_id
         self.config = config
         self.search_policy = search_policy
-        self.other_agent_policies = {
-            i: RandomOtherAgentPolicy(model, i) for i in model.possible_agents if i != agent_id}
+        self.other_agent_policies = other_agent_policies
         self.num_agents = len(model.possible_agents)
         self.action_space = list(range(model.action_spaces[agent_id].n))
         self._num_sims = num_sims if num_sims is not None else config.num_sims
@@ -104,7 +108,7 @@ class POMCP:
         self._per_replica = per
         self._engine = PomcpEngine(model, agent_id, config, num_trees=self._K,
                                    num_sims=per, tree_key_base=self._rank * self._K,
-                                   wall_clock=per is None)
+                                   wall_clock=per is None, type_policies=type_policies)
         self.step_limit = self._engine.step_limit
         self._logger = logging.getLogger()
         self._last_action = None

@@ -17,7 +17,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 
 from oracle.ref_harness import (  # noqa: E402
-    import_reference, reference_available, reference_episode, reference_intmcp_episode)
+    import_reference, reference_available, reference_episode, reference_intmcp_episode,
+    reference_potmmcp_episode)
 from oracle.run import oracle_episode, oracle_intmcp_episode  # noqa: E402
 
 SQRT2 = math.sqrt(2)
@@ -105,6 +106,64 @@ def run_intmcp_case(name):
             raise SystemExit(f"oracle disagrees with reference in case {name} seed {seed}")
         out["episodes"].append({"config": dict(cfg), "env_seed": env_seed, "trace": tr,
                                 "records": rr})
+    return out
+
+
+# POTMMCP (potmmcp.py:18-301) with fixed-distribution policies (planning/
+# policies.py): ego policies of the meta-policy, the other agent's mixture
+# policies, meta_policy[other][ego] weights (dict order matters: it is
+# random.choices' order).  No oracle restatement: the GPU tests compare against
+# these reference records directly.
+POTMMCP_SPECS = {
+    "A": {"ego": {"u": [0.2] * 5, "acc": [0.1, 0.5, 0.1, 0.2, 0.1],
+                  "stay": [0.6, 0.1, 0.1, 0.1, 0.1]},
+          "other": {"o_u": [0.2] * 5, "o_fast": [0.05, 0.7, 0.05, 0.1, 0.1]},
+          "meta": {"o_u": {"u": 0.5, "acc": 0.25, "stay": 0.25}, "o_fast": {"stay": 0.7, "u": 0.3}}},
+    # zero-probability actions and a deterministic other-agent policy
+    "B": {"ego": {"a": [0.2] * 5, "b": [0.0, 0.0, 0.5, 0.5, 0.0]},
+          "other": {"x": [0.3, 0.1, 0.1, 0.4, 0.1], "y": [0.2] * 5, "z": [0.0, 1.0, 0.0, 0.0, 0.0]},
+          "meta": {"x": {"b": 1.0}, "y": {"a": 0.5, "b": 0.5}, "z": {"a": 1.0}}},
+    "PE": {"ego": {"u": [0.25] * 4, "fw": [0.7, 0.1, 0.1, 0.1]},
+           "other": {"u": [0.25] * 4, "side": [0.1, 0.4, 0.4, 0.1]},
+           "meta": {"u": {"u": 0.5, "fw": 0.5}, "side": {"fw": 1.0}}},
+}
+POTMMCP_CFG = dict(TEST_CFG, state_belief_only=False)
+POTMMCP_CASES = {
+    # name: (cfg overrides, spec, num_sims, [(planner seed, env seed)], ego, max_steps, env)
+    "potmmcp_pucb": ({"action_selection": "pucb"}, "A", 64, [(30, 30), (31, 31)], "0", 50,
+                     "Driving-v1"),
+    "potmmcp_ucb_ego1": ({}, "B", 48, [(32, 32)], "1", 50, "Driving-v1"),
+    "potmmcp_pe_pucb": ({"action_selection": "pucb"}, "PE", 48, [(33, 33)], "0", 100,
+                        "PursuitEvasion-v1"),
+}
+# batched trees: the first step of trees 0..5 (keys (seed, k)), one episode each
+POTMMCP_TREES = ({"action_selection": "pucb"}, "A", 96, 34, 34, 6)
+
+
+def run_potmmcp_case(name):
+    over, spec, num_sims, pairs, ego, max_steps, env = POTMMCP_CASES[name]
+    out = {"case": name, "env": env, "num_sims": num_sims, "ego": ego, "max_steps": max_steps,
+           "spec": POTMMCP_SPECS[spec], "episodes": []}
+    for seed, env_seed in pairs:
+        cfg = dict(POTMMCP_CFG, **over)
+        cfg["seed"] = seed
+        tr, rr = reference_potmmcp_episode(cfg, num_sims, env_seed, POTMMCP_SPECS[spec], ego=ego,
+                                           max_steps=max_steps, env=env)
+        out["episodes"].append({"config": dict(cfg), "env_seed": env_seed, "trace": tr,
+                                "records": rr})
+    return out
+
+
+def run_potmmcp_trees():
+    over, spec, num_sims, seed, env_seed, n = POTMMCP_TREES
+    cfg = dict(POTMMCP_CFG, **over)
+    cfg["seed"] = seed
+    out = {"case": "potmmcp_trees", "env": "Driving-v1", "num_sims": num_sims, "ego": "0",
+           "spec": POTMMCP_SPECS[spec], "config": dict(cfg), "env_seed": env_seed, "trees": []}
+    for k in range(n):
+        tr, rr = reference_potmmcp_episode(cfg, num_sims, env_seed, POTMMCP_SPECS[spec], tree=k,
+                                           max_steps=2)
+        out["trees"].append({"tree": k, "trace": tr, "records": rr})
     return out
 
 
@@ -235,8 +294,8 @@ def _write(out_dir, name, data):
 
 
 def main(only=None, out_dir=HERE):
-    """only: None (every fixture), "ipomcp", "meta" (config + tracker
-    fixtures only) or a list of I-NTMCP case names."""
+    """only: None (every fixture), "ipomcp", "potmmcp", "meta" (config +
+    tracker fixtures only) or a list of I-NTMCP case names."""
     if not reference_available():
         raise SystemExit("reference not available (container-only script)")
     os.makedirs(out_dir, exist_ok=True)
@@ -255,6 +314,14 @@ def main(only=None, out_dir=HERE):
         _write(out_dir, name, data)
         n = sum(len(e["records"]) for e in data["episodes"])
         print(f"{name}: {len(data['episodes'])} episodes, {n} records")
+    for name in POTMMCP_CASES if only in (None, "potmmcp") else ():
+        data = run_potmmcp_case(name)
+        _write(out_dir, name, data)
+        n = sum(len(e["records"]) for e in data["episodes"])
+        print(f"{name}: {len(data['episodes'])} episodes, {n} records")
+    if only in (None, "potmmcp"):
+        _write(out_dir, "potmmcp_trees", run_potmmcp_trees())
+        print("potmmcp_trees written")
     if only in (None, "meta"):
         _write(out_dir, "config_kats", config_kats())
         _write(out_dir, "config_checks", config_checks())
@@ -275,6 +342,8 @@ if __name__ == "__main__":
         del argv[i:i + 2]
     if "--ipomcp" in argv:
         main(only="ipomcp", out_dir=out)
+    elif "--potmmcp" in argv:
+        main(only="potmmcp", out_dir=out)
     elif "--meta" in argv:
         main(only="meta", out_dir=out)
     elif "--intmcp" in argv:

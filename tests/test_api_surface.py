@@ -44,7 +44,7 @@ def test_potmmcp_meta_policy_expected_action_probs():
     assert probs == pytest.approx({0: 0.75, 1: 0.125, 2: 0.125, 3: 0.0, 4: 0.0})
     with pytest.raises(NotImplementedError):
         meta.sample_action({})
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(NotImplementedError):   # history-dependent / neural policies
         P.POTMMCP(m, "0", None, {}, meta)
 
 

@@ -42,6 +42,7 @@ def test_struct_layout_matches_header(tmp_path):
         "pomcp_grid": [f[0] for f in N.PomcpGrid._fields_],
         "pomcp_pe_grid": [f[0] for f in N.PomcpPeGrid._fields_],
         "pomcp_merged_root": [f[0] for f in N.PomcpMergedRoot._fields_],
+        "pomcp_type_policies": [f[0] for f in N.PomcpTypePolicies._fields_],
         "intmcp_config": [f[0] for f in N.IntmcpConfig._fields_],
         "intmcp_root_stats": [f[0] for f in N.IntmcpRootStats._fields_],
     }
@@ -60,6 +61,7 @@ def test_struct_layout_matches_header(tmp_path):
     for st, cls in (("pomcp_config", N.PomcpConfig), ("pomcp_root_stats", N.PomcpRootStats),
                     ("pomcp_grid", N.PomcpGrid), ("pomcp_pe_grid", N.PomcpPeGrid),
                     ("pomcp_merged_root", N.PomcpMergedRoot),
+                    ("pomcp_type_policies", N.PomcpTypePolicies),
                     ("intmcp_config", N.IntmcpConfig), ("intmcp_root_stats", N.IntmcpRootStats)):
         assert int(out[st]) == ctypes.sizeof(cls), st
         for f in fields[st]:
