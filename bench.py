@@ -195,10 +195,11 @@ def parse():
                          "(overflow is detected and fails the run)")
     ap.add_argument("--env", default="Driving-v1", choices=["Driving-v1", "PursuitEvasion-v1"],
                     help="Driving-v1 is BASELINE.json's metric; PursuitEvasion-v1 is config 3")
-    ap.add_argument("--planner", default="pomcp", choices=["pomcp", "intmcp"],
+    ap.add_argument("--planner", default="pomcp", choices=["pomcp", "intmcp", "potmmcp"],
                     help="pomcp: BASELINE.json's metric (C2/C3); intmcp: config 5, I-NTMCP "
                          "nesting level 1, one planner pair per lane (--trees pairs, --sims "
-                         "simulations per nesting level)")
+                         "simulations per nesting level); potmmcp: POTMMCP with fixed-"
+                         "distribution policies (SURVEY §8(f) rank 4), pucb")
     ap.add_argument("--arena", default=None,
                     help="intmcp: per-tree NODES,STATS,LOG arena sizes (skips the calibration "
                          "probe, e.g. for profiling runs)")
@@ -225,6 +226,24 @@ TEST_CFG = dict(discount=0.95, search_time_limit=0.1, c=math.sqrt(2), truncated=
                 action_selection="ucb", pucb_exploration_fraction=0.25, known_bounds=None,
                 step_limit=None, epsilon=0.92, state_belief_only=True)
 DEEP_CFG = dict(TEST_CFG, discount=0.99, epsilon=0.01)   # depth_limit 459
+# POTMMCP bench: the policy set of tests/golden/potmmcp_pucb.json (three ego
+# policies under a meta-policy, a two-policy other-agent mixture)
+TM_CFG = dict(TEST_CFG, action_selection="pucb", state_belief_only=False)
+TM_SPEC = {"ego": {"u": [0.2] * 5, "acc": [0.1, 0.5, 0.1, 0.2, 0.1],
+                   "stay": [0.6, 0.1, 0.1, 0.1, 0.1]},
+           "other": {"o_u": [0.2] * 5, "o_fast": [0.05, 0.7, 0.05, 0.1, 0.1]},
+           "meta": {"o_u": {"u": 0.5, "acc": 0.25, "stay": 0.25}, "o_fast": {"stay": 0.7, "u": 0.3}}}
+B_TM_LEVEL = 16 * 5   # TM: a level reads the node's action_probs and writes their moving average
+
+
+def type_policies(model):
+    from posggym_baselines_amd.planning import OtherAgentMixturePolicy, POTMMCPMetaPolicy
+    from posggym_baselines_amd.planning.policies import FixedDistributionPolicy
+    from posggym_baselines_amd.planning.potmmcp import type_policy_tables
+    ego = {k: FixedDistributionPolicy(model, "0", k, v) for k, v in TM_SPEC["ego"].items()}
+    oth = {k: FixedDistributionPolicy(model, "1", k, v) for k, v in TM_SPEC["other"].items()}
+    meta = POTMMCPMetaPolicy(model, "0", ego, TM_SPEC["meta"])
+    return type_policy_tables(model, "0", meta, OtherAgentMixturePolicy(model, "1", oth))
 
 
 def cpu_baseline(sims, trees, seed, env="Driving-v1", first_tree=0, base=None):
@@ -443,7 +462,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     cpu = None
     base_cfg = DEEP_CFG if args.deep else TEST_CFG
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    tm = args.planner == "potmmcp"
+    if tm:
+        if args.env != "Driving-v1" or args.deep:
+            raise SystemExit("--planner potmmcp: Driving-v1, default configuration")
+        base_cfg = TM_CFG
+    # (no CPU leg for POTMMCP: the oracle has no restatement of it -- its parity
+    # is pinned to the reference's own records)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not tm:
         # before any GPU call: the worker processes are forked from this one
         procs = max(1, min(args.cpu_procs, os.cpu_count() or 1))
         sample = args.cpu_sample_sims if not args.deep else max(64, args.cpu_sample_sims // 8)
@@ -473,7 +499,7 @@ def main():
                            overflow_slots=1024)
     stream = torch.cuda.Stream(device=dev)
     bp = BatchedPOMCP(model, "0", cfg, B, S, capacities=caps, stream=stream.cuda_stream,
-                      device=dev)
+                      device=dev, type_policies=type_policies(model) if tm else None)
     bp.init_synthetic(1000)
     bp.engine.rekey(args.seed ^ (rank << 32))
     A = bp.engine.A
@@ -524,6 +550,8 @@ def main():
     expands = sum(s.n_expansions for s in st)
     new_nodes = sum(s.n_new_nodes for s in st)
     alg_bytes = B_SIM * sims + b_level(A) * levels + b_expand(A) * expands + B_NEW_NODE * new_nodes
+    if tm:   # the action_probs of every stepped node (+ 8A written per leaf expansion)
+        alg_bytes += B_TM_LEVEL * levels + 8 * A * expands
     # the root level of every simulation is served from LDS / registers except
     # its particle-log append: its other bytes never reach HBM
     root_levels = min(sims, levels)
@@ -545,7 +573,8 @@ def main():
     env_desc = ("PursuitEvasion-v1 16x16 max_obs_distance=12" if args.env == "PursuitEvasion-v1"
                 else "Driving-v1 14x14RoundAbout")
     out = {
-        "metric": f"MCTS simulations/sec on {args.env} (POMCP exact search)",
+        "metric": (f"MCTS simulations/sec on {args.env} (POTMMCP exact search, fixed-distribution "
+                   "policies)" if tm else f"MCTS simulations/sec on {args.env} (POMCP exact search)"),
         "value": value,
         "unit": "simulations/s",
         "n_gpus": world,
@@ -558,12 +587,14 @@ def main():
         "dtype": "f64",
         "data": f"synthetic {args.env} belief states (env seed 1000+b), build's {args.env} "
                 "restatement",
-        "config": {"workload": f"POMCP {env_desc} exact search, {B} roots x {S} "
-                               f"sims per GPU, ucb c=sqrt2 gamma={cfg.discount} "
-                               f"depth_limit={cfg.depth_limit}, "
+        "config": {"workload": f"{'POTMMCP' if tm else 'POMCP'} {env_desc} exact search, {B} roots "
+                               f"x {S} sims per GPU, {cfg.action_selection} c=sqrt2 "
+                               f"gamma={cfg.discount} depth_limit={cfg.depth_limit}, "
+                               + ("3 ego policies under a meta-policy, 2 other-agent policies "
+                                  "(fixed distributions), " if tm else "")
                                + (f"{B // K} planner(s) x {K} replica trees merged on the device, "
                                   if K > 1 else "")
-                               + f"root-parallel all-reduce over {world} GPU(s)",
+                               + f"root-parallel all-gather over {world} GPU(s)",
                    "trees_per_gpu": B, "sims_per_tree": S, "depth_limit": cfg.depth_limit,
                    "root_parallel": K, "planners_per_gpu": B // K,
                    "sims_per_planner_step": S * K,

@@ -701,9 +701,18 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
           va = sel4(q == a, pre[part_vt(q < A ? q : 0)], va);
         }
         // the chosen action's child slots (second round trip)
+#ifdef POMCP_ABLATE_CUTSLOT   // ablation build only: no child lookup for a child beyond the limits
+        const bool skipc = depth + 1 > p.depth_limit || t + 1 > p.step_limit;
+#else
+        constexpr bool skipc = false;
+#endif
         uint4 sl[kSlots];
   #pragma unroll
-        for (int q = 0; q < kSlots; ++q) sl[q] = ap[part_slot(a, q)];
+        for (int q = 0; q < kSlots; ++q) sl[q] = make_uint4(0, 0, 0, 0);
+        if (!skipc) {
+  #pragma unroll
+          for (int q = 0; q < kSlots; ++q) sl[q] = ap[part_slot(a, q)];
+        }
         la_step();   // the next step's draws, while the child line is in flight
         PT_MARK(3);
         uint32_t n0, n1;
@@ -711,14 +720,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         int done;
         uint64_t okey;
         tree_step(a, ao, j, &n0, &n1, &r, &done, &okey);
-        bool match;
-        const int ks = find_slot(sl, okey, &match);
+        bool match = false;
+        const int ks = skipc ? 0 : find_slot(sl, okey, &match);
         PT_MARK(12);
         const uint32_t ani = (uint32_t)(blk * A + a);
         uint32_t cid = 0;
         int cblk = -1, cvis = 1, ccode = epol + 1, existed = 0;
         leaf_rc = -1;
-        if (ks >= 0) {
+        if (skipc) {
+          cid = ani * kSlots + 1u;
+        } else if (ks >= 0) {
           uint4 sk = sl[0];
   #pragma unroll
           for (int q = 1; q < kSlots; ++q)

@@ -305,7 +305,7 @@ class BatchedPOMCP:
 
     def __init__(self, model, agent_id, config: MCTSConfig, num_trees: int, num_sims: int,
                  *, searches: int = 1, reroot: bool = False, capacities=None, stream=None,
-                 tree_key_base: int = 0, device: Optional[int] = None):
+                 tree_key_base: int = 0, device: Optional[int] = None, type_policies=None):
         from posggym_baselines_amd.planning.engine import plan_capacities
         if capacities is None:
             step_limit = config.step_limit or model.spec.max_episode_steps
@@ -315,7 +315,8 @@ class BatchedPOMCP:
         self.num_sims = num_sims
         self.engine = PomcpEngine(model, agent_id, config, num_trees=num_trees,
                                   capacities=capacities, stream=stream,
-                                  tree_key_base=tree_key_base, device=device)
+                                  tree_key_base=tree_key_base, device=device,
+                                  type_policies=type_policies)
         self.engine.reset()
 
     def init_synthetic(self, env_seed_base: int = 1000):

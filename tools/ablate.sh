@@ -9,7 +9,8 @@ set -o pipefail
 if [ "$1" = build ]; then
   mkdir -p variants
   for v in "base:" "philox3:-DPB_PHILOX_ROUNDS=3" "nosel:-DPOMCP_ABLATE_SELECT" \
-           "nobelief:-DPOMCP_ABLATE_BELIEF" "nolog:-DPOMCP_ABLATE_LOG"; do
+           "nobelief:-DPOMCP_ABLATE_BELIEF" "nolog:-DPOMCP_ABLATE_LOG" \
+           "nocutslot:-DPOMCP_ABLATE_CUTSLOT"; do
     n=${v%%:*}; f=${v#*:}
     POMCP_LIB_PATH=$PWD/variants/lib_$n.so POMCP_EXTRA_FLAGS="$f" \
       python -c "import sys; sys.path.insert(0,'posggym-baselines_amd'); from posggym_baselines_amd import build; build.build(force=True)" || exit 1
