@@ -483,7 +483,7 @@ static int launch_search(pomcp_ctx* ctx, int32_t num_sims, int final_sel) {
   if (ctx->dp.tm && !ctx->tm_set) return fail(ctx, POMCP_E_STATE, "search: pomcp_set_type_policies first");
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   if (resolve_search_kind(ctx) == POMCP_SEARCH_WAVE) return launch_search_wave(ctx, num_sims, final_sel);
-  const int tpb = ctx->dp.tm ? kTPBSmall : search_tpb(ctx->dp.B);
+  const int tpb = search_tpb(ctx->dp.B);
   const dim3 grid((unsigned)((ctx->dp.B + tpb - 1) / tpb)), block((unsigned)tpb);
   // kernel per (environment, selection rule, workgroup size); the action count is the model's
   using KFn = void (*)(DevParams, int, int);
@@ -493,11 +493,11 @@ static int launch_search(pomcp_ctx* ctx, int32_t num_sims, int final_sel) {
    {k_search<EnvPursuitEvasion, POMCP_SEL_PUCB, 4, T, TM>,                                        \
     k_search<EnvPursuitEvasion, POMCP_SEL_UCB, 4, T, TM>,                                         \
     k_search<EnvPursuitEvasion, POMCP_SEL_UNIFORM, 4, T, TM>}}
-  static const KFn table[3][2][3] = {PB_SEARCH_ROW(kTPB, 0), PB_SEARCH_ROW(kTPBSmall, 0),
-                                     PB_SEARCH_ROW(kTPBSmall, 1)};
+  static const KFn table[4][2][3] = {PB_SEARCH_ROW(kTPB, 0), PB_SEARCH_ROW(kTPBSmall, 0),
+                                     PB_SEARCH_ROW(kTPB, 1), PB_SEARCH_ROW(kTPBSmall, 1)};
 #undef PB_SEARCH_ROW
   const int e = ctx->dp.env == POMCP_ENV_PURSUIT_EVASION ? 1 : 0;
-  const int row = ctx->dp.tm ? 2 : (tpb == kTPB ? 0 : 1);
+  const int row = (ctx->dp.tm ? 2 : 0) + (tpb == kTPB ? 0 : 1);
   hipLaunchKernelGGL(table[row][e][ctx->dp.sel], grid, block, 0, ctx->stream, ctx->dp,
                      (int)num_sims, final_sel);
   HIP_TRY(ctx, hipGetLastError());

@@ -134,7 +134,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   // the wave's shared particle log (pomcp_device.h LogRec); wpos is the same in
   // every lane still in the loop (advanced by ballot at convergent points)
   const WaveLog wl(p.plog, p.Np, wave, TM);
-  const TmTables* const tmt = p.tmt;
+  // TM: the policy tables staged in LDS (every draw and prior reads them)
+  __shared__ __attribute__((aligned(16))) char tm_lds[TM != 0 ? sizeof(TmTables) : 16];
+  if constexpr (TM != 0) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(p.tmt);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(tm_lds);
+    for (int i = (int)threadIdx.x; i < (int)(sizeof(TmTables) / 4); i += TPB) dst[i] = src[i];
+    __syncthreads();
+  }
+  const TmTables* const tmt = reinterpret_cast<const TmTables*>(tm_lds);
   uint32_t pid = 0;   // TM: the running simulation's other-agent policy (its particle's)
   int epol = 0;       // TM: the ego policy drawn for it
   const int islots = p.islots;   // kSlots (fewer: overflow-map tests)
@@ -1055,7 +1063,8 @@ PB_SEARCH_INST(EnvDriving, 5, kTPB, 0)
 PB_SEARCH_INST(EnvPursuitEvasion, 4, kTPB, 0)
 PB_SEARCH_INST(EnvDriving, 5, kTPBSmall, 0)
 PB_SEARCH_INST(EnvPursuitEvasion, 4, kTPBSmall, 0)
-// type-based (POTMMCP) searches always launch one-wave workgroups
+PB_SEARCH_INST(EnvDriving, 5, kTPB, 1)
+PB_SEARCH_INST(EnvPursuitEvasion, 4, kTPB, 1)
 PB_SEARCH_INST(EnvDriving, 5, kTPBSmall, 1)
 PB_SEARCH_INST(EnvPursuitEvasion, 4, kTPBSmall, 1)
 #undef PB_SEARCH_INST
