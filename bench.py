@@ -42,9 +42,8 @@ B_SIM, B_NEW_NODE = 16, 28
 B_LOG_APPEND = 16   # of b_level: the particle-log record (the root level's only HBM term)
 
 
-def b_level(A, agg=False):
-    """agg: the engine keeps ActionNode.agg (I-NTMCP: +8 B read, +8 B written)."""
-    return 8 + 12 * A + 84 + (16 if agg else 0)
+def b_level(A):
+    return 8 + 12 * A + 84
 
 
 def b_expand(A):
@@ -301,7 +300,10 @@ def b_other(A):
     return 8 + 4 * A + 16
 
 
-B_STAT, B_NODE_HASH = 32, 48
+# per obs node created: its INode (32) + the {obs key, child} slot naming it
+# (12; an overflow child's hash entry is 16).  Statistics entries cost no
+# bytes inside the search: the node arena is cleared at reset (csrc/intmcp.hip).
+B_NODE_IM = 44
 
 
 def cpu_baseline_intmcp(sims, pairs, seed, env="Driving-v1"):
@@ -411,8 +413,8 @@ def main_intmcp(args):
         nodes += s.n_nodes[0] + s.n_nodes[1] - s0[2]
         stats += s.n_stats[0] + s.n_stats[1] - s0[3]
     sims_timed = 2 * S * searched * args.steps
-    alg_bytes = (B_SIM * sims_timed + b_level(A, agg=True) * (lv0 + lv1) + b_other(A) * lv1
-                 + B_STAT * stats + B_NODE_HASH * nodes) / args.steps
+    alg_bytes = (B_SIM * sims_timed + b_level(A) * (lv0 + lv1) + b_other(A) * lv1
+                 + B_NODE_IM * nodes) / args.steps
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     traffic = _pmc_traffic("pmc_intmcp.json", lib_sha, trees=B, sims=S, env=args.env)
     out = {

@@ -86,7 +86,7 @@ int intmcp_get_root_belief(intmcp_ctx* ctx, int32_t pair, uint32_t* out, int32_t
 /* Diagnostics: one tree's node records (32 B each: parent i32, info u32,
  * visits i32, t i32, stats i32, -, obs key u64; info = parent action:3 |
  * absorbing:1 | path_ok:1 | registered:3 | registration order 6 x 3 bits) and
- * statistics entries (32 B: visits i32, -, value f64, total f64, agg f64);
+ * statistics entries (32 B: visits i32, -, value f64, total f64, agg f64 = 0: not kept);
  * tree 0 = level 1, tree 1 = level 0. */
 int intmcp_get_nodes(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int32_t capacity,
                      int32_t* count);

@@ -27,16 +27,30 @@ namespace pb {
 constexpr int kImPath = 128;          // tree levels per simulation
 constexpr int kImMaxA = 6;            // registration order: 6 x 3 bits (INode.info)
 constexpr int kImRegPath = 3;         // path levels held in registers (deeper ones in p.path)
-// A node's block, two 128 B lines: line 0 = the INode (32 B) + the head
-// {visits, -, value} of each action's statistics (16 B each); line 1 = their
-// {total, agg} tails.  A node view (selection, the other agent's softmax)
-// is one line; the chosen action's tail is read for the backup only.
-constexpr int64_t kImBlock = 256;
-// Node blocks are interleaved by wavefront: per wave [2 trees][Nn][W lanes]
-// blocks (W = 64, fewer in a last partial wave), so the pairs of a wave keep
-// node n of their trees side by side and a wave's loads spread over the blocks
-// in use, not over 64 separate per-pair slabs (fewer pages per load
-// instruction to translate).  B x 2 x Nn blocks in all.
+// A node: its line (128 B) = the INode (32 B) + the head {visits, -, value}
+// of each action's statistics (16 B each), and one 32 B action record per
+// action (the None action A included): the action's total (ActionNode
+// total_value; agg is not kept) and kImInline obs-child slots
+// {obs key, child id} (id 0: empty -- a tree's node 0 is never a child).
+// A node view (selection, the other agent's softmax) is its line; the chosen
+// action's record is loaded right after selection, so the obs child is found
+// in registers once the step has produced the observation (no probe round
+// trip); a (node, action) with more than kImInline children keeps the rest in
+// the per-tree hash map (IHash), probed only when the inline slots are full.
+// Blocks start zeroed (the arena is cleared at create and reset; nodes are
+// never reused within an episode), so statistics need no initialising writes.
+constexpr int kImInline = 2;
+constexpr int64_t kImLine = 128;
+constexpr int64_t kImRec = 32;                              // {total f64, 2 x {okey u64, child i32}}
+constexpr int64_t kImRecs = 6 * kImRec;                     // records of actions 0..5 (kImMaxA)
+constexpr int64_t kImBlock = kImLine + kImRecs;             // 320 B per node (packed extraction ABI)
+// Nodes are interleaved by wavefront: per wave [2 trees][Nn] slabs of W nodes
+// (W = 64, fewer in a last partial wave), each slab = the W node lines then
+// the W nodes' records ([W][128 B] [W][192 B]), so the pairs of a wave keep
+// node n of their trees side by side (a view load is W whole lines) and a
+// wave's loads spread over the slabs in use, not over 64 separate per-pair
+// arenas (fewer pages per load instruction to translate).  B x 2 x Nn x
+// kImBlock bytes in all.
 __host__ __device__ __forceinline__ int im_wave_width(int B, int b) {
   const int w0 = b - b % kWave;
   return B - w0 < kWave ? B - w0 : kWave;
@@ -44,9 +58,15 @@ __host__ __device__ __forceinline__ int im_wave_width(int B, int b) {
 __host__ __device__ __forceinline__ int64_t im_node_stride(int B, int b) {   // node n -> n + 1
   return (int64_t)im_wave_width(B, b) * kImBlock;
 }
+// node n's line (tree k of pair b)
 __host__ __device__ __forceinline__ int64_t im_node_off(int64_t Nn, int B, int b, int k, int64_t n) {
   const int64_t w0 = b - b % kWave;
-  return (w0 * 2 * Nn + ((int64_t)k * Nn + n) * im_wave_width(B, b) + (b - w0)) * kImBlock;
+  return w0 * 2 * Nn * kImBlock + ((int64_t)k * Nn + n) * im_node_stride(B, b) + (b - w0) * kImLine;
+}
+// a node's action records, relative to its line
+__host__ __device__ __forceinline__ int64_t im_rec_delta(int B, int b) {
+  const int64_t j = b - (b - b % kWave);
+  return (im_wave_width(B, b) - j) * kImLine + j * kImRecs;
 }
 constexpr uint32_t kImNoSupport = 0xFFFFFFFFu;
 constexpr int32_t kImSkip = -2;       // intmcp_update action: leave the pair untouched
@@ -97,9 +117,10 @@ struct ImParams {
   int64_t Nn, Ns, Nl, H, Nr, Nsp;   // per tree: nodes, stat entries, log records, hash slots;
                                     // per pair: root belief, support particles
   IHdr* hdr;
-  char* nodes;          // node blocks (kImBlock B), wave-interleaved: im_node_off
+  char* nodes;          // node lines + action records (kImBlock B a node), wave-interleaved:
+                        // im_node_off, im_rec_delta
   int64_t nstride;      // kImBlock (the packed block size of the extraction ABI)
-  IHash* hash;          // [B][2][H]
+  IHash* hash;          // [B][2][H] obs children beyond a record's inline slots
   IRec* log;            // [B][2][Nl]
   uint4* root;          // [B][2][Nr] {v0, v1, nested, support slot}
   ISup* sup;            // [B][2][Nr]
@@ -132,6 +153,7 @@ struct ImPair {
   int pair;
   char* nb[2];     // node blocks of the level-1 (0) and level-0 (1) trees
   int64_t ns;      // node n -> n + 1 (im_node_stride)
+  int64_t ro;      // node line -> its action records (im_rec_delta)
   IHash* hs[2];
   IRec* lg[2];
   uint4* rootb;   // [2][Nr]
@@ -164,6 +186,7 @@ struct ImPair {
       lg[k] = p.log + ((int64_t)b * 2 + k) * p.Nl;
     }
     ns = im_node_stride(p.B, b);
+    ro = im_rec_delta(p.B, b);
     rootb = p.root + (int64_t)b * 2 * p.Nr;
     sup = p.sup + (int64_t)b * 2 * p.Nr;
     supp = p.supp + (int64_t)b * 2 * p.Nsp;
@@ -208,17 +231,32 @@ struct ImPair {
     o.search_depth = h.search_depth;
   }
 
-  // A node's block (kImBlock): the INode with the heads of its actions'
-  // statistics (node.py:120-178) in one line, so a node and its statistics
-  // arrive together (they used to be an index apart: two dependent loads).
+  // A node's line: the INode with the heads of its actions' statistics
+  // (node.py:120-178), so a node and its statistics arrive together (they
+  // used to be an index apart: two dependent loads).
   __device__ __forceinline__ INode& N(int k, int n) const {
     return *reinterpret_cast<INode*>(nb[k] + (int64_t)n * ns);
   }
   __device__ __forceinline__ uint4* H(int k, int n) const {   // {visits, -, value} per action
     return reinterpret_cast<uint4*>(nb[k] + (int64_t)n * ns + 32);
   }
-  __device__ __forceinline__ uint4* T(int k, int n) const {   // {total, agg} per action
-    return reinterpret_cast<uint4*>(nb[k] + (int64_t)n * ns + 128);
+  // action a's record: words 0-1 total, slot i = words 2+3i (okey lo, hi), 4+3i (child)
+  __device__ __forceinline__ uint32_t* R(int k, int n, int a) const {
+    return reinterpret_cast<uint32_t*>(nb[k] + (int64_t)n * ns + ro + (int64_t)a * kImRec);
+  }
+  struct Rec {
+    uint4 w[2];
+  };
+  __device__ __forceinline__ Rec rec(int k, int n, int a) const {
+    const uint4* r = reinterpret_cast<const uint4*>(R(k, n, a));
+    Rec v;
+    v.w[0] = r[0];
+    v.w[1] = r[1];
+    return v;
+  }
+  __device__ __forceinline__ void set_total(int k, int n, int a, double total) const {
+    *reinterpret_cast<uint2*>(R(k, n, a)) =
+        make_uint2((uint32_t)__double2loint(total), (uint32_t)__double2hiint(total));
   }
   // the node and the {visits, -, value} head of every action's statistics,
   // issued together (entries of unregistered actions are never used)
@@ -289,16 +327,23 @@ struct ImPair {
   __device__ uint32_t hkey(uint32_t na, uint64_t okey) const {
     return ovf_hash(na, okey) & (uint32_t)(p.H - 1);
   }
-  __device__ int find(int k, int n, int a, uint64_t okey) {
-    const uint32_t na = ((uint32_t)n << 3) | (uint32_t)a;
-    uint32_t s = hkey(na, okey);
-    for (int64_t probe = 0; probe < p.H; ++probe) {
-      const IHash e = hs[k][s];
-      if (e.child < 0) return -1;
-      if (e.na == na && e.okey == okey) return e.child;
-      s = (s + 1) & (uint32_t)(p.H - 1);
+  // a new obs node, child (n, a, okey) (visits 0); -1 if the arena is full
+  __device__ int new_node(int k, int n, int a, uint64_t okey, int parent_t) {
+    if (h.n_nodes[k] >= p.Nn) {
+      fail(POMCP_E_ARENA);
+      return -1;
     }
-    return -1;
+    const int c = h.n_nodes[k]++;
+    INode x;
+    x.parent = n;
+    x.info = (uint32_t)a;
+    x.visits = 0;
+    x.t = (parent_t >= 0 ? parent_t : N(k, n).t) + 1;
+    x.stats = -1;
+    x.support = kImNoSupport;
+    x.okey = okey;
+    N(k, c) = x;
+    return c;
   }
   // The obs child (n, a, okey); created (visits 0) if missing (INTMCP.traverse /
   // history extension, intmcp.py:797-809, 466).
@@ -306,34 +351,43 @@ struct ImPair {
   // known to the caller (saves reloading the parent).
   __device__ int child(int k, int n, int a, uint64_t okey, bool* created = nullptr,
                        int parent_t = -1) {
-    const uint32_t na = ((uint32_t)n << 3) | (uint32_t)a;
-    const uint32_t s = hkey(na, okey);
-    return child_from(k, n, a, okey, s, hs[k][s], created, parent_t);
+    return child_rec(k, n, a, okey, rec(k, n, a), created, parent_t);
   }
-  // child(), with the first probe (slot s, entry e) already loaded
-  __device__ int child_from(int k, int n, int a, uint64_t okey, uint32_t s, IHash e,
-                            bool* created, int parent_t) {
-    const uint32_t na = ((uint32_t)n << 3) | (uint32_t)a;
+  // child(), with (n, a)'s record r already loaded: the inline slots, then
+  // (both full, neither matching) the hash map.  A (node, action)'s children
+  // fill its inline slots in creation order before any goes to the map, so
+  // a miss with a free slot means the child is missing.
+  __device__ int child_rec(int k, int n, int a, uint64_t okey, const Rec& r, bool* created,
+                           int parent_t) {
+    const uint32_t lo = (uint32_t)okey, hi = (uint32_t)(okey >> 32);
     if (created) *created = false;
+    const int c0 = (int)r.w[1].x, c1 = (int)r.w[1].w;
+    if (c0 != 0 && r.w[0].z == lo && r.w[0].w == hi) return c0;
+    if (c1 != 0 && r.w[1].y == lo && r.w[1].z == hi) return c1;
+    if (c1 == 0) {   // a free inline slot: create the child there
+      if (created) *created = true;
+      const int c = new_node(k, n, a, okey, parent_t);
+      if (c < 0) return -1;
+      uint32_t* w = R(k, n, a);
+      if (c0 == 0) {
+        *reinterpret_cast<uint2*>(w + 2) = make_uint2(lo, hi);
+        w[4] = (uint32_t)c;
+      } else {
+        w[5] = lo;
+        w[6] = hi;
+        w[7] = (uint32_t)c;
+      }
+      return c;
+    }
+    const uint32_t na = ((uint32_t)n << 3) | (uint32_t)a;
+    uint32_t s = hkey(na, okey);
     for (int64_t probe = 0; probe < p.H; ++probe) {
-      if (probe > 0) e = hs[k][s];
+      const IHash e = hs[k][s];
       if (e.child >= 0 && e.na == na && e.okey == okey) return e.child;
       if (e.child < 0) {
         if (created) *created = true;
-        if (h.n_nodes[k] >= p.Nn) {
-          fail(POMCP_E_ARENA);
-          return -1;
-        }
-        const int c = h.n_nodes[k]++;
-        INode x;
-        x.parent = n;
-        x.info = (uint32_t)a;
-        x.visits = 0;
-        x.t = (parent_t >= 0 ? parent_t : N(k, n).t) + 1;
-        x.stats = -1;
-        x.support = kImNoSupport;
-        x.okey = okey;
-        N(k, c) = x;
+        const int c = new_node(k, n, a, okey, parent_t);
+        if (c < 0) return -1;
         IHash ne;
         ne.okey = okey;
         ne.na = na;
@@ -357,23 +411,13 @@ struct ImPair {
       return;
     }
     x.info = (x.info & ~(7u << 5)) | ((uint32_t)(nr + 1) << 5) | ((uint32_t)a << (8 + 3 * nr));
-    if (a < p.A && x.stats < 0) {
+    if (a < p.A && x.stats < 0) {   // the statistics: zero since the arena was cleared
       if (h.n_stats[k] + p.A > p.Ns) {
         fail(POMCP_E_ARENA);
         return;
       }
       x.stats = h.n_stats[k];
       h.n_stats[k] += p.A;
-      for (int q = 0; q < p.A; ++q) {
-        IStat z;
-        z.visits = 0;
-        z.pad = 0;
-        z.value = 0.0;
-        z.total = 0.0;
-        z.agg = 0.0;
-        H(k, n)[q] = make_uint4(0, 0, 0, 0);
-        T(k, n)[q] = make_uint4(0, 0, 0, 0);
-      }
     }
   }
   // reg() of node n whose INode the caller holds current (x, updated): no reads
@@ -393,10 +437,6 @@ struct ImPair {
       }
       x.stats = h.n_stats[k];
       h.n_stats[k] += p.A;
-      for (int q = 0; q < p.A; ++q) {
-        H(k, n)[q] = make_uint4(0, 0, 0, 0);
-        T(k, n)[q] = make_uint4(0, 0, 0, 0);
-      }
       N(k, n).stats = x.stats;
     }
     N(k, n).info = x.info;
@@ -438,10 +478,6 @@ struct ImPair {
       }
       x.stats = h.n_stats[k];
       h.n_stats[k] += p.A;
-      for (int q = 0; q < p.A; ++q) {
-        H(k, n)[q] = make_uint4(0, 0, 0, 0);
-        T(k, n)[q] = make_uint4(0, 0, 0, 0);
-      }
       N(k, n).stats = x.stats;
     }
     x.info = info;
@@ -650,15 +686,16 @@ struct ImPair {
 
   // ----------------------------------------------------------- simulate
   // INTMCP._simulate (intmcp.py:444-517) from node n of tree k; returns the
-  // search depth.  Each level loads the child's whole block (node +
-  // statistics) once: it updates the child's visits / flags and is the next
-  // level's view.  The path keeps each level's statistics as they were before
-  // (visits, value, total, agg), so the backup writes without reading; the
-  // first kImRegPath levels stay in registers.
+  // search depth.  Each level loads the child's line (node + statistics
+  // heads) once: it updates the child's visits / flags and is the next
+  // level's view; and the chosen action's record (total, obs children).  The
+  // path keeps each level's statistics as they were before (visits, value,
+  // total), so the backup writes without reading; the first kImRegPath levels
+  // stay in registers.
   __device__ int simulate(int k, uint32_t s0, uint32_t s1, uint32_t nested, int n, View v) {
     int depth = 0, plen = 0;
     double leaf = 0.0;
-    uint4 rp[kImRegPath][3];   // {n, a, done, -}, {r, value0}, {total0, agg0} | visits0 in [0].w
+    uint4 rp[kImRegPath][3];   // {n, a, done, visits0}, {r, value0}, {total0, -}
     View nv;                   // the other agent's history node (level 1), prefetched
     bool have_nv = false;
     INode pnx;                 // the previous level's history node, as it is now
@@ -679,8 +716,10 @@ struct ImPair {
         break;          // not once per depth at which some lane reached a leaf
       }
       const int a = select(k, v);
-      // the chosen action's {total, agg}: needed by the backup only (no wait)
-      const uint4 s2 = T(k, n)[a];
+      // the chosen action's record: its obs children (found once the step has
+      // produced the observation) and total (for the backup), in flight
+      // while the other agent's action and the step are computed
+      const Rec ra = rec(k, n, a);
       uint4 sa = v.sh[0];
 #pragma unroll
       for (int q = 1; q < kImMaxA; ++q)
@@ -697,6 +736,10 @@ struct ImPair {
       } else {
         ao = other_action(k, nested);
       }
+      // at level 1, the record of the other agent's history extension
+      // (nested, ao), in flight during the step
+      Rec rn;
+      if (k == 0) rn = rec(1, (int)nested, ao);
       uint32_t n0, n1, nn = 0u;
       double r;
       int done;
@@ -704,21 +747,13 @@ struct ImPair {
       const uint32_t j = Env::kStepDraws ? d_model(2) : 0u;
       Env::step(m, me, s0, s1, (uint32_t)a, (uint32_t)ao, j, &n0, &n1, &r, &done);
       const uint64_t okey = Env::obs_key(m, me, n0, n1);
-      // the child (a, obs) here and, at level 1, the other agent's history
-      // extension: both first probes in flight together, one probe chain each
-      const uint32_t na = ((uint32_t)n << 3) | (uint32_t)a;
-      const uint32_t hsl = hkey(na, okey);
-      const IHash he = hs[k][hsl];
       if (k == 0) {
         const uint64_t ok = Env::obs_key(m, p.other, n0, n1);
-        const uint32_t nna = ((uint32_t)nested << 3) | (uint32_t)ao;
-        const uint32_t nsl = hkey(nna, ok);
-        const IHash ne = hs[1][nsl];
-        const int cn = child_from(1, (int)nested, ao, ok, nsl, ne, nullptr, -1);
+        const int cn = child_rec(1, (int)nested, ao, ok, rn, nullptr, -1);
         nn = cn < 0 ? 0u : (uint32_t)cn;
       }
-      bool created;   // one probe chain: found, or created where the probe ended
-      const int c = child_from(k, n, a, okey, hsl, he, &created, x.t);
+      bool created;
+      const int c = child_rec(k, n, a, okey, ra, &created, x.t);
       if (c < 0) return depth;
       if (nested_k) {   // the next level's other-agent view (no wait)
         nv = view(1, (int)nn);
@@ -740,6 +775,7 @@ struct ImPair {
       }
       const uint4 e0 = make_uint4((uint32_t)n, (uint32_t)a, (uint32_t)done, sa.x);
       const uint4 e1 = make_uint4((uint32_t)__double2loint(r), (uint32_t)__double2hiint(r), sa.z, sa.w);
+      const uint4 s2 = make_uint4(ra.w[0].x, ra.w[0].y, 0u, 0u);   // total0
       if (plen < kImRegPath) {
 #pragma unroll
         for (int l = 0; l < kImRegPath; ++l)
@@ -770,15 +806,12 @@ struct ImPair {
       const int vis = (int)e0.w + 1;
       const double value0 = hilo_d(e1.z, e1.w);
       const double total = hilo_d(e2.x, e2.y) + g;
-      const double delta = g - value0;
-      const double value = value0 + delta / (double)vis;
-      const double agg = hilo_d(e2.z, e2.w) + delta * (g - value);
+      const double value = value0 + (g - value0) / (double)vis;
       const uint4 head = make_uint4((uint32_t)vis, 0u, (uint32_t)__double2loint(value),
                                     (uint32_t)__double2hiint(value));
       H(k, (int)e0.x)[e0.y] = head;
       if (k == 0 && (int)e0.x == rv_root) rv[(2 + e0.y) * kWave] = head;   // the cached root view
-      T(k, (int)e0.x)[e0.y] = make_uint4((uint32_t)__double2loint(total), (uint32_t)__double2hiint(total),
-                                         (uint32_t)__double2loint(agg), (uint32_t)__double2hiint(agg));
+      set_total(k, (int)e0.x, (int)e0.y, total);
       mm_update(k, value);
     };
     for (int l = plen - 1; l >= kImRegPath; --l) {

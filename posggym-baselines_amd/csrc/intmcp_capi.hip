@@ -39,15 +39,16 @@ __global__ __launch_bounds__(64) void k_im_root_stats(ImParams d, intmcp_root_st
   const int nr = im_nreg(node.info);
   o.num_children = nr;
   if (node.stats >= 0) {
-    const uint4* hv = reinterpret_cast<const uint4*>(blk + 32);    // node block: intmcp.hip
-    const uint4* tv = reinterpret_cast<const uint4*>(blk + 128);
+    const uint4* hv = reinterpret_cast<const uint4*>(blk + 32);    // node line: intmcp.hip
+    const char* rv = blk + im_rec_delta(d.B, t);                   // its action records
     for (int i = 0; i < nr && i < POMCP_MAX_ACTIONS; ++i) {
       const int a = im_order(node.info, i);
       o.child_action[i] = a;
       if (a < d.A) {
+        const uint2 tot = *reinterpret_cast<const uint2*>(rv + kImRec * a);
         o.child_visits[i] = (int)hv[a].x;
         o.child_values[i] = hilo_d(hv[a].z, hv[a].w);
-        o.child_totals[i] = hilo_d(tv[a].x, tv[a].y);
+        o.child_totals[i] = hilo_d(tot.x, tot.y);
       }
     }
   }
@@ -101,15 +102,18 @@ static int im_copy(intmcp_ctx* ctx, T* dst, const T* src, size_t n) {
   return POMCP_OK;
 }
 
-// blocks 0..n-1 of one tree of one pair, packed (the device layout interleaves
-// them by wave: im_node_off)
+// nodes 0..n-1 of one tree of one pair, packed as [n][kImBlock] (line, then
+// the action records; the device layout interleaves them by wave:
+// im_node_off, im_rec_delta)
 static int im_copy_blocks(intmcp_ctx* ctx, std::vector<char>& out, int pair, int tree, int n) {
   out.resize((size_t)n * kImBlock);
   if (n == 0) return POMCP_OK;
-  IM_TRY(ctx, hipMemcpy2DAsync(out.data(), kImBlock,
-                               ctx->ip.nodes + im_node_off(ctx->ip.Nn, ctx->ip.B, pair, tree, 0),
-                               im_node_stride(ctx->ip.B, pair), kImBlock, n, hipMemcpyDeviceToHost,
+  const char* line0 = ctx->ip.nodes + im_node_off(ctx->ip.Nn, ctx->ip.B, pair, tree, 0);
+  const size_t ns = (size_t)im_node_stride(ctx->ip.B, pair);
+  IM_TRY(ctx, hipMemcpy2DAsync(out.data(), kImBlock, line0, ns, kImLine, n, hipMemcpyDeviceToHost,
                                ctx->stream));
+  IM_TRY(ctx, hipMemcpy2DAsync(out.data() + kImLine, kImBlock, line0 + im_rec_delta(ctx->ip.B, pair),
+                               ns, kImRecs, n, hipMemcpyDeviceToHost, ctx->stream));
   IM_TRY(ctx, hipStreamSynchronize(ctx->stream));
   return POMCP_OK;
 }
@@ -277,6 +281,10 @@ int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, in
 int intmcp_reset(intmcp_ctx* ctx) {
   if (!ctx) return POMCP_E_INVALID;
   IM_TRY(ctx, hipSetDevice(ctx->device));
+  // node lines and records start zeroed: statistics and inline child slots
+  // need no initialising writes (intmcp.hip, kImBlock)
+  IM_TRY(ctx, hipMemsetAsync(ctx->ip.nodes, 0, (size_t)ctx->ip.B * 2 * ctx->ip.Nn * kImBlock,
+                             ctx->stream));
   const int64_t slots = (int64_t)ctx->ip.B * 2 * ctx->ip.H;
   const int64_t cblocks = std::min<int64_t>((slots + 255) / 256, 256 * 64);
   hipLaunchKernelGGL(k_im_clear_hash, dim3((unsigned)cblocks), dim3(256), 0, ctx->stream, ctx->ip.hash,
@@ -448,13 +456,13 @@ int intmcp_get_stats(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int
     if (x->stats < 0) continue;
     for (int a = 0; a < ctx->ip.A && x->stats + a < n; ++a)
     {
-      const char* bk = blocks.data() + (size_t)i * ns;   // head {visits, -, value}, tail {total, agg}
+      const char* bk = blocks.data() + (size_t)i * ns;   // head {visits, -, value}; record {total, ...}
       IStat st;
       std::memcpy(&st.visits, bk + 32 + 16 * (size_t)a, 4);
       st.pad = 0;
       std::memcpy(&st.value, bk + 32 + 16 * (size_t)a + 8, 8);
-      std::memcpy(&st.total, bk + 128 + 16 * (size_t)a, 8);
-      std::memcpy(&st.agg, bk + 128 + 16 * (size_t)a + 8, 8);
+      std::memcpy(&st.total, bk + kImLine + kImRec * (size_t)a, 8);
+      st.agg = 0.0;   // not kept
       o[x->stats + a] = st;
     }
   }

@@ -47,11 +47,13 @@ from posggym_baselines_amd.planning.search_policy import RandomSearchPolicy
 from posggym_baselines_amd.planning.utils import PlanningStatTracker
 
 INT32_MAX = 2**31 - 1
+# a node's device bytes: its 128 B line + six 32 B action records (csrc/intmcp.hip kImBlock)
+INTMCP_NODE_BYTES = 320
 
 
 @dataclass
 class IntmcpCapacities:
-    max_nodes: int              # obs nodes per tree (256 B node block each: node + statistics)
+    max_nodes: int              # obs nodes per tree (320 B each: node line + action records)
     max_stats: int              # action statistics per tree (allocation counter limit)
     max_log: int                # particle log records per tree (16 B)
     hash_slots: int             # obs-child map slots per tree (16 B)
@@ -61,7 +63,7 @@ class IntmcpCapacities:
     discount_pow_size: int
 
     def bytes_per_pair(self, num_actions: int = 5) -> int:
-        return (2 * (self.max_nodes * 256 + self.max_log * 16
+        return (2 * (self.max_nodes * INTMCP_NODE_BYTES + self.max_log * 16
                      + self.hash_slots * 16) + 4 * self.max_root_belief * 16
                 + 2 * self.max_support_particles * 8 + self.max_root_belief * 8)
 
@@ -117,10 +119,10 @@ def plan_intmcp_wallclock_capacities(config, step_limit: int, num_actions: int,
     sims = max(64, math.ceil(per_level * INTMCP_WALL_CLOCK_SIMS_PER_S))
     searches = (step_limit if step_limit < INT32_MAX else 100) + 1
     caps = plan_intmcp_capacities(config, step_limit, sims, searches, num_actions)
-    # per node and pair: two trees x (256 B block + 16 B log record + <=64 B of
+    # per node and pair: two trees x (320 B node + 16 B log record + <=64 B of
     # hash slots); per-search arrays (root belief, support) keep their worst case
-    per_node = 2 * (256 + 16 + 64)
-    fixed = caps.bytes_per_pair(num_actions) - caps.max_nodes * 2 * 256 \
+    per_node = 2 * (INTMCP_NODE_BYTES + 16 + 64)
+    fixed = caps.bytes_per_pair(num_actions) - caps.max_nodes * 2 * INTMCP_NODE_BYTES \
         - caps.max_log * 2 * 16 - caps.hash_slots * 2 * 16
     nodes = (INTMCP_WALL_CLOCK_HBM_BUDGET - fixed) // per_node
     nodes = max(1 << 16, min(caps.max_nodes, nodes, _INTMCP_ID_LIMIT))

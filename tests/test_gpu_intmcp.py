@@ -48,6 +48,23 @@ def test_batched_pairs_match_oracle(env, ego, sel, B):
         assert got[b] == exp, f"pair {b}"
 
 
+@pytest.mark.parametrize("env", ["Driving-v1", "PursuitEvasion-v1"])
+def test_bench_workload_pairs_match_oracle(env):
+    """The bench's 256 simulations per level (bench.py --planner intmcp,
+    TEST_CFG of the bench), 3 lockstep steps of 130 pairs: sampled pairs equal
+    the oracle planner with their tree key (every step record, incl. the
+    level-0 nodes the root's histories name)."""
+    from gpu_util import batched_intmcp_episodes
+    from oracle.run import oracle_intmcp_episode
+    seeds = [900 + b for b in range(130)]
+    steps, sims = 3, 256
+    got = batched_intmcp_episodes(TEST_CFG, sims, seeds, steps, env=env, ego="0")
+    for b in (0, 65, 129):
+        _, exp = oracle_intmcp_episode(TEST_CFG, sims, seeds[b], ego="0", tree=b,
+                                       max_steps=steps, env=env)
+        assert got[b] == exp, f"pair {b}"
+
+
 def test_batched_many_pairs_properties():
     """4096 pairs, one step: every pair searched 2 x num_sims simulations, its
     level-1 root visits equal num_sims, and the root's children visits sum to it."""
