@@ -28,6 +28,7 @@ struct EnvDriving {
   using Model = DrvModel;
   static constexpr int kStepDraws = 1;
   static constexpr int kEnvId = POMCP_ENV_DRIVING;
+  static constexpr int kA = 5;   // actions per agent
 
   __device__ static __forceinline__ void step(const Model& m, int ego, uint32_t s0, uint32_t s1,
                                               uint32_t a_ego, uint32_t a_oth, uint32_t j,
@@ -76,6 +77,7 @@ struct EnvPursuitEvasion {
   using Model = PeModel;
   static constexpr int kStepDraws = 0;
   static constexpr int kEnvId = POMCP_ENV_PURSUIT_EVASION;
+  static constexpr int kA = 4;   // actions per agent
 
   __device__ static __forceinline__ void step(const Model& m, int ego, uint32_t s0, uint32_t s1,
                                               uint32_t a_ego, uint32_t a_oth, uint32_t /*j*/,

@@ -60,7 +60,9 @@ __host__ __device__ inline double host_exp_special(double tmp, uint64_t sbits, u
   return y * 0x1p-1022;
 }
 
-__host__ __device__ inline double host_exp(double x) {
+// tab: kHostExpTab or a copy of it (a kernel may stage it in LDS: the
+// lookup is otherwise a dependent global load per exp)
+__host__ __device__ inline double host_exp_tab(double x, const uint64_t* tab) {
   constexpr double kInvLn2N = 0x1.71547652b82fep7;    // 128 / ln 2
   constexpr double kShift = 0x1.8p52;
   constexpr double kNegLn2hiN = -0x1.62e42fefa0000p-8;
@@ -86,8 +88,8 @@ __host__ __device__ inline double host_exp(double x) {
   const double r = hx_fma(kd, kNegLn2loN, hx_fma(kd, kNegLn2hiN, x));
   const uint32_t idx = 2u * (uint32_t)(ki & 127u);
   const uint64_t top = ki << 45;
-  const double tail = hx_dbl(kHostExpTab[idx]);
-  const uint64_t sbits = kHostExpTab[idx + 1] + top;
+  const double tail = hx_dbl(tab[idx]);
+  const uint64_t sbits = tab[idx + 1] + top;
   const double r2 = r * r;
   const double p23 = hx_fma(r, kC3, kC2);
   const double p45 = hx_fma(r, kC5, kC4);
@@ -96,5 +98,7 @@ __host__ __device__ inline double host_exp(double x) {
   const double scale = hx_dbl(sbits);
   return hx_fma(scale, tmp, scale);
 }
+
+__host__ __device__ inline double host_exp(double x) { return host_exp_tab(x, kHostExpTab); }
 
 }  // namespace pb

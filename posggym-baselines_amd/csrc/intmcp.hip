@@ -136,7 +136,39 @@ struct ImParams {
   const uint64_t* in_obs;
   int32_t* out;         // [B][2] {root absorbing, error}
   uint64_t* out_obs;    // [B] synthetic roots
+  uint64_t* timing;     // [B][kImPhases] (diagnostics build, -DPOMCP_PHASE_TIMING)
 };
+
+// Phase timing (diagnostics build, -DPOMCP_PHASE_TIMING): per-lane s_memtime
+// deltas per section of k_im_search; each mark first drains every outstanding
+// memory operation, so a section is charged the waits of the loads it issued.
+constexpr int kImPhases = 12;
+enum : int { IP_START = 0, IP_SELECT, IP_OTHER, IP_STEP, IP_CHILD, IP_DESCEND, IP_EXPAND,
+             IP_ROLLOUT, IP_BACKUP, IP_SIMEND };
+#ifdef POMCP_PHASE_TIMING
+#define IM_MARK(slot)                                        \
+  do {                                                       \
+    __builtin_amdgcn_s_waitcnt(0);                           \
+    const uint64_t im_now_ = __builtin_amdgcn_s_memtime();   \
+    pt[slot] += im_now_ - pt_last;                           \
+    pt_last = im_now_;                                       \
+  } while (0)
+#define IM_MARK_P(slot)                                      \
+  do {                                                       \
+    __builtin_amdgcn_s_waitcnt(0);                           \
+    const uint64_t im_now_ = __builtin_amdgcn_s_memtime();   \
+    P.pt[slot] += im_now_ - P.pt_last;                       \
+    P.pt_last = im_now_;                                     \
+  } while (0)
+#elif defined(POMCP_ASM_MARKS)   // analysis builds (-S): section markers in the assembly
+#define IM_MARK(slot) asm volatile(";@@IMARK " #slot)
+#define IM_MARK_P(slot) IM_MARK(slot)
+#else
+#define IM_MARK(slot) \
+  do {                \
+  } while (0)
+#define IM_MARK_P(slot) IM_MARK(slot)
+#endif
 
 __device__ __forceinline__ uint32_t im_paction(uint32_t info) { return info & 7u; }
 __host__ __device__ __forceinline__ bool im_absorbing(uint32_t info) { return (info >> 3) & 1u; }
@@ -148,6 +180,7 @@ __host__ __device__ __forceinline__ int im_order(uint32_t info, int k) { return 
 template <class Env>
 struct ImPair {
   using Model = typename Env::Model;
+  static constexpr int kNA = Env::kA;   // == p.A (intmcp_create checks num_actions)
   const ImParams& p;
   const Model& m;
   int pair;
@@ -169,8 +202,10 @@ struct ImPair {
   int lt_n = 0;
   uint4* rv = nullptr;
   int rv_root = -1;
-  // the rollout's discount powers (k_im_search: staged in LDS)
+  // the rollout's discount powers and the exp table of the other agent's
+  // softmax (k_im_search: staged in LDS)
   const double* dp = nullptr;
+  const uint64_t* exp_tab = kHostExpTab;
   // k_im_search only: one-word lookahead per RNG stream.  la_fill computes the
   // next word of every stream whose last word was consumed, at points where the
   // wave waits on a load anyway; draw() consumes it.  Each stream is consumed
@@ -178,6 +213,10 @@ struct ImPair {
   // unconsumed word (la_pend).
   uint32_t la_w[6];
   uint32_t la_pend = 0u;
+#ifdef POMCP_PHASE_TIMING
+  uint64_t pt[kImPhases] = {};
+  uint64_t pt_last = 0;
+#endif
 
   __device__ ImPair(const ImParams& pp, const Model& mm, int b) : p(pp), m(mm), pair(b) {
     for (int k = 0; k < 2; ++k) {
@@ -262,14 +301,14 @@ struct ImPair {
   // issued together (entries of unregistered actions are never used)
   struct View {
     INode x;
-    uint4 sh[kImMaxA];
+    uint4 sh[kNA];
   };
   __device__ __forceinline__ View view(int k, int n) const {
     View v;
     v.x = N(k, n);
     const uint4* s = H(k, n);
 #pragma unroll
-    for (int q = 0; q < kImMaxA; ++q) v.sh[q] = q < p.A ? s[q] : make_uint4(0, 0, 0, 0);
+    for (int q = 0; q < kNA; ++q) v.sh[q] = s[q];
     return v;
   }
   __device__ void rv_put(const View& v) {
@@ -278,14 +317,14 @@ struct ImPair {
     rv[0] = w[0];
     rv[kWave] = w[1];
 #pragma unroll
-    for (int q = 0; q < kImMaxA; ++q) rv[(2 + q) * kWave] = v.sh[q];
+    for (int q = 0; q < kNA; ++q) rv[(2 + q) * kWave] = v.sh[q];
   }
   __device__ View rv_get() const {
     View v;
     uint4 w[2] = {rv[0], rv[kWave]};
     __builtin_memcpy(&v.x, w, sizeof(INode));
 #pragma unroll
-    for (int q = 0; q < kImMaxA; ++q) v.sh[q] = rv[(2 + q) * kWave];
+    for (int q = 0; q < kNA; ++q) v.sh[q] = rv[(2 + q) * kWave];
     return v;
   }
   __device__ void fail(int code) {
@@ -510,9 +549,9 @@ struct ImPair {
 #pragma unroll
     for (int i = 0; i < kImMaxA; ++i) {
       const int a = im_order(v.x.info, i);
-      uint4 r = v.sh[0];
+      uint4 r = make_uint4(0, 0, 0, 0);   // (the None action: no statistics)
 #pragma unroll
-      for (int j = 1; j < kImMaxA; ++j)
+      for (int j = 0; j < kNA; ++j)
         r = sel4(j == a, v.sh[j], r);
       q[i] = i < nr ? r : make_uint4(0, 0, 0, 0);
     }
@@ -588,7 +627,7 @@ struct ImPair {
 #pragma unroll
     for (int i = 0; i < kImMaxA; ++i) {
       if (i >= nr) break;
-      pr[i] = host_exp((double)(int)q[i].x / sq);   // == math.exp (host_exp.h)
+      pr[i] = host_exp_tab((double)(int)q[i].x / sq, exp_tab);   // == math.exp (host_exp.h)
       total = i == 0 ? pr[i] : total + pr[i];
     }
     // random.choices(children, weights=p / sum): cum weights, x = random() * total
@@ -712,6 +751,7 @@ struct ImPair {
       if (im_nreg(x.info) < p.A) {                 // leaf: add the missing children
         INode xe = x;
         expand_known(k, n, xe);
+        IM_MARK(IP_EXPAND);
         roll_t = x.t;   // the rollout runs after the loop: once for the whole wave,
         break;          // not once per depth at which some lane reached a leaf
       }
@@ -719,10 +759,11 @@ struct ImPair {
       // the chosen action's record: its obs children (found once the step has
       // produced the observation) and total (for the backup), in flight
       // while the other agent's action and the step are computed
+      IM_MARK(IP_SELECT);
       const Rec ra = rec(k, n, a);
       uint4 sa = v.sh[0];
 #pragma unroll
-      for (int q = 1; q < kImMaxA; ++q)
+      for (int q = 1; q < kNA; ++q)
         sa = sel4(q == a, v.sh[q], sa);
       // the other agent's action (intmcp.py:602-615): at level 1 its
       // history node's view was loaded when the previous level created it
@@ -738,6 +779,7 @@ struct ImPair {
       }
       // at level 1, the record of the other agent's history extension
       // (nested, ao), in flight during the step
+      IM_MARK(IP_OTHER);
       Rec rn;
       if (k == 0) rn = rec(1, (int)nested, ao);
       uint32_t n0, n1, nn = 0u;
@@ -747,13 +789,15 @@ struct ImPair {
       const uint32_t j = Env::kStepDraws ? d_model(2) : 0u;
       Env::step(m, me, s0, s1, (uint32_t)a, (uint32_t)ao, j, &n0, &n1, &r, &done);
       const uint64_t okey = Env::obs_key(m, me, n0, n1);
+      const uint64_t ok = k == 0 ? Env::obs_key(m, p.other, n0, n1) : 0ull;
+      IM_MARK(IP_STEP);
       if (k == 0) {
-        const uint64_t ok = Env::obs_key(m, p.other, n0, n1);
-        const int cn = child_rec(1, (int)nested, ao, ok, rn, nullptr, -1);
+        const int cn = child_rec(1, (int)nested, ao, ok, rn, nullptr, nested_k ? nv.x.t : -1);
         nn = cn < 0 ? 0u : (uint32_t)cn;
       }
       bool created;
       const int c = child_rec(k, n, a, okey, ra, &created, x.t);
+      IM_MARK(IP_CHILD);
       if (c < 0) return depth;
       if (nested_k) {   // the next level's other-agent view (no wait)
         nv = view(1, (int)nn);
@@ -790,6 +834,7 @@ struct ImPair {
         path[plen * 3 + 2] = make_int4((int)s2.x, (int)s2.y, (int)s2.z, (int)s2.w);
       }
       ++plen;
+      IM_MARK(IP_DESCEND);
       if (done) break;
       n = c;
       v = cv;
@@ -799,6 +844,7 @@ struct ImPair {
       ++depth;
     }
     if (roll_t >= 0) leaf = rollout(k, s0, s1, roll_t, depth);
+    IM_MARK(IP_ROLLOUT);
     double g = leaf;
     auto backup = [&](uint4 e0, uint4 e1, uint4 e2) {   // node.py:166-178
       const double r = hilo_d(e1.x, e1.y);
@@ -822,6 +868,7 @@ struct ImPair {
 #pragma unroll
     for (int l = kImRegPath - 1; l >= 0; --l)
       if (l < plen) backup(rp[l][0], rp[l][1], rp[l][2]);
+    IM_MARK(IP_BACKUP);
     return depth;
   }
 
@@ -1315,6 +1362,8 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
   __shared__ double slog[kImLogLds];                  // math.log(N): no global load per selection
   __shared__ uint4 srv[kImRootWords * kWave];         // level-1 root views, one column per lane
   __shared__ double sdp[kImDpowLds];                  // discount powers (rollout)
+  __shared__ uint64_t sexp[256];                      // host_exp's 2^(k/128) table
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) sexp[i] = kHostExpTab[i];
   const int ltn = p.logtab_n < kImLogLds ? (int)p.logtab_n : kImLogLds;
   for (int i = threadIdx.x; i < ltn; i += blockDim.x) slog[i] = p.logtab[i];
   const bool dp_lds = p.dpow_n <= kImDpowLds;
@@ -1328,6 +1377,10 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
   P.lt_n = ltn;
   P.rv = srv + threadIdx.x;
   if (dp_lds) P.dp = sdp;
+  P.exp_tab = sexp;
+#ifdef POMCP_PHASE_TIMING
+  P.pt_last = __builtin_amdgcn_s_memtime();
+#endif
   if (flags & kImBegin) {
     P.h.num_sims = 0;
     P.h.search_depth = 0;
@@ -1387,20 +1440,27 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
           if (im_nreg(v.x.info) == 0) {
             P.expand_known(1, n, v.x);   // nothing registered: fresh, zero statistics
 #pragma unroll
-            for (int q = 0; q < kImMaxA; ++q) v.sh[q] = make_uint4(0, 0, 0, 0);
+            for (int q = 0; q < ImPair<Env>::kNA; ++q) v.sh[q] = make_uint4(0, 0, 0, 0);
           }
+          IM_MARK_P(IP_START);
           P.simulate(1, q.x, q.y, 0u, n, v);
           P.N(1, n).visits = v.x.visits + 1;   // (simulate writes no INode of its start)
         } else {
           const auto v = P.rv_get();
+          IM_MARK_P(IP_START);
           const int d = P.simulate(0, hp.x, hp.y, hp.z, root, v);
           P.N(0, root).visits = v.x.visits + 1;
           P.rv[0].z = (uint32_t)(v.x.visits + 1);   // INode.visits: bytes 8-11
           if (d > P.h.search_depth) P.h.search_depth = d;
         }
         P.h.num_sims += 1;
+        IM_MARK_P(IP_SIMEND);
       }
     }
+#ifdef POMCP_PHASE_TIMING
+    if (p.timing != nullptr)
+      for (int i = 0; i < kImPhases; ++i) p.timing[(int64_t)b * kImPhases + i] += P.pt[i];
+#endif
     if (!(flags & kImFinal) || P.h.err != 0) {   // no action from a failed search
       if (P.h.err != 0 && (flags & kImFinal)) P.h.last_action = -1;
       P.store_search();

@@ -469,6 +469,34 @@ int intmcp_get_stats(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int
   return POMCP_OK;
 }
 
+// Debug: per-pair phase cycles of k_im_search (diagnostics build only): the
+// first call allocates and zeroes the counters; later searches add to them.
+int intmcp_debug_phase_timing(intmcp_ctx* ctx, uint64_t* out, int32_t capacity, int32_t* count) {
+  if (!ctx || !count) return POMCP_E_INVALID;
+#ifndef POMCP_PHASE_TIMING
+  (void)out;
+  (void)capacity;
+  *count = 0;
+  return POMCP_E_UNSUPPORTED;
+#else
+  const size_t n = (size_t)kImPhases * (size_t)ctx->ip.B;
+  if (ctx->ip.timing == nullptr) {
+    void* p = nullptr;
+    if (im_alloc(ctx, &p, sizeof(uint64_t) * n) != POMCP_OK) return POMCP_E_HIP;
+    IM_TRY(ctx, hipMemset(p, 0, sizeof(uint64_t) * n));
+    ctx->ip.timing = reinterpret_cast<uint64_t*>(p);
+    *count = 0;
+    return POMCP_OK;
+  }
+  *count = (int32_t)n;
+  if (out && capacity >= *count) {
+    IM_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    IM_TRY(ctx, hipMemcpy(out, ctx->ip.timing, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
+  }
+  return POMCP_OK;
+#endif
+}
+
 int intmcp_get_support(intmcp_ctx* ctx, int32_t pair, int32_t* entries, int32_t capacity_entries,
                        int32_t* n_entries, uint32_t* particles, int32_t capacity_particles,
                        int32_t* n_particles) {
