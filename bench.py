@@ -416,6 +416,11 @@ def main_intmcp(args):
     alg_bytes = (B_SIM * sims_timed + b_level(A) * (lv0 + lv1) + b_other(A) * lv1
                  + B_NODE_IM * nodes) / args.steps
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    # the level-1 root's view (node + statistics heads) is served from LDS
+    # (ImPair::rv): those bytes of every level-1 simulation's root level never
+    # reach HBM
+    alg_bytes_hbm = alg_bytes - (8 + 12 * A) * S * searched
+    achieved_hbm = alg_bytes_hbm / (kernel_ms * 1e-3) / 1e9
     traffic = _pmc_traffic("pmc_intmcp.json", lib_sha, trees=B, sims=S, env=args.env)
     out = {
         "metric": f"I-NTMCP simulations/sec on {args.env} (nesting level 1, exact search)",
@@ -443,7 +448,9 @@ def main_intmcp(args):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "k_im_search", "kernel_ms": kernel_ms,
-                     "alg_bytes_per_launch": alg_bytes},
+                     "alg_bytes_per_launch": alg_bytes,
+                     "alg_bytes_hbm_per_launch": alg_bytes_hbm,
+                     "achieved_hbm": achieved_hbm, "frac_hbm": achieved_hbm / HBM_PEAK_GBS},
     }
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_intmcp(2048, 16, args.seed, args.env)

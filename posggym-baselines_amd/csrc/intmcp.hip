@@ -24,7 +24,14 @@
 
 namespace pb {
 
-constexpr int kImPath = 128;          // tree levels per simulation
+constexpr int kImPath = 128;
+// Widening factor of the bounded FP32 fast path of the other agent's
+// softmax (ImPair::sample_action).  Test builds set it
+// large so that the exact fallbacks run often (tests/test_gpu_intmcp.py
+// parity under tools/ab_im.sh variants); any value >= 1 keeps results exact.
+#ifndef IM_FAST_SLACK
+#define IM_FAST_SLACK 1.0f
+#endif          // tree levels per simulation
 constexpr int kImMaxA = 6;            // registration order: 6 x 3 bits (INode.info)
 constexpr int kImRegPath = 3;         // path levels held in registers (deeper ones in p.path)
 // A node: its line (128 B) = the INode (32 B) + the head {visits, -, value}
@@ -564,6 +571,12 @@ struct ImPair {
     uint4 q[kImMaxA];
     child_stats(v, nr, q);
     if (p.sel == POMCP_SEL_UCB) {
+      // the first unvisited child in registration order, if any
+      int zero = -1;
+#pragma unroll
+      for (int i = kImMaxA - 1; i >= 0; --i)
+        if (i < nr && q[i].x == 0u) zero = i;
+      if (zero >= 0) return im_order(x.info, zero);
       const double log_n = logn(x.visits);
       double best = -__builtin_inf();
       int ba = 0;
@@ -574,8 +587,11 @@ struct ImPair {
         if (i >= nr) break;
         const int a = im_order(x.info, i);
         const int sv = (int)q[i].x;
-        if (sv == 0) return a;
+#ifdef IM_ABLATE_SELECT   // ablation build only (measurement): no FP64 div / sqrt
+        const double v = hilo_d(q[i].z, q[i].w) + p.c * log_n * (double)sv;
+#else
         const double v = normalize(k, hilo_d(q[i].z, q[i].w)) + p.c * sqrt(log_n / (double)sv);
+#endif
         if (v > best) {
           best = v;
           ba = a;
@@ -619,15 +635,56 @@ struct ImPair {
     const INode& x = v.x;
     const int nr = im_nreg(x.info);
     if (x.visits == 0 || nr == 0) return (int)d_act(p.other, (uint32_t)p.A);
-    const double sq = sqrt((double)x.visits);
     uint4 q[kImMaxA];
     child_stats(v, nr, q);
+    const double d = d_sel_float();   // random.choices' random() (the stream's only draw here)
+#ifndef IM_EXACT_SOFTMAX
+    // The choice from bounded FP32 weights: p_i = 2^(x_i log2 e), x_i =
+    // visits_i / sqrt(N), relative error < x 2.4e-7 + 1.2e-7 (1-ulp rsq / exp2,
+    // FP32 rounding); the cumulative weights c_i are then within
+    // E/2 = 4.8e-7 x_max + 1.2e-6 of the exact FP64 ones (c <= 1), u = random()
+    // within 6e-8.  When u is farther than E from every c_i the bisection's
+    // answer is the exact one; otherwise (~1e-3 of draws) the exact FP64
+    // softmax below decides.  (IM_EXACT_SOFTMAX: the exact path only.)
+    {
+      const float rs = __builtin_amdgcn_rsqf((float)x.visits);
+      float pf[kImMaxA];
+      float tot = 0.0f, xmax = 0.0f;
+#pragma unroll
+      for (int i = 0; i < kImMaxA; ++i) {
+        const float t = (float)q[i].x * rs;
+        pf[i] = i < nr ? __builtin_amdgcn_exp2f(t * 1.44269504f) : 0.0f;
+        if (i < nr) xmax = __builtin_fmaxf(xmax, t);
+        tot += pf[i];
+      }
+      const float rt = __builtin_amdgcn_rcpf(tot);
+      const float E = IM_FAST_SLACK * (1e-6f * xmax + 2.4e-6f);
+      const float uf = (float)d;
+      bool amb = !(xmax <= 80.0f);
+      int lo = nr - 1;
+      float acc = 0.0f;
+#pragma unroll
+      for (int i = 0; i < kImMaxA - 1; ++i) {
+        if (i < nr - 1) {
+          acc += pf[i] * rt;
+          amb |= __builtin_fabsf(uf - acc) <= E;
+          if (lo == nr - 1 && uf < acc) lo = i;
+        }
+      }
+      if (!amb) return im_order(x.info, lo);
+    }
+#endif
+    const double sq = sqrt((double)x.visits);
     double pr[kImMaxA];
     double total = 0.0;
 #pragma unroll
     for (int i = 0; i < kImMaxA; ++i) {
       if (i >= nr) break;
+#ifdef IM_ABLATE_SOFTMAX   // ablation build only (measurement): no exp / division
+      pr[i] = (double)(int)q[i].x + 1.0;
+#else
       pr[i] = host_exp_tab((double)(int)q[i].x / sq, exp_tab);   // == math.exp (host_exp.h)
+#endif
       total = i == 0 ? pr[i] : total + pr[i];
     }
     // random.choices(children, weights=p / sum): cum weights, x = random() * total
@@ -636,7 +693,11 @@ struct ImPair {
 #pragma unroll
     for (int i = 0; i < kImMaxA; ++i) {
       if (i >= nr) break;
+#ifdef IM_ABLATE_SOFTMAX
+      const double w = pr[i];
+#else
       const double w = pr[i] / total;
+#endif
       acc = i == 0 ? w : acc + w;
       cum[i] = acc;
     }
@@ -644,7 +705,7 @@ struct ImPair {
 #pragma unroll
     for (int i = 1; i < kImMaxA; ++i)
       if (i == nr - 1) last = cum[i];
-    const double u = d_sel_float() * (last + 0.0);
+    const double u = d * (last + 0.0);
     // bisect_right(cum, u, 0, nr - 1) over the non-decreasing cum: the first
     // i < nr - 1 with u < cum[i], else nr - 1 (a scan keeps cum in registers)
     int lo = nr - 1;
