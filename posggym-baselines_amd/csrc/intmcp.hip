@@ -34,8 +34,10 @@ constexpr int kImPath = 128;
 #endif          // tree levels per simulation
 constexpr int kImMaxA = 6;            // registration order: 6 x 3 bits (INode.info)
 constexpr int kImRegPath = 3;         // path levels held in registers (deeper ones in p.path)
-// A node: its line (128 B) = the INode (32 B) + the head {visits, -, value}
-// of each action's statistics (16 B each), and one 32 B action record per
+// A node: its line (128 B) = the INode {parent, info, visits, t} (16 B), the
+// head {visits u32, value f64} of each action's statistics (12 B each, from
+// byte 16) and, at byte 80, the cold fields (ICold: obs key, statistics
+// index, support slot: never read by a simulation); and one 32 B action record per
 // action (the None action A included): the action's total (ActionNode
 // total_value; agg is not kept) and kImInline obs-child slots
 // {obs key, child id} (id 0: empty -- a tree's node 0 is never a child).
@@ -80,17 +82,23 @@ constexpr int32_t kImSkip = -2;       // intmcp_update action: leave the pair un
 constexpr int kWave64 = 64;           // lanes of a wave (k_im_update's wave mode)
 constexpr int kImLogLds = 2048;       // math.log(N) entries staged in LDS by k_im_search
 constexpr int kImDpowLds = 64;        // discount powers staged in LDS by k_im_search
-constexpr int kImRootWords = 8;       // the level-1 root's view (INode + 6 heads) in LDS, uint4s
+constexpr int kImRootWords = 7;       // the level-1 root's view (INode + <= 6 heads) in LDS, uint4s
 
-struct INode {          // 32 B
+struct INode {          // 16 B, line bytes 0-15
   int32_t parent;
   uint32_t info;        // paction:3 | absorbing:1 | path_ok:1 | nreg:3 | order 6 x 3 bits
+                        // | statistics allocated:1 (bit 26)
   int32_t visits;
   int32_t t;
+};
+struct ICold {          // 16 B, line bytes 80-95
+  uint64_t okey;
   int32_t stats;        // first of A IStat entries (-1: none registered yet)
   uint32_t support;     // support slot while materialising beliefs (level-0 tree)
-  uint64_t okey;
 };
+constexpr int64_t kImHeads = 16;      // line byte of action 0's head (12 B each)
+constexpr int64_t kImCold = 80;       // line byte of the ICold
+constexpr uint32_t kImStatsBit = 1u << 26;
 struct IStat {          // 32 B: ActionNode visits / value / total_value / agg
   int32_t visits, pad;
   double value, total, agg;
@@ -182,6 +190,7 @@ __host__ __device__ __forceinline__ bool im_absorbing(uint32_t info) { return (i
 __device__ __forceinline__ bool im_path_ok(uint32_t info) { return (info >> 4) & 1u; }
 __host__ __device__ __forceinline__ int im_nreg(uint32_t info) { return (int)((info >> 5) & 7u); }
 __host__ __device__ __forceinline__ int im_order(uint32_t info, int k) { return (int)((info >> (8 + 3 * k)) & 7u); }
+__device__ __forceinline__ bool im_has_stats(uint32_t info) { return (info & kImStatsBit) != 0u; }
 
 // One planner pair (lane): pointers, counters, RNG.
 template <class Env>
@@ -283,8 +292,11 @@ struct ImPair {
   __device__ __forceinline__ INode& N(int k, int n) const {
     return *reinterpret_cast<INode*>(nb[k] + (int64_t)n * ns);
   }
-  __device__ __forceinline__ uint4* H(int k, int n) const {   // {visits, -, value} per action
-    return reinterpret_cast<uint4*>(nb[k] + (int64_t)n * ns + 32);
+  __device__ __forceinline__ ICold& C(int k, int n) const {
+    return *reinterpret_cast<ICold*>(nb[k] + (int64_t)n * ns + kImCold);
+  }
+  __device__ __forceinline__ uint32_t* H(int k, int n, int a) const {   // {visits, value} of action a
+    return reinterpret_cast<uint32_t*>(nb[k] + (int64_t)n * ns + kImHeads + 12 * (int64_t)a);
   }
   // action a's record: words 0-1 total, slot i = words 2+3i (okey lo, hi), 4+3i (child)
   __device__ __forceinline__ uint32_t* R(int k, int n, int a) const {
@@ -304,34 +316,56 @@ struct ImPair {
     *reinterpret_cast<uint2*>(R(k, n, a)) =
         make_uint2((uint32_t)__double2loint(total), (uint32_t)__double2hiint(total));
   }
-  // the node and the {visits, -, value} head of every action's statistics,
-  // issued together (entries of unregistered actions are never used)
+  // the node and the head of every action's statistics as {visits, -,
+  // value} (entries of unregistered actions are never used): the line's
+  // first 16 + 12 A bytes, ceil((16 + 12 A) / 16) loads
   struct View {
     INode x;
     uint4 sh[kNA];
   };
+  static constexpr int kViewLoads = (int)((kImHeads + 12 * kNA + 15) / 16);
   __device__ __forceinline__ View view(int k, int n) const {
-    View v;
-    v.x = N(k, n);
-    const uint4* s = H(k, n);
+    const uint4* l = reinterpret_cast<const uint4*>(nb[k] + (int64_t)n * ns);
+    uint32_t w[4 * kViewLoads];
 #pragma unroll
-    for (int q = 0; q < kNA; ++q) v.sh[q] = s[q];
+    for (int i = 0; i < kViewLoads; ++i) {
+      const uint4 u = l[i];
+      w[4 * i] = u.x;
+      w[4 * i + 1] = u.y;
+      w[4 * i + 2] = u.z;
+      w[4 * i + 3] = u.w;
+    }
+    View v;
+    v.x.parent = (int32_t)w[0];
+    v.x.info = w[1];
+    v.x.visits = (int32_t)w[2];
+    v.x.t = (int32_t)w[3];
+#pragma unroll
+    for (int q = 0; q < kNA; ++q) v.sh[q] = make_uint4(w[4 + 3 * q], 0u, w[5 + 3 * q], w[6 + 3 * q]);
+    return v;
+  }
+  // a node just created (INode x, zero statistics): its view without a load
+  __device__ __forceinline__ static View fresh_view(const INode& x) {
+    View v;
+    v.x = x;
+#pragma unroll
+    for (int q = 0; q < kNA; ++q) v.sh[q] = make_uint4(0, 0, 0, 0);
     return v;
   }
   __device__ void rv_put(const View& v) {
-    uint4 w[2];
-    __builtin_memcpy(w, &v.x, sizeof(INode));
-    rv[0] = w[0];
-    rv[kWave] = w[1];
+    rv[0] = make_uint4((uint32_t)v.x.parent, v.x.info, (uint32_t)v.x.visits, (uint32_t)v.x.t);
 #pragma unroll
-    for (int q = 0; q < kNA; ++q) rv[(2 + q) * kWave] = v.sh[q];
+    for (int q = 0; q < kNA; ++q) rv[(1 + q) * kWave] = v.sh[q];
   }
   __device__ View rv_get() const {
     View v;
-    uint4 w[2] = {rv[0], rv[kWave]};
-    __builtin_memcpy(&v.x, w, sizeof(INode));
+    const uint4 w = rv[0];
+    v.x.parent = (int32_t)w.x;
+    v.x.info = w.y;
+    v.x.visits = (int32_t)w.z;
+    v.x.t = (int32_t)w.w;
 #pragma unroll
-    for (int q = 0; q < kNA; ++q) v.sh[q] = rv[(2 + q) * kWave];
+    for (int q = 0; q < kNA; ++q) v.sh[q] = rv[(1 + q) * kWave];
     return v;
   }
   __device__ void fail(int code) {
@@ -373,8 +407,10 @@ struct ImPair {
   __device__ uint32_t hkey(uint32_t na, uint64_t okey) const {
     return ovf_hash(na, okey) & (uint32_t)(p.H - 1);
   }
-  // a new obs node, child (n, a, okey) (visits 0); -1 if the arena is full
-  __device__ int new_node(int k, int n, int a, uint64_t okey, int parent_t) {
+  // a new obs node, child (n, a, okey) (visits 0); -1 if the arena is full.
+  // hot = false: the caller writes the INode itself (*xo)
+  __device__ int new_node(int k, int n, int a, uint64_t okey, int parent_t, INode* xo = nullptr,
+                          bool hot = true) {
     if (h.n_nodes[k] >= p.Nn) {
       fail(POMCP_E_ARENA);
       return -1;
@@ -385,10 +421,13 @@ struct ImPair {
     x.info = (uint32_t)a;
     x.visits = 0;
     x.t = (parent_t >= 0 ? parent_t : N(k, n).t) + 1;
-    x.stats = -1;
-    x.support = kImNoSupport;
-    x.okey = okey;
-    N(k, c) = x;
+    if (hot) N(k, c) = x;
+    ICold o;
+    o.okey = okey;
+    o.stats = -1;
+    o.support = kImNoSupport;
+    C(k, c) = o;
+    if (xo) *xo = x;
     return c;
   }
   // The obs child (n, a, okey); created (visits 0) if missing (INTMCP.traverse /
@@ -403,8 +442,9 @@ struct ImPair {
   // (both full, neither matching) the hash map.  A (node, action)'s children
   // fill its inline slots in creation order before any goes to the map, so
   // a miss with a free slot means the child is missing.
+  // xo / hot: as new_node's, for a created child
   __device__ int child_rec(int k, int n, int a, uint64_t okey, const Rec& r, bool* created,
-                           int parent_t) {
+                           int parent_t, INode* xo = nullptr, bool hot = true) {
     const uint32_t lo = (uint32_t)okey, hi = (uint32_t)(okey >> 32);
     if (created) *created = false;
     const int c0 = (int)r.w[1].x, c1 = (int)r.w[1].w;
@@ -412,17 +452,10 @@ struct ImPair {
     if (c1 != 0 && r.w[1].y == lo && r.w[1].z == hi) return c1;
     if (c1 == 0) {   // a free inline slot: create the child there
       if (created) *created = true;
-      const int c = new_node(k, n, a, okey, parent_t);
+      const int c = new_node(k, n, a, okey, parent_t, xo, hot);
       if (c < 0) return -1;
       uint32_t* w = R(k, n, a);
-      if (c0 == 0) {
-        *reinterpret_cast<uint2*>(w + 2) = make_uint2(lo, hi);
-        w[4] = (uint32_t)c;
-      } else {
-        w[5] = lo;
-        w[6] = hi;
-        w[7] = (uint32_t)c;
-      }
+      *reinterpret_cast<uint3*>(w + (c0 == 0 ? 2 : 5)) = make_uint3(lo, hi, (uint32_t)c);
       return c;
     }
     const uint32_t na = ((uint32_t)n << 3) | (uint32_t)a;
@@ -432,7 +465,7 @@ struct ImPair {
       if (e.child >= 0 && e.na == na && e.okey == okey) return e.child;
       if (e.child < 0) {
         if (created) *created = true;
-        const int c = new_node(k, n, a, okey, parent_t);
+        const int c = new_node(k, n, a, okey, parent_t, xo, hot);
         if (c < 0) return -1;
         IHash ne;
         ne.okey = okey;
@@ -457,12 +490,13 @@ struct ImPair {
       return;
     }
     x.info = (x.info & ~(7u << 5)) | ((uint32_t)(nr + 1) << 5) | ((uint32_t)a << (8 + 3 * nr));
-    if (a < p.A && x.stats < 0) {   // the statistics: zero since the arena was cleared
+    if (a < p.A && !im_has_stats(x.info)) {   // the statistics: zero since the arena was cleared
       if (h.n_stats[k] + p.A > p.Ns) {
         fail(POMCP_E_ARENA);
         return;
       }
-      x.stats = h.n_stats[k];
+      x.info |= kImStatsBit;
+      C(k, n).stats = h.n_stats[k];
       h.n_stats[k] += p.A;
     }
   }
@@ -476,14 +510,14 @@ struct ImPair {
       return;
     }
     x.info = (x.info & ~(7u << 5)) | ((uint32_t)(nr + 1) << 5) | ((uint32_t)a << (8 + 3 * nr));
-    if (a < p.A && x.stats < 0) {
+    if (a < p.A && !im_has_stats(x.info)) {
       if (h.n_stats[k] + p.A > p.Ns) {
         fail(POMCP_E_ARENA);
         return;
       }
-      x.stats = h.n_stats[k];
+      x.info |= kImStatsBit;
+      C(k, n).stats = h.n_stats[k];
       h.n_stats[k] += p.A;
-      N(k, n).stats = x.stats;
     }
     N(k, n).info = x.info;
   }
@@ -515,16 +549,16 @@ struct ImPair {
       }
       info = (info & ~(7u << 5)) | ((uint32_t)(nr + 1) << 5) | ((uint32_t)a << (8 + 3 * nr));
       ++nr;
-      alloc |= x.stats < 0;
+      alloc |= !im_has_stats(info);
     }
     if (alloc) {
       if (h.n_stats[k] + p.A > p.Ns) {
         fail(POMCP_E_ARENA);
         return;
       }
-      x.stats = h.n_stats[k];
+      info |= kImStatsBit;
+      C(k, n).stats = h.n_stats[k];
       h.n_stats[k] += p.A;
-      N(k, n).stats = x.stats;
     }
     x.info = info;
     N(k, n).info = info;
@@ -852,19 +886,29 @@ struct ImPair {
       const uint64_t okey = Env::obs_key(m, me, n0, n1);
       const uint64_t ok = k == 0 ? Env::obs_key(m, p.other, n0, n1) : 0ull;
       IM_MARK(IP_STEP);
-      if (k == 0) {
-        const int cn = child_rec(1, (int)nested, ao, ok, rn, nullptr, nested_k ? nv.x.t : -1);
-        nn = cn < 0 ? 0u : (uint32_t)cn;
-      }
+      // the child (a, obs): found in the record, its view loaded; created,
+      // its view is known (the descent writes its INode below).  Then, at
+      // level 1, the other agent's history extension likewise.  (Loads are
+      // issued before the stores of a creation: a wait for a load also waits
+      // for every store issued before it.)
       bool created;
-      const int c = child_rec(k, n, a, okey, ra, &created, x.t);
-      IM_MARK(IP_CHILD);
+      INode cx;
+      const int c = child_rec(k, n, a, okey, ra, &created, x.t, &cx, false);
       if (c < 0) return depth;
-      if (nested_k) {   // the next level's other-agent view (no wait)
-        nv = view(1, (int)nn);
-        have_nv = true;
+      View cv;
+      if (!created) cv = view(k, c);
+      if (k == 0) {
+        bool ncr;
+        INode nx;
+        const int cn = child_rec(1, (int)nested, ao, ok, rn, &ncr, nested_k ? nv.x.t : -1, &nx);
+        nn = cn < 0 ? 0u : (uint32_t)cn;
+        if (nested_k) {   // the next level's other-agent view (no wait)
+          nv = ncr ? fresh_view(nx) : view(1, (int)nn);
+          have_nv = true;
+        }
       }
-      View cv = view(k, c);
+      if (created) cv = fresh_view(cx);
+      IM_MARK(IP_CHILD);
       la_fill();   // the next level's RNG words, while the child's view is in flight
       cv.x.visits = created ? 1 : cv.x.visits + 1;
       uint32_t info = cv.x.info;
@@ -916,8 +960,8 @@ struct ImPair {
       const double value = value0 + (g - value0) / (double)vis;
       const uint4 head = make_uint4((uint32_t)vis, 0u, (uint32_t)__double2loint(value),
                                     (uint32_t)__double2hiint(value));
-      H(k, (int)e0.x)[e0.y] = head;
-      if (k == 0 && (int)e0.x == rv_root) rv[(2 + e0.y) * kWave] = head;   // the cached root view
+      *reinterpret_cast<uint3*>(H(k, (int)e0.x, (int)e0.y)) = make_uint3(head.x, head.z, head.w);
+      if (k == 0 && (int)e0.x == rv_root) rv[(1 + e0.y) * kWave] = head;   // the cached root view
       set_total(k, (int)e0.x, (int)e0.y, total);
       mm_update(k, value);
     };
@@ -942,7 +986,7 @@ struct ImPair {
   // node's `support` field while the caller has that table's slots marked
   // (mark_support), else a scan
   __device__ int find_support(int sel, int n, int count) {
-    const uint32_t s = N(1, n).support;
+    const uint32_t s = C(1, n).support;
     if (s != kImNoSupport) return (int)s < count && sup_tab(sel)[s].node == n ? (int)s : -1;
     const ISup* t = sup_tab(sel);
     for (int i = 0; i < count; ++i)
@@ -951,7 +995,7 @@ struct ImPair {
   }
   __device__ void mark_support(int sel, int count, bool on) {
     const ISup* t = sup_tab(sel);
-    for (int i = 0; i < count; ++i) N(1, t[i].node).support = on ? (uint32_t)i : kImNoSupport;
+    for (int i = 0; i < count; ++i) C(1, t[i].node).support = on ? (uint32_t)i : kImNoSupport;
   }
 
   // BeliefRejectionSampler (belief.py:145-194, use_rejected_samples=True) for a
@@ -1074,12 +1118,12 @@ __device__ void im_support(ImPair<Env>& P, int sel, int size, int* nsup) {
         const int lead = __ffsll((long long)todo) - 1;
         const int ln = __shfl(nodeid, lead);
         const uint64_t peers = __ballot(on && nodeid == ln);
-        int s = (int)P.N(1, ln).support;
-        if (P.N(1, ln).support == kImNoSupport) {
+        int s = (int)P.C(1, ln).support;
+        if (P.C(1, ln).support == kImNoSupport) {
           s = n++;
           tab[s].node = ln;
           tab[s].size = 0;
-          P.N(1, ln).support = (uint32_t)s;
+          P.C(1, ln).support = (uint32_t)s;
         }
         tab[s].size += __popcll(peers);
         if (on && nodeid == ln) rb[i].w = (uint32_t)s;
@@ -1089,18 +1133,18 @@ __device__ void im_support(ImPair<Env>& P, int sel, int size, int* nsup) {
   } else {
     for (int i = 0; i < size; ++i) {
       const int nodeid = (int)rb[i].z;
-      int s = (int)P.N(1, nodeid).support;
-      if (P.N(1, nodeid).support == kImNoSupport) {
+      int s = (int)P.C(1, nodeid).support;
+      if (P.C(1, nodeid).support == kImNoSupport) {
         s = n++;
         tab[s].node = nodeid;
         tab[s].size = 0;   // count for now
-        P.N(1, nodeid).support = (uint32_t)s;
+        P.C(1, nodeid).support = (uint32_t)s;
       }
       tab[s].size += 1;
       rb[i].w = (uint32_t)s;
     }
   }
-  for (int q = 0; q < n; ++q) P.N(1, tab[q].node).support = kImNoSupport;
+  for (int q = 0; q < n; ++q) P.C(1, tab[q].node).support = kImNoSupport;
   for (int q = 0; q < n; ++q) {
     prob[q] = 0.0 + 1.0 * ((double)tab[q].size / (double)size);
     tab[q].size = 0;
@@ -1113,13 +1157,13 @@ __device__ void im_support(ImPair<Env>& P, int sel, int size, int* nsup) {
 template <class Env, bool kWave = false>
 __device__ void im_extract_support(ImPair<Env>& P, int sel, int nsup) {
   ISup* tab = P.sup_tab(sel);
-  for (int q = 0; q < nsup; ++q) P.N(1, tab[q].node).support = (uint32_t)q;
+  for (int q = 0; q < nsup; ++q) P.C(1, tab[q].node).support = (uint32_t)q;
   for (int q = 0; q < nsup; ++q) tab[q].cap = 0;
   const int nlog = P.h.n_log[1];
   if constexpr (kWave) {
     for (int base = 0; base < nlog; base += kWave64) {
       const int i = base + (int)(threadIdx.x & 63);
-      const uint32_t s = i < nlog ? P.N(1, P.lg[1][i].node).support : kImNoSupport;
+      const uint32_t s = i < nlog ? P.C(1, P.lg[1][i].node).support : kImNoSupport;
       uint64_t todo = __ballot(s != kImNoSupport);
       while (todo) {
         const uint32_t ls = (uint32_t)__shfl((int)s, __ffsll((long long)todo) - 1);
@@ -1130,7 +1174,7 @@ __device__ void im_extract_support(ImPair<Env>& P, int sel, int nsup) {
     }
   } else {
     for (int i = 0; i < nlog; ++i) {
-      const uint32_t s = P.N(1, P.lg[1][i].node).support;
+      const uint32_t s = P.C(1, P.lg[1][i].node).support;
       if (s != kImNoSupport) tab[s].cap += 1;
     }
   }
@@ -1143,7 +1187,7 @@ __device__ void im_extract_support(ImPair<Env>& P, int sel, int nsup) {
   }
   if (off > P.p.Nsp) {
     P.fail(POMCP_E_ARENA);
-    for (int q = 0; q < nsup; ++q) P.N(1, tab[q].node).support = kImNoSupport;
+    for (int q = 0; q < nsup; ++q) P.C(1, tab[q].node).support = kImNoSupport;
     return;
   }
   uint2* parts = P.sup_parts(sel);
@@ -1154,7 +1198,7 @@ __device__ void im_extract_support(ImPair<Env>& P, int sel, int nsup) {
       uint32_t s = kImNoSupport;
       if (i < nlog) {
         r = P.lg[1][i];
-        s = P.N(1, r.node).support;
+        s = P.C(1, r.node).support;
       }
       uint64_t todo = __ballot(s != kImNoSupport);
       while (todo) {   // each slot of the batch: its records in lane (= insertion) order
@@ -1169,11 +1213,11 @@ __device__ void im_extract_support(ImPair<Env>& P, int sel, int nsup) {
   } else {
     for (int i = 0; i < nlog; ++i) {
       const IRec r = P.lg[1][i];
-      const uint32_t s = P.N(1, r.node).support;
+      const uint32_t s = P.C(1, r.node).support;
       if (s != kImNoSupport) parts[tab[s].off + tab[s].size++] = make_uint2(r.v0, r.v1);
     }
   }
-  for (int q = 0; q < nsup; ++q) P.N(1, tab[q].node).support = kImNoSupport;
+  for (int q = 0; q < nsup; ++q) P.C(1, tab[q].node).support = kImNoSupport;
 }
 
 // Every obs-child map slot empty ({0, 0, -1}), grid-stride over all pairs'
@@ -1199,10 +1243,13 @@ __global__ __launch_bounds__(64) void k_im_reset(ImParams p) {
     r.info = 1u << 4;   // path_ok
     r.visits = 0;
     r.t = 0;
-    r.stats = -1;
-    r.support = kImNoSupport;
-    r.okey = 0;
-    *reinterpret_cast<INode*>(p.nodes + im_node_off(p.Nn, p.B, b, k, 0)) = r;
+    ICold o;
+    o.okey = 0;
+    o.stats = -1;
+    o.support = kImNoSupport;
+    char* const line = p.nodes + im_node_off(p.Nn, p.B, b, k, 0);
+    *reinterpret_cast<INode*>(line) = r;
+    *reinterpret_cast<ICold*>(line + kImCold) = o;
     h.n_nodes[k] = 1;
     h.n_stats[k] = 0;
     h.n_log[k] = 0;
@@ -1304,12 +1351,12 @@ __global__ __launch_bounds__(64) void k_im_update(ImParams p) {
           const int sel = P.h.sup_sel ^ 1;
           im_support<Env, kWave>(P, sel, n, &nsup);
           ISup* tab = P.sup_tab(sel);
-          const uint64_t o0 = P.N(1, tab[0].node).okey;
+          const uint64_t o0 = P.C(1, tab[0].node).okey;
           Env::sample_agent_initial(sm, p.other, o0, draw_model, &s0, &s1);   // probe
           int off = 0;
           for (int q = 0; q < nsup && P.h.err == 0; ++q) {
             P.traverse(1, tab[q].node);
-            const uint64_t oq = P.N(1, tab[q].node).okey;
+            const uint64_t oq = P.C(1, tab[q].node).okey;
             tab[q].off = off;
             tab[q].size = 0;
             uint2* pp = P.sup_parts(sel) + off;
@@ -1389,7 +1436,7 @@ __global__ __launch_bounds__(64) void k_im_update(ImParams p) {
             P.traverse(1, m);
             if (im_absorbing(P.N(1, m).info)) continue;
             const int tq = (int)ceil(prob[q] * (double)p.n_target);
-            P.reinvig_nested(m, (int)im_paction(P.N(1, m).info), P.N(1, m).okey, tq, sel, q);
+            P.reinvig_nested(m, (int)im_paction(P.N(1, m).info), P.C(1, m).okey, tq, sel, q);
           }
           P.mark_support(sel ^ 1, P.h.pad, false);
           int used = 0;
@@ -1529,7 +1576,6 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
     }
     // max_value_action_selection (intmcp.py:718-732)
     const INode x = P.N(0, root);
-    const uint4* const rs = P.H(0, root);
     const int nr = im_nreg(x.info);
     if (nr == 0) {
       action = (int)P.d_sel((uint32_t)p.A);
@@ -1538,7 +1584,8 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
       int ties[6], nt = 0;
       for (int i = 0; i < nr; ++i) {
         const int a = im_order(x.info, i);
-        const double v = hilo_d(rs[a].z, rs[a].w);
+        const uint32_t* const hd = P.H(0, root, a);
+        const double v = hilo_d(hd[1], hd[2]);
         if (v == mx) {
           ties[nt++] = a;
         } else if (v > mx) {

@@ -38,16 +38,16 @@ __global__ __launch_bounds__(64) void k_im_root_stats(ImParams d, intmcp_root_st
   o.error = h.err;
   const int nr = im_nreg(node.info);
   o.num_children = nr;
-  if (node.stats >= 0) {
-    const uint4* hv = reinterpret_cast<const uint4*>(blk + 32);    // node line: intmcp.hip
+  if (im_has_stats(node.info)) {
     const char* rv = blk + im_rec_delta(d.B, t);                   // its action records
     for (int i = 0; i < nr && i < POMCP_MAX_ACTIONS; ++i) {
       const int a = im_order(node.info, i);
       o.child_action[i] = a;
       if (a < d.A) {
+        const uint32_t* hv = reinterpret_cast<const uint32_t*>(blk + kImHeads + 12 * a);   // node line
         const uint2 tot = *reinterpret_cast<const uint2*>(rv + kImRec * a);
-        o.child_visits[i] = (int)hv[a].x;
-        o.child_values[i] = hilo_d(hv[a].z, hv[a].w);
+        o.child_visits[i] = (int)hv[0];
+        o.child_values[i] = hilo_d(hv[1], hv[2]);
         o.child_totals[i] = hilo_d(tot.x, tot.y);
       }
     }
@@ -425,13 +425,27 @@ int intmcp_get_nodes(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int
   const int n = ctx->host_hdr[pair].n_nodes[tree];
   *count = n;
   if (!out || capacity < n) return POMCP_OK;
-  // the INode of every block (layout: intmcp.hip ImPair::N)
+  // the 32 B record of include/intmcp.h from each node's INode and ICold
+  // (layout: intmcp.hip ImPair::N, ImPair::C)
   const int64_t ns = kImBlock;
   std::vector<char> blocks;
   rc = im_copy_blocks(ctx, blocks, pair, tree, n);
   if (rc != POMCP_OK) return rc;
-  INode* o = reinterpret_cast<INode*>(out);
-  for (int i = 0; i < n; ++i) std::memcpy(&o[i], blocks.data() + (size_t)i * ns, sizeof(INode));
+  struct NodeRec {
+    int32_t parent;
+    uint32_t info;
+    int32_t visits, t, stats;
+    uint32_t support;
+    uint64_t okey;
+  };
+  NodeRec* o = reinterpret_cast<NodeRec*>(out);
+  for (int i = 0; i < n; ++i) {
+    INode x;
+    ICold c;
+    std::memcpy(&x, blocks.data() + (size_t)i * ns, sizeof(INode));
+    std::memcpy(&c, blocks.data() + (size_t)i * ns + kImCold, sizeof(ICold));
+    o[i] = NodeRec{x.parent, x.info & ~kImStatsBit, x.visits, x.t, c.stats, c.support, c.okey};
+  }
   return POMCP_OK;
 }
 
@@ -452,18 +466,18 @@ int intmcp_get_stats(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int
   if (rc != POMCP_OK) return rc;
   IStat* o = reinterpret_cast<IStat*>(out);
   for (int i = 0; i < nn; ++i) {
-    const INode* x = reinterpret_cast<const INode*>(blocks.data() + (size_t)i * ns);
-    if (x->stats < 0) continue;
-    for (int a = 0; a < ctx->ip.A && x->stats + a < n; ++a)
-    {
-      const char* bk = blocks.data() + (size_t)i * ns;   // head {visits, -, value}; record {total, ...}
+    const char* bk = blocks.data() + (size_t)i * ns;   // head {visits, value}; record {total, ...}
+    ICold c;
+    std::memcpy(&c, bk + kImCold, sizeof(ICold));
+    if (c.stats < 0) continue;
+    for (int a = 0; a < ctx->ip.A && c.stats + a < n; ++a) {
       IStat st;
-      std::memcpy(&st.visits, bk + 32 + 16 * (size_t)a, 4);
+      std::memcpy(&st.visits, bk + kImHeads + 12 * (size_t)a, 4);
       st.pad = 0;
-      std::memcpy(&st.value, bk + 32 + 16 * (size_t)a + 8, 8);
+      std::memcpy(&st.value, bk + kImHeads + 12 * (size_t)a + 4, 8);
       std::memcpy(&st.total, bk + kImLine + kImRec * (size_t)a, 8);
       st.agg = 0.0;   // not kept
-      o[x->stats + a] = st;
+      o[c.stats + a] = st;
     }
   }
   return POMCP_OK;
