@@ -59,11 +59,13 @@ def main():
                          kernel)
     write = read_counter(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE",
                          kernel)
-    # skip the warmup launch: every timed launch re-searches the same restored roots
-    f_avg = sum(fetch[1:]) / max(1, len(fetch) - 1) if len(fetch) > 1 else fetch[0]
-    w_avg = sum(write[1:]) / max(1, len(write) - 1) if len(write) > 1 else write[0]
-    hbm = (2 * f_avg + w_avg) * 1024
+    # the timed launches are the last `steps` ones (before them: the warmup and,
+    # for I-NTMCP, the arena-calibration probe's small launches)
     b = bench_line(os.path.join(src, "bench_trace.log"))
+    k = max(1, int(b.get("steps", 1)))
+    f_avg = sum(fetch[-k:]) / len(fetch[-k:])
+    w_avg = sum(write[-k:]) / len(write[-k:])
+    hbm = (2 * f_avg + w_avg) * 1024
     cfg = b["config"]
     summary = {
         "tag": tag, "bench": b, kernel: stats,
