@@ -19,6 +19,11 @@ int pomcp_debug_host_exp(const double* x, int32_t n, double* out);
  * when capacity >= count. */
 typedef struct pomcp_ctx pomcp_ctx;
 int pomcp_debug_phase_timing(pomcp_ctx* ctx, uint64_t* out, int32_t capacity, int32_t* count);
+/* k_im_search phase cycles per wave (libpomcp_hip built with
+ * -DPOMCP_PHASE_TIMING; POMCP_E_UNSUPPORTED otherwise), same protocol as
+ * pomcp_debug_phase_timing (tools/phase_timing_im.py). */
+typedef struct intmcp_ctx intmcp_ctx;
+int intmcp_debug_phase_timing(intmcp_ctx* ctx, uint64_t* out, int32_t capacity, int32_t* count);
 /* Only the first n (1..6) inline obs-child slots of each action node are used,
  * the overflow map holds the rest (tests of that path).  Before the first search. */
 int pomcp_debug_set_inline_slots(pomcp_ctx* ctx, int32_t n);
