@@ -58,6 +58,8 @@ struct pomcp_ctx {
 constexpr int kWaveSearchMaxTrees = 256;
 // and only while its per-tree scratch log stays small
 constexpr int64_t kWaveSearchMaxScratch = (int64_t)4 << 30;
+// step-tree producers for depth limits up to this (use_step_tree)
+constexpr int kStepTreeMaxDepth = 8;
 
 static void make_model(const pomcp_grid* g, DrvModel* m) {
   std::memcpy(&m->g, g, sizeof(DrvGrid));
@@ -455,6 +457,16 @@ int32_t pomcp_search_kernel_used(const pomcp_ctx* ctx) {
   return ctx ? resolve_search_kind(ctx) : POMCP_E_INVALID;
 }
 
+// The wave search with step-tree producer waves (pomcp_search_lds.hip) when
+// simulations are short enough that the producers' prediction of their draws
+// (depth_limit + 1 words per simulation) mostly holds and the first three
+// levels are most of a simulation; POMCP_STEP_TREE=0/1 forces it off / on.
+static bool use_step_tree(const pomcp_ctx* ctx) {
+  const char* f = std::getenv("POMCP_STEP_TREE");
+  if (f != nullptr && f[0] != '\0') return f[0] != '0';
+  return ctx->dp.depth_limit <= kStepTreeMaxDepth;
+}
+
 static int launch_search_wave(pomcp_ctx* ctx, int32_t num_sims, int final_sel) {
   if (!ctx->dp.lscr) {   // the per-tree scratch log, on first use
     void* q = nullptr;
@@ -463,14 +475,19 @@ static int launch_search_wave(pomcp_ctx* ctx, int32_t num_sims, int final_sel) {
     ctx->dp.lscr = reinterpret_cast<LogRec*>(q);
   }
   using KFn = void (*)(DevParams, int, int);
-  static const KFn table[2][3] = {
-      {k_search_lds<EnvDriving, POMCP_SEL_PUCB, 5>, k_search_lds<EnvDriving, POMCP_SEL_UCB, 5>,
-       k_search_lds<EnvDriving, POMCP_SEL_UNIFORM, 5>},
-      {k_search_lds<EnvPursuitEvasion, POMCP_SEL_PUCB, 4>, k_search_lds<EnvPursuitEvasion, POMCP_SEL_UCB, 4>,
-       k_search_lds<EnvPursuitEvasion, POMCP_SEL_UNIFORM, 4>}};
+#define PB_LDS_ROW(NP)                                                                          \
+  {{k_search_lds<EnvDriving, POMCP_SEL_PUCB, 5, NP>, k_search_lds<EnvDriving, POMCP_SEL_UCB, 5, NP>, \
+    k_search_lds<EnvDriving, POMCP_SEL_UNIFORM, 5, NP>},                                         \
+   {k_search_lds<EnvPursuitEvasion, POMCP_SEL_PUCB, 4, NP>,                                      \
+    k_search_lds<EnvPursuitEvasion, POMCP_SEL_UCB, 4, NP>,                                       \
+    k_search_lds<EnvPursuitEvasion, POMCP_SEL_UNIFORM, 4, NP>}}
+  static const KFn table[2][2][3] = {PB_LDS_ROW(0), PB_LDS_ROW(kSpecProducers)};
+#undef PB_LDS_ROW
   const int e = ctx->dp.env == POMCP_ENV_PURSUIT_EVASION ? 1 : 0;
-  hipLaunchKernelGGL(table[e][ctx->dp.sel], dim3((unsigned)ctx->dp.B), dim3(kWave), 0, ctx->stream,
-                     ctx->dp, (int)num_sims, final_sel);
+  const int spec = use_step_tree(ctx) ? 1 : 0;
+  hipLaunchKernelGGL(table[spec][e][ctx->dp.sel], dim3((unsigned)ctx->dp.B),
+                     dim3((unsigned)(kWave * (1 + spec * kSpecProducers))), 0, ctx->stream, ctx->dp,
+                     (int)num_sims, final_sel);
   HIP_TRY(ctx, hipGetLastError());
   hipLaunchKernelGGL(k_log_merge, dim3((unsigned)search_waves(ctx->dp.B)), dim3(kWave), 0,
                      ctx->stream, ctx->dp);

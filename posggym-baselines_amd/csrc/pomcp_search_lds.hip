@@ -47,11 +47,39 @@
 
 namespace pb {
 
-constexpr int kLdsPoolBytes = 136 * 1024;          // tree blocks; + model, path, caches below
-constexpr int kLdsPoolParts = kLdsPoolBytes / 16;
+// tree blocks (+ model, path, caches below); with step-tree producers (NP > 0)
+// their slots take 15 KB of it
+__host__ __device__ constexpr int lds_pool_bytes(int NP) { return (NP > 0 ? 124 : 136) * 1024; }
 constexpr int kLdsDpow = 256;                      // discount powers cached in LDS
 constexpr int kLdsBelief = 128;                    // root beliefs up to this size live in LDS
-__host__ __device__ constexpr int lds_pool_blocks(int A) { return kLdsPoolParts / (8 * A); }
+__host__ __device__ constexpr int lds_pool_blocks(int A, int NP = 0) {
+  return lds_pool_bytes(NP) / 16 / (8 * A);
+}
+// Speculative step tree (NP producer waves): for simulation k the producers
+// evaluate the generative step of every action sequence of the first
+// kSpecLevels tree levels (A + A^2 + A^3 steps and observation keys) with the
+// draws simulation k will use -- the model and the other agent's streams
+// advance by exactly depth_limit + 1 words per simulation that does not
+// terminate (mcts.py:315-328, 405-452: the tree levels plus the rollout reach
+// the depth limit), and the belief stream by one -- into one of kSpecSlots LDS
+// slots; the search wave checks the slot's counters against its own at the
+// start of the simulation and reads a level's steps out of the slot instead of
+// computing them (a mismatch, after a terminated simulation: it computes them
+// as before and re-bases the producers' prediction).
+constexpr int kSpecLevels = 3;
+constexpr int kSpecProducers = 3;
+constexpr int kSpinMax = 1 << 22;   // s_sleep 1 polls (~0.1 s) before a hand-off counts as broken
+constexpr int kSpecSlots = 4;
+__host__ __device__ constexpr int spec_entries(int A) { return A + A * A + A * A * A; }
+enum : int { SP_NEXT = 0, SP_CONSUMED = 1, SP_STOP = 2, SP_SYNC_K = 3, SP_SYNC_M = 4, SP_SYNC_O = 5 };
+
+// wave-uniform (the whole wave reads the same word): scalar branches on it
+__device__ __forceinline__ int lds_acquire(int* x) {
+  return uni(__hip_atomic_load(x, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+__device__ __forceinline__ void lds_release(int* x, int v) {
+  __hip_atomic_store(x, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 // One RNG stream as a VGPR page of 64 consecutive draws (philox.h: draw j =
 // word j & 3 of block j >> 2): lane i holds draw base + i; a draw is one
@@ -82,12 +110,19 @@ __device__ __forceinline__ uint4 rl4(uint4 v, int l) {
   return make_uint4(rlu(v.x, l), rlu(v.y, l), rlu(v.z, l), rlu(v.w, l));
 }
 
-template <class Env, int SEL, int NA>
-__global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, int final_sel) {
+template <class Env, int SEL, int NA, int NP>
+__global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int num_sims, int final_sel) {
   static_assert(NA >= 2 && NA <= kMaxA, "action count");
+  static_assert(NA * NA * NA <= 2 * kWave, "step tree: two level-2 passes");
   constexpr int A = NA;   // == p.A (host dispatch)
-  constexpr int C = lds_pool_blocks(A);
+  constexpr int C = lds_pool_blocks(A, NP);
+  constexpr int NE = spec_entries(A);
   __shared__ typename Env::Model sm;
+  // step-tree slots: {n0, n1, obs key lo, obs key hi | done << 31} and the reward
+  __shared__ uint4 sp_e[NP > 0 ? kSpecSlots * NE : 1];
+  __shared__ double sp_r[NP > 0 ? kSpecSlots * NE : 1];
+  __shared__ int sp_hdr[kSpecSlots * 4];   // per slot: simulation + 1, model / other counters
+  __shared__ int sp_ctl[8];
   __shared__ uint4 pool[C * 8 * A];
   __shared__ uint4 path[(kMaxPath + 1) * 3];
   __shared__ double dpw[kLdsDpow];
@@ -97,8 +132,9 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
   __shared__ double nl_v[C];
   __shared__ int32_t nl_n[C];
   stage_model(p.model, sm);
-  const int tree = (int)blockIdx.x;   // grid = B workgroups of one wave
+  const int tree = (int)blockIdx.x;   // grid = B workgroups: the search wave + NP producers
   const int lane = lane_id();
+  const int wv = (int)(threadIdx.x >> 6);   // 0: the search wave
   const int al = lane >> 3 < A ? lane >> 3 : A - 1;   // this lane's action group
   const int ql = lane & 7;                             // part of the action's line
   char* const an = reinterpret_cast<char*>(p.an + tree_base_lines(tree, p.Nb, blk_lines(A)));
@@ -175,7 +211,7 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
 
   // ---- the blocks into LDS (part q of action a's line <- its HBM part)
   const int nstage = n_blocks < C ? n_blocks : C;
-  if (lane < 8 * A) {
+  if (wv == 0 && lane < 8 * A) {
     const int a = lane >> 3, q = lane & 7;
     int b = 0;
     for (; b + 4 <= nstage; b += 4) {
@@ -188,16 +224,31 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
     }
     for (; b < nstage; ++b) *lpart(b, a, q) = hld(b, a, q);
   }
-  for (int b = lane; b < nstage; b += kWave) {
+  for (int b = lane; wv == 0 && b < nstage; b += kWave) {
     const uint4 x = hblk(b)[1];
     nl_n[b] = (int)x.y + 1;
     nl_v[b] = hilo_d(x.z, x.w);
   }
   const int ndp = p.dpow_n < kLdsDpow ? p.dpow_n : kLdsDpow;
-  for (int i = lane; i < ndp; i += kWave) dpw[i] = p.dpow[i];
+  for (int i = (int)threadIdx.x; i < ndp; i += (int)blockDim.x) dpw[i] = p.dpow[i];
   const bool bel_lds = bsize <= kLdsBelief;
   if (bel_lds)
-    for (int i = lane; i < bsize; i += kWave) bel[i] = rbel[i];
+    for (int i = (int)threadIdx.x; i < bsize; i += (int)blockDim.x) bel[i] = rbel[i];
+  // the step tree's prediction: simulation k of this launch draws the model and
+  // the other agent's words from sync_m / sync_o + (k - sync_k) * (depth_limit + 1)
+  const int d1 = p.depth_limit + 1;
+  const int dm = Env::kStepDraws ? d1 : 0;
+  int syn_k = 0, syn_m = (int)sd.ctr, syn_o = (int)(p.other == 0 ? s0s.ctr : s1s.ctr);
+  const uint32_t bctr0 = sb.ctr;
+  if (NP > 0 && threadIdx.x == 0) {
+    sp_ctl[SP_NEXT] = 0;
+    sp_ctl[SP_CONSUMED] = 0;
+    sp_ctl[SP_STOP] = 0;
+    sp_ctl[SP_SYNC_K] = syn_k;
+    sp_ctl[SP_SYNC_M] = syn_m;
+    sp_ctl[SP_SYNC_O] = syn_o;
+    for (int i = 0; i < kSpecSlots; ++i) sp_hdr[4 * i] = 0;
+  }
   __syncthreads();
   auto dpow = [&](int k) { return k < kLdsDpow ? dpw[k] : p.dpow[k]; };
   auto logtab = [&](int n) { return p.logtab[n < p.logtab_n ? n : 0]; };
@@ -234,7 +285,99 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
     return b;
   };
 
-  bool run = err == 0 && !root_abs;   // mcts.py:270-272
+  // ---- producer waves: the step tree of every coming simulation, in order
+  if (NP > 0 && wv > 0) {
+    const uint32_t oth_sid = (uint32_t)(S_ACT_BASE + p.other);
+    for (;;) {
+      // claim the next simulation (lane 0 adds 1, the other lanes 0)
+      const int j = uni(__hip_atomic_fetch_add(&sp_ctl[SP_NEXT], lane == 0 ? 1 : 0, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP));
+      if (j >= num_sims) break;
+      // slot j % kSpecSlots is free once the search wave is done with simulation j - kSpecSlots
+      bool stop = false;
+      int spins = 0;
+      while (lds_acquire(&sp_ctl[SP_CONSUMED]) < j - kSpecSlots + 1) {
+        if (lds_acquire(&sp_ctl[SP_STOP]) != 0 || ++spins > kSpinMax) {
+#ifdef POMCP_SPIN_DEBUG
+          if (spins > kSpinMax && lane == 0)
+            printf("producer %d: j %d consumed %d stop %d\n", wv, j, sp_ctl[SP_CONSUMED], sp_ctl[SP_STOP]);
+#endif
+          stop = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (stop || lds_acquire(&sp_ctl[SP_STOP]) != 0) break;
+#ifdef POMCP_SPIN_DEBUG
+      if (lane == 0 && j < 8) printf("producer %d: claimed %d\n", wv, j);
+#endif
+      const int sk = uni(lds_acquire(&sp_ctl[SP_SYNC_K]));
+      const uint32_t cm = (uint32_t)uni(lds_acquire(&sp_ctl[SP_SYNC_M])) + (uint32_t)((j - sk) * dm);
+      const uint32_t co = (uint32_t)uni(lds_acquire(&sp_ctl[SP_SYNC_O])) + (uint32_t)((j - sk) * d1);
+      // the simulation's draws, one lane each: 0 its particle (belief.py:55),
+      // 1..3 the model's shuffle draw of level 0..2, 4..6 the other agent's action
+      uint32_t sid = S_BELIEF, ctr = bctr0 + (uint32_t)j;
+      if (lane >= 1 && lane <= 3) {
+        sid = S_MODEL;
+        ctr = cm + (uint32_t)(lane - 1);
+      } else if (lane >= 4) {
+        sid = oth_sid;
+        ctr = co + (uint32_t)(lane - 4);
+      }
+      const uint32_t w = philox_word(seed, tkey, sid, ctr);
+      const uint4 pr = particle(uniform_int(rlu(w, 0), (uint32_t)bsize));
+      uint32_t jm[kSpecLevels], ao[kSpecLevels];
+#pragma unroll
+      for (int l = 0; l < kSpecLevels; ++l) {
+        jm[l] = Env::kStepDraws ? uniform_int(rlu(w, 1 + l), 2u) : 0u;
+        ao[l] = uniform_int(rlu(w, 4 + l), (uint32_t)A);
+      }
+      const int slot = j % kSpecSlots;
+      uint4* const E = sp_e + slot * NE;
+      double* const ER = sp_r + slot * NE;
+      auto put = [&](int e, uint32_t n0, uint32_t n1, double r, int dn) {
+        const uint64_t ok = Env::obs_key(sm, p.ego, n0, n1);
+        E[e] = make_uint4(n0, n1, (uint32_t)ok, (uint32_t)(ok >> 32) | ((uint32_t)dn << 31));
+        ER[e] = r;
+      };
+      // levels 0 and 1: lane a0 * A + a1
+      uint32_t q0 = 0u, q1 = 0u;
+      if (lane < A * A) {
+        const uint32_t a0 = (uint32_t)lane / A, a1 = (uint32_t)lane % A;
+        uint32_t m0, m1;
+        double r;
+        int dn;
+        Env::step(sm, p.ego, pr.y, pr.z, a0, ao[0], jm[0], &m0, &m1, &r, &dn);
+        if (a1 == 0u) put((int)a0, m0, m1, r, dn);
+        Env::step(sm, p.ego, m0, m1, a1, ao[1], jm[1], &q0, &q1, &r, &dn);
+        put(A + lane, q0, q1, r, dn);
+      }
+      // level 2: entries lane and lane + 64, from level-1 state e / A
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int e = lane + kWave * h;
+        const int pfx = e / A < A * A ? e / A : 0;
+        const uint32_t x0 = (uint32_t)__shfl((int)q0, pfx), x1 = (uint32_t)__shfl((int)q1, pfx);
+        if (e < A * A * A) {
+          uint32_t m0, m1;
+          double r;
+          int dn;
+          Env::step(sm, p.ego, x0, x1, (uint32_t)(e % A), ao[2], jm[2], &m0, &m1, &r, &dn);
+          put(A + A * A + e, m0, m1, r, dn);
+        }
+      }
+#ifdef POMCP_SPIN_DEBUG
+      if (lane == 0 && j < 8) printf("producer %d: publish %d slot %d\n", wv, j, slot);
+#endif
+      if (lane == 0) {
+        sp_hdr[4 * slot + 1] = (int)cm;
+        sp_hdr[4 * slot + 2] = (int)co;
+        lds_release(&sp_hdr[4 * slot], j + 1);   // after every lane's entries
+      }
+    }
+  }
+
+  bool run = wv == 0 && err == 0 && !root_abs;   // mcts.py:270-272
   if (run && root_t == 0) {
     err = POMCP_E_STATE;
     run = false;
@@ -344,6 +487,31 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
     int t = (int)pr.x;
     uint32_t s0 = pr.y, s1 = pr.z;
     int depth = 0, plen = 0;
+    // the step tree of this simulation (NP > 0): usable when the producers'
+    // counters are this simulation's
+    bool spv = false;
+    int sp_base = 0, pidx = 0;
+    if (NP > 0) {
+      const int slot = it % kSpecSlots;
+      int spins = 0;
+      while (lds_acquire(&sp_hdr[4 * slot]) != it + 1) {
+        if (++spins > kSpinMax) {   // bounded: a broken hand-off fails the search, never hangs
+#ifdef POMCP_SPIN_DEBUG
+          if (lane == 0)
+            printf("search wave: sim %d slot %d seq %d next %d consumed %d\n", it, slot,
+                   sp_hdr[4 * slot], sp_ctl[SP_NEXT], sp_ctl[SP_CONSUMED]);
+#endif
+          err = POMCP_E_HIP;
+          run = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (!run) break;
+      const uint32_t oc = p.other == 0 ? s0s.ctr : s1s.ctr;
+      spv = uniu((uint32_t)sp_hdr[4 * slot + 1]) == sd.ctr && uniu((uint32_t)sp_hdr[4 * slot + 2]) == oc;
+      sp_base = slot * NE;
+    }
     int blk = root_blk, nv = root_visits;
     double lg = root_log(root_blk, root_visits);   // math.log(nv), mcts.py:534
     double ret = 0.0;
@@ -356,17 +524,38 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
     // -------------------------------------------------- the tree levels
     while (phase == TP_LEVEL) {
       const double log_n = lg;
-      const uint32_t j = d_model(2);                     // drawn before the selection:
-      const uint32_t ao = d_act(p.other, (uint32_t)A);     // independent streams
-      PT_MARK(1);
-      const uint4 v = ldp(blk, al, ql);                    // part ql of action al's line
-      PT_MARK(2);
-      // every action's generative step at once (mcts.py:331-352)
+      // every action's generative step at once (mcts.py:331-352): lane group a's
+      // results for action a, from the step tree or computed here
       uint32_t n0, n1;
       double r;
       int done;
-      Env::step(sm, p.ego, s0, s1, (uint32_t)al, ao, j, &n0, &n1, &r, &done);
-      const uint64_t okey = Env::obs_key(sm, p.ego, n0, n1);
+      uint64_t okey;
+      uint4 v;                                             // part ql of action al's line
+      if (NP > 0 && spv && depth < kSpecLevels) {
+        const int e = sp_base + (depth == 0 ? 0 : (depth == 1 ? A : A + A * A)) + pidx * A + al;
+        const uint4 x = sp_e[e];
+        r = sp_r[e];
+        v = ldp(blk, al, ql);
+        PT_MARK(2);
+        n0 = x.x;
+        n1 = x.y;
+        okey = (uint64_t)x.z | ((uint64_t)(x.w & 0x7FFFFFFFu) << 32);
+        done = (int)(x.w >> 31);
+        if (Env::kStepDraws) ++sd.ctr;   // the words the step tree used
+        if (p.other == 0) {
+          ++s0s.ctr;
+        } else {
+          ++s1s.ctr;
+        }
+      } else {
+        const uint32_t j = d_model(2);                     // drawn before the selection:
+        const uint32_t ao = d_act(p.other, (uint32_t)A);     // independent streams
+        PT_MARK(1);
+        v = ldp(blk, al, ql);
+        PT_MARK(2);
+        Env::step(sm, p.ego, s0, s1, (uint32_t)al, ao, j, &n0, &n1, &r, &done);
+        okey = Env::obs_key(sm, p.ego, n0, n1);
+      }
       PT_MARK(3);
       // _search_action_selection (mcts.py:492-563) on lanes 8a
       PT_MARK(4);
@@ -546,6 +735,7 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
         phase = TP_ROLL;
       } else {
         blk = cblk;   // the next level
+        pidx = pidx * A + a;
         node_n(cblk, &nv, &lg);
       }
       PT_MARK(7);
@@ -611,15 +801,34 @@ __global__ __launch_bounds__(64) void k_search_lds(DevParams p, int num_sims, in
     ++root_visits;                                          // mcts.py:288
     max_depth = depth > max_depth ? depth : max_depth;
     ++sims;
+    if (NP > 0) {
+      if (lane == 0) lds_release(&sp_ctl[SP_CONSUMED], it + 1);   // the slot is free
+      // the next simulation's counters off the prediction (this one terminated
+      // early): re-base the producers
+      const uint32_t oc = p.other == 0 ? s0s.ctr : s1s.ctr;
+      if (sd.ctr != (uint32_t)(syn_m + (it + 1 - syn_k) * dm) ||
+          oc != (uint32_t)(syn_o + (it + 1 - syn_k) * d1)) {
+        syn_k = it + 1;
+        syn_m = (int)sd.ctr;
+        syn_o = (int)oc;
+        if (lane == 0) {
+          sp_ctl[SP_SYNC_M] = syn_m;
+          sp_ctl[SP_SYNC_O] = syn_o;
+          lds_release(&sp_ctl[SP_SYNC_K], syn_k);
+        }
+      }
+    }
     PT_MARK(9);
     __builtin_amdgcn_wave_barrier();
   }
 #ifdef POMCP_PHASE_TIMING
-  if (p.timing != nullptr && tree == 0 && lane == 0)
+  if (p.timing != nullptr && tree == 0 && wv == 0 && lane == 0)
     for (int i = 0; i < 16; ++i) p.timing[i] = pt[i];
 #endif
+  if (NP > 0 && wv == 0 && lane == 0) lds_release(&sp_ctl[SP_STOP], 1);   // the producers exit
   flush_log();
   __syncthreads();
+  if (wv > 0) return;
 
   // ------------------------------------------------------------------ results
   const bool have = err == 0 && !root_abs && root_blk >= 0;
@@ -762,12 +971,14 @@ __global__ __launch_bounds__(64) void k_log_merge(DevParams p) {
   if (lane == kWave - 1) p.wlog[sw] = base + incl;
 }
 
-#define PB_SEARCH_LDS_INST(E, NA)                                             \
-  template __global__ void k_search_lds<E, POMCP_SEL_PUCB, NA>(DevParams, int, int);  \
-  template __global__ void k_search_lds<E, POMCP_SEL_UCB, NA>(DevParams, int, int);   \
-  template __global__ void k_search_lds<E, POMCP_SEL_UNIFORM, NA>(DevParams, int, int);
-PB_SEARCH_LDS_INST(EnvDriving, 5)
-PB_SEARCH_LDS_INST(EnvPursuitEvasion, 4)
+#define PB_SEARCH_LDS_INST(E, NA, NP)                                             \
+  template __global__ void k_search_lds<E, POMCP_SEL_PUCB, NA, NP>(DevParams, int, int);  \
+  template __global__ void k_search_lds<E, POMCP_SEL_UCB, NA, NP>(DevParams, int, int);   \
+  template __global__ void k_search_lds<E, POMCP_SEL_UNIFORM, NA, NP>(DevParams, int, int);
+PB_SEARCH_LDS_INST(EnvDriving, 5, 0)
+PB_SEARCH_LDS_INST(EnvPursuitEvasion, 4, 0)
+PB_SEARCH_LDS_INST(EnvDriving, 5, kSpecProducers)
+PB_SEARCH_LDS_INST(EnvPursuitEvasion, 4, kSpecProducers)
 #undef PB_SEARCH_LDS_INST
 
 }  // namespace pb

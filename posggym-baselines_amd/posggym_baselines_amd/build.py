@@ -17,7 +17,7 @@ INCLUDE = os.path.join(REPO, "include")
 OUT = os.environ.get("POMCP_LIB_PATH") or os.path.join(PKG, "_lib", "libpomcp_hip.so")
 SOURCES = [os.path.join(CSRC, "pomcp_capi.hip")]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in
-                  ("pomcp_kernels.hip", "pomcp_search.hip", "pomcp_device.h", "driving.h",
+                  ("pomcp_kernels.hip", "pomcp_search.hip", "pomcp_search_lds.hip", "pomcp_device.h", "driving.h",
                    "driving_vec.h", "philox.h", "envs.h", "pursuit_evasion.h", "host_exp.h", "host_exp_table.h", "intmcp.hip", "intmcp_capi.hip")] + [
     os.path.join(INCLUDE, "pomcp.h"), os.path.join(INCLUDE, "pomcp_debug.h"),
     os.path.join(INCLUDE, "intmcp.h")]

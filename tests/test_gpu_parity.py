@@ -13,13 +13,18 @@ from oracle.run import make_oracle, oracle_record
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["lane", "wave"])
+@pytest.fixture(autouse=True, params=["lane", "wave", "wave_tree", "wave_plain"])
 def search_kernel(request, monkeypatch):
-    """Every parity test runs on both search kernels: k_search (a tree per lane,
-    tree in HBM) and k_search_lds (a wave per tree, tree in LDS); they must give
-    the same bits as the reference / oracle."""
-    monkeypatch.setenv("POMCP_SEARCH_KERNEL", request.param)
-    return request.param
+    """Every parity test runs on every search kernel: k_search (a tree per lane,
+    tree in HBM) and k_search_lds (a wave per tree, tree in LDS) -- with its
+    step-tree producer waves as the engine picks them ("wave"), forced on for
+    any depth limit ("wave_tree") and off ("wave_plain"); they must give the
+    same bits as the reference / oracle."""
+    kind, _, tree = request.param.partition("_")
+    monkeypatch.setenv("POMCP_SEARCH_KERNEL", kind)
+    if tree:
+        monkeypatch.setenv("POMCP_STEP_TREE", "1" if tree == "tree" else "0")
+    return kind
 
 SQRT2 = math.sqrt(2)
 TEST_CFG = dict(discount=0.95, search_time_limit=0.1, c=SQRT2, truncated=False,
