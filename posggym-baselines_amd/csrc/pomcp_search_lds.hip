@@ -776,26 +776,61 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
     PT_MARK(8);
     // ------------------------------------------------------ backup (mcts.py:374-381)
     __builtin_amdgcn_wave_barrier();
-    double gr = ret;
-    for (int l = plen - 1; l >= 0; --l) {
+    if (plen <= kWave) {
+      // lane l < plen backs up level l: its return is the reference's chain from
+      // the leaf (gr = r + discount * gr, level by level) stopped at l, then its
+      // Welford update; the levels' records are distinct (a node appears once
+      // per path), so all levels are written at once
+      const bool mine = lane < plen;
+      const int lv = mine ? lane : 0;
       // {visits, -, value} and {total, -} before, {block << 3 | a | done << 31, r}
-      const uint4 e0 = path[3 * l], e1 = path[3 * l + 1], e2 = path[3 * l + 2];
-      const double r = hilo_d(e2.y, e2.z);
-      gr = (e2.x >> 31) ? r : r + p.discount * gr;
+      const uint4 e0 = path[3 * lv], e1 = path[3 * lv + 1], e2 = path[3 * lv + 2];
+      const double rl = hilo_d(e2.y, e2.z);
+      const uint32_t dl = e2.x >> 31;
+      double gr = ret;
+      for (int l = plen - 1; l >= 0; --l) {
+        const double r = rl_d(rl, l);
+        const double g2 = rlu(dl, l) ? r : r + p.discount * gr;
+        gr = l >= lane ? g2 : gr;
+      }
       const int n = (int)e0.x + 1;
       const double value0 = hilo_d(e0.z, e0.w);
       const double total = hilo_d(e1.x, e1.y) + gr;
       const double delta = gr - value0;
       const double value = value0 + delta / (double)n;
       const uint32_t ba = e2.x & 0x7FFFFFFFu;
-      if (lane == 0) {
+      if (mine) {
         stp((int)(ba >> 3), (int)(ba & 7u), 0,
             make_uint4((uint32_t)n, 0u, (uint32_t)__double2loint(value), (uint32_t)__double2hiint(value)));
         stp((int)(ba >> 3), (int)(ba & 7u), 1,
             make_uint4((uint32_t)__double2loint(total), (uint32_t)__double2hiint(total), 0u, 0u));
       }
-      if (value > mm_max) mm_max = value;   // utils.py:29-32
-      if (value < mm_min) mm_min = value;
+      for (int l = 0; l < plen; ++l) {   // utils.py:29-32 (min / max: any order)
+        const double x = rl_d(value, l);
+        if (x > mm_max) mm_max = x;
+        if (x < mm_min) mm_min = x;
+      }
+    } else {   // a path longer than a wave (kMaxPath + 1 levels): level by level
+      double gr = ret;
+      for (int l = plen - 1; l >= 0; --l) {
+        const uint4 e0 = path[3 * l], e1 = path[3 * l + 1], e2 = path[3 * l + 2];
+        const double r = hilo_d(e2.y, e2.z);
+        gr = (e2.x >> 31) ? r : r + p.discount * gr;
+        const int n = (int)e0.x + 1;
+        const double value0 = hilo_d(e0.z, e0.w);
+        const double total = hilo_d(e1.x, e1.y) + gr;
+        const double delta = gr - value0;
+        const double value = value0 + delta / (double)n;
+        const uint32_t ba = e2.x & 0x7FFFFFFFu;
+        if (lane == 0) {
+          stp((int)(ba >> 3), (int)(ba & 7u), 0,
+              make_uint4((uint32_t)n, 0u, (uint32_t)__double2loint(value), (uint32_t)__double2hiint(value)));
+          stp((int)(ba >> 3), (int)(ba & 7u), 1,
+              make_uint4((uint32_t)__double2loint(total), (uint32_t)__double2hiint(total), 0u, 0u));
+        }
+        if (value > mm_max) mm_max = value;
+        if (value < mm_min) mm_min = value;
+      }
     }
     pend_flush();
     ++root_visits;                                          // mcts.py:288
