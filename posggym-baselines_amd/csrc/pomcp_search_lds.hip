@@ -47,9 +47,18 @@
 
 namespace pb {
 
+#ifndef PB_SPEC_PRODUCERS   // measurement builds only (tools/dbg/st4.sh)
+#define PB_SPEC_PRODUCERS 2
+#endif
+#ifndef PB_SPEC_SLOTS
+#define PB_SPEC_SLOTS 3
+#endif
+#ifndef PB_SPEC_POOL_KB
+#define PB_SPEC_POOL_KB 128
+#endif
 // tree blocks (+ model, path, caches below); with step-tree producers (NP > 0)
 // their slots take 15 KB of it
-__host__ __device__ constexpr int lds_pool_bytes(int NP) { return (NP > 0 ? 124 : 136) * 1024; }
+__host__ __device__ constexpr int lds_pool_bytes(int NP) { return (NP > 0 ? PB_SPEC_POOL_KB : 136) * 1024; }
 constexpr int kLdsDpow = 256;                      // discount powers cached in LDS
 constexpr int kLdsBelief = 128;                    // root beliefs up to this size live in LDS
 __host__ __device__ constexpr int lds_pool_blocks(int A, int NP = 0) {
@@ -67,9 +76,9 @@ __host__ __device__ constexpr int lds_pool_blocks(int A, int NP = 0) {
 // computing them (a mismatch, after a terminated simulation: it computes them
 // as before and re-bases the producers' prediction).
 constexpr int kSpecLevels = 3;
-constexpr int kSpecProducers = 3;
+constexpr int kSpecProducers = PB_SPEC_PRODUCERS;
 constexpr int kSpinMax = 1 << 22;   // s_sleep 1 polls (~0.1 s) before a hand-off counts as broken
-constexpr int kSpecSlots = 4;
+constexpr int kSpecSlots = PB_SPEC_SLOTS;
 __host__ __device__ constexpr int spec_entries(int A) { return A + A * A + A * A * A; }
 enum : int { SP_NEXT = 0, SP_CONSUMED = 1, SP_STOP = 2, SP_SYNC_K = 3, SP_SYNC_M = 4, SP_SYNC_O = 5 };
 
