@@ -600,11 +600,19 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
         const double range = mm_max - mm_min;
         const int n = (int)v.x;
         const double val = hilo_d(v.z, v.w);
+#ifdef PB_ABL_NOSEL
+        const double nvq = val + (nz ? range : 0.0);
+#else
         const double nvq = nz ? (val - mm_min) / range : val;
+#endif
         double sc;
         if (SEL == POMCP_SEL_UCB) {                        // mcts.py:529-546
           if (nv >= p.logtab_n) err = POMCP_E_ARENA;
+#ifdef PB_ABL_NOSEL   // ablation (results wrong, measurement only): no FP64 UCB arithmetic
+          sc = nvq - (double)n;
+#else
           sc = nvq + p.c * sqrt(log_n / (double)(n > 0 ? n : 1));
+#endif
         } else {                                           // PUCB, mcts.py:502-527
           const double noise = 1.0 / (double)A;
           const double prior = (1.0 / (double)A) * (1.0 - p.pucb_f) + p.pucb_f * noise;
@@ -693,6 +701,9 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
         run = false;
         break;
       }
+#ifdef PB_ABL_NOLOG   // ablation (results wrong, measurement only): no particle-log records
+      rb_n = 0;
+#endif
       if (rb_n == kWave) flush_log();
       {
         const bool mine = lane == rb_n;                      // mcts.py:371
