@@ -166,7 +166,10 @@ int pomcp_search_continue(pomcp_ctx* ctx, int32_t num_sims);
  *                      throughput kernel for thousands of trees);
  *   POMCP_SEARCH_WAVE  one wave per tree, tree blocks in LDS (k_search_lds: a
  *                      lone planner's latency, mcts.py:285's loop as fast as one
- *                      tree allows). */
+ *                      tree allows); for depth limits <= 8 the tree's workgroup
+ *                      adds step-tree producer waves that evaluate the first
+ *                      three levels' generative steps ahead of the search
+ *                      (environment POMCP_STEP_TREE=0 / 1 forces them off / on). */
 typedef enum pomcp_search_kernel {
   POMCP_SEARCH_AUTO = 0,
   POMCP_SEARCH_LANE = 1,
