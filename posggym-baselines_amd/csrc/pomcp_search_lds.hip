@@ -130,7 +130,8 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
   // step-tree slots: {n0, n1, obs key lo, obs key hi | done << 31} and the reward
   __shared__ uint4 sp_e[NP > 0 ? kSpecSlots * NE : 1];
   __shared__ double sp_r[NP > 0 ? kSpecSlots * NE : 1];
-  __shared__ int sp_hdr[kSpecSlots * 4];   // per slot: simulation + 1, model / other counters
+  // per slot: simulation + 1, model / other counters, -, the simulation's particle {t, v0, v1}, -
+  __shared__ int sp_hdr[kSpecSlots * 8];
   __shared__ int sp_ctl[8];
   __shared__ uint4 pool[C * 8 * A];
   __shared__ uint4 path[(kMaxPath + 1) * 3];
@@ -256,7 +257,7 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
     sp_ctl[SP_SYNC_K] = syn_k;
     sp_ctl[SP_SYNC_M] = syn_m;
     sp_ctl[SP_SYNC_O] = syn_o;
-    for (int i = 0; i < kSpecSlots; ++i) sp_hdr[4 * i] = 0;
+    for (int i = 0; i < kSpecSlots; ++i) sp_hdr[8 * i] = 0;
   }
   __syncthreads();
   auto dpow = [&](int k) { return k < kLdsDpow ? dpw[k] : p.dpow[k]; };
@@ -379,9 +380,12 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
       if (lane == 0 && j < 8) printf("producer %d: publish %d slot %d\n", wv, j, slot);
 #endif
       if (lane == 0) {
-        sp_hdr[4 * slot + 1] = (int)cm;
-        sp_hdr[4 * slot + 2] = (int)co;
-        lds_release(&sp_hdr[4 * slot], j + 1);   // after every lane's entries
+        sp_hdr[8 * slot + 1] = (int)cm;
+        sp_hdr[8 * slot + 2] = (int)co;
+        sp_hdr[8 * slot + 4] = (int)pr.x;
+        sp_hdr[8 * slot + 5] = (int)pr.y;
+        sp_hdr[8 * slot + 6] = (int)pr.z;
+        lds_release(&sp_hdr[8 * slot], j + 1);   // after every lane's entries
       }
     }
   }
@@ -400,7 +404,11 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
   }
   if (num_sims <= 0) run = false;
   uint4 pf = make_uint4(0, 0, 0, 0);
-  if (run) pf = particle(d_belief((uint32_t)bsize));   // the first simulation's particle
+  // the first simulation's particle (with producers: theirs, from its slot)
+  if (run) {
+    if (NP > 0) ++sb.ctr;
+    else pf = particle(d_belief((uint32_t)bsize));
+  }
   // the pending node update of the previous level's node, or of the leaf just
   // expanded: N of its next arrival and math.log(N), stored one level later,
   // when the log load has landed
@@ -491,10 +499,11 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
   int sims = 0, max_depth = 0;
   for (int it = 0; it < num_sims && run; ++it) {
     // ------------------------------------------------ start (mcts.py:286-287)
-    const uint4 pr = pf;                                   // belief.py:55
-    if (sims + 1 < num_sims) pf = particle(d_belief((uint32_t)bsize));
-    int t = (int)pr.x;
-    uint32_t s0 = pr.y, s1 = pr.z;
+    uint4 pr = pf;                                         // belief.py:55
+    if (sims + 1 < num_sims) {
+      if (NP > 0) ++sb.ctr;
+      else pf = particle(d_belief((uint32_t)bsize));
+    }
     int depth = 0, plen = 0;
     // the step tree of this simulation (NP > 0): usable when the producers'
     // counters are this simulation's
@@ -503,12 +512,12 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
     if (NP > 0) {
       const int slot = it % kSpecSlots;
       int spins = 0;
-      while (lds_acquire(&sp_hdr[4 * slot]) != it + 1) {
+      while (lds_acquire(&sp_hdr[8 * slot]) != it + 1) {
         if (++spins > kSpinMax) {   // bounded: a broken hand-off fails the search, never hangs
 #ifdef POMCP_SPIN_DEBUG
           if (lane == 0)
             printf("search wave: sim %d slot %d seq %d next %d consumed %d\n", it, slot,
-                   sp_hdr[4 * slot], sp_ctl[SP_NEXT], sp_ctl[SP_CONSUMED]);
+                   sp_hdr[8 * slot], sp_ctl[SP_NEXT], sp_ctl[SP_CONSUMED]);
 #endif
           err = POMCP_E_HIP;
           run = false;
@@ -518,9 +527,13 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
       }
       if (!run) break;
       const uint32_t oc = p.other == 0 ? s0s.ctr : s1s.ctr;
-      spv = uniu((uint32_t)sp_hdr[4 * slot + 1]) == sd.ctr && uniu((uint32_t)sp_hdr[4 * slot + 2]) == oc;
+      spv = uniu((uint32_t)sp_hdr[8 * slot + 1]) == sd.ctr && uniu((uint32_t)sp_hdr[8 * slot + 2]) == oc;
       sp_base = slot * NE;
+      pr = make_uint4((uint32_t)sp_hdr[8 * slot + 4], (uint32_t)sp_hdr[8 * slot + 5],
+                      (uint32_t)sp_hdr[8 * slot + 6], 0u);   // the producer's draw of it
     }
+    int t = (int)pr.x;
+    uint32_t s0 = pr.y, s1 = pr.z;
     int blk = root_blk, nv = root_visits;
     double lg = root_log(root_blk, root_visits);   // math.log(nv), mcts.py:534
     double ret = 0.0;
