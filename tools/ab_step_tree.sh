@@ -1,3 +1,5 @@
+#!/bin/bash
+# usage (via gpurun): bash tools/ab_step_tree.sh -> gpurun_out/st7/
 # A/B: search-wave priority; producer / slot counts again with the particle hand-off
 set -o pipefail
 mkdir -p gpurun_out/st7

@@ -1,3 +1,5 @@
+#!/bin/bash
+# usage (via gpurun): bash tools/ablate_wave.sh -> gpurun_out/st5/
 # ablations of the exact single tree (measurement builds in /tmp; results wrong)
 set -o pipefail
 mkdir -p gpurun_out/st5
