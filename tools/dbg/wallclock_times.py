@@ -1,6 +1,6 @@
 """Per-step update / search times of a wall-clock INTMCP (or, with `pomcp` as
 the second argument, POMCP) episode (diagnostics):
-    python tools/dbg/intmcp_wallclock_times.py TIME_LIMIT [pomcp]"""
+    python tools/dbg/wallclock_times.py TIME_LIMIT [pomcp|intmcp] [MAX_STEPS]"""
 import os
 import sys
 import time
@@ -34,10 +34,12 @@ def main():
         extra = "" if pomcp else (f" nodes {list(planner._engine.root_stats()[0].n_nodes)} log "
                                   f"{list(planner._engine.root_stats()[0].n_log)}")
         print(f"step {time.time() - t:.2f} s: update {st['update_time']:.3f} search "
-              f"{st['search_time']:.3f} sims {st['num_sims']}" + extra, flush=True)
+              f"{st['search_time']:.3f} sims {st['num_sims']} arena_full "
+              f"{st.get('arena_full')}" + extra, flush=True)
         return a
 
-    run_episode(step, 41, max_steps=10)
+    steps = int(sys.argv[3]) if len(sys.argv) > 3 else 10
+    run_episode(step, 41, max_steps=steps)
     planner.close()
 
 
