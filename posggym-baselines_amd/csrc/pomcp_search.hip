@@ -122,7 +122,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   stage_model(p.model, sm);
   const int lid = (int)threadIdx.x;
   const int lane = lid & (kWave - 1);
-  const int wave = (int)(blockIdx.x * (TPB / kWave) + (threadIdx.x >> 6));
+#ifdef PB_XCD_REMAP   // measurement builds: workgroups of one XCD (dispatched round-robin) on one contiguous eighth of the trees
+  const int nwg = (int)gridDim.x;
+  const int bx = nwg % 8 == 0 ? (int)((blockIdx.x & 7u) * (unsigned)(nwg / 8) + (blockIdx.x >> 3)) : (int)blockIdx.x;
+#else
+  const int bx = (int)blockIdx.x;
+#endif
+  const int wave = bx * (TPB / kWave) + (int)(threadIdx.x >> 6);
   const int tree = wave * kWave + lane;
   const bool valid = tree < p.B;
   const int tt = valid ? tree : 0;
