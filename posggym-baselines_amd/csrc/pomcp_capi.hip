@@ -53,8 +53,9 @@ struct pomcp_ctx {
 
 // Wave-per-tree search (k_search_lds) for batches up to this many trees: one
 // tree per CU at a time, so beyond one round of 256 trees the tree-per-lane
-// kernel's throughput wins (256 trees 27.0 M vs 23.6 M
-// simulations/s, 1,024 trees 31.7 M vs 94.8 M).
+// kernel's throughput wins (DESIGN.md §6, 65,536 simulations per tree: 256
+// trees 44.7 M vs ~24 M simulations/s; 1,024 trees would run four rounds,
+// ~45 M, vs 86-95 M).
 constexpr int kWaveSearchMaxTrees = 256;
 // and only while its per-tree scratch log stays small
 constexpr int64_t kWaveSearchMaxScratch = (int64_t)4 << 30;
@@ -489,8 +490,12 @@ static int launch_search_wave(pomcp_ctx* ctx, int32_t num_sims, int final_sel) {
                      dim3((unsigned)(kWave * (1 + spec * kSpecProducers))), 0, ctx->stream, ctx->dp,
                      (int)num_sims, final_sel);
   HIP_TRY(ctx, hipGetLastError());
-  hipLaunchKernelGGL(k_log_merge, dim3((unsigned)search_waves(ctx->dp.B)), dim3(kWave), 0,
-                     ctx->stream, ctx->dp);
+  const int nsw = search_waves(ctx->dp.B);
+  hipLaunchKernelGGL(k_log_merge, dim3((unsigned)(ctx->dp.B < kWave ? ctx->dp.B : kWave), (unsigned)nsw),
+                     dim3(256), 0, ctx->stream, ctx->dp);
+  HIP_TRY(ctx, hipGetLastError());
+  hipLaunchKernelGGL(k_log_merge_end, dim3((unsigned)((nsw + 63) / 64)), dim3(64), 0, ctx->stream,
+                     ctx->dp, nsw);
   HIP_TRY(ctx, hipGetLastError());
   return POMCP_OK;
 }

@@ -1014,29 +1014,48 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
 
 // After k_search_lds: append every tree's scratch records of the launch
 // (stats.n_levels of them, in insertion order) to its search wave's shared
-// log, trees in lane order -- one wave per search wave.  A tree's records keep
-// their order; k_extract / k_compact_log separate the trees by lane tag.
-__global__ __launch_bounds__(64) void k_log_merge(DevParams p) {
-  const int sw = (int)blockIdx.x;
-  const int lane = lane_id();
-  const int tree = sw * kWave + lane;
-  const uint32_t cnt = tree < p.B ? (uint32_t)p.stats[tree].n_levels : 0u;
-  uint32_t incl = cnt;   // inclusive prefix over the lanes
+// log, trees in lane order.  A tree's records keep their order; k_extract /
+// k_compact_log separate the trees by lane tag.  One workgroup per (tree lane,
+// search wave) -- grid (min(B, 64), search waves) -- copies one tree's records
+// to its range (the prefix of the lower lanes' counts), so the trees of a
+// batch are copied in parallel (one wave copied them in turn: 64 trees x 65,536
+// simulations took ~0.1 s); k_log_merge_end then moves each log's end.
+__global__ __launch_bounds__(256) void k_log_merge(DevParams p) {
+  const int l = (int)blockIdx.x, sw = (int)blockIdx.y;
+  __shared__ uint32_t s_off, s_n;
+  if (threadIdx.x < kWave) {
+    const int lane = (int)threadIdx.x;
+    const int tree = sw * kWave + lane;
+    const uint32_t cnt = tree < p.B ? (uint32_t)p.stats[tree].n_levels : 0u;
+    uint32_t incl = cnt;   // inclusive prefix over the lanes
 #pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
-    if (lane >= o) incl += y;
+    for (int o = 1; o < kWave; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+      if (lane >= o) incl += y;
+    }
+    const uint32_t base = uniu(p.wlog[sw]);
+    if (lane == l) {
+      s_off = base + incl - cnt;
+      s_n = cnt;
+    }
   }
-  const uint32_t base = uniu(p.wlog[sw]);
+  __syncthreads();
+  const uint32_t n = s_n, off = s_off;
   const WaveLog wl(p.plog, p.Np, sw);
+  const LogRec* const src = p.lscr + (int64_t)(sw * kWave + l) * p.Np;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) wl.store(off + i, src[i]);
+}
+
+// The end of every search wave's log after k_log_merge (a lane per search wave).
+__global__ void k_log_merge_end(DevParams p, int nsw) {
+  const int sw = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (sw >= nsw) return;
+  uint32_t total = 0u;
   for (int l = 0; l < kWave; ++l) {
-    const uint32_t n = rlu(cnt, l);
-    if (n == 0u) continue;
-    const uint32_t off = base + rlu(incl, l) - n;
-    const LogRec* src = p.lscr + (int64_t)(sw * kWave + l) * p.Np;
-    for (uint32_t i = (uint32_t)lane; i < n; i += kWave) wl.store(off + i, src[i]);
+    const int tree = sw * kWave + l;
+    if (tree < p.B) total += (uint32_t)p.stats[tree].n_levels;
   }
-  if (lane == kWave - 1) p.wlog[sw] = base + incl;
+  p.wlog[sw] += total;
 }
 
 #define PB_SEARCH_LDS_INST(E, NA, NP)                                             \
