@@ -38,6 +38,10 @@
 //     atomics); k_log_merge then appends every tree's records to the search
 //     waves' shared logs (pomcp_device.h WaveLog) in tree order, so re-root,
 //     extraction and compaction read the same log as after k_search.
+//   * with NP step-tree producer waves in the tree's workgroup (NP > 0, depth
+//     limits <= 8): the producers evaluate every action sequence of each
+//     coming simulation's first three levels and hand over its particle, so the
+//     search wave reads a level's steps from LDS (kSpecLevels, below).
 // Block layout in LDS: [block][action] 128 B lines {stats, total, slots 0..5}
 // plus the node's {N, log N}; in HBM the (A + 1)-line layout of
 // pomcp_device.h, converted part by part when staged in and written back.
