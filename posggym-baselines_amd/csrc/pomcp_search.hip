@@ -137,8 +137,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   // this tree's blocks: interleaved with the wave's other trees (pomcp_device.h)
   char* const an = reinterpret_cast<char*>(p.an + tree_base_lines(tt, p.Nb, L));
   const int64_t blk_bytes = blk_stride_lines(L) * 128;   // block b at an + b * blk_bytes
-  // the wave's shared particle log (pomcp_device.h LogRec); wpos is the same in
-  // every lane still in the loop (advanced by ballot at convergent points)
+  // the wave's shared particle log (pomcp_device.h LogRec), appended at the
+  // per-wave LDS counter wcnt (below)
   const WaveLog wl(p.plog, p.Np, wave, TM);
   // TM: the policy tables staged in LDS (every draw and prior reads them)
   __shared__ __attribute__((aligned(16))) char tm_lds[TM != 0 ? sizeof(TmTables) : 16];
@@ -153,20 +153,26 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   int epol = 0;       // TM: the ego policy drawn for it
   const int islots = p.islots;   // kSlots (fewer: overflow-map tests)
   const uint32_t wpos0 = p.wlog[wave];
-  uint32_t wpos = wpos0;
   bool app = false;          // this lane has a record to append
   LogRec rec = {0u, 0u, 0u};
-  auto append = [&]() {      // call where every lane still in the loop is active
-    const uint64_t m = __ballot(app);
-    if (m != 0ull) {
+  // A lane's particle-log record (mcts.py:371) waits in `rec` and is stored
+  // inside the NEXT level, after that level's child-line loads: vmcnt
+  // completes in order on gfx950, so a store issued before a load makes the
+  // wait for that load also wait for the store's acknowledgement (appended
+  // right after a level, the record delayed the next child-line wait: +5%
+  // simulations/s).  The level code is divergent, so positions
+  // come from a per-wave LDS counter (one ds_add per active set, lanes in
+  // lane order); each lane's records stay in its insertion order.
+  __shared__ uint32_t wcnt[TPB / kWave];
+  if (lane == 0) wcnt[threadIdx.x >> 6] = wpos0;
+  __builtin_amdgcn_wave_barrier();
+  auto append = [&]() {
+    if (app) {
 #ifndef POMCP_ABLATE_LOG   // ablation build only: no particle-log stores
-      if (app) {
-        const uint32_t at = wpos + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-        wl.store(at, rec);
-        if constexpr (TM != 0) wl.aux[at] = pid;
-      }
+      const uint32_t at = atomicAdd(&wcnt[threadIdx.x >> 6], 1u);
+      wl.store(at, rec);
+      if constexpr (TM != 0) wl.aux[at] = pid;
 #endif
-      wpos += (uint32_t)__popcll(m);
       app = false;
     }
   };
@@ -675,7 +681,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
       root_logn = logtab(root_visits + 1);   // the next simulation's (no wait)
       PT_MARK(0);
     }
-    append();
     // refill the lookahead words the root level consumed while the first level's
     // statistics line (issued by descend) is in flight
     if (phase != TP_DONE) {
@@ -729,6 +734,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         }
         la_step();   // the next step's draws, while the child line is in flight
         PT_MARK(3);
+        append();   // the previous level's record, after this level's loads
         uint32_t n0, n1;
         double r;
         int done;
@@ -806,8 +812,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         }
         PT_MARK(4);
       }
-      append();
     }
+    append();   // the last level's record
     // ------------------------------------------------------ the rollout
     while (phase == TP_ROLL) {                               // mcts.py:414-450
       if (!(rdepth <= p.depth_limit && t <= p.step_limit)) {
