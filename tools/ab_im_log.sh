@@ -1,5 +1,7 @@
 #!/bin/bash
-# A/B (via gpurun): I-NTMCP with a level's log record stored after the next
+# A/B (via gpurun): I-NTMCP with a level's log record stored after the next level's
+# record loads.  The -DIM_LOG_DEFER patch was measured (-1%) and reverted: re-apply
+# it to simulate() before running this; otherwise both builds are equal.
 # level's record loads (-DIM_LOG_DEFER): parity with that build, then the bench.
 set -o pipefail
 mkdir -p gpurun_out/imlog
