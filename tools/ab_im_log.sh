@@ -2,7 +2,6 @@
 # A/B (via gpurun): I-NTMCP with a level's log record stored after the next level's
 # record loads.  The -DIM_LOG_DEFER patch was measured (-1%) and reverted: re-apply
 # it to simulate() before running this; otherwise both builds are equal.
-# level's record loads (-DIM_LOG_DEFER): parity with that build, then the bench.
 set -o pipefail
 mkdir -p gpurun_out/imlog
 for v in "base:" "defer:-DIM_LOG_DEFER"; do
