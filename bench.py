@@ -121,6 +121,10 @@ def _build_if_missing():
     from posggym_baselines_amd import build as nb
     if not os.path.exists(_native.LIB_PATH):
         nb.build()
+    elif not os.environ.get("POMCP_LIB_PATH") and not nb.up_to_date():
+        print(f"bench.py: WARNING: {_native.LIB_PATH} is older than its sources (csrc/, "
+              "include/); this run measures that library (config.lib_sha16 names it) -- "
+              "rebuild with __graft_entry__.build()", file=sys.stderr, flush=True)
 
 
 class _ClockSampler:
@@ -208,6 +212,9 @@ def parse():
     ap.add_argument("--deep", action="store_true",
                     help="gamma=0.99, epsilon=0.01 (depth_limit 459, rollout-dominated)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sub", action="store_true",
+                    help="skip the secondary-configuration records (`sub`) the default run "
+                         "appends after the headline (profiling runs)")
     ap.add_argument("--cpu-sample-sims", type=int, default=16384)
     ap.add_argument("--cpu-sample-trees", type=int, default=4)
     ap.add_argument("--cpu-procs", type=int, default=16,
@@ -282,8 +289,17 @@ def cpu_baseline_parallel(sims, procs, seed, env="Driving-v1", base=None):
     each); rate = all simulations / the slowest process's
     search time.  Forked before this process touches the GPU."""
     import multiprocessing as mp
-    with mp.get_context("fork").Pool(procs) as pool:
+    # close + join (not the context manager, whose exit is terminate(): it
+    # SIGTERMs the workers, which a profiler's signal handler reports as an abort)
+    pool = mp.get_context("fork").Pool(procs)
+    try:
         res = pool.map(_cpu_worker, [(sims, b, seed, env, base) for b in range(procs)])
+        pool.close()
+    except BaseException:
+        pool.terminate()
+        raise
+    finally:
+        pool.join()
     total = sum(r[0] for r in res)
     return {"value": total / max(r[1] for r in res), "unit": "simulations/s", "cores": procs,
             "kind": "port",
@@ -333,26 +349,22 @@ def cpu_baseline_intmcp(sims, pairs, seed, env="Driving-v1"):
                       "oracle/intmcp.py, 1 thread"}
 
 
-def main_intmcp(args):
+def run_intmcp(dev, B, S, env, steps, warmup, seed=0, arena=None):
+    """I-NTMCP nesting level 1 (BASELINE config 5): B planner pairs x S
+    simulations per level, one batched k_im_search launch per step.  Returns
+    the bench fields (value, ms_per_step, roofline, config)."""
     import torch
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1:
-        raise SystemExit("--planner intmcp is a single-GPU configuration (BASELINE config 5)")
-    _build_if_missing()
-    lib_sha = _lib_sha16()
-    torch.cuda.set_device(0)
-    dev = torch.cuda.current_device()
     from posggym_baselines_amd.envs import DrivingModel, PursuitEvasionModel
     from posggym_baselines_amd.planning import BatchedINTMCP, MCTSConfig
     from posggym_baselines_amd.planning.intmcp import plan_intmcp_capacities
-    B, S = args.trees, args.sims
-    cfg = MCTSConfig(seed=args.seed, num_sims=S, **dict(TEST_CFG, state_belief_only=False))
-    model = PursuitEvasionModel() if args.env == "PursuitEvasion-v1" else DrivingModel()
+    lib_sha = _lib_sha16()
+    cfg = MCTSConfig(seed=seed, num_sims=S, **dict(TEST_CFG, state_belief_only=False))
+    model = PursuitEvasionModel() if env == "PursuitEvasion-v1" else DrivingModel()
     A = model.action_spaces["0"].n
-    searches = args.warmup + args.steps + 1
+    searches = warmup + steps + 1
     caps = plan_intmcp_capacities(cfg, model.spec.max_episode_steps, S, searches, A)
-    if args.arena:
-        nodes, nstats, nlog = (int(x) for x in args.arena.split(","))
+    if arena:
+        nodes, nstats, nlog = (int(x) for x in arena.split(","))
         caps.max_nodes, caps.max_stats, caps.max_log = nodes, nstats, nlog
         caps.hash_slots = 1 << max(4, (2 * nodes - 1).bit_length())
     elif B > 1024:
@@ -383,68 +395,58 @@ def main_intmcp(args):
     stream = torch.cuda.Stream(device=dev)
     bp = BatchedINTMCP(model, "0", cfg, B, S, capacities=caps, stream=stream.cuda_stream,
                        device=dev)
-    bp.init_synthetic(1000)
-    for _ in range(args.warmup):
-        with torch.cuda.stream(stream):
-            bp.search(fetch=False)
-    torch.cuda.synchronize()
-    st0 = [(s.n_log[0], s.n_log[1], s.n_nodes[0] + s.n_nodes[1], s.n_stats[0] + s.n_stats[1])
-           for s in bp.engine.root_stats()]
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        with torch.cuda.stream(stream):
-            ev[k][0].record(stream)
-            bp.search(fetch=False)
-            ev[k][1].record(stream)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-    st = bp.engine.root_stats()
-    if any(s.error for s in st):
-        raise SystemExit("I-NTMCP search reported an error")
-    searched = sum(1 for s in st if not s.root_absorbing)
-    lv0 = lv1 = nodes = stats = 0
-    for s, s0 in zip(st, st0):
-        lv1 += s.n_log[0] - s0[0]
-        lv0 += s.n_log[1] - s0[1]
-        nodes += s.n_nodes[0] + s.n_nodes[1] - s0[2]
-        stats += s.n_stats[0] + s.n_stats[1] - s0[3]
-    sims_timed = 2 * S * searched * args.steps
+    try:
+        bp.init_synthetic(1000)
+        for _ in range(warmup):
+            with torch.cuda.stream(stream):
+                bp.search(fetch=False)
+        torch.cuda.synchronize()
+        st0 = [(s.n_log[0], s.n_log[1], s.n_nodes[0] + s.n_nodes[1], s.n_stats[0] + s.n_stats[1])
+               for s in bp.engine.root_stats()]
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(steps)]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            with torch.cuda.stream(stream):
+                ev[k][0].record(stream)
+                bp.search(fetch=False)
+                ev[k][1].record(stream)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / steps
+        st = bp.engine.root_stats()
+        if any(s.error for s in st):
+            raise SystemExit("I-NTMCP search reported an error")
+        searched = sum(1 for s in st if not s.root_absorbing)
+        lv0 = lv1 = nodes = stats = 0
+        for s, s0 in zip(st, st0):
+            lv1 += s.n_log[0] - s0[0]
+            lv0 += s.n_log[1] - s0[1]
+            nodes += s.n_nodes[0] + s.n_nodes[1] - s0[2]
+            stats += s.n_stats[0] + s.n_stats[1] - s0[3]
+        nodes_used = max(max(s.n_nodes[0], s.n_nodes[1]) for s in st)
+    finally:
+        bp.close()
+    sims_timed = 2 * S * searched * steps
     alg_bytes = (B_SIM * sims_timed + b_level(A) * (lv0 + lv1) + b_other(A) * lv1
-                 + B_NODE_IM * nodes) / args.steps
+                 + B_NODE_IM * nodes) / steps
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     # the level-1 root's view (node + statistics heads) is served from LDS
     # (ImPair::rv): those bytes of every level-1 simulation's root level never
     # reach HBM
     alg_bytes_hbm = alg_bytes - (8 + 12 * A) * S * searched
     achieved_hbm = alg_bytes_hbm / (kernel_ms * 1e-3) / 1e9
-    traffic = _pmc_traffic("pmc_intmcp.json", lib_sha, trees=B, sims=S, env=args.env)
-    out = {
-        "metric": f"I-NTMCP simulations/sec on {args.env} (nesting level 1, exact search)",
-        "value": sims_timed / elapsed,
-        "unit": "simulations/s",
-        "n_gpus": 1,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": elapsed * 1e3 / args.steps,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f64",
-        "data": f"synthetic {args.env} roots (env seed 1000+b), build's {args.env} restatement",
-        "config": {"workload": f"I-NTMCP nesting 1 {args.env}, {B} planner pairs x {S} sims per "
-                               "level x 2 levels per step (one batched launch), ucb c=sqrt2 "
-                               "gamma=0.95 depth_limit=2",
-                   "pairs": B, "sims_per_level": S, "pairs_searched": searched,
+    traffic = _pmc_traffic("pmc_intmcp.json", lib_sha, trees=B, sims=S, env=env)
+    return {
+        "value": sims_timed / elapsed, "ms_per_step": elapsed * 1e3 / steps,
+        "workload": f"I-NTMCP nesting 1 {env}, {B} planner pairs x {S} sims per level x 2 levels "
+                    "per step (one batched launch), ucb c=sqrt2 gamma=0.95 depth_limit=2",
+        "config": {"pairs": B, "sims_per_level": S, "pairs_searched": searched,
                    "device": _device_info(dev), "lib_sha16": lib_sha,
                    "arena_per_pair": {"max_nodes": caps.max_nodes, "max_stats": caps.max_stats,
                                       "max_log": caps.max_log, "hash_slots": caps.hash_slots,
-                                      "bytes": caps.bytes_per_pair(A),
-                                      "nodes_used": max(max(s.n_nodes[0], s.n_nodes[1])
-                                                        for s in st)}},
+                                      "bytes": caps.bytes_per_pair(A), "nodes_used": nodes_used}},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "k_im_search", "kernel_ms": kernel_ms,
@@ -452,10 +454,265 @@ def main_intmcp(args):
                      "alg_bytes_hbm_per_launch": alg_bytes_hbm,
                      "achieved_hbm": achieved_hbm, "frac_hbm": achieved_hbm / HBM_PEAK_GBS},
     }
+
+
+def main_intmcp(args):
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        raise SystemExit("--planner intmcp is a single-GPU configuration (BASELINE config 5)")
+    _build_if_missing()
+    torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+    r = run_intmcp(dev, args.trees, args.sims, args.env, args.steps, args.warmup, args.seed,
+                   args.arena)
+    out = {
+        "metric": f"I-NTMCP simulations/sec on {args.env} (nesting level 1, exact search)",
+        "value": r["value"],
+        "unit": "simulations/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": r["ms_per_step"],
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": f"synthetic {args.env} roots (env seed 1000+b), build's {args.env} restatement",
+        "config": dict({"workload": r["workload"]}, **r["config"]),
+        "roofline": r["roofline"],
+    }
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_intmcp(2048, 16, args.seed, args.env)
     print(json.dumps(out), flush=True)
-    bp.close()
+
+
+def run_pomcp(dev, *, env, B, S, K, base_cfg, tm, steps, warmup, seed=0, max_blocks=512,
+              world=1, rank=0, dist=None, update_step=False, clocks=False):
+    """`steps` timed POMCP steps on B synthetic roots (S simulations each; K
+    replica trees per planner, merged on the device).  A step is restore() +
+    one k_search launch + the root-parallel exchange, or with `update_step` a
+    whole planning step: search, the environment's answer (pomcp_synthetic_step)
+    and update() -- re-root, extraction, reinvigoration, subtree compaction --
+    before the restore of the next step."""
+    import torch
+    from posggym_baselines_amd.envs import DrivingModel, PursuitEvasionModel
+    from posggym_baselines_amd.planning import BatchedPOMCP, MCTSConfig
+    from posggym_baselines_amd.planning.engine import plan_capacities
+    from posggym_baselines_amd.planning.parallel import gather_buffer_tensor, merge_buffer_tensor
+    lib_sha = _lib_sha16()
+    cfg = MCTSConfig(seed=seed, num_sims=S, **base_cfg)
+    model = PursuitEvasionModel() if env == "PursuitEvasion-v1" else DrivingModel()
+    A = model.action_spaces["0"].n
+    step_limit = model.spec.max_episode_steps
+    mb = min(max_blocks, S + 64)
+    note = ""
+    if update_step:
+        # the re-root keeps the chosen child's particles (its visits: thousands)
+        # in the root belief: size that buffer from a 1,024-root probe of the same
+        # workload (x1.5; an overflow still fails loudly, POMCP_E_ARENA)
+        n_target = cfg.num_particles + cfg.extra_particles
+        pc = plan_capacities(cfg, step_limit, S, 1, reroot=True, max_blocks=mb,
+                             overflow_slots=1024)
+        nprobe = min(B, 1024)
+        probe = BatchedPOMCP(model, "0", cfg, nprobe, S, capacities=pc, device=dev)
+        try:
+            probe.init_synthetic(1000)
+            acts = probe.search()
+            probe.engine.update(acts, probe.engine.synthetic_step(1000, acts))
+            probe.engine.search(1, fetch=False)
+            bmax = max(s.belief_size for s in probe.engine.root_stats())
+        finally:
+            probe.close()
+        caps = plan_capacities(cfg, step_limit, S, 1, reroot=True, max_blocks=mb,
+                               overflow_slots=1024)
+        caps.max_belief = min(caps.max_belief, int(1.5 * bmax) + 2 * n_target + 64)
+        free = torch.cuda.mem_get_info(dev)[0]
+        while B > 1024 and caps.bytes_per_tree(A) * B > 0.92 * free:
+            B //= 2
+            note = f" (halved to fit {free / 2**30:.0f} GiB)"
+    else:
+        caps = plan_capacities(cfg, step_limit, S, 1, reroot=False, max_blocks=mb,
+                               overflow_slots=1024)
+    stream = torch.cuda.Stream(device=dev)
+    bp = BatchedPOMCP(model, "0", cfg, B, S, capacities=caps, stream=stream.cuda_stream,
+                      device=dev, type_policies=type_policies(model) if tm else None)
+    try:
+        bp.init_synthetic(1000)
+        bp.engine.rekey(seed ^ (rank << 32))
+        merge = merge_buffer_tensor(bp.engine, f"cuda:{dev}")
+        gather = gather_buffer_tensor(bp.engine, world, f"cuda:{dev}") if world > 1 else None
+        upd_ms = []
+
+        def step(events=None):
+            with torch.cuda.stream(stream):
+                bp.restore()
+                if events is not None:
+                    events[0].record(stream)
+                if update_step:
+                    acts = bp.search(fetch=True)
+                else:
+                    bp.search(fetch=False)
+                if events is not None:
+                    events[1].record(stream)
+                if update_step:
+                    obs = bp.engine.synthetic_step(1000, acts)
+                    t1 = time.perf_counter()
+                    bp.engine.update(acts, obs)   # synchronises
+                    if events is not None:
+                        upd_ms.append((time.perf_counter() - t1) * 1e3)
+                    return
+                # the root-parallel decision: one all-gather of every rank's exchange
+                # records (RCCL, same stream), then the device merge of each planner's
+                # world x K replicas in replica order (pomcp_merge_roots) -- the same
+                # FP64 sums and action on every rank
+                if world > 1:
+                    dist.all_gather_into_tensor(gather, merge)
+                bp.engine.merge_roots(K, fetch=False, world=world if world > 1 else 0)
+
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        if not update_step:
+            bp.engine.root_stats()   # raises on any per-tree error (arena overflow, ...)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(steps)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        with _ClockSampler() if clocks else _NoClocks() as clk:
+            t0 = time.perf_counter()
+            for k in range(steps):
+                step(ev[k])
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            elapsed = time.perf_counter() - t0
+        kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / steps
+        if world > 1:
+            t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=f"cuda:{dev}")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed, kernel_ms = float(t[0]), float(t[1])
+        if update_step:   # the search statistics of the last timed step (before its update)
+            bp.restore()
+            with torch.cuda.stream(stream):
+                bp.search(fetch=False)
+            torch.cuda.synchronize()
+        st = bp.engine.root_stats()
+        sims = sum(s.num_sims for s in st)          # counted by the kernel, last timed launch
+        levels = sum(s.n_levels for s in st)
+        expands = sum(s.n_expansions for s in st)
+        new_nodes = sum(s.n_new_nodes for s in st)
+        deferred = sum(s.n_deferred for s in st)
+        rollout = sum(s.n_rollout_steps for s in st)
+        blocks_used = max(s.n_blocks for s in st)
+        log_used = max(s.n_log for s in st)
+        if not update_step:
+            merged = bp.engine.merge_roots(K, world=world if world > 1 else 0)   # checks errors
+            if not all(0 <= m.action < A for m in merged):
+                raise SystemExit("merged action out of range")
+    finally:
+        bp.close()
+    alg_bytes = B_SIM * sims + b_level(A) * levels + b_expand(A) * expands + B_NEW_NODE * new_nodes
+    if tm:   # the action_probs of every stepped node (+ 8A written per leaf expansion)
+        alg_bytes += B_TM_LEVEL * levels + 8 * A * expands
+    # the root level of every simulation is served from LDS / registers except
+    # its particle-log append (DESIGN.md §4): its other bytes never reach HBM
+    root_levels = min(sims, levels)
+    alg_bytes_hbm = alg_bytes - (b_level(A) - B_LOG_APPEND) * root_levels
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    achieved_hbm = alg_bytes_hbm / (kernel_ms * 1e-3) / 1e9
+    counted = sims
+    if world > 1:
+        t = torch.tensor([counted], dtype=torch.float64, device=f"cuda:{dev}")
+        dist.all_reduce(t)   # every rank's counted simulations
+        counted = int(t.item())
+    # every timed step re-searches the same restored roots: the same count each step
+    value = counted * steps / elapsed
+    traffic = None if update_step else _pmc_traffic("pmc_search.json", lib_sha, trees=B, sims=S,
+                                                     env=env)
+    env_desc = ("PursuitEvasion-v1 16x16 max_obs_distance=12" if env == "PursuitEvasion-v1"
+                else "Driving-v1 14x14RoundAbout")
+    r = {
+        "value": value, "ms_per_step": elapsed * 1e3 / steps, "counted": counted,
+        "sims_per_step": sims, "B": B, "caps": caps, "clocks": clk.samples, "lib_sha": lib_sha,
+        "workload": f"{'POTMMCP' if tm else 'POMCP'} {env_desc} exact search, {B} roots{note} "
+                    f"x {S} sims per GPU, {cfg.action_selection} c=sqrt2 "
+                    f"gamma={cfg.discount} depth_limit={cfg.depth_limit}, "
+                    + ("3 ego policies under a meta-policy, 2 other-agent policies "
+                       "(fixed distributions), " if tm else "")
+                    + (f"{B // K} planner(s) x {K} replica trees merged on the device, "
+                       if K > 1 else "")
+                    + ("each step = search + env step + update() (re-root, extraction, "
+                       "reinvigoration, subtree compaction)" if update_step else
+                       f"root-parallel all-gather over {world} GPU(s)"),
+        "rollout_steps_per_sim": rollout / max(sims, 1),
+        "deferred_levels_per_sim": deferred / max(sims, 1),
+        "blocks_used": blocks_used, "log_used": log_used, "depth_limit": cfg.depth_limit,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "k_search" if B > 256 or K > 1 else "k_search_lds",
+                     "kernel_ms": kernel_ms,
+                     "alg_bytes_per_launch": alg_bytes,
+                     # the same without the root level's LDS-served bytes
+                     "alg_bytes_hbm_per_launch": alg_bytes_hbm,
+                     "achieved_hbm": achieved_hbm, "frac_hbm": achieved_hbm / HBM_PEAK_GBS},
+    }
+    if update_step:
+        r["update_ms"] = sum(upd_ms) / max(1, len(upd_ms))
+    return r
+
+
+class _NoClocks:
+    samples = []
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+def _sub(name, r):
+    """A compact record of one secondary configuration (the `sub` list)."""
+    d = {"name": name, "workload": r["workload"], "value": r["value"], "unit": "simulations/s",
+         "ms_per_step": r["ms_per_step"], "kernel": r["roofline"]["kernel"],
+         "kernel_ms": r["roofline"]["kernel_ms"], "frac": r["roofline"]["frac"],
+         "frac_hbm": r["roofline"]["frac_hbm"]}
+    if "update_ms" in r:
+        d["update_ms"] = r["update_ms"]
+    return d
+
+
+def sub_records(dev, seed):
+    """BASELINE configs 2 (one root, both single-planner modes), 3 (with the
+    update()-inclusive step, so the reinvigoration kernel runs in the timed
+    region) and 5, each with a few timed steps; a failure is recorded, never
+    fatal to the headline line."""
+    jobs = [
+        ("C2 exact single tree (1 x 65536 sims)",
+         lambda: run_pomcp(dev, env="Driving-v1", B=1, S=65536, K=1, base_cfg=TEST_CFG, tm=False,
+                           steps=3, warmup=1, seed=seed)),
+        ("C2 one planner, 1024 replica trees x 64 sims",
+         lambda: run_pomcp(dev, env="Driving-v1", B=1024, S=64, K=1024, base_cfg=TEST_CFG,
+                           tm=False, steps=20, warmup=5, seed=seed)),
+        ("C3 PursuitEvasion-v1 65536 x 65536, update()-inclusive step",
+         lambda: run_pomcp(dev, env="PursuitEvasion-v1", B=65536, S=65536, K=1,
+                           base_cfg=TEST_CFG, tm=False, steps=2, warmup=1, seed=seed,
+                           update_step=True)),
+        ("C5 I-NTMCP nesting 1, 65536 pairs x 256 sims per level",
+         lambda: run_intmcp(dev, 65536, 256, "Driving-v1", 3, 1, seed)),
+    ]
+    out = []
+    for name, job in jobs:
+        t0 = time.perf_counter()
+        try:
+            d = _sub(name, job())
+        except BaseException as e:   # SystemExit included: the headline line still prints
+            d = {"name": name, "error": f"{type(e).__name__}: {e}"}
+        d["wall_s"] = round(time.perf_counter() - t0, 1)
+        out.append(d)
+    return out
 
 
 def main():
@@ -494,140 +751,49 @@ def main():
     dev = torch.cuda.current_device()
     if world > 1:
         dist.barrier()   # rank 0's build is complete
-    lib_sha = _lib_sha16()
-    from posggym_baselines_amd.envs import DrivingModel, PursuitEvasionModel
-    from posggym_baselines_amd.planning import BatchedPOMCP, MCTSConfig
-    from posggym_baselines_amd.planning.engine import plan_capacities
-    from posggym_baselines_amd.planning.parallel import gather_buffer_tensor, merge_buffer_tensor
-
     B, S, K = args.trees, args.sims, args.root_parallel
-    cfg = MCTSConfig(seed=args.seed, num_sims=S, **base_cfg)
-    model = PursuitEvasionModel() if args.env == "PursuitEvasion-v1" else DrivingModel()
-    caps = plan_capacities(cfg, model.spec.max_episode_steps, S, 1, reroot=False,
-                           max_blocks=min(args.max_blocks, S + 64),
-                           overflow_slots=1024)
-    stream = torch.cuda.Stream(device=dev)
-    bp = BatchedPOMCP(model, "0", cfg, B, S, capacities=caps, stream=stream.cuda_stream,
-                      device=dev, type_policies=type_policies(model) if tm else None)
-    bp.init_synthetic(1000)
-    bp.engine.rekey(args.seed ^ (rank << 32))
-    A = bp.engine.A
-    merge = merge_buffer_tensor(bp.engine, f"cuda:{dev}")
-    gather = gather_buffer_tensor(bp.engine, world, f"cuda:{dev}") if world > 1 else None
-
-    def step(events=None):
-        with torch.cuda.stream(stream):
-            bp.restore()
-            if events is not None:
-                events[0].record(stream)
-            bp.search(fetch=False)
-            if events is not None:
-                events[1].record(stream)
-            # the root-parallel decision: one all-gather of every rank's exchange
-            # records (RCCL, same stream), then the device merge of each planner's
-            # world x K replicas in replica order (pomcp_merge_roots) -- the same
-            # FP64 sums and action on every rank
-            if world > 1:
-                dist.all_gather_into_tensor(gather, merge)
-            bp.engine.merge_roots(K, fetch=False, world=world if world > 1 else 0)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    st = bp.engine.root_stats()   # raises on any per-tree error (arena overflow, ...)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    with _ClockSampler() as clocks:
-        t0 = time.perf_counter()
-        for k in range(args.steps):
-            step(ev[k])
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
-    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-    if world > 1:
-        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=f"cuda:{dev}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms = float(t[0]), float(t[1])
-    st = bp.engine.root_stats()
-    sims = sum(s.num_sims for s in st)          # counted by the kernel, last timed launch
-    levels = sum(s.n_levels for s in st)
-    expands = sum(s.n_expansions for s in st)
-    new_nodes = sum(s.n_new_nodes for s in st)
-    alg_bytes = B_SIM * sims + b_level(A) * levels + b_expand(A) * expands + B_NEW_NODE * new_nodes
-    if tm:   # the action_probs of every stepped node (+ 8A written per leaf expansion)
-        alg_bytes += B_TM_LEVEL * levels + 8 * A * expands
-    # the root level of every simulation is served from LDS / registers except
-    # its particle-log append: its other bytes never reach HBM
-    root_levels = min(sims, levels)
-    alg_bytes_hbm = alg_bytes - (b_level(A) - B_LOG_APPEND) * root_levels
-    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    achieved_hbm = alg_bytes_hbm / (kernel_ms * 1e-3) / 1e9
-    counted = sims
-    if world > 1:
-        t = torch.tensor([counted], dtype=torch.float64, device=f"cuda:{dev}")
-        dist.all_reduce(t)   # every rank's counted simulations
-        counted = int(t.item())
-    # every timed step re-searches the same restored roots: the same count each step
-    total_sims = counted * args.steps
-    value = total_sims / elapsed
-    merged = bp.engine.merge_roots(K, world=world if world > 1 else 0)   # checks replica errors
-    if not all(0 <= m.action < A for m in merged):
-        raise SystemExit("merged action out of range")
-    traffic = _pmc_traffic("pmc_search.json", lib_sha, trees=B, sims=S, env=args.env)
-    env_desc = ("PursuitEvasion-v1 16x16 max_obs_distance=12" if args.env == "PursuitEvasion-v1"
-                else "Driving-v1 14x14RoundAbout")
+    r = run_pomcp(dev, env=args.env, B=B, S=S, K=K, base_cfg=base_cfg, tm=tm, steps=args.steps,
+                  warmup=args.warmup, seed=args.seed, max_blocks=args.max_blocks, world=world,
+                  rank=rank, dist=dist if world > 1 else None, clocks=True)
+    caps = r["caps"]
     out = {
         "metric": (f"MCTS simulations/sec on {args.env} (POTMMCP exact search, fixed-distribution "
                    "policies)" if tm else f"MCTS simulations/sec on {args.env} (POMCP exact search)"),
-        "value": value,
+        "value": r["value"],
         "unit": "simulations/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed * 1e3 / args.steps,
+        "ms_per_step": r["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": f"synthetic {args.env} belief states (env seed 1000+b), build's {args.env} "
                 "restatement",
-        "config": {"workload": f"{'POTMMCP' if tm else 'POMCP'} {env_desc} exact search, {B} roots "
-                               f"x {S} sims per GPU, {cfg.action_selection} c=sqrt2 "
-                               f"gamma={cfg.discount} depth_limit={cfg.depth_limit}, "
-                               + ("3 ego policies under a meta-policy, 2 other-agent policies "
-                                  "(fixed distributions), " if tm else "")
-                               + (f"{B // K} planner(s) x {K} replica trees merged on the device, "
-                                  if K > 1 else "")
-                               + f"root-parallel all-gather over {world} GPU(s)",
-                   "trees_per_gpu": B, "sims_per_tree": S, "depth_limit": cfg.depth_limit,
+        "config": {"workload": r["workload"],
+                   "trees_per_gpu": B, "sims_per_tree": S, "depth_limit": r["depth_limit"],
                    "root_parallel": K, "planners_per_gpu": B // K,
                    "sims_per_planner_step": S * K,
-                   "rollout_steps_per_sim": sum(s.n_rollout_steps for s in st) / max(sims, 1),
+                   "rollout_steps_per_sim": r["rollout_steps_per_sim"],
+                   "deferred_levels_per_sim": r["deferred_levels_per_sim"],
                    "parallelism": f"root-parallel x{world}",
-                   "device": dict(_device_info(dev), during_run=clocks.samples),
-                   "lib_sha16": lib_sha, "counted_sims_per_step": counted,
+                   "device": dict(_device_info(dev), during_run=r["clocks"]),
+                   "lib_sha16": r["lib_sha"], "counted_sims_per_step": r["counted"],
                    "arena": {"max_blocks": caps.max_blocks,
-                             "max_blocks_used": max(s.n_blocks for s in st),
+                             "max_blocks_used": r["blocks_used"],
                              "max_particles": caps.max_particles,
-                             "max_particles_used": max(s.n_log for s in st)}},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_search", "kernel_ms": kernel_ms,
-                     "alg_bytes_per_launch": alg_bytes,
-                     # the same without the root level's LDS-served bytes
-                     "alg_bytes_hbm_per_launch": alg_bytes_hbm,
-                     "achieved_hbm": achieved_hbm, "frac_hbm": achieved_hbm / HBM_PEAK_GBS},
+                             "max_particles_used": r["log_used"]}},
+        "roofline": r["roofline"],
     }
     if cpu is not None:
         out["cpu_baseline"] = cpu
+    default_run = (world == 1 and not tm and not args.deep and args.env == "Driving-v1"
+                   and B == 65536 and S == 65536 and K == 1)
+    if rank == 0 and default_run and not args.no_sub:
+        out["sub"] = sub_records(dev, args.seed)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    bp.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -121,7 +121,9 @@ typedef struct pomcp_root_stats {
   int64_t n_new_nodes;          /* obs nodes created (mcts.py:369) */
   int64_t n_rollout_steps;      /* model steps in _rollout (mcts.py:414-450) */
   int64_t n_probes;             /* obs-child hash bucket probes */
-  int32_t n_obs_nodes, n_blocks, n_log, pad;
+  int32_t n_obs_nodes, n_blocks, n_log;
+  int32_t n_deferred;           /* levels whose child (beyond the depth / step limits) was
+                                   not looked up: deferred records */
 } pomcp_root_stats;
 
 typedef struct pomcp_ctx pomcp_ctx;
@@ -222,6 +224,17 @@ typedef struct pomcp_type_policies {
   int32_t meta_policy[POMCP_MAX_TYPE_POLICIES][POMCP_MAX_TYPE_POLICIES];
   double meta_weight[POMCP_MAX_TYPE_POLICIES][POMCP_MAX_TYPE_POLICIES];
   double expected_prior[POMCP_MAX_ACTIONS];
+  /* The base planner (MCTS / IPOMCP / POMCP, mcts.py:22-739) with fixed-
+   * distribution policies runs on the same machinery; zeros = POTMMCP:
+   *   no_meta_draw     no sample_policy draw per simulation (ego policy 0 = the
+   *                    search policy, potmmcp.py:381-389 is POTMMCP's only);
+   *   no_mixture_draw  no policy draw per initial particle (the other agent is
+   *                    one stateless policy, index 0: state_belief_only=True);
+   *   ego_uniform      the ego's rollout draws Discrete.sample() (RandomSearchPolicy,
+   *                    search_policy.py:170) instead of random.choices over ego_pi;
+   *   other_uniform    the other agent draws Discrete.sample()
+   *                    (RandomOtherAgentPolicy, other_policy.py:151). */
+  int32_t no_meta_draw, no_mixture_draw, ego_uniform, other_uniform;
 } pomcp_type_policies;
 int pomcp_set_type_policies(pomcp_ctx* ctx, const pomcp_type_policies* tp);
 
@@ -307,6 +320,14 @@ int pomcp_merge_roots(pomcp_ctx* ctx, int32_t group, int32_t world, pomcp_merged
  * the model's b0 under env key (env_seed_base + b, 0x40000000) and the ego's
  * initial obs is written to obs_keys_out (host, [num_trees], may be NULL). */
 int pomcp_synthetic_obs(pomcp_ctx* ctx, uint64_t env_seed_base, uint64_t* obs_keys_out);
+/* The environment's answer to the planners' actions (env.step of the episode
+ * loop, exp_utils.py:481-505, for the synthetic roots): tree b's true initial
+ * state (as pomcp_synthetic_obs) stepped with actions[b] (host, [num_trees]) and
+ * the other agent's uniformly drawn action (env key's action stream); the ego's
+ * next observation -> obs_keys_out (host, may be NULL).  For update()-inclusive
+ * benchmark steps. */
+int pomcp_synthetic_step(pomcp_ctx* ctx, uint64_t env_seed_base, const int32_t* actions,
+                         uint64_t* obs_keys_out);
 /* Save / restore the complete post-update root state (headers, root nodes,
  * root belief, RNG counters) so a timed loop can re-search the same roots. */
 int pomcp_snapshot(pomcp_ctx* ctx);

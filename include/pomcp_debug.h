@@ -24,6 +24,13 @@ int pomcp_debug_phase_timing(pomcp_ctx* ctx, uint64_t* out, int32_t capacity, in
  * pomcp_debug_phase_timing (tools/phase_timing_im.py). */
 typedef struct intmcp_ctx intmcp_ctx;
 int intmcp_debug_phase_timing(intmcp_ctx* ctx, uint64_t* out, int32_t capacity, int32_t* count);
+/* I-NTMCP: the other agent's softmax (sample_action, intmcp.py:763-791) takes
+ * its choice from bounded FP32 weights and falls back to the exact FP64 path
+ * near a cumulative weight; `slack` (>= 1, default 1) widens that bound, so a
+ * large value sends most draws down the exact path (results stay exact).  From
+ * this call on the exact-path draws are counted: intmcp_debug_exact_draws. */
+int intmcp_debug_set_softmax_slack(intmcp_ctx* ctx, float slack);
+int intmcp_debug_exact_draws(intmcp_ctx* ctx, uint64_t* count);
 /* Only the first n (1..6) inline obs-child slots of each action node are used,
  * the overflow map holds the rest (tests of that path).  Before the first search. */
 int pomcp_debug_set_inline_slots(pomcp_ctx* ctx, int32_t n);

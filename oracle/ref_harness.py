@@ -440,3 +440,139 @@ def reference_potmmcp_episode(cfg_kwargs, num_sims, env_seed, spec, ego="0", tre
     trace = run_episode(step, env_seed, ego=ego, max_steps=max_steps, env=env)
     planner.close()
     return trace, records
+
+
+# ------------------------------------------- MCTS / IPOMCP / POMCP, any policies
+def make_reference_mcts(model, agent_id, cfg_kwargs, num_sims, streams, spec,
+                        planner_cls="IPOMCP"):
+    """The reference base planner (``MCTS`` / ``IPOMCP`` / ``POMCP``,
+    mcts.py:22-739, ipomcp.py:11-38, pomcp.py:9-35) with fixed-distribution
+    policies, wired to ``streams`` like ``make_reference_potmmcp``:
+      spec["search"]: None (``RandomSearchPolicy``) or the ego's action
+        probabilities (``SearchPolicyWrapper`` of a ``FixedDistributionPolicy``,
+        search_policy.py:188-224: prior of every node, rollouts);
+      spec["other"]: {"kind": "random"} (``RandomOtherAgentPolicy``), {"kind":
+        "fixed", "probs": [...]} (a stateless ``FixedDistributionPolicy``, used
+        with state_belief_only=True) or {"kind": "mixture", "policies": {id:
+        probs}} (``OtherAgentMixturePolicy``, state_belief_only=False)."""
+    P = import_reference()
+    import posggym_baselines.planning.belief as B
+    import posggym_baselines.planning.mcts as mcts_mod
+    import posggym_baselines.planning.other_policy as op_mod
+    import posggym_baselines.planning.search_policy as sp_mod
+    from oracle.rng import S_ACT_BASE, S_BELIEF, S_MIXTURE, S_SELECT, StreamRandom
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "posggym-baselines_amd"))
+    from posggym_baselines_amd.planning.policies import FixedDistributionPolicy
+
+    select = StreamRandom(streams, S_SELECT)
+    belief_rng = StreamRandom(streams, S_BELIEF)
+    rnd = types.ModuleType("random_shim")
+    rnd.Random = lambda seed=None: belief_rng
+    rnd.choice = select.choice
+    rnd.choices = select.choices
+    rnd.random = select.random
+    mcts_mod.random = rnd
+    B.random = rnd
+    mix = types.ModuleType("random_shim_mixture")
+    mix.choice = StreamRandom(streams, S_MIXTURE).choice
+    op_mod.random = mix
+    clock = _FakeClock()
+    mcts_mod.time = clock
+    from posggym_baselines.planning.utils import KnownBounds
+    kw = dict(cfg_kwargs)
+    if kw.get("known_bounds") is not None:
+        kw["known_bounds"] = KnownBounds(*kw["known_bounds"])
+    config = P.MCTSConfig(**kw)
+    other = [i for i in model.possible_agents if i != agent_id][0]
+
+    def fixed(i, pid, probs):
+        return FixedDistributionPolicy(model, i, pid, probs,
+                                       StreamRandom(streams, S_ACT_BASE + int(i)))
+
+    if spec.get("search") is None:
+        search = P.RandomSearchPolicy(model, agent_id)
+    else:
+        search = sp_mod.SearchPolicyWrapper(fixed(agent_id, "search", spec["search"]))
+    o = spec["other"]
+    if o["kind"] == "random":
+        others = {other: P.RandomOtherAgentPolicy(model, other)}
+    elif o["kind"] == "fixed":
+        others = {other: fixed(other, "fixed", o["probs"])}
+    else:
+        others = {other: P.OtherAgentMixturePolicy(
+            model, other, {k: fixed(other, k, v) for k, v in o["policies"].items()})}
+    if planner_cls == "POMCP":
+        assert o["kind"] == "random"
+        planner = P.POMCP(model, agent_id, config, search_policy=search)
+    else:
+        planner = getattr(P, planner_cls)(model, agent_id, config, others, search)
+    inner = planner._simulate
+    count = [0]
+
+    def simulate(hps, obs_node, depth, search_policy):
+        if depth == 0:
+            count[0] += 1
+            if count[0] >= num_sims:
+                clock.now += 1e9
+                count[0] = 0
+        return inner(hps, obs_node, depth, search_policy)
+
+    planner._simulate = simulate
+    return planner
+
+
+def reference_mcts_record(planner, searched, action, spec):
+    """``reference_potmmcp_record`` for the base planner: the particles' other-
+    agent policy index is 0 unless the other agent is a mixture."""
+    from oracle.episode import fhex
+    rec = {"searched": searched, "action": int(action)}
+    if not searched:
+        return rec
+    root = planner.root
+    other = [i for i in planner.model.possible_agents if i != planner.agent_id][0]
+    if spec["other"]["kind"] == "mixture":
+        oth_ids = list(planner.other_agent_policies[other].policies)
+        parts = [(p.state, p.t, p.policy_state[other]["policy_id"]) for p in root.belief.particles]
+    else:
+        oth_ids = [0]
+        parts = [(p.state, p.t, 0) for p in root.belief.particles]
+    st = planner.step_statistics
+    rec["belief_size"] = len(parts)
+    rec["belief_digest"] = potmmcp_belief_digest(parts, oth_ids, planner.model.pack_words)
+    rec["num_sims"] = int(st["num_sims"])
+    rec["prior"] = [fhex(root.action_probs[a]) for a in range(len(root.action_probs))]
+    if rec["num_sims"] > 0:
+        kids = root.get_child_nodes()
+        rec["search_depth"] = int(st["search_depth"])
+        rec["root_visits"] = int(root.visits)
+        rec["child_visits"] = [int(c.visits) for c in kids]
+        rec["child_values"] = [fhex(c.value) for c in kids]
+        rec["child_totals"] = [fhex(c.total_value) for c in kids]
+        rec["min_value"] = fhex(st["min_value"])
+        rec["max_value"] = fhex(st["max_value"])
+    return rec
+
+
+def reference_mcts_episode(cfg_kwargs, num_sims, env_seed, spec, ego="0", tree=0, max_steps=50,
+                           env="Driving-v1", planner_cls="IPOMCP"):
+    """One full episode with the real reference base planner. Returns (trace, records)."""
+    from oracle.envs import make_model
+    from oracle.episode import run_episode
+    from oracle.rng import Streams
+
+    streams = Streams(cfg_kwargs.get("seed") or 0, tree)
+    model = make_model(env, streams)
+    planner = make_reference_mcts(model, ego, cfg_kwargs, num_sims, streams, spec, planner_cls)
+    planner.reset()
+    records = []
+
+    def step(obs):
+        searched = not planner.root.is_absorbing
+        a = planner.step(obs)
+        records.append(reference_mcts_record(planner, searched, a, spec))
+        return a
+
+    trace = run_episode(step, env_seed, ego=ego, max_steps=max_steps, env=env)
+    planner.close()
+    return trace, records

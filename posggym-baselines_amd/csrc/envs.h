@@ -8,6 +8,7 @@
 //                              joint step + the ego's reward and
 //                              terminated-or-all-done flag (mcts.py:333-344)
 //   obs_key(m, ego, n0, n1)    the ego's packed observation
+//   done_of(ego, n0, n1)       step's done flag, from the next state alone
 //   sample_initial(m, draw, &s0, &s1)             model.sample_initial_state
 //   sample_agent_initial(m, ego, obs, draw, &s0, &s1)
 //                              model.sample_agent_initial_state (false: obs
@@ -36,8 +37,13 @@ struct EnvDriving {
     drv_step2_vec(m, s0, s1, ego == 0 ? a_ego : a_oth, ego == 0 ? a_oth : a_ego, j, n0, n1);
     const uint32_t e0 = ego == 0 ? s0 : s1, e1 = ego == 0 ? *n0 : *n1;
     *r = drv_reward_vec(m, e0, e1);
-    *done = (((e1 >> 15) & 3u) != 0u ||
-             (((*n0 >> 15) & 3u) != 0u && ((*n1 >> 15) & 3u) != 0u)) ? 1 : 0;
+    *done = done_of(ego, *n0, *n1);
+  }
+  // the ego's terminated-or-all-done flag of a next state (mcts.py:340-344):
+  // a function of the state alone (deferred records, pomcp_device.h)
+  __device__ static __forceinline__ int done_of(int ego, uint32_t n0, uint32_t n1) {
+    const uint32_t e1 = ego == 0 ? n0 : n1;
+    return (((e1 >> 15) & 3u) != 0u || (((n0 >> 15) & 3u) != 0u && ((n1 >> 15) & 3u) != 0u)) ? 1 : 0;
   }
   __device__ static __forceinline__ uint64_t obs_key(const Model& m, int ego, uint32_t n0,
                                                      uint32_t n1) {
@@ -86,7 +92,10 @@ struct EnvPursuitEvasion {
     pe_step(m, s0, s1, ego == 0 ? a_ego : a_oth, ego == 0 ? a_oth : a_ego, n0, n1, &prog,
             &outcome);
     *r = pe_reward(m, ego, s0, prog, outcome);
-    *done = pe_done(*n0) ? 1 : 0;   // both agents terminate together
+    *done = done_of(ego, *n0, *n1);
+  }
+  __device__ static __forceinline__ int done_of(int /*ego*/, uint32_t n0, uint32_t /*n1*/) {
+    return pe_done(n0) ? 1 : 0;   // both agents terminate together
   }
   __device__ static __forceinline__ uint64_t obs_key(const Model& m, int ego, uint32_t n0,
                                                      uint32_t n1) {

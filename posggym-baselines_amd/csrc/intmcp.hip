@@ -24,14 +24,14 @@
 
 namespace pb {
 
-constexpr int kImPath = 128;
-// Widening factor of the bounded FP32 fast path of the other agent's
-// softmax (ImPair::sample_action).  Test builds set it
-// large so that the exact fallbacks run often (tests/test_gpu_intmcp.py
-// parity under tools/ab_im.sh variants); any value >= 1 keeps results exact.
+constexpr int kImPath = 128;          // tree levels per simulation
+// Default widening factor of the bounded FP32 fast path of the other agent's
+// softmax (ImPair::sample_action, ImParams::fast_slack): 1 = the proven
+// bound; any value >= 1 keeps results exact, and tests widen it at run time
+// (intmcp_debug_set_softmax_slack) so that the exact fallbacks run often.
 #ifndef IM_FAST_SLACK
 #define IM_FAST_SLACK 1.0f
-#endif          // tree levels per simulation
+#endif
 constexpr int kImMaxA = 6;            // registration order: 6 x 3 bits (INode.info)
 constexpr int kImRegPath = 3;         // path levels held in registers (deeper ones in p.path)
 // A node: its line (128 B) = the INode {parent, info, visits, t} (16 B), the
@@ -152,6 +152,13 @@ struct ImParams {
   int32_t* out;         // [B][2] {root absorbing, error}
   uint64_t* out_obs;    // [B] synthetic roots
   uint64_t* timing;     // [B][kImPhases] (diagnostics build, -DPOMCP_PHASE_TIMING)
+  // the other agent's softmax (sample_action): the fast path's bound is widened
+  // by fast_slack (1 = the product's bound; tests widen it so the exact FP64
+  // path runs on most draws, intmcp_debug_set_softmax_slack), and the exact-path
+  // draws are counted when exact_draws is set (tests only)
+  float fast_slack;
+  int32_t pad2;
+  unsigned long long* exact_draws;
 };
 
 // Phase timing (diagnostics build, -DPOMCP_PHASE_TIMING): per-lane s_memtime
@@ -692,7 +699,7 @@ struct ImPair {
         tot += pf[i];
       }
       const float rt = __builtin_amdgcn_rcpf(tot);
-      const float E = IM_FAST_SLACK * (1e-6f * xmax + 2.4e-6f);
+      const float E = p.fast_slack * (1e-6f * xmax + 2.4e-6f);
       const float uf = (float)d;
       bool amb = !(xmax <= 80.0f);
       int lo = nr - 1;
@@ -708,6 +715,7 @@ struct ImPair {
       if (!amb) return im_order(x.info, lo);
     }
 #endif
+    if (p.exact_draws != nullptr) atomicAdd(p.exact_draws, 1ull);   // tests: fallbacks fired
     const double sq = sqrt((double)x.visits);
     double pr[kImMaxA];
     double total = 0.0;

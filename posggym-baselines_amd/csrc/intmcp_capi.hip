@@ -192,6 +192,7 @@ int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, in
     ctx->model_bytes = sizeof(DrvModel);
   }
   ImParams& d = ctx->ip;
+  d.fast_slack = IM_FAST_SLACK;
   d.B = c.num_trees;
   d.A = c.num_actions;
   d.ego = c.ego_agent;
@@ -509,6 +510,32 @@ int intmcp_debug_phase_timing(intmcp_ctx* ctx, uint64_t* out, int32_t capacity, 
   }
   return POMCP_OK;
 #endif
+}
+
+// Debug: the other agent's softmax fast path (ImPair::sample_action) with its
+// bound widened `slack` times (>= 1 keeps results exact; a large slack sends
+// most draws to the exact FP64 path); from this call on, exact-path draws are
+// counted (intmcp_debug_exact_draws).
+int intmcp_debug_set_softmax_slack(intmcp_ctx* ctx, float slack) {
+  if (!ctx || !(slack >= 1.0f)) return POMCP_E_INVALID;
+  if (ctx->ip.exact_draws == nullptr) {
+    void* p = nullptr;
+    if (im_alloc(ctx, &p, sizeof(unsigned long long)) != POMCP_OK) return POMCP_E_HIP;
+    IM_TRY(ctx, hipMemsetAsync(p, 0, sizeof(unsigned long long), ctx->stream));
+    ctx->ip.exact_draws = reinterpret_cast<unsigned long long*>(p);
+  }
+  ctx->ip.fast_slack = slack;
+  return POMCP_OK;
+}
+
+int intmcp_debug_exact_draws(intmcp_ctx* ctx, uint64_t* count) {
+  if (!ctx || !count) return POMCP_E_INVALID;
+  *count = 0;
+  if (ctx->ip.exact_draws == nullptr) return POMCP_OK;
+  IM_TRY(ctx, hipMemcpyAsync(count, ctx->ip.exact_draws, sizeof(uint64_t), hipMemcpyDeviceToHost,
+                             ctx->stream));
+  IM_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return POMCP_OK;
 }
 
 int intmcp_get_support(intmcp_ctx* ctx, int32_t pair, int32_t* entries, int32_t capacity_entries,

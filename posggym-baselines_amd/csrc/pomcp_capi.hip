@@ -164,8 +164,10 @@ static int validate(const pomcp_config* c, std::string* why) {
     return bad("max_blocks");
   if (c->num_actions < 2 || c->num_actions > kMaxA) { *why = "the search kernel supports 2 to 5 actions"; return POMCP_E_UNSUPPORTED; }
   if (c->max_particles < 1 || c->max_particles * kWave > UINT32_MAX) return bad("max_particles");
-  if (c->max_blocks * c->num_actions * kSlots + 1 + c->overflow_slots >= (int64_t)kIdMask)
-    return bad("obs node ids exceed 2^26 (max_blocks * A * 6 + overflow_slots)");
+  // ids: inline slots (max_blocks * A * 6), overflow entries, deferred records
+  // (max_blocks * A, pomcp_device.h)
+  if (c->max_blocks * c->num_actions * (kSlots + 1) + 1 + c->overflow_slots >= (int64_t)kIdMask)
+    return bad("obs node ids exceed 2^26 (max_blocks * A * 7 + overflow_slots)");
   if (c->max_belief < 2 * (c->num_particles + c->extra_particles)) return bad("max_belief too small");
   if (c->overflow_slots < kBucket || (c->overflow_slots & (c->overflow_slots - 1)) != 0 ||
       c->overflow_slots > (1ll << 28))
@@ -247,6 +249,7 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
   d.H = c.overflow_slots;
   d.bucket_mask = (uint32_t)(c.overflow_slots / kBucket - 1);
   d.ovf_base = (uint32_t)(c.max_blocks * c.num_actions * kSlots + 1);
+  d.cut_base = d.ovf_base + (uint32_t)c.overflow_slots;
   d.islots = kSlots;
   d.tm = c.type_based;
   d.lines = blk_lines(d.A, d.tm);
@@ -419,8 +422,7 @@ int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_key
     if (rc != POMCP_OK) return rc;
     hipLaunchKernelGGL(k_compact, dim3(grid_blocks(B)), dim3(256), 0, ctx->stream, ctx->dp);
     HIP_TRY(ctx, hipGetLastError());
-    hipLaunchKernelGGL(k_compact_log, dim3(grid_blocks(search_waves(B))), dim3(256), 0,
-                       ctx->stream, ctx->dp);
+    PB_ENV_LAUNCH(ctx, k_compact_log, dim3(grid_blocks(search_waves(B))), dim3(256), ctx->dp);
     HIP_TRY(ctx, hipGetLastError());
   }
   HIP_TRY(ctx, hipMemcpyAsync(ctx->host_upd.data(), ctx->dp.upd_out, sizeof(int32_t) * 2 * B,
@@ -625,6 +627,12 @@ int pomcp_set_type_policies(pomcp_ctx* ctx, const pomcp_type_policies* tp) {
   TmTables t{};
   t.n_ego = ne;
   t.n_other = no;
+  t.no_meta_draw = tp->no_meta_draw != 0;
+  t.no_mixture_draw = tp->no_mixture_draw != 0;
+  t.ego_uniform = tp->ego_uniform != 0;
+  t.other_uniform = tp->other_uniform != 0;
+  if (t.no_mixture_draw && no != 1)
+    return fail(ctx, POMCP_E_INVALID, "set_type_policies: no_mixture_draw needs one other-agent policy");
   // random.choices' cumulative weights (itertools.accumulate) and total = cum[-1] + 0.0
   auto cum = [](const double* w, int n, double* c, double* total) {
     double acc = 0.0;
@@ -841,6 +849,23 @@ int pomcp_synthetic_obs(pomcp_ctx* ctx, uint64_t env_seed_base, uint64_t* obs_ke
                                 hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   }
+  return POMCP_OK;
+}
+
+int pomcp_synthetic_step(pomcp_ctx* ctx, uint64_t env_seed_base, const int32_t* actions,
+                         uint64_t* obs_keys_out) {
+  if (!ctx || !actions) return POMCP_E_INVALID;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  const int B = ctx->dp.B;
+  HIP_TRY(ctx, hipMemcpyAsync((void*)ctx->dp.in_actions, actions, sizeof(int32_t) * B,
+                              hipMemcpyHostToDevice, ctx->stream));
+  PB_ENV_LAUNCH(ctx, k_synthetic_step, dim3(grid_blocks(B)), dim3(256), ctx->dp, env_seed_base);
+  HIP_TRY(ctx, hipGetLastError());
+  if (obs_keys_out) {
+    HIP_TRY(ctx, hipMemcpyAsync(obs_keys_out, ctx->dp.out_obs, sizeof(uint64_t) * B,
+                                hipMemcpyDeviceToHost, ctx->stream));
+  }
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   return POMCP_OK;
 }
 

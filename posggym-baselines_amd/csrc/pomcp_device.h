@@ -70,6 +70,17 @@ __host__ __device__ constexpr int part_vt(int a) { return 2 + a; }   // {value, 
 // tree's records keep their insertion order; k_extract separates them again.
 constexpr int kIdBits = 26;                       // obs node ids < 2^26 (pomcp_create checks)
 constexpr uint32_t kIdMask = (1u << kIdBits) - 1u;
+// Deferred records (k_search): a simulation that reaches an obs node whose
+// children lie beyond the depth / step limits (mcts.py:315) only needs its
+// child for the particle record -- the child is never stepped into during this
+// search (mcts.py:315 returns 0 for it, whatever its slot holds).  Such a record
+// carries id = cut_base + action node index instead of the child's id, and
+// the child slot is neither read nor written by the search; the child's
+// observation key and absorbing flag follow from the record's state (both are
+// functions of the next state, envs.h), so the re-root materialises the
+// children of the records it keeps (k_compact_log) and drops the rest with
+// the garbage-collected part of the tree.  Only labels and the time of the
+// slot writes change: every arrival is still one record, in order.
 struct LogRec {
   uint32_t id;      // obs node id | lane << kIdBits
   uint32_t v0, v1;
@@ -143,6 +154,10 @@ constexpr uint64_t kCodeMask = 15ull << kCodeShift;
 // entries keep it in flags bits 1..4.
 struct TmTables {
   int32_t n_ego, n_other, pad[2];
+  // the base planner's modes (pomcp_type_policies): no sample_policy draw, no
+  // mixture draw per initial particle, Discrete.sample() for the ego's rollout /
+  // the other agent
+  int32_t no_meta_draw, no_mixture_draw, ego_uniform, other_uniform;
   double prior[kTmMax + 1][kTmMax];     // [code][a]: the action_probs a node starts with
   double ego_cum[kTmMax][kTmMax];       // ego policy k's action draw (rollouts)
   double ego_tot[kTmMax];
@@ -194,6 +209,7 @@ struct DevParams {
   int64_t Nb, Np, Nr, H;
   uint32_t bucket_mask;
   uint32_t ovf_base;    // node ids >= ovf_base are overflow entries
+  uint32_t cut_base;    // ids >= cut_base: deferred records (cut_base + action node index), below
   int32_t islots;       // inline obs slots in use per action node (kSlots; fewer only in
                         // tests of the overflow map: pomcp_debug_set_inline_slots)
   int32_t lines;        // lines per block (blk_lines(A, tm))

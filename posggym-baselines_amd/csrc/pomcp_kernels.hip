@@ -465,7 +465,7 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
         // type-based: the other agent's policy of the particle,
         // OtherAgentMixturePolicy.sample_initial_state (potmmcp.py:83-87)
         uint32_t pid = 0u;
-        if (p.tm)
+        if (p.tm && !p.tmt->no_mixture_draw)
           pid = uniform_int(uniu(philox_word(T.seed, T.tkey, S_MIXTURE, T.c_mix++)),
                             (uint32_t)p.tmt->n_other);
         if (lane == 0) nb[n] = make_uint4(1u, s0, s1, pid);
@@ -529,9 +529,10 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
                 const uint4 hp = pbel[uniform_int(wb, (uint32_t)T.bsize)];
                 // the other agent's action: uniform, or (type-based) by the
                 // particle's policy (OtherAgentMixturePolicy.sample_action)
-                const uint32_t ao = p.tm ? (uint32_t)tm_choice(p.tmt->oth_cum[hp.w], p.tmt->oth_tot[hp.w],
-                                                               p.A, wa)
-                                         : uniform_int(wa, (uint32_t)p.A);
+                const uint32_t ao = p.tm && !p.tmt->other_uniform
+                                        ? (uint32_t)tm_choice(p.tmt->oth_cum[hp.w], p.tmt->oth_tot[hp.w],
+                                                              p.A, wa)
+                                        : uniform_int(wa, (uint32_t)p.A);
                 uint32_t n0, n1;
                 double r;
                 int done;
@@ -795,40 +796,73 @@ __global__ __launch_bounds__(256) void k_compact(DevParams p) {
   }
 }
 
+__device__ __forceinline__ uint64_t ld_agent_u64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // One wave per SEARCH wave: filter that wave's shared particle log to the
 // records of obs nodes that survived k_compact (insertion order kept) and
-// relabel them; every tree's record count is recounted.
+// relabel them; every tree's record count is recounted.  A deferred record
+// (pomcp_device.h: an arrival at a child beyond the depth / step limits,
+// never looked up by k_search) whose action node survived gets its child
+// here: the child's observation key and absorbing flag follow from the
+// record's state (Env::obs_key, Env::done_of); it is found among the action
+// node's inline slots or inserted there (compare-and-swap: the wave's lanes
+// insert concurrently), else in the overflow map (one record at a time), and
+// its absorbing flag is that of its LAST arrival (mcts.py:370, records in log
+// order).  Which slot a child takes is a label (ActionNode.children is only
+// ever looked up by observation in the reference), so results are unchanged.
+template <class Env>
 __global__ __launch_bounds__(256) void k_compact_log(DevParams p) {
+  __shared__ typename Env::Model sm;
+  stage_model(p.model, sm);
   const int sw = blockIdx.x * kTreesPerBlock + (threadIdx.x >> 6);
   const int wi = threadIdx.x >> 6;
   const int lane = lane_id();
   if (sw >= (p.B + kWave - 1) / kWave) return;
   __shared__ int32_t kept[kTreesPerBlock][kWave];
   __shared__ int32_t act[kTreesPerBlock][kWave];
+  __shared__ int32_t made[kTreesPerBlock][kWave];   // children materialised per tree
+  __shared__ int32_t bad[kTreesPerBlock][kWave];    // overflow map full
   const int mytree = sw * kWave + lane;
   kept[wi][lane] = 0;
+  made[wi][lane] = 0;
+  bad[wi][lane] = 0;
   act[wi][lane] = mytree < p.B ? p.cnt[mytree] : 0;
   __builtin_amdgcn_wave_barrier();
   const WaveLog wl(p.plog, p.Np, sw, p.tm);
   const uint32_t n = p.wlog[sw];
   const uint32_t A = (uint32_t)p.A;
+  const int64_t bstride = blk_stride_lines(p.lines);
   uint32_t out = 0;
   for (uint32_t base = 0; base < n; base += kWave) {
     const uint32_t i = base + (uint32_t)lane;
     LogRec r = {0u, 0u, 0u};
     uint32_t aux = 0u;
-    bool keep = false;
+    bool keep = false, mat = false;
+    uint32_t l = 0u, nani = 0u;
+    uint64_t okey = 0ull;
+    int done = 0;
+    int32_t nid = -1;
+    int32_t* vis = nullptr;   // the node's visits (zeroed by k_compact): + 1 per record
     if (i < n) {
       r = wl.load(i);
       if (p.tm) aux = wl.aux[i];
-      const uint32_t l = r.id >> kIdBits;
+      l = r.id >> kIdBits;
       const uint32_t id = r.id & kIdMask;
       const int tree = sw * kWave + (int)l;
       keep = true;
       if (act[wi][l]) {
-        int32_t nid = -1;
-        int32_t* vis = nullptr;   // the node's visits (zeroed by k_compact): + 1 per record
-        if (id >= p.ovf_base) {
+        if (id >= p.cut_base) {   // deferred record: its child is materialised below
+          const uint32_t ani = id - p.cut_base;
+          const int nb = ld_agent(p.cmap + (int64_t)tree * p.Nb + (int)(ani / A));
+          if (nb >= 0) {
+            mat = true;
+            nani = (uint32_t)nb * A + ani % A;
+            okey = Env::obs_key(sm, p.ego, r.v0, r.v1);
+            done = Env::done_of(p.ego, r.v0, r.v1);
+          }
+        } else if (id >= p.ovf_base) {
           nid = ld_agent(p.ovf_new + (int64_t)tree * p.H + (id - p.ovf_base));
           if (nid >= 0) vis = &p.ovf[(int64_t)tree * p.H + ((uint32_t)nid - p.ovf_base)].visits;
         } else if (id >= 1u) {
@@ -837,16 +871,127 @@ __global__ __launch_bounds__(256) void k_compact_log(DevParams p) {
           if (nb >= 0) {
             nid = (int32_t)(((uint32_t)nb * A + ani % A) * kSlots + k + 1u);
             uint4* const bp = reinterpret_cast<uint4*>(p.an + tree_base_lines(tree, p.Nb, p.lines) +
-                                                       (int64_t)nb * blk_stride_lines(p.lines));
+                                                       (int64_t)nb * bstride);
             vis = reinterpret_cast<int32_t*>(bp + part_slot((int)(ani % A), (int)k)) + 3;
           }
         }
-        keep = nid >= 0;
-        if (vis != nullptr) atomicAdd(vis, 1);
-        r.id = (uint32_t)nid | (l << kIdBits);
+        keep = nid >= 0 || mat;
       }
-      if (keep) atomicAdd(&kept[wi][l], 1);
     }
+    // ---- deferred records: find or insert the child
+    uint32_t* flagw = nullptr;   // the word holding the child's absorbing flag ...
+    uint32_t fbit = 0u;          // ... and its bit
+    if (__ballot(mat) != 0ull) {
+      const int tree = sw * kWave + (int)l;
+      bool need_ovf = false;
+      if (mat) {   // inline slots, filled in order; concurrent inserts by CAS on the key
+        uint4* const sl0 = reinterpret_cast<uint4*>(p.an + tree_base_lines(tree, p.Nb, p.lines) +
+                                                    (int64_t)(nani / A) * bstride) +
+                           part_slot((int)(nani % A), 0);
+        const uint64_t nk = okey | kValidBit | ((uint64_t)done << 63);
+        uint64_t kk[kSlots];
+#pragma unroll
+        for (int q = 0; q < kSlots; ++q)
+          kk[q] = q < p.islots ? ld_agent_u64(reinterpret_cast<const uint64_t*>(sl0 + q)) : kValidBit;
+        int ks = -1;
+#pragma unroll
+        for (int q = kSlots - 1; q >= 0; --q)
+          if ((kk[q] & kValidBit) != 0ull && (kk[q] & kObsMask) == okey) ks = q;
+        for (int q = 0; ks < 0 && q < p.islots; ++q) {
+          uint64_t exp = 0ull;
+#pragma unroll
+          for (int e = 0; e < kSlots; ++e) exp = e == q ? kk[e] : exp;   // (selects: registers)
+          if ((exp & kValidBit) != 0ull) continue;   // taken by another observation
+          const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long*>(sl0 + q),
+                                         (unsigned long long)exp, (unsigned long long)nk);
+          if (old == exp) {   // inserted: a leaf child (no block), visits counted below
+            __hip_atomic_store(reinterpret_cast<int32_t*>(sl0 + q) + 2, -1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            atomicAdd(&made[wi][l], 1);
+            ks = q;
+          } else if ((old & kValidBit) != 0ull && (old & kObsMask) == okey) {
+            ks = q;   // another lane of this chunk inserted it
+          }
+        }
+        if (ks >= 0) {
+          nid = (int32_t)(nani * kSlots + (uint32_t)ks + 1u);
+          vis = reinterpret_cast<int32_t*>(sl0 + ks) + 3;
+          flagw = reinterpret_cast<uint32_t*>(sl0 + ks) + 1;
+          fbit = 1u << 31;
+        } else {
+          need_ovf = true;
+        }
+      }
+      // overflow map: one record at a time, the wave probing a bucket's 16 entries
+      uint64_t om = __ballot(need_ovf);
+      while (om != 0ull) {
+        const int j = __ffsll((long long)om) - 1;
+        om &= om - 1ull;
+        const int jt = sw * kWave + rl((int)l, j);
+        const uint32_t jani = rlu(nani, j);
+        const uint64_t jkey = ((uint64_t)rlu((uint32_t)(okey >> 32), j) << 32) | rlu((uint32_t)okey, j);
+        const uint32_t jdone = rlu((uint32_t)done, j);
+        OvfSlot* const ovf = p.ovf + (int64_t)jt * p.H;
+        const uint32_t epoch = (uint32_t)p.hdr[jt].epoch;   // k_compact's new generation
+        const uint64_t key = jkey | ((uint64_t)epoch << kEpochShift);
+        uint32_t b = ovf_hash(jani, jkey) & p.bucket_mask;
+        int32_t jid = -1;
+        for (uint32_t probe = 0; probe <= p.bucket_mask && jid < 0; ++probe) {
+          OvfSlot* const e = ovf + (int64_t)b * kBucket + (lane & (kBucket - 1));
+          uint64_t sk = 0ull;
+          uint32_t san = 0u;
+          if (lane < kBucket) {
+            sk = ld_agent_u64(&e->key);
+            san = ld_agent_u32(&e->an);
+          }
+          const bool live = lane < kBucket && (uint32_t)(sk >> kEpochShift) == epoch;
+          const uint64_t mm = __ballot(live && sk == key && san == jani);
+          const uint64_t em = __ballot(lane < kBucket && !live);
+          if (mm != 0ull || em != 0ull) {
+            const int L = __ffsll((long long)(mm != 0ull ? mm : em)) - 1;
+            if (mm == 0ull && lane == L) {   // insert a leaf child
+              reinterpret_cast<uint4*>(e)[0] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), jani, jdone);
+              reinterpret_cast<uint4*>(e)[1] = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
+              atomicAdd(&made[wi][jt & (kWave - 1)], 1);
+            }
+            __threadfence();
+            jid = (int32_t)(b * kBucket + (uint32_t)L);
+          }
+          b = (b + 1) & p.bucket_mask;
+        }
+        if (lane == j) {
+          if (jid >= 0) {
+            nid = (int32_t)(p.ovf_base + (uint32_t)jid);
+            vis = &ovf[jid].visits;
+            flagw = &ovf[jid].flags;
+            fbit = 1u;
+          } else {   // the overflow map is full
+            keep = false;
+            bad[wi][l] = 1;
+          }
+        }
+      }
+      // the absorbing flag of each child = that of its last arrival in this
+      // chunk (earlier chunks were applied before, in log order)
+      bool last = flagw != nullptr;
+      const uint64_t fp = reinterpret_cast<uint64_t>(flagw);
+      uint64_t fm = __ballot(last);
+      while (fm != 0ull) {
+        const int j = __ffsll((long long)fm) - 1;
+        fm &= fm - 1ull;
+        const uint64_t pj = ((uint64_t)rlu((uint32_t)(fp >> 32), j) << 32) | rlu((uint32_t)fp, j);
+        if (last && lane < j && fp == pj) last = false;
+      }
+      if (last) {
+        if (done) atomicOr(flagw, fbit);
+        else atomicAnd(flagw, ~fbit);
+      }
+    }
+    if (act[wi][l] && i < n) {
+      if (vis != nullptr) atomicAdd(vis, 1);
+      if (keep) r.id = (uint32_t)nid | (l << kIdBits);
+    }
+    if (keep) atomicAdd(&kept[wi][l], 1);
     const uint64_t mk = __ballot(keep);
     __builtin_amdgcn_s_waitcnt(0);   // the whole chunk is loaded before any store
     if (keep) {
@@ -857,7 +1002,14 @@ __global__ __launch_bounds__(256) void k_compact_log(DevParams p) {
     out += (uint32_t)__popcll(mk);
   }
   __builtin_amdgcn_wave_barrier();
-  if (mytree < p.B) p.hdr[mytree].n_log = kept[wi][lane];
+  if (mytree < p.B) {
+    p.hdr[mytree].n_log = kept[wi][lane];
+    if (made[wi][lane] != 0) p.hdr[mytree].n_nodes += made[wi][lane];
+    if (bad[wi][lane] != 0) {
+      p.hdr[mytree].error = POMCP_E_ARENA;
+      p.upd_out[2 * mytree + 1] = POMCP_E_ARENA;
+    }
+  }
   if (lane == 0) p.wlog[sw] = out;
 }
 
@@ -876,6 +1028,33 @@ __global__ __launch_bounds__(256) void k_synthetic_obs(DevParams p, uint64_t env
   uint32_t s0, s1;
   Env::sample_initial(sm, [&](uint32_t n) { return env.model(n); }, &s0, &s1);
   const uint64_t key = Env::obs_key(sm, p.ego, s0, s1);
+  if (lane_id() == 0) p.out_obs[tree] = key;
+}
+
+// Synthetic environment step (bench: an update()-inclusive planning step): tree
+// b's true initial state again (the same draws as k_synthetic_obs), one joint
+// step with the ego's action in_actions[b] and the other agent's action drawn
+// uniformly from the env key's action stream, the ego's next observation.
+template <class Env>
+__global__ __launch_bounds__(256) void k_synthetic_step(DevParams p, uint64_t env_seed_base) {
+  __shared__ typename Env::Model sm;
+  stage_model(p.model, sm);
+  const int tree = blockIdx.x * kTreesPerBlock + (threadIdx.x >> 6);
+  if (tree >= p.B) return;
+  Streams env;
+  env.seed = env_seed_base + (uint64_t)tree;
+  env.tree = 0x40000000u;
+  for (int k = 0; k < 5; ++k) env.ctr[k] = 0;
+  uint32_t s0, s1;
+  Env::sample_initial(sm, [&](uint32_t n) { return env.model(n); }, &s0, &s1);
+  const int a = p.in_actions[tree];
+  const uint32_t ao = env.act(p.other, (uint32_t)p.A);
+  const uint32_t j = Env::kStepDraws ? env.model(2) : 0u;
+  uint32_t n0, n1;
+  double r;
+  int done;
+  Env::step(sm, p.ego, s0, s1, (uint32_t)(a >= 0 && a < p.A ? a : 0), ao, j, &n0, &n1, &r, &done);
+  const uint64_t key = Env::obs_key(sm, p.ego, n0, n1);
   if (lane_id() == 0) p.out_obs[tree] = key;
 }
 

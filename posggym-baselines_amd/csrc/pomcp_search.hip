@@ -192,7 +192,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   uint32_t c_bel = h->ctr[0], c_sel = h->ctr[1], c_mod = h->ctr[2], c_a0 = h->ctr[3],
            c_a1 = h->ctr[4];
   const int log0 = n_log, blocks0 = n_blocks, nodes0 = n_nodes;
-  int c_rollout = 0, c_probes = 0;
+  int c_rollout = 0, c_probes = 0, c_defer = 0;
 #ifdef POMCP_PHASE_TIMING
   uint64_t pt[16];
   for (int i = 0; i < 16; ++i) pt[i] = 0;
@@ -233,8 +233,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   // or, TM, by its particle's policy (OtherAgentMixturePolicy.sample_action)
   auto take_oth = [&]() -> uint32_t {
     pend_s = 0;
-    if constexpr (TM != 0) return (uint32_t)tm_choice(tmt->oth_cum[pid], tmt->oth_tot[pid], A, w_oth);
-    else return uniform_int(w_oth, (uint32_t)A);
+    if constexpr (TM != 0) {
+      if (tmt->other_uniform) return uniform_int(w_oth, (uint32_t)A);
+      return (uint32_t)tm_choice(tmt->oth_cum[pid], tmt->oth_tot[pid], A, w_oth);
+    } else {
+      return uniform_int(w_oth, (uint32_t)A);
+    }
   };
   auto take_mod = [&](uint32_t n) { return Env::kStepDraws ? uniform_int(w_mod, n) : 0u; };
   // ObsNode.add_child for every action (mcts.py:279-281, 318-321): zeroed block
@@ -583,9 +587,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         r0_on = 0;
         if constexpr (TM != 0) {   // sample_policy (potmmcp.py:381-389), select stream
           pid = pr.w;
-          const int i = tm_choice(tmt->meta_cum[pid], tmt->meta_tot[pid], tmt->meta_len[pid],
-                                  philox_word(seed, tkey, S_SELECT, c_sel++));
-          epol = tmt->meta_idx[pid][i];
+          if (!tmt->no_meta_draw) {   // (the base planner: one search policy, no draw)
+            const int i = tm_choice(tmt->meta_cum[pid], tmt->meta_tot[pid], tmt->meta_len[pid],
+                                    philox_word(seed, tkey, S_SELECT, c_sel++));
+            epol = tmt->meta_idx[pid][i];
+          }
         }
         if (0 > p.depth_limit || t > p.step_limit) {            // mcts.py:315
           ret = 0.0;
@@ -719,11 +725,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
           sa = sel4(q == a, st[q], sa);
           va = sel4(q == a, pre[part_vt(q < A ? q : 0)], va);
         }
-        // the chosen action's child slots (second round trip)
-#ifdef POMCP_ABLATE_CUTSLOT   // ablation build only: no child lookup for a child beyond the limits
-        const bool skipc = depth + 1 > p.depth_limit || t + 1 > p.step_limit;
-#else
+        // the chosen action's child slots (second round trip) -- except for a
+        // child beyond the depth / step limits (mcts.py:315): the simulation
+        // stops there whatever its slot holds, so its record is deferred
+        // (pomcp_device.h: no slot read or write; the re-root materialises the
+        // children that survive it).  TM looks it up: the node's prior moves
+        // on arrivals at existing children (potmmcp.py:255-264).
+#ifdef POMCP_EAGER_CUT   // measurement builds only (A/B): the round-3 eager lookup
         constexpr bool skipc = false;
+#else
+        const bool skipc = TM == 0 && (depth + 1 > p.depth_limit || t + 1 > p.step_limit);
 #endif
         uint4 sl[kSlots];
   #pragma unroll
@@ -748,7 +759,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         int cblk = -1, cvis = 1, ccode = epol + 1, existed = 0;
         leaf_rc = -1;
         if (skipc) {
-          cid = ani * kSlots + 1u;
+          cid = p.cut_base + ani;
+          ++c_defer;
         } else if (ks >= 0) {
           uint4 sk = sl[0];
   #pragma unroll
@@ -823,7 +835,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         // TM, the simulation's drawn policy (potmmcp.py:221-229)
         const uint32_t aw = d_act_word(p.ego);
         uint32_t ae;
-        if constexpr (TM != 0) ae = (uint32_t)tm_choice(tmt->ego_cum[epol], tmt->ego_tot[epol], A, aw);
+        if constexpr (TM != 0)
+          ae = tmt->ego_uniform ? uniform_int(aw, (uint32_t)A)
+                                : (uint32_t)tm_choice(tmt->ego_cum[epol], tmt->ego_tot[epol], A, aw);
         else ae = uniform_int(aw, (uint32_t)A);
         const uint32_t j = take_mod(2);
         const uint32_t ao = take_oth();                       // other_policy.py:151
@@ -1064,7 +1078,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   so->n_obs_nodes = n_nodes;
   so->n_blocks = n_blocks;
   so->n_log = n_log;
-  so->pad = 0;
+  so->n_deferred = c_defer;
 }
 
 #define PB_SEARCH_INST(E, NA, T, TM)                                                 \

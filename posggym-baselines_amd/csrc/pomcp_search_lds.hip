@@ -1012,7 +1012,7 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
     so->n_obs_nodes = n_nodes;
     so->n_blocks = n_blocks;
     so->n_log = n_log;
-    so->pad = 0;
+    so->n_deferred = 0;
   }
 }
 

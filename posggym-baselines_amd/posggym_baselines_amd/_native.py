@@ -141,7 +141,7 @@ class PomcpRootStats(C.Structure):
         ("n_obs_nodes", C.c_int32),
         ("n_blocks", C.c_int32),
         ("n_log", C.c_int32),
-        ("pad", C.c_int32),
+        ("n_deferred", C.c_int32),
     ]
 
 
@@ -174,6 +174,10 @@ class PomcpTypePolicies(C.Structure):
         ("meta_policy", (C.c_int32 * POMCP_MAX_TYPE_POLICIES) * POMCP_MAX_TYPE_POLICIES),
         ("meta_weight", (C.c_double * POMCP_MAX_TYPE_POLICIES) * POMCP_MAX_TYPE_POLICIES),
         ("expected_prior", C.c_double * POMCP_MAX_ACTIONS),
+        ("no_meta_draw", C.c_int32),
+        ("no_mixture_draw", C.c_int32),
+        ("ego_uniform", C.c_int32),
+        ("other_uniform", C.c_int32),
     ]
 
 
@@ -206,6 +210,7 @@ SIGNATURES = [
     ("pomcp_allgather_root", C.c_int, [_CTX, C.c_void_p, C.c_int32]),
     ("pomcp_merge_roots", C.c_int, [_CTX, C.c_int32, C.c_int32, C.POINTER(PomcpMergedRoot)]),
     ("pomcp_synthetic_obs", C.c_int, [_CTX, C.c_uint64, _PU64]),
+    ("pomcp_synthetic_step", C.c_int, [_CTX, C.c_uint64, _P32, _PU64]),
     ("pomcp_snapshot", C.c_int, [_CTX]),
     ("pomcp_restore", C.c_int, [_CTX]),
     ("pomcp_driving_sample_initial_state", C.c_int,
@@ -227,6 +232,8 @@ DEBUG_SIGNATURES = [
     ("pomcp_debug_phase_timing", C.c_int,
      [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32, C.POINTER(C.c_int32)]),
     ("pomcp_debug_set_inline_slots", C.c_int, [C.c_void_p, C.c_int32]),
+    ("intmcp_debug_set_softmax_slack", C.c_int, [C.c_void_p, C.c_float]),
+    ("intmcp_debug_exact_draws", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
 ]
 
 

@@ -23,9 +23,12 @@ class Capacities:
     log_table_size: int
     discount_pow_size: int
 
-    def bytes_per_tree(self, num_actions: int) -> int:
-        return (self.max_blocks * num_actions * 128 + self.overflow_slots * 32
-                + self.max_particles * 16 + 2 * self.max_belief * 16)
+    def bytes_per_tree(self, num_actions: int, type_based: bool = False) -> int:
+        """HBM of one tree (pomcp_create): (A + 1 [+ 1]) x 128 B per block, 32 B
+        overflow entries, 12 [16] B particle records, two 16 B root beliefs."""
+        tm = 1 if type_based else 0
+        return (self.max_blocks * (num_actions + 1 + tm) * 128 + self.overflow_slots * 32
+                + self.max_particles * (12 + 4 * tm) + 2 * self.max_belief * 16)
 
 
 def _next_pow2(n: int) -> int:
@@ -33,6 +36,8 @@ def _next_pow2(n: int) -> int:
 
 
 ID_LIMIT = (1 << 26) - 1   # obs node ids share a log word with the lane (pomcp_device.h)
+# ids per block and action: 6 inline child slots + 1 deferred-record id (pomcp_device.h)
+IDS_PER_ACTION = 7
 
 
 def plan_capacities(config, step_limit: int, num_sims: int, searches: int = 1,
@@ -53,7 +58,7 @@ def plan_capacities(config, step_limit: int, num_sims: int, searches: int = 1,
     ovf = min(ovf, 1 << 24)
     if max_blocks is None:
         # one expansion per simulation at most, within the obs node id space
-        nb = min(total + 2 * searches + 16, (ID_LIMIT - 1 - ovf) // (num_actions * 6))
+        nb = min(total + 2 * searches + 16, (ID_LIMIT - 1 - ovf) // (num_actions * IDS_PER_ACTION))
     else:
         nb = max_blocks
     np_ = total * min(levels, 64) + searches * 2 * n_target + 64
@@ -86,7 +91,7 @@ def plan_wallclock_capacities(config, step_limit: int, num_trees: int = 1, num_a
     sims = math.ceil(config.search_time_limit * WALL_CLOCK_SIMS_PER_S)
     sims = min(sims, WALL_CLOCK_HBM_BUDGET // (2 * per_sim * max(1, num_trees)))
     ovf = 1 << 16
-    nb_id = (ID_LIMIT - 1 - ovf) // (num_actions * 6)
+    nb_id = (ID_LIMIT - 1 - ovf) // (num_actions * IDS_PER_ACTION)
     sims = max(256, min(sims, nb_id // 2 - 64))
     caps = plan_capacities(config, step_limit, sims, 2, num_actions=num_actions,
                            overflow_slots=ovf)
@@ -198,9 +203,11 @@ class PomcpEngine:
         if type_policies is not None:
             self._check(lib.pomcp_set_type_policies(ctx, C.byref(type_policies)),
                         "set_type_policies")
-        # search kernel override (tests / benchmarks): POMCP_SEARCH_KERNEL=lane|wave
+        # search kernel override (tests / benchmarks): POMCP_SEARCH_KERNEL=lane|wave.
+        # A type-based (POTMMCP) context has only the lane kernel: the process-wide
+        # override does not apply to it (an explicit set_search_kernel still raises)
         kind = os.environ.get("POMCP_SEARCH_KERNEL", "auto")
-        if kind != "auto":
+        if kind != "auto" and not (self.type_based and kind == "wave"):
             self.set_search_kernel(kind)
 
     # ------------------------------------------------------------------
@@ -341,6 +348,17 @@ class PomcpEngine:
         self._check(self._lib.pomcp_synthetic_obs(
             self._ctx, int(env_seed_base), out.ctypes.data_as(C.POINTER(C.c_uint64))),
             "synthetic_obs")
+        return out
+
+    def synthetic_step(self, env_seed_base, actions):
+        """The synthetic roots' environment answer to ``actions`` (bench): the
+        ego's next observation key per tree (``pomcp_synthetic_step``)."""
+        a = np.ascontiguousarray(np.broadcast_to(np.asarray(actions, dtype=np.int32),
+                                                 (self.num_trees,)))
+        out = np.zeros(self.num_trees, dtype=np.uint64)
+        self._check(self._lib.pomcp_synthetic_step(
+            self._ctx, int(env_seed_base), a.ctypes.data_as(C.POINTER(C.c_int32)),
+            out.ctypes.data_as(C.POINTER(C.c_uint64))), "synthetic_step")
         return out
 
     def snapshot(self):

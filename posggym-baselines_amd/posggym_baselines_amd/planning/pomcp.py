@@ -65,25 +65,27 @@ class RootView:
 class POMCP:
     """Partially Observable Monte-Carlo Planning, GPU-resident tree.
 
-    Only the uniform random search policy is executed on the device
-    (``RandomSearchPolicy``), matching the reference's POMCP test setup
-    (``tests/planning/test_pomcp.py:36-74``); other agents are random
-    (``pomcp.py:28-31``).
+    Other agents are random (``pomcp.py:28-31``).  The search policy is the
+    uniform random one (``RandomSearchPolicy``, the reference's POMCP test
+    setup, ``tests/planning/test_pomcp.py:36-74``: the plain kernel) or a
+    fixed-distribution one (``SearchPolicyWrapper(FixedDistributionPolicy)``:
+    node priors and rollouts, planning/ipomcp.py); history-dependent
+    (network) search policies raise ``NotImplementedError``.
     """
 
     def __init__(self, model, agent_id: str, config: MCTSConfig, search_policy: SearchPolicy,
                  *, num_sims: Optional[int] = None, process_group=None):
-        if not isinstance(search_policy, RandomSearchPolicy):
-            raise NotImplementedError(
-                "the GPU POMCP engine runs the uniform random rollout policy in-kernel; "
-                f"{type(search_policy).__name__} is not supported")
+        from posggym_baselines_amd.planning.ipomcp import base_type_tables
         if not config.state_belief_only:
             # pomcp.py:32-34 calls config.replace(...), which does not exist on the
             # dataclass (AttributeError in the reference); dataclasses.replace is
             # what it means.  Recorded in DESIGN.md.
             config = dataclasses.replace(config, state_belief_only=True)
         others = {i: RandomOtherAgentPolicy(model, i) for i in model.possible_agents if i != agent_id}
-        self._init_planner(model, agent_id, config, search_policy, others, num_sims, process_group)
+        tables = base_type_tables(model, agent_id, config, others, search_policy)
+        self.type_policies = tables
+        self._init_planner(model, agent_id, config, search_policy, others, num_sims, process_group,
+                           type_policies=tables)
 
     def _init_planner(self, model, agent_id, config, search_policy, other_agent_policies,
                       num_sims, process_group, type_policies=None):

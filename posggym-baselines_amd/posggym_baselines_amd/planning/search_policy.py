@@ -1,9 +1,11 @@
 """Search (rollout / prior) policies — ``search_policy.py:16-185``.
 
-The GPU engine implements the uniform random rollout policy in-kernel
-(``RandomSearchPolicy``: ``sample_action`` = ``Discrete.sample``, uniform
-``get_pi``, no value).  Neural / posggym.agents search policies are out of
-scope for this build and are rejected by ``POMCP``.
+The GPU engine runs the uniform random policy in-kernel (``RandomSearchPolicy``:
+``sample_action`` = ``Discrete.sample``, uniform ``get_pi``, no value) and a
+``SearchPolicyWrapper`` of a fixed-distribution policy (planning/policies.py:
+node priors and rollouts, planning/ipomcp.py).  Neural / posggym.agents search
+policies are out of scope for this build and are rejected by the
+planners.
 """
 import abc
 from typing import Dict, Optional
@@ -86,7 +88,14 @@ class SearchPolicyWrapper(SearchPolicy):
         return self.policy.sample_action(state)
 
     def get_pi(self, state):
-        return self.policy.get_pi(state)
+        # search_policy.py:214-220: the policy's probs dict, missing actions as 0.0
+        pi = self.policy.get_pi(state).probs
+        n = self.policy.model.action_spaces[self.policy.agent_id].n
+        if len(pi) != n:
+            for a in range(n):
+                if a not in pi:
+                    pi[a] = 0.0
+        return pi
 
     def get_value(self, state):
         return self.policy.get_value(state)

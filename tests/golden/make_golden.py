@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 
 from oracle.ref_harness import (  # noqa: E402
     import_reference, reference_available, reference_episode, reference_intmcp_episode,
-    reference_potmmcp_episode)
+    reference_mcts_episode, reference_potmmcp_episode)
 from oracle.run import oracle_episode, oracle_intmcp_episode  # noqa: E402
 
 SQRT2 = math.sqrt(2)
@@ -167,6 +167,59 @@ def run_potmmcp_trees():
     return out
 
 
+# The base planner (MCTS / IPOMCP / POMCP, mcts.py:22-739) with non-random
+# policies (fixed distributions, planning/policies.py): a search policy whose
+# prior seeds every node (mcts.py:621-645) and drives the rollouts, other
+# agents drawn per particle from a mixture's policy state (mcts.py:602-615).
+# No oracle restatement: the GPU tests compare against these reference records.
+MCTS_SPECS = {
+    "fs": {"search": [0.1, 0.5, 0.1, 0.2, 0.1], "other": {"kind": "random"}},
+    "mix": {"search": None,
+            "other": {"kind": "mixture", "policies": {"o_u": [0.2] * 5,
+                                                      "o_fast": [0.05, 0.7, 0.05, 0.1, 0.1]}}},
+    "fs_mix": {"search": [0.0, 0.0, 0.5, 0.5, 0.0],
+               "other": {"kind": "mixture", "policies": {"x": [0.3, 0.1, 0.1, 0.4, 0.1],
+                                                         "z": [0.0, 1.0, 0.0, 0.0, 0.0],
+                                                         "y": [0.2] * 5}}},
+    "fixed_other": {"search": [0.6, 0.1, 0.1, 0.1, 0.1],
+                    "other": {"kind": "fixed", "probs": [0.3, 0.1, 0.1, 0.4, 0.1]}},
+    "pe_fs": {"search": [0.7, 0.1, 0.1, 0.1], "other": {"kind": "random"}},
+    "pe_mix": {"search": None,
+               "other": {"kind": "mixture", "policies": {"u": [0.25] * 4,
+                                                         "side": [0.1, 0.4, 0.4, 0.1]}}},
+}
+MCTS_CASES = {
+    # name: (planner class, cfg overrides, spec, num_sims, [(planner seed, env seed)], ego,
+    #        max_steps, env)
+    "mcts_pomcp_fs_pucb": ("POMCP", {"action_selection": "pucb"}, "fs", 64, [(40, 40), (41, 41)],
+                           "0", 50, "Driving-v1"),
+    "mcts_pomcp_fs_ucb": ("POMCP", {}, "fs", 64, [(42, 42)], "0", 50, "Driving-v1"),
+    "mcts_ipomcp_mix_pucb": ("IPOMCP", {"action_selection": "pucb", "state_belief_only": False},
+                             "mix", 64, [(43, 43), (44, 44)], "0", 50, "Driving-v1"),
+    "mcts_ipomcp_fs_mix_ucb_ego1": ("IPOMCP", {"state_belief_only": False}, "fs_mix", 48,
+                                    [(45, 45)], "1", 50, "Driving-v1"),
+    "mcts_fixed_other_pucb": ("MCTS", {"action_selection": "pucb"}, "fixed_other", 48,
+                              [(46, 46)], "0", 50, "Driving-v1"),
+    "mcts_pe_fs_ucb": ("POMCP", {}, "pe_fs", 48, [(47, 47)], "0", 100, "PursuitEvasion-v1"),
+    "mcts_pe_mix_pucb": ("IPOMCP", {"action_selection": "pucb", "state_belief_only": False},
+                         "pe_mix", 48, [(48, 48)], "1", 100, "PursuitEvasion-v1"),
+}
+
+
+def run_mcts_case(name):
+    cls, over, spec, num_sims, pairs, ego, max_steps, env = MCTS_CASES[name]
+    out = {"case": name, "planner": cls, "env": env, "num_sims": num_sims, "ego": ego,
+           "max_steps": max_steps, "spec": MCTS_SPECS[spec], "episodes": []}
+    for seed, env_seed in pairs:
+        cfg = dict(TEST_CFG, **over)
+        cfg["seed"] = seed
+        tr, rr = reference_mcts_episode(cfg, num_sims, env_seed, MCTS_SPECS[spec], ego=ego,
+                                        max_steps=max_steps, env=env, planner_cls=cls)
+        out["episodes"].append({"config": dict(cfg), "env_seed": env_seed, "trace": tr,
+                                "records": rr})
+    return out
+
+
 def config_kats():
     """MCTSConfig derived fields (config.py:47-55) from the reference itself."""
     P = import_reference()
@@ -294,7 +347,7 @@ def _write(out_dir, name, data):
 
 
 def main(only=None, out_dir=HERE):
-    """only: None (every fixture), "ipomcp", "potmmcp", "meta" (config +
+    """only: None (every fixture), "ipomcp", "potmmcp", "mcts", "meta" (config +
     tracker fixtures only) or a list of I-NTMCP case names."""
     if not reference_available():
         raise SystemExit("reference not available (container-only script)")
@@ -322,6 +375,11 @@ def main(only=None, out_dir=HERE):
     if only in (None, "potmmcp"):
         _write(out_dir, "potmmcp_trees", run_potmmcp_trees())
         print("potmmcp_trees written")
+    for name in MCTS_CASES if only in (None, "mcts") else ():
+        data = run_mcts_case(name)
+        _write(out_dir, name, data)
+        n = sum(len(e["records"]) for e in data["episodes"])
+        print(f"{name}: {len(data['episodes'])} episodes, {n} records")
     if only in (None, "meta"):
         _write(out_dir, "config_kats", config_kats())
         _write(out_dir, "config_checks", config_checks())
@@ -344,6 +402,8 @@ if __name__ == "__main__":
         main(only="ipomcp", out_dir=out)
     elif "--potmmcp" in argv:
         main(only="potmmcp", out_dir=out)
+    elif "--mcts" in argv:
+        main(only="mcts", out_dir=out)
     elif "--meta" in argv:
         main(only="meta", out_dir=out)
     elif "--intmcp" in argv:

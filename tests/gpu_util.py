@@ -77,6 +77,8 @@ def gpu_episode(cfg_kwargs, num_sims, env_seed, ego="0", max_steps=50, env="Driv
         return a
 
     trace = run_episode(step, env_seed, ego=ego, max_steps=max_steps, env=env)
+    if exact is not None:
+        exact.append(_exact_draws(planner._engine._ctx))
     planner.close()
     return trace, records
 
@@ -187,10 +189,30 @@ def intmcp_state_record(eng, pair, searched, action):
                          st.min_value, st.max_value, parts, nested)
 
 
-def gpu_intmcp_episode(cfg_kwargs, num_sims, env_seed, ego="0", max_steps=50, env="Driving-v1"):
+def _softmax_debug(ctx, slack):
+    """Widen the I-NTMCP fast softmax bound (intmcp_debug_set_softmax_slack) and
+    start counting exact-path draws."""
+    from posggym_baselines_amd import _native as N
+    assert N.load().intmcp_debug_set_softmax_slack(ctx, float(slack)) == 0
+
+
+def _exact_draws(ctx):
+    import ctypes as C
+    from posggym_baselines_amd import _native as N
+    n = C.c_uint64()
+    assert N.load().intmcp_debug_exact_draws(ctx, C.byref(n)) == 0
+    return int(n.value)
+
+
+def gpu_intmcp_episode(cfg_kwargs, num_sims, env_seed, ego="0", max_steps=50, env="Driving-v1",
+                       softmax_slack=None, exact=None):
+    """softmax_slack: the fast softmax bound's widening (None: the product's);
+    the exact-path draws of the episode are appended to `exact` (a list)."""
     from posggym_baselines_amd.planning import INTMCP
     model = product_model(env)
     planner = INTMCP.initialize(model, ego, product_config(cfg_kwargs, num_sims), 1, None)
+    if softmax_slack is not None:
+        _softmax_debug(planner._engine._ctx, softmax_slack)
     planner.reset()
     records = []
 
@@ -201,11 +223,14 @@ def gpu_intmcp_episode(cfg_kwargs, num_sims, env_seed, ego="0", max_steps=50, en
         return a
 
     trace = run_episode(step, env_seed, ego=ego, max_steps=max_steps, env=env)
+    if exact is not None:
+        exact.append(_exact_draws(planner._engine._ctx))
     planner.close()
     return trace, records
 
 
-def batched_intmcp_episodes(cfg_kwargs, num_sims, env_seeds, steps, env="Driving-v1", ego="0"):
+def batched_intmcp_episodes(cfg_kwargs, num_sims, env_seeds, steps, env="Driving-v1", ego="0",
+                            softmax_slack=None, exact=None):
     """Lockstep I-NTMCP episodes of len(env_seeds) planner pairs in ONE engine
     (pair b = tree key b, env seed env_seeds[b]), at most `steps` real steps;
     a pair whose episode ended is skipped (INTMCP_SKIP).  Per-pair record lists
@@ -220,6 +245,8 @@ def batched_intmcp_episodes(cfg_kwargs, num_sims, env_seeds, steps, env="Driving
     B = len(env_seeds)
     bp = BatchedINTMCP(model, ego, product_config(cfg_kwargs, num_sims), B, num_sims,
                        searches=steps)
+    if softmax_slack is not None:
+        _softmax_debug(bp.engine._ctx, softmax_slack)
     envs = []
     for s in env_seeds:
         es = Streams(s, ENV_TREE_BASE)
@@ -254,5 +281,7 @@ def batched_intmcp_episodes(cfg_kwargs, num_sims, env_seeds, steps, env="Driving
             envs[b][2], envs[b][3] = ts.state, ts.observations
             envs[b][4] = bool(ts.all_done)
             last[b] = a
+    if exact is not None:
+        exact.append(_exact_draws(bp.engine._ctx))
     bp.close()
     return records

@@ -101,7 +101,8 @@ def test_engine_rejects_unsupported_search_policy():
 
 def test_ipomcp_validates_other_agent_policies():
     """IPOMCP / MCTS (ipomcp.py:11-38, mcts.py:22-91): every other agent needs a
-    policy; only RandomOtherAgentPolicy runs in-kernel (checked before any GPU use)."""
+    policy; random and fixed-distribution policies run in-kernel, others raise
+    (checked before any GPU use)."""
     from posggym_baselines_amd.envs import DrivingModel
     from posggym_baselines_amd.planning import (IPOMCP, MCTS, MCTSConfig, OtherAgentPolicy,
                                                 RandomSearchPolicy)

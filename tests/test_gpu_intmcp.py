@@ -2,7 +2,12 @@
 every step record of the reference goldens (level-1 root statistics, root
 particles with the other agent's histories, every level-0 node those histories
 name: visits, children, particles) must match bit for bit."""
+import os
+import sys
+
 import pytest
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
 
 from golden_util import INTMCP_CASES, cfg_kwargs, load
 from gpu_util import gpu_intmcp_episode
@@ -29,40 +34,80 @@ TEST_CFG = dict(discount=0.95, search_time_limit=0.1, c=2 ** 0.5, truncated=Fals
                 step_limit=None, epsilon=0.92, seed=3, state_belief_only=False)
 
 
-@pytest.mark.parametrize("env,ego,sel,B", [("Driving-v1", "0", "ucb", 150),
-                                           ("PursuitEvasion-v1", "1", "uniform", 150),
-                                           ("Driving-v1", "0", "ucb", 1100)])
-def test_batched_pairs_match_oracle(env, ego, sel, B):
-    """Planner pairs in one engine, lockstep episodes: pair b equals the oracle
-    planner with tree key b.  150 pairs: the update runs a wave per pair
-    (shared log scans); 1,100 pairs: a lane per pair."""
+def _check_all_pairs(name, got):
+    """Every pair's records against the oracle's digest (tests/golden/
+    make_oracle_digests.py); a mismatching pair is rerun on the oracle so the
+    failure shows the first differing step."""
+    from golden_util import load
+    from make_oracle_digests import CASES, oracle_pair, record_digest
+    fx = load("oracle_digests")[name]
+    assert len(got) == len(fx["digests"]) == CASES[name]["pairs"]
+    bad = [b for b, recs in enumerate(got) if record_digest(recs) != fx["digests"][b]]
+    if bad:
+        b = bad[0]
+        exp = oracle_pair(CASES[name], b)
+        for t, (g, e) in enumerate(zip(got[b], exp)):
+            assert g == e, f"{name}: {len(bad)} pairs differ; pair {b} step {t}"
+        assert len(got[b]) == len(exp), f"{name}: pair {b} step count"
+        raise AssertionError(f"{name}: {len(bad)} pairs differ (first {b}): digest only")
+
+
+def _run_case(name, softmax_slack=None, exact=None):
     from gpu_util import batched_intmcp_episodes
-    from oracle.run import oracle_intmcp_episode
-    cfg = dict(TEST_CFG, action_selection=sel)
-    seeds = [500 + b for b in range(B)]
-    steps, sims = 4, 48
-    got = batched_intmcp_episodes(cfg, sims, seeds, steps, env=env, ego=ego)
-    for b in (0, 1, 63, 64, 100, 127, 128, 149, B - 1):
-        _, exp = oracle_intmcp_episode(cfg, sims, seeds[b], ego=ego, tree=b, max_steps=steps,
-                                       env=env)
-        assert got[b] == exp, f"pair {b}"
+    from make_oracle_digests import CASES, case_cfg
+    c = CASES[name]
+    seeds = [c["seed0"] + b for b in range(c["pairs"])]
+    return batched_intmcp_episodes(case_cfg(c), c["sims"], seeds, c["steps"], env=c["env"],
+                                   ego=c["ego"], softmax_slack=softmax_slack, exact=exact)
 
 
-@pytest.mark.parametrize("env", ["Driving-v1", "PursuitEvasion-v1"])
-def test_bench_workload_pairs_match_oracle(env):
+@pytest.mark.parametrize("name", ["im_drv_ucb_48", "im_pe_uniform_48"])
+def test_batched_pairs_match_oracle(name):
+    """Planner pairs in one engine, lockstep episodes (4 steps, 48 simulations
+    per level): EVERY pair b equals the oracle planner with tree key b.  1,100
+    Driving pairs (the update runs a lane per pair) and 150 PursuitEvasion pairs
+    (a wave per pair, shared log scans)."""
+    _check_all_pairs(name, _run_case(name))
+
+
+@pytest.mark.parametrize("name", ["im_drv_ucb_256", "im_pe_ucb_256"])
+def test_bench_workload_pairs_match_oracle(name):
     """The bench's 256 simulations per level (bench.py --planner intmcp,
-    TEST_CFG of the bench), 3 lockstep steps of 130 pairs: sampled pairs equal
-    the oracle planner with their tree key (every step record, incl. the
+    TEST_CFG of the bench), 3 lockstep steps of 130 pairs: every pair equals
+    the oracle planner with its tree key (every step record, incl. the
     level-0 nodes the root's histories name)."""
-    from gpu_util import batched_intmcp_episodes
-    from oracle.run import oracle_intmcp_episode
-    seeds = [900 + b for b in range(130)]
-    steps, sims = 3, 256
-    got = batched_intmcp_episodes(TEST_CFG, sims, seeds, steps, env=env, ego="0")
-    for b in (0, 65, 129):
-        _, exp = oracle_intmcp_episode(TEST_CFG, sims, seeds[b], ego="0", tree=b,
-                                       max_steps=steps, env=env)
-        assert got[b] == exp, f"pair {b}"
+    _check_all_pairs(name, _run_case(name))
+
+
+def test_softmax_exact_fallback_fires_and_is_exact():
+    """The other agent's softmax (intmcp.py:763-791) takes its choice from
+    bounded FP32 weights and falls back to the exact FP64 path near a
+    cumulative weight.  With the product's bound the fallback
+    fires on a small fraction of draws; with the bound widened 3000x it takes
+    most draws.  Both runs of the bench workload's 130 Driving pairs are
+    bit-exact against the oracle, and both count exact-path draws."""
+    n1, n3000 = [], []
+    _check_all_pairs("im_drv_ucb_256", _run_case("im_drv_ucb_256", softmax_slack=1.0, exact=n1))
+    _check_all_pairs("im_drv_ucb_256", _run_case("im_drv_ucb_256", softmax_slack=3000.0,
+                                                 exact=n3000))
+    assert n1[0] > 0 and n3000[0] > 10 * n1[0], (n1, n3000)
+
+
+@pytest.mark.parametrize("case", INTMCP_CASES)
+def test_gpu_intmcp_goldens_exact_softmax_path(case):
+    """The reference goldens with the fast softmax bound widened 3000x (the
+    exact FP64 path decides most draws): still bit-exact, and the exact path
+    ran."""
+    data = load(case)
+    exact = []
+    for ep in data["episodes"]:
+        kw = cfg_kwargs(ep["config"])
+        trace, records = gpu_intmcp_episode(kw, data["num_sims"], ep["env_seed"],
+                                            ego=data["ego"], max_steps=data["max_steps"],
+                                            env=data["env"], softmax_slack=3000.0, exact=exact)
+        assert records == ep["records"], case
+        assert trace == ep["trace"]
+    assert sum(exact) > 0, case
 
 
 def test_batched_many_pairs_properties():

@@ -125,3 +125,20 @@ def test_intmcp_depleted_branch_unreachable_for_valid_configs():
     finally:
         OI._Planner._nested_sim = orig
     assert hits == []
+
+
+@pytest.mark.parametrize("name", ["im_drv_ucb_48", "im_pe_uniform_48", "im_drv_ucb_256",
+                                  "im_pe_ucb_256"])
+def test_oracle_digests_fixture(name):
+    """tests/golden/oracle_digests.json (the GPU suite compares every batched
+    I-NTMCP pair against it): a sample of its per-pair digests recomputed from
+    the oracle here."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from make_oracle_digests import CASES, oracle_pair, record_digest
+    fx = load("oracle_digests")[name]
+    assert {k: v for k, v in fx.items() if k != "digests"} == CASES[name]
+    n = CASES[name]["pairs"]
+    for b in sorted({0, 1, 63, 64, n // 2, n - 1}):
+        assert record_digest(oracle_pair(CASES[name], b)) == fx["digests"][b], f"pair {b}"

@@ -98,3 +98,45 @@ def test_potmmcp_rejects_before_device_work():
     meta.policies["rnn"] = Recurrent()
     with pytest.raises(NotImplementedError):
         POTMMCP(m, "0", cfg, {"1": mix}, meta)
+
+
+def test_base_planner_type_tables():
+    """MCTS / IPOMCP / POMCP with fixed-distribution policies (planning/ipomcp.py
+    base_type_tables): one ego policy (the search policy, no sample_policy
+    draw), the node prior = its get_pi, the other agent's policies and draw
+    kinds; random policies on both sides stay on the plain kernel; the
+    reference's own failures (mixture with state_belief_only=True, a stateless
+    policy with state_belief_only=False) are raised up front."""
+    import pytest
+    from posggym_baselines_amd.envs import DrivingModel
+    from posggym_baselines_amd.planning import (MCTSConfig, OtherAgentMixturePolicy,
+                                                RandomOtherAgentPolicy, RandomSearchPolicy)
+    from posggym_baselines_amd.planning.ipomcp import base_type_tables
+    from posggym_baselines_amd.planning.policies import FixedDistributionPolicy
+    from posggym_baselines_amd.planning.search_policy import SearchPolicyWrapper
+    m = DrivingModel()
+    cfg = MCTSConfig(discount=0.95, search_time_limit=0.1, c=1.4, truncated=False, seed=0,
+                     state_belief_only=True)
+    cfg_h = MCTSConfig(discount=0.95, search_time_limit=0.1, c=1.4, truncated=False, seed=0,
+                       state_belief_only=False)
+    fs = SearchPolicyWrapper(FixedDistributionPolicy(m, "0", "s", [0.1, 0.5, 0.1, 0.2, 0.1]))
+    rnd_o = {"1": RandomOtherAgentPolicy(m, "1")}
+    assert base_type_tables(m, "0", cfg, rnd_o, RandomSearchPolicy(m, "0")) is None
+    tp = base_type_tables(m, "0", cfg, rnd_o, fs)
+    assert (tp.num_ego, tp.num_other, tp.no_meta_draw, tp.no_mixture_draw, tp.ego_uniform,
+            tp.other_uniform) == (1, 1, 1, 1, 0, 1)
+    assert list(tp.ego_pi[0])[:5] == list(tp.expected_prior)[:5] == [0.1, 0.5, 0.1, 0.2, 0.1]
+    mix = OtherAgentMixturePolicy(m, "1", {"a": FixedDistributionPolicy(m, "1", "a", [0.2] * 5),
+                                           "b": FixedDistributionPolicy(m, "1", "b",
+                                                                        [0, 1, 0, 0, 0])})
+    tp = base_type_tables(m, "0", cfg_h, {"1": mix}, RandomSearchPolicy(m, "0"))
+    assert (tp.num_other, tp.no_mixture_draw, tp.ego_uniform, tp.other_uniform) == (2, 0, 1, 0)
+    assert list(tp.ego_pi[0])[:5] == [1.0 / 5] * 5 and list(tp.other_pi[1])[:5] == [0, 1, 0, 0, 0]
+    with pytest.raises(ValueError):
+        base_type_tables(m, "0", cfg, {"1": mix}, fs)
+    fixed = {"1": FixedDistributionPolicy(m, "1", "f", [0.3, 0.1, 0.1, 0.4, 0.1])}
+    tp = base_type_tables(m, "0", cfg, fixed, RandomSearchPolicy(m, "0"))
+    assert (tp.no_mixture_draw, tp.other_uniform, list(tp.other_pi[0])[:5]) == \
+        (1, 0, [0.3, 0.1, 0.1, 0.4, 0.1])
+    with pytest.raises(ValueError):
+        base_type_tables(m, "0", cfg_h, fixed, fs)

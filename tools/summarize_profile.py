@@ -13,6 +13,7 @@ is doubled (MI355X_MICROARCH.md "HBM"); WRITE_SIZE is exact for 16-B stores.
 import csv
 import json
 import os
+import re
 import shutil
 import sys
 
@@ -23,9 +24,26 @@ def read_counter(path, name, kernel="k_search"):
     vals = []
     with open(path) as f:
         for row in csv.DictReader(f):
-            if kernel in row["Kernel_Name"] and row["Counter_Name"] == name:
-                vals.append(float(row["Counter_Value"]))
-    return vals
+            if KNAME[kernel].search(row["Kernel_Name"]) and row["Counter_Name"] == name:
+                vals.append((int(row.get("Dispatch_Id", len(vals))), float(row["Counter_Value"])))
+    return [v for _, v in sorted(vals)]   # dispatch order: the timed launches are the last
+
+
+KNAME = {"k_search": re.compile(r"\bk_search<"), "k_im_search": re.compile(r"\bk_im_search<")}
+
+
+def timed_launches(path, kernel):
+    """Durations (ns) of the kernel's dispatches in dispatch order, from a
+    rocprofv3 --kernel-trace CSV (empty if the file is absent)."""
+    if not os.path.exists(path):
+        return []
+    rows = []
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if KNAME[kernel].search(row["Kernel_Name"]):
+                rows.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"])))
+    rows.sort()
+    return [e - s for s, e in rows]
 
 
 def bench_line(log):
@@ -51,9 +69,9 @@ def main():
     stats = {}
     with open(os.path.join(src, "trace", "run_kernel_stats.csv")) as f:
         for row in csv.DictReader(f):
-            if kernel in row["Name"]:
+            if KNAME[kernel].search(row["Name"]):
                 stats = {"name": row["Name"], "calls": int(row["Calls"]),
-                         "avg_ms": float(row["AverageNs"]) / 1e6,
+                         "avg_ms_all_calls": float(row["AverageNs"]) / 1e6,
                          "min_ms": float(row["MinNs"]) / 1e6, "max_ms": float(row["MaxNs"]) / 1e6}
     fetch = read_counter(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE",
                          kernel)
@@ -63,6 +81,16 @@ def main():
     # for I-NTMCP, the arena-calibration probe's small launches)
     b = bench_line(os.path.join(src, "bench_trace.log"))
     k = max(1, int(b.get("steps", 1)))
+    # avg_ms: the TIMED launches only (the last `steps` dispatches of the kernel in
+    # the kernel trace), not the warmup or an arena-calibration probe's launches
+    durs = timed_launches(os.path.join(src, "trace", "run_kernel_trace.csv"), kernel)
+    if len(durs) >= k:
+        stats["avg_ms"] = sum(durs[-k:]) / k / 1e6
+        stats["timed_launches"] = k
+        stats["timed_ms"] = [d / 1e6 for d in durs[-k:]]
+    else:   # no kernel trace kept (profiles before round 4): the all-calls average
+        stats["avg_ms"] = stats["avg_ms_all_calls"]
+        stats["timed_launches"] = None
     f_avg = sum(fetch[-k:]) / len(fetch[-k:])
     w_avg = sum(write[-k:]) / len(write[-k:])
     hbm = (2 * f_avg + w_avg) * 1024
