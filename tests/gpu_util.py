@@ -77,8 +77,6 @@ def gpu_episode(cfg_kwargs, num_sims, env_seed, ego="0", max_steps=50, env="Driv
         return a
 
     trace = run_episode(step, env_seed, ego=ego, max_steps=max_steps, env=env)
-    if exact is not None:
-        exact.append(_exact_draws(planner._engine._ctx))
     planner.close()
     return trace, records
 
