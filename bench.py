@@ -212,6 +212,10 @@ def parse():
     ap.add_argument("--deep", action="store_true",
                     help="gamma=0.99, epsilon=0.01 (depth_limit 459, rollout-dominated)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--update-step", action="store_true",
+                    help="each timed step = search + the environment's answer + update() "
+                         "(re-root, extraction, reinvigoration, subtree compaction) instead of a "
+                         "restore() + search (single GPU)")
     ap.add_argument("--no-sub", action="store_true",
                     help="skip the secondary-configuration records (`sub`) the default run "
                          "appends after the headline (profiling runs)")
@@ -752,9 +756,12 @@ def main():
     if world > 1:
         dist.barrier()   # rank 0's build is complete
     B, S, K = args.trees, args.sims, args.root_parallel
+    if args.update_step and (world > 1 or K > 1):
+        raise SystemExit("--update-step: one GPU, independent planners")
     r = run_pomcp(dev, env=args.env, B=B, S=S, K=K, base_cfg=base_cfg, tm=tm, steps=args.steps,
                   warmup=args.warmup, seed=args.seed, max_blocks=args.max_blocks, world=world,
-                  rank=rank, dist=dist if world > 1 else None, clocks=True)
+                  rank=rank, dist=dist if world > 1 else None, clocks=True,
+                  update_step=args.update_step)
     caps = r["caps"]
     out = {
         "metric": (f"MCTS simulations/sec on {args.env} (POTMMCP exact search, fixed-distribution "
@@ -772,8 +779,8 @@ def main():
         "data": f"synthetic {args.env} belief states (env seed 1000+b), build's {args.env} "
                 "restatement",
         "config": {"workload": r["workload"],
-                   "trees_per_gpu": B, "sims_per_tree": S, "depth_limit": r["depth_limit"],
-                   "root_parallel": K, "planners_per_gpu": B // K,
+                   "trees_per_gpu": r["B"], "sims_per_tree": S, "depth_limit": r["depth_limit"],
+                   "root_parallel": K, "planners_per_gpu": r["B"] // K,
                    "sims_per_planner_step": S * K,
                    "rollout_steps_per_sim": r["rollout_steps_per_sim"],
                    "deferred_levels_per_sim": r["deferred_levels_per_sim"],
@@ -786,10 +793,12 @@ def main():
                              "max_particles_used": r["log_used"]}},
         "roofline": r["roofline"],
     }
+    if "update_ms" in r:
+        out["update_ms"] = r["update_ms"]
     if cpu is not None:
         out["cpu_baseline"] = cpu
     default_run = (world == 1 and not tm and not args.deep and args.env == "Driving-v1"
-                   and B == 65536 and S == 65536 and K == 1)
+                   and B == 65536 and S == 65536 and K == 1 and not args.update_step)
     if rank == 0 and default_run and not args.no_sub:
         out["sub"] = sub_records(dev, args.seed)
     if rank == 0:

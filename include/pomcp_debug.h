@@ -8,6 +8,10 @@ extern "C" {
 /* out[4*i + k] = {sqrt(a), a / b, a + 0.95 * b, (a - b) / (a + b)} computed on
  * device 0 in FP64 (checks the device FP64 path is correctly rounded). */
 int pomcp_debug_fp_selftest(const double* a, const double* b, int32_t n, double* out);
+/* out[2i] = rcp_nr(x[i]), out[2i + 1] = rsq_nr(x[i]) on device 0: the FP64
+ * 1/x and 1/sqrt(x) of k_search's fast UCB scores (hardware estimate + two
+ * Newton steps), whose error bound decides when the exact scores are needed. */
+int pomcp_debug_fast_recip(const double* x, int32_t n, double* out);
 /* out[i] = host_exp(x[i]) on device 0 (FP64): the I-NTMCP softmax's exp, a
  * bit-exact restatement of the host libm's exp (csrc/host_exp.h). */
 int pomcp_debug_exp(const double* x, int32_t n, double* out);
@@ -24,6 +28,10 @@ int pomcp_debug_phase_timing(pomcp_ctx* ctx, uint64_t* out, int32_t capacity, in
  * pomcp_debug_phase_timing (tools/phase_timing_im.py). */
 typedef struct intmcp_ctx intmcp_ctx;
 int intmcp_debug_phase_timing(intmcp_ctx* ctx, uint64_t* out, int32_t capacity, int32_t* count);
+/* k_search_lds (the wave-per-tree kernel): polls of a late step-tree hand-off
+ * before the search wave stops its producer waves and computes the rest of the
+ * launch itself (0 = the default, ~0.1 s); results are the same either way. */
+int pomcp_debug_set_spin_limit(pomcp_ctx* ctx, int32_t polls);
 /* I-NTMCP: the other agent's softmax (sample_action, intmcp.py:763-791) takes
  * its choice from bounded FP32 weights and falls back to the exact FP64 path
  * near a cumulative weight; `slack` (>= 1, default 1) widens that bound, so a

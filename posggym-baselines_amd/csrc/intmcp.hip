@@ -619,6 +619,43 @@ struct ImPair {
         if (i < nr && q[i].x == 0u) zero = i;
       if (zero >= 0) return im_order(x.info, zero);
       const double log_n = logn(x.visits);
+#ifndef IM_ABLATE_SELECT
+      // Fast scores first, the exact ones only for near-ties of different
+      // statistics: as k_search's select_action (pomcp_search.hip), in
+      // registration order
+      {
+        const double lo = h.mm_min[k], hi = h.mm_max[k];
+        const bool nz = hi > lo;
+        const double rr = nz ? rcp_nr(hi - lo) : 1.0;
+        const double csl = p.c * sqrt(log_n);
+        double sf[kImMaxA], mg[kImMaxA];
+        int bi = 0;
+        double bf = -__builtin_inf(), bm = 0.0;
+        uint4 sb = q[0];
+#pragma unroll
+        for (int i = 0; i < kImMaxA; ++i) {
+          const double v = hilo_d(q[i].z, q[i].w);
+          const double qf = nz ? (v - lo) * rr : v;
+          const double ef = csl * rsq_nr((double)((int)q[i].x > 0 ? (int)q[i].x : 1));
+          sf[i] = qf + ef;
+          mg[i] = __builtin_fabs(qf) + ef;
+          if (i < nr && sf[i] > bf) {
+            bf = sf[i];
+            bm = mg[i];
+            bi = i;
+          }
+        }
+#pragma unroll
+        for (int i = 1; i < kImMaxA; ++i) sb = sel4(i == bi, q[i], sb);
+        bool amb = false;
+#pragma unroll
+        for (int i = 0; i < kImMaxA; ++i) {
+          const bool same = q[i].x == sb.x && q[i].z == sb.z && q[i].w == sb.w;
+          amb |= i < nr && i != bi && !same && !(bf - sf[i] > 1e-12 * (mg[i] + bm));
+        }
+        if (!amb && nr > 0) return im_order(x.info, bi);
+      }
+#endif
       double best = -__builtin_inf();
       int ba = 0;
       // unrolled with a bound check: the arrays stay in registers (a loop to

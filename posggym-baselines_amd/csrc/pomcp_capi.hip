@@ -409,8 +409,8 @@ int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_key
   // then the per-tree update (initial belief / re-root + reinvigoration)
   PB_ENV_LAUNCH(ctx, k_reroot_child, dim3(grid_blocks(B)), dim3(256), ctx->dp);
   HIP_TRY(ctx, hipGetLastError());
-  hipLaunchKernelGGL(k_extract, dim3(grid_blocks(search_waves(B))), dim3(256), 0, ctx->stream,
-                     ctx->dp);
+  hipLaunchKernelGGL(k_extract, dim3((unsigned)search_waves(B)), dim3(64 * kLogWaves), 0,
+                     ctx->stream, ctx->dp);
   HIP_TRY(ctx, hipGetLastError());
   PB_ENV_LAUNCH(ctx, k_update, dim3(grid_blocks(B)), dim3(256), ctx->dp);
   HIP_TRY(ctx, hipGetLastError());
@@ -422,7 +422,8 @@ int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_key
     if (rc != POMCP_OK) return rc;
     hipLaunchKernelGGL(k_compact, dim3(grid_blocks(B)), dim3(256), 0, ctx->stream, ctx->dp);
     HIP_TRY(ctx, hipGetLastError());
-    PB_ENV_LAUNCH(ctx, k_compact_log, dim3(grid_blocks(search_waves(B))), dim3(256), ctx->dp);
+    PB_ENV_LAUNCH(ctx, k_compact_log, dim3((unsigned)search_waves(B)), dim3(64 * kLogWaves),
+                  ctx->dp);
     HIP_TRY(ctx, hipGetLastError());
   }
   HIP_TRY(ctx, hipMemcpyAsync(ctx->host_upd.data(), ctx->dp.upd_out, sizeof(int32_t) * 2 * B,
@@ -1025,6 +1026,24 @@ int pomcp_debug_fp_selftest(const double* a, const double* b, int32_t n, double*
   return e == hipSuccess ? POMCP_OK : POMCP_E_HIP;
 }
 
+// Debug: rcp_nr / rsq_nr (the fast UCB scores' 1/x and 1/sqrt(x)) on the
+// device, for the error bound their exact fallback relies on.
+int pomcp_debug_fast_recip(const double* x, int32_t n, double* out) {
+  if (!x || !out || n <= 0) return POMCP_E_INVALID;
+  double *dx = nullptr, *dout = nullptr;
+  if (hipMalloc(&dx, sizeof(double) * n) != hipSuccess) return POMCP_E_HIP;
+  if (hipMalloc(&dout, sizeof(double) * 2 * n) != hipSuccess) {
+    (void)hipFree(dx);
+    return POMCP_E_HIP;
+  }
+  (void)hipMemcpy(dx, x, sizeof(double) * n, hipMemcpyHostToDevice);
+  hipLaunchKernelGGL(k_fast_recip, dim3((n + 255) / 256), dim3(256), 0, 0, dx, n, dout);
+  hipError_t e = hipMemcpy(out, dout, sizeof(double) * 2 * n, hipMemcpyDeviceToHost);
+  (void)hipFree(dx);
+  (void)hipFree(dout);
+  return e == hipSuccess ? POMCP_OK : POMCP_E_HIP;
+}
+
 // Debug: device exp (the I-NTMCP softmax, intmcp.py:784-786) for comparison
 // with the host's math.exp.
 int pomcp_debug_exp(const double* x, int32_t n, double* out) {
@@ -1054,6 +1073,14 @@ int pomcp_debug_host_exp(const double* x, int32_t n, double* out) {
 int pomcp_debug_set_inline_slots(pomcp_ctx* ctx, int32_t n) {
   if (!ctx || n < 1 || n > kSlots) return POMCP_E_INVALID;
   ctx->dp.islots = n;
+  return POMCP_OK;
+}
+
+// Debug: k_search_lds's bound on waiting for a step-tree hand-off (polls; 0 =
+// the default), so a test can make every hand-off late.
+int pomcp_debug_set_spin_limit(pomcp_ctx* ctx, int32_t polls) {
+  if (!ctx || polls < 0) return POMCP_E_INVALID;
+  ctx->dp.spin_max = polls;
   return POMCP_OK;
 }
 

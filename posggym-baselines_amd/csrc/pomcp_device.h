@@ -213,6 +213,8 @@ struct DevParams {
   int32_t islots;       // inline obs slots in use per action node (kSlots; fewer only in
                         // tests of the overflow map: pomcp_debug_set_inline_slots)
   int32_t lines;        // lines per block (blk_lines(A, tm))
+  int32_t spin_max;     // k_search_lds: polls of a late step-tree hand-off before the search
+                        // wave runs on without producers (0: the default; tests shrink it)
   int32_t tm;           // type-based search (POTMMCP): tmt, prior lines, log aux
   const TmTables* tmt;
   TreeHdr* hdr;
@@ -283,6 +285,24 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
 }
 __device__ __forceinline__ double uni_d(double v) {
   return __hiloint2double(uni(__double2hiint(v)), uni(__double2loint(v)));
+}
+
+// 1 / x and 1 / sqrt(x) in FP64: the hardware estimates (v_rcp_f64 /
+// v_rsq_f64, relative error ~2^-23) refined by two Newton steps each, to a few
+// ulp (the fast UCB scores of k_search, select_action: their error bound
+// decides when the exact scores are needed).
+__device__ __forceinline__ double rcp_nr(double x) {
+  double y = __builtin_amdgcn_rcp(x);
+  double e = __builtin_fma(-x, y, 1.0);
+  y = __builtin_fma(y, e, y);
+  e = __builtin_fma(-x, y, 1.0);
+  return __builtin_fma(y, e, y);
+}
+__device__ __forceinline__ double rsq_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double hx = 0.5 * x;
+  y = y * __builtin_fma(-hx, y * y, 1.5);
+  return y * __builtin_fma(-hx, y * y, 1.5);
 }
 
 __device__ __forceinline__ uint32_t spread16(uint32_t x) {

@@ -389,31 +389,38 @@ __global__ __launch_bounds__(256) void k_reroot_child(DevParams p) {
   if (T.lane == 0) p.want[tree] = want;
 }
 
-// Re-root, step 2: one wavefront per SEARCH wave scans that wave's shared log
-// once, in order, and appends each record of a wanted child to its tree's new
-// root belief ({root_t + 1, v0, v1}), preserving insertion order per tree.
-__global__ __launch_bounds__(256) void k_extract(DevParams p) {
-  const int sw = blockIdx.x * kTreesPerBlock + (threadIdx.x >> 6);   // search wave
+// Re-root, step 2: one WORKGROUP (kLogWaves waves) per SEARCH wave scans that
+// wave's shared log once, in order, and appends each record of a wanted child
+// to its tree's new root belief ({root_t + 1, v0, v1}), preserving insertion
+// order per tree.  A pass reads 64 kLogWaves consecutive records (one per
+// thread); a record's place is its tree's count so far + the matches of the
+// same tree in the earlier waves of the pass + its rank in its own wave.  (One
+// wave per log took ~0.3 s at 65,536 trees x 65,536 simulations: one
+// dependent round trip per 64 records.)
+constexpr int kLogWaves = 4;
+__global__ __launch_bounds__(64 * kLogWaves) void k_extract(DevParams p) {
+  const int sw = blockIdx.x;   // search wave
   const int lane = lane_id();
-  __shared__ uint32_t want[kTreesPerBlock][kWave];
-  __shared__ int32_t cnt[kTreesPerBlock][kWave];
-  __shared__ uint32_t tval[kTreesPerBlock][kWave];
-  __shared__ int64_t dst[kTreesPerBlock][kWave];
-  const int wi = threadIdx.x >> 6;
-  const int nwaves = (p.B + kWave - 1) / kWave;
-  if (sw >= nwaves) return;
-  const int tree = sw * kWave + lane;
-  const bool valid = tree < p.B;
-  const TreeHdr h = p.hdr[valid ? tree : 0];
-  want[wi][lane] = valid ? p.want[tree] : 0xFFFFFFFFu;
-  cnt[wi][lane] = 0;
-  tval[wi][lane] = (uint32_t)h.root_t + 1u;
-  dst[wi][lane] = ((int64_t)tree * 2 + (h.belief_sel ^ 1)) * p.Nr;
-  __builtin_amdgcn_wave_barrier();
+  const int w = (int)(threadIdx.x >> 6);
+  __shared__ uint32_t want[kWave];
+  __shared__ int32_t cnt[kWave];
+  __shared__ uint32_t tval[kWave];
+  __shared__ int64_t dst[kWave];
+  __shared__ int32_t wc[kLogWaves][kWave];   // this pass's matches per wave and tree
+  if (w == 0) {
+    const int tree = sw * kWave + lane;
+    const bool valid = tree < p.B;
+    const TreeHdr h = p.hdr[valid ? tree : 0];
+    want[lane] = valid ? p.want[tree] : 0xFFFFFFFFu;
+    cnt[lane] = 0;
+    tval[lane] = (uint32_t)h.root_t + 1u;
+    dst[lane] = ((int64_t)tree * 2 + (h.belief_sel ^ 1)) * p.Nr;
+  }
+  __syncthreads();
   const WaveLog wl(p.plog, p.Np, sw, p.tm);
   const uint32_t n = p.wlog[sw];
-  for (uint32_t base = 0; base < n; base += kWave) {
-    const uint32_t i = base + (uint32_t)lane;
+  for (uint32_t base = 0; base < n; base += kWave * kLogWaves) {
+    const uint32_t i = base + (uint32_t)threadIdx.x;
     LogRec r = {0xFFFFFFFFu, 0u, 0u};
     uint32_t aux = 0u;   // type-based: the particle's other-agent policy
     if (i < n) {
@@ -421,21 +428,39 @@ __global__ __launch_bounds__(256) void k_extract(DevParams p) {
       if (p.tm) aux = wl.aux[i];
     }
     const uint32_t l = r.id >> kIdBits;
-    const bool m = i < n && want[wi][l] == r.id;
+    const bool m = i < n && want[l] == r.id;
+    wc[w][lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    // ranks in this wave, in lane order (matches are few: one child per tree)
+    int rank = 0;
     uint64_t mask = __ballot(m);
-    while (mask) {   // matches of this chunk in log order
+    while (mask) {
       const int j = __ffsll((long long)mask) - 1;
       mask &= mask - 1ull;
       const int lj = __builtin_amdgcn_readlane((int)l, j);
-      const int pos = cnt[wi][lj];
       if (lane == j) {
-        if (pos < p.Nr) p.belief[dst[wi][lj] + pos] = make_uint4(tval[wi][lj], r.v0, r.v1, aux);
-        cnt[wi][lj] = pos + 1;
+        rank = wc[w][lj];
+        wc[w][lj] = rank + 1;
       }
       __builtin_amdgcn_wave_barrier();
     }
+    __syncthreads();
+    if (m) {
+      int pos = cnt[l] + rank;
+      for (int v = 0; v < w; ++v) pos += wc[v][l];
+      if (pos < p.Nr) p.belief[dst[l] + pos] = make_uint4(tval[l], r.v0, r.v1, aux);
+    }
+    __syncthreads();
+    if (w == 0) {
+      int add = 0;
+#pragma unroll
+      for (int v = 0; v < kLogWaves; ++v) add += wc[v][lane];
+      cnt[lane] += add;
+    }
+    __syncthreads();
   }
-  if (valid) p.cnt[tree] = cnt[wi][lane];
+  const int tree = sw * kWave + lane;
+  if (w == 0 && tree < p.B) p.cnt[tree] = cnt[lane];
 }
 
 template <class Env>
@@ -800,43 +825,71 @@ __device__ __forceinline__ uint64_t ld_agent_u64(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One wave per SEARCH wave: filter that wave's shared particle log to the
-// records of obs nodes that survived k_compact (insertion order kept) and
-// relabel them; every tree's record count is recounted.  A deferred record
-// (pomcp_device.h: an arrival at a child beyond the depth / step limits,
-// never looked up by k_search) whose action node survived gets its child
-// here: the child's observation key and absorbing flag follow from the
-// record's state (Env::obs_key, Env::done_of); it is found among the action
-// node's inline slots or inserted there (compare-and-swap: the wave's lanes
-// insert concurrently), else in the overflow map (one record at a time), and
-// its absorbing flag is that of its LAST arrival (mcts.py:370, records in log
-// order).  Which slot a child takes is a label (ActionNode.children is only
-// ever looked up by observation in the reference), so results are unchanged.
+// One WORKGROUP (kLogWaves waves, as k_extract) per SEARCH wave: filter that
+// wave's shared particle log to the records of obs nodes that survived
+// k_compact (insertion order kept) and relabel them; every tree's record count
+// is recounted.  A deferred record (pomcp_device.h: an arrival at a child
+// beyond the depth / step limits, never looked up by k_search) whose action
+// node survived gets its child here: the child's observation key and
+// absorbing flag follow from the record's state (Env::obs_key, Env::done_of);
+// it is found among the action node's inline slots or inserted there
+// (compare-and-swap: the threads insert concurrently), else in the overflow
+// map (the pass's such records one at a time, by wave 0), and its absorbing
+// flag is that of its LAST arrival (mcts.py:370; records in log order).  Which
+// slot a child takes is a label (ActionNode.children is only ever looked up by
+// observation in the reference), so results are unchanged.  A pass reads
+// 64 kLogWaves consecutive records, one per thread; all of them are loaded
+// before any is stored, and a kept record goes to a place at or before its
+// own, so the log is filtered in place.
 template <class Env>
-__global__ __launch_bounds__(256) void k_compact_log(DevParams p) {
+__global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
   __shared__ typename Env::Model sm;
   stage_model(p.model, sm);
-  const int sw = blockIdx.x * kTreesPerBlock + (threadIdx.x >> 6);
-  const int wi = threadIdx.x >> 6;
+  constexpr int T = 64 * kLogWaves;
+  const int sw = blockIdx.x;
+  const int w = (int)(threadIdx.x >> 6);
   const int lane = lane_id();
-  if (sw >= (p.B + kWave - 1) / kWave) return;
-  __shared__ int32_t kept[kTreesPerBlock][kWave];
-  __shared__ int32_t act[kTreesPerBlock][kWave];
-  __shared__ int32_t made[kTreesPerBlock][kWave];   // children materialised per tree
-  __shared__ int32_t bad[kTreesPerBlock][kWave];    // overflow map full
-  const int mytree = sw * kWave + lane;
-  kept[wi][lane] = 0;
-  made[wi][lane] = 0;
-  bad[wi][lane] = 0;
-  act[wi][lane] = mytree < p.B ? p.cnt[mytree] : 0;
-  __builtin_amdgcn_wave_barrier();
+  const int t = (int)threadIdx.x;
+  __shared__ int32_t kept[kWave];
+  __shared__ int32_t act[kWave];
+  __shared__ int32_t made[kWave];   // children materialised per tree
+  __shared__ int32_t bad[kWave];    // overflow map full
+  __shared__ int32_t wsum[kLogWaves];
+  __shared__ int32_t ovq[T];        // threads whose child goes to the overflow map, in order
+  __shared__ int32_t ovres[T];      // per thread: its overflow entry (-1: map full)
+  __shared__ uint32_t ovd[5][T];    // per thread: tree lane, action node, key lo / hi, done
+  __shared__ uint64_t fpl[T];       // the pass's children (flag word addresses), thread order
+  if (w == 0) {
+    const int mytree = sw * kWave + lane;
+    kept[lane] = 0;
+    made[lane] = 0;
+    bad[lane] = 0;
+    act[lane] = mytree < p.B ? p.cnt[mytree] : 0;
+  }
+  __syncthreads();
+  // a thread's place among the workgroup's threads with f set (thread order);
+  // every thread calls it
+  auto wg_rank = [&](bool f, int* total) -> int {
+    const uint64_t m = __ballot(f);
+    if (lane == 0) wsum[w] = __popcll(m);
+    __syncthreads();
+    int pre = 0, tot = 0;
+#pragma unroll
+    for (int v = 0; v < kLogWaves; ++v) {
+      pre += v < w ? wsum[v] : 0;
+      tot += wsum[v];
+    }
+    __syncthreads();
+    *total = tot;
+    return pre + __popcll(m & ((1ull << lane) - 1ull));
+  };
   const WaveLog wl(p.plog, p.Np, sw, p.tm);
   const uint32_t n = p.wlog[sw];
   const uint32_t A = (uint32_t)p.A;
   const int64_t bstride = blk_stride_lines(p.lines);
   uint32_t out = 0;
-  for (uint32_t base = 0; base < n; base += kWave) {
-    const uint32_t i = base + (uint32_t)lane;
+  for (uint32_t base = 0; base < n; base += T) {
+    const uint32_t i = base + (uint32_t)t;
     LogRec r = {0u, 0u, 0u};
     uint32_t aux = 0u;
     bool keep = false, mat = false;
@@ -845,14 +898,14 @@ __global__ __launch_bounds__(256) void k_compact_log(DevParams p) {
     int done = 0;
     int32_t nid = -1;
     int32_t* vis = nullptr;   // the node's visits (zeroed by k_compact): + 1 per record
+    const int tree = sw * kWave + (int)((i < n ? wl.id[i] : 0u) >> kIdBits);
     if (i < n) {
       r = wl.load(i);
       if (p.tm) aux = wl.aux[i];
       l = r.id >> kIdBits;
       const uint32_t id = r.id & kIdMask;
-      const int tree = sw * kWave + (int)l;
       keep = true;
-      if (act[wi][l]) {
+      if (act[l]) {
         if (id >= p.cut_base) {   // deferred record: its child is materialised below
           const uint32_t ani = id - p.cut_base;
           const int nb = ld_agent(p.cmap + (int64_t)tree * p.Nb + (int)(ani / A));
@@ -879,10 +932,9 @@ __global__ __launch_bounds__(256) void k_compact_log(DevParams p) {
       }
     }
     // ---- deferred records: find or insert the child
-    uint32_t* flagw = nullptr;   // the word holding the child's absorbing flag ...
-    uint32_t fbit = 0u;          // ... and its bit
-    if (__ballot(mat) != 0ull) {
-      const int tree = sw * kWave + (int)l;
+    if (__syncthreads_or(mat ? 1 : 0)) {
+      uint32_t* flagw = nullptr;   // the word holding the child's absorbing flag ...
+      uint32_t fbit = 0u;          // ... and its bit
       bool need_ovf = false;
       if (mat) {   // inline slots, filled in order; concurrent inserts by CAS on the key
         uint4* const sl0 = reinterpret_cast<uint4*>(p.an + tree_base_lines(tree, p.Nb, p.lines) +
@@ -907,10 +959,10 @@ __global__ __launch_bounds__(256) void k_compact_log(DevParams p) {
           if (old == exp) {   // inserted: a leaf child (no block), visits counted below
             __hip_atomic_store(reinterpret_cast<int32_t*>(sl0 + q) + 2, -1, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
-            atomicAdd(&made[wi][l], 1);
+            atomicAdd(&made[l], 1);
             ks = q;
           } else if ((old & kValidBit) != 0ull && (old & kObsMask) == okey) {
-            ks = q;   // another lane of this chunk inserted it
+            ks = q;   // another thread of this pass inserted it
           }
         }
         if (ks >= 0) {
@@ -922,95 +974,118 @@ __global__ __launch_bounds__(256) void k_compact_log(DevParams p) {
           need_ovf = true;
         }
       }
-      // overflow map: one record at a time, the wave probing a bucket's 16 entries
-      uint64_t om = __ballot(need_ovf);
-      while (om != 0ull) {
-        const int j = __ffsll((long long)om) - 1;
-        om &= om - 1ull;
-        const int jt = sw * kWave + rl((int)l, j);
-        const uint32_t jani = rlu(nani, j);
-        const uint64_t jkey = ((uint64_t)rlu((uint32_t)(okey >> 32), j) << 32) | rlu((uint32_t)okey, j);
-        const uint32_t jdone = rlu((uint32_t)done, j);
-        OvfSlot* const ovf = p.ovf + (int64_t)jt * p.H;
-        const uint32_t epoch = (uint32_t)p.hdr[jt].epoch;   // k_compact's new generation
-        const uint64_t key = jkey | ((uint64_t)epoch << kEpochShift);
-        uint32_t b = ovf_hash(jani, jkey) & p.bucket_mask;
-        int32_t jid = -1;
-        for (uint32_t probe = 0; probe <= p.bucket_mask && jid < 0; ++probe) {
-          OvfSlot* const e = ovf + (int64_t)b * kBucket + (lane & (kBucket - 1));
-          uint64_t sk = 0ull;
-          uint32_t san = 0u;
-          if (lane < kBucket) {
-            sk = ld_agent_u64(&e->key);
-            san = ld_agent_u32(&e->an);
-          }
-          const bool live = lane < kBucket && (uint32_t)(sk >> kEpochShift) == epoch;
-          const uint64_t mm = __ballot(live && sk == key && san == jani);
-          const uint64_t em = __ballot(lane < kBucket && !live);
-          if (mm != 0ull || em != 0ull) {
-            const int L = __ffsll((long long)(mm != 0ull ? mm : em)) - 1;
-            if (mm == 0ull && lane == L) {   // insert a leaf child
-              reinterpret_cast<uint4*>(e)[0] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), jani, jdone);
-              reinterpret_cast<uint4*>(e)[1] = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
-              atomicAdd(&made[wi][jt & (kWave - 1)], 1);
+      // overflow map: the pass's such records in thread (= log) order, one at a
+      // time, by wave 0 (its 16 lanes probe a bucket)
+      int novf = 0;
+      const int opos = wg_rank(need_ovf, &novf);
+      if (need_ovf) {
+        ovq[opos] = t;
+        ovd[0][t] = l;
+        ovd[1][t] = nani;
+        ovd[2][t] = (uint32_t)okey;
+        ovd[3][t] = (uint32_t)(okey >> 32);
+        ovd[4][t] = (uint32_t)done;
+      }
+      __syncthreads();
+      if (novf > 0) {
+        if (w == 0) {
+          for (int x = 0; x < novf; ++x) {
+            const int jt = ovq[x];
+            const int jl = (int)ovd[0][jt];
+            const int jtree = sw * kWave + jl;
+            const uint32_t jani = ovd[1][jt];
+            const uint64_t jkey = ((uint64_t)ovd[3][jt] << 32) | ovd[2][jt];
+            const uint32_t jdone = ovd[4][jt];
+            OvfSlot* const ovf = p.ovf + (int64_t)jtree * p.H;
+            const uint32_t epoch = (uint32_t)p.hdr[jtree].epoch;   // k_compact's generation
+            const uint64_t key = jkey | ((uint64_t)epoch << kEpochShift);
+            uint32_t b = ovf_hash(jani, jkey) & p.bucket_mask;
+            int32_t jid = -1;
+            for (uint32_t probe = 0; probe <= p.bucket_mask && jid < 0; ++probe) {
+              OvfSlot* const e = ovf + (int64_t)b * kBucket + (lane & (kBucket - 1));
+              uint64_t sk = 0ull;
+              uint32_t san = 0u;
+              if (lane < kBucket) {
+                sk = ld_agent_u64(&e->key);
+                san = ld_agent_u32(&e->an);
+              }
+              const bool live = lane < kBucket && (uint32_t)(sk >> kEpochShift) == epoch;
+              const uint64_t mm = __ballot(live && sk == key && san == jani);
+              const uint64_t em = __ballot(lane < kBucket && !live);
+              if (mm != 0ull || em != 0ull) {
+                const int L = __ffsll((long long)(mm != 0ull ? mm : em)) - 1;
+                if (mm == 0ull && lane == L) {   // insert a leaf child
+                  reinterpret_cast<uint4*>(e)[0] =
+                      make_uint4((uint32_t)key, (uint32_t)(key >> 32), jani, jdone);
+                  reinterpret_cast<uint4*>(e)[1] = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
+                  atomicAdd(&made[jl], 1);
+                }
+                __threadfence();
+                jid = (int32_t)(b * kBucket + (uint32_t)L);
+              }
+              b = (b + 1) & p.bucket_mask;
             }
-            __threadfence();
-            jid = (int32_t)(b * kBucket + (uint32_t)L);
+            if (lane == 0) ovres[jt] = jid;
           }
-          b = (b + 1) & p.bucket_mask;
         }
-        if (lane == j) {
+        __syncthreads();
+        if (need_ovf) {
+          const int32_t jid = ovres[t];
           if (jid >= 0) {
+            OvfSlot* const ovf = p.ovf + (int64_t)tree * p.H;
             nid = (int32_t)(p.ovf_base + (uint32_t)jid);
             vis = &ovf[jid].visits;
             flagw = &ovf[jid].flags;
             fbit = 1u;
           } else {   // the overflow map is full
             keep = false;
-            bad[wi][l] = 1;
+            bad[l] = 1;
           }
         }
       }
-      // the absorbing flag of each child = that of its last arrival in this
-      // chunk (earlier chunks were applied before, in log order)
-      bool last = flagw != nullptr;
+      // the absorbing flag of each child = that of its last arrival: the pass's
+      // children in thread order; the last thread naming a child sets it
+      int nf = 0;
       const uint64_t fp = reinterpret_cast<uint64_t>(flagw);
-      uint64_t fm = __ballot(last);
-      while (fm != 0ull) {
-        const int j = __ffsll((long long)fm) - 1;
-        fm &= fm - 1ull;
-        const uint64_t pj = ((uint64_t)rlu((uint32_t)(fp >> 32), j) << 32) | rlu((uint32_t)fp, j);
-        if (last && lane < j && fp == pj) last = false;
+      const int fpos = wg_rank(flagw != nullptr, &nf);
+      if (flagw != nullptr) fpl[fpos] = fp;
+      __syncthreads();
+      if (flagw != nullptr) {
+        bool last = true;
+        for (int x = fpos + 1; x < nf; ++x) last &= fpl[x] != fp;
+        if (last) {
+          if (done) atomicOr(flagw, fbit);
+          else atomicAnd(flagw, ~fbit);
+        }
       }
-      if (last) {
-        if (done) atomicOr(flagw, fbit);
-        else atomicAnd(flagw, ~fbit);
-      }
+      __threadfence();   // the pass's inserts and flags land before the next pass's
     }
-    if (act[wi][l] && i < n) {
+    if (act[l] && i < n) {
       if (vis != nullptr) atomicAdd(vis, 1);
       if (keep) r.id = (uint32_t)nid | (l << kIdBits);
     }
-    if (keep) atomicAdd(&kept[wi][l], 1);
-    const uint64_t mk = __ballot(keep);
-    __builtin_amdgcn_s_waitcnt(0);   // the whole chunk is loaded before any store
+    if (keep) atomicAdd(&kept[l], 1);
+    int nk = 0;
+    const int at = wg_rank(keep, &nk);   // (every thread has loaded its record)
     if (keep) {
-      const uint32_t at = out + (uint32_t)__popcll(mk & ((1ull << lane) - 1ull));
-      wl.store(at, r);
-      if (p.tm) wl.aux[at] = aux;
+      wl.store(out + (uint32_t)at, r);
+      if (p.tm) wl.aux[out + (uint32_t)at] = aux;
     }
-    out += (uint32_t)__popcll(mk);
+    out += (uint32_t)nk;
   }
-  __builtin_amdgcn_wave_barrier();
-  if (mytree < p.B) {
-    p.hdr[mytree].n_log = kept[wi][lane];
-    if (made[wi][lane] != 0) p.hdr[mytree].n_nodes += made[wi][lane];
-    if (bad[wi][lane] != 0) {
-      p.hdr[mytree].error = POMCP_E_ARENA;
-      p.upd_out[2 * mytree + 1] = POMCP_E_ARENA;
+  __syncthreads();
+  if (w == 0) {
+    const int mytree = sw * kWave + lane;
+    if (mytree < p.B) {
+      p.hdr[mytree].n_log = kept[lane];
+      if (made[lane] != 0) p.hdr[mytree].n_nodes += made[lane];
+      if (bad[lane] != 0) {
+        p.hdr[mytree].error = POMCP_E_ARENA;
+        p.upd_out[2 * mytree + 1] = POMCP_E_ARENA;
+      }
     }
+    if (lane == 0) p.wlog[sw] = out;
   }
-  if (lane == 0) p.wlog[sw] = out;
 }
 
 // Synthetic roots: env b0 sample for tree b under key (env_seed_base + b,
@@ -1189,6 +1264,13 @@ __global__ __launch_bounds__(64) void k_merge_roots(const double* src, int B, in
 __global__ void k_exp_selftest(const double* x, int n, double* out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = host_exp(x[i]);   // the I-NTMCP softmax's exp (host_exp.h)
+}
+
+__global__ void k_fast_recip(const double* x, int n, double* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[2 * i + 0] = rcp_nr(x[i]);
+  out[2 * i + 1] = rsq_nr(x[i]);
 }
 
 __global__ void k_fp_selftest(const double* a, const double* b, int n, double* out) {

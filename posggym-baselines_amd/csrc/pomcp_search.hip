@@ -297,19 +297,68 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
       const bool nz = mm_max > mm_min;   // utils.py:34-39
       const double range = mm_max - mm_min;
       double sc[A];
+      bool exact = true;   // sc[] holds the reference's scores (else a is decided)
       if (SEL == POMCP_SEL_UCB) {          // mcts.py:529-546
         if (nv >= p.logtab_n) err = POMCP_E_ARENA;
-#pragma unroll
-        for (int q = 0; q < A; ++q) {
-          const double v = hilo_d(st[q].z, st[q].w);
 #ifdef POMCP_ABLATE_SELECT   // ablation build only (tools/ablate.sh): no FP64 div / sqrt, breaks parity
-          sc[q] = v + p.c * log_n * (double)(int)st[q].x;
+#pragma unroll
+        for (int q = 0; q < A; ++q)
+          sc[q] = hilo_d(st[q].z, st[q].w) + p.c * log_n * (double)(int)st[q].x;
 #else
-          const double nvq = nz ? (v - mm_min) / range : v;
-          const int n = (int)st[q].x > 0 ? (int)st[q].x : 1;
-          sc[q] = nvq + p.c * sqrt(log_n / (double)n);
-#endif
+        // Fast scores: (v - min) * rcp(range) + c sqrt(log N) rsq(n), each
+        // within a few ulp of the reference's (v - min) / range + c
+        // sqrt(log N / n) (rcp_nr / rsq_nr: |fast - exact| < 4e-15 (|q| + e)).
+        // When the leader beats every action with different statistics by
+        // more than 1e-12 of their magnitudes, the reference's strict '>'
+        // scan picks the same action; otherwise (~6e-4 of selections, mostly
+        // exact ties of different statistics) the exact scores decide.
+        // Actions with equal statistics have equal scores either way (the
+        // first of them wins in both).
+        {
+          const double rr = nz ? rcp_nr(range) : 1.0;
+          const double csl = p.c * sqrt(log_n);
+          double sf[A], mg[A];
+#pragma unroll
+          for (int q = 0; q < A; ++q) {
+            const double v = hilo_d(st[q].z, st[q].w);
+            const int n = (int)st[q].x > 0 ? (int)st[q].x : 1;
+            const double qf = nz ? (v - mm_min) * rr : v;
+            const double ef = csl * rsq_nr((double)n);
+            sf[q] = qf + ef;
+            mg[q] = __builtin_fabs(qf) + ef;
+          }
+          int af = 0;
+          double bf = sf[0], bm = mg[0];
+          uint4 sb = st[0];
+#pragma unroll
+          for (int q = 1; q < A; ++q) {
+            if (sf[q] > bf) {
+              bf = sf[q];
+              bm = mg[q];
+              af = q;
+            }
+          }
+#pragma unroll
+          for (int q = 1; q < A; ++q) sb = sel4(q == af, st[q], sb);
+          bool amb = false;
+#pragma unroll
+          for (int q = 0; q < A; ++q) {
+            const bool same = st[q].x == sb.x && st[q].z == sb.z && st[q].w == sb.w;
+            amb |= q != af && !same && !(bf - sf[q] > 1e-12 * (mg[q] + bm));
+          }
+          a = af;
+          exact = amb;
         }
+        if (exact) {
+#pragma unroll
+          for (int q = 0; q < A; ++q) {
+            const double v = hilo_d(st[q].z, st[q].w);
+            const double nvq = nz ? (v - mm_min) / range : v;
+            const int n = (int)st[q].x > 0 ? (int)st[q].x : 1;
+            sc[q] = nvq + p.c * sqrt(log_n / (double)n);
+          }
+        }
+#endif
       } else {                             // PUCB, mcts.py:502-527
         const double noise = 1.0 / (double)A;
         const double sqrt_n = sqrt((double)nv);
@@ -322,12 +371,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
           sc[q] = (n > 0 ? nvq : 0.0) + p.c * prior * (sqrt_n / (double)(1 + n));
         }
       }
-      double best = sc[0];
+      if (exact) {
+        a = 0;
+        double best = sc[0];
 #pragma unroll
-      for (int q = 1; q < A; ++q) {
-        if (sc[q] > best) {
-          best = sc[q];
-          a = q;
+        for (int q = 1; q < A; ++q) {
+          if (sc[q] > best) {
+            best = sc[q];
+            a = q;
+          }
         }
       }
       if (SEL == POMCP_SEL_UCB) {   // mcts.py:539-540: the first unvisited child wins

@@ -307,11 +307,15 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
       const int j = uni(__hip_atomic_fetch_add(&sp_ctl[SP_NEXT], lane == 0 ? 1 : 0, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_WORKGROUP));
       if (j >= num_sims) break;
-      // slot j % kSpecSlots is free once the search wave is done with simulation j - kSpecSlots
+      // slot j % kSpecSlots is free once the search wave is done with simulation
+      // j - kSpecSlots.  The search wave releases SP_STOP when it ends (or stops
+      // waiting for the producers, below), so this wait always ends; the large
+      // bound is a last resort only (a producer that leaves early makes the
+      // search wave fall back to computing its simulations, never an error)
       bool stop = false;
       int spins = 0;
       while (lds_acquire(&sp_ctl[SP_CONSUMED]) < j - kSpecSlots + 1) {
-        if (lds_acquire(&sp_ctl[SP_STOP]) != 0 || ++spins > kSpinMax) {
+        if (lds_acquire(&sp_ctl[SP_STOP]) != 0 || ++spins > 16 * kSpinMax) {
 #ifdef POMCP_SPIN_DEBUG
           if (spins > kSpinMax && lane == 0)
             printf("producer %d: j %d consumed %d stop %d\n", wv, j, sp_ctl[SP_CONSUMED], sp_ctl[SP_STOP]);
@@ -501,6 +505,10 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
     rb_n = 0;
   };
   int sims = 0, max_depth = 0;
+  // polls of a late hand-off before the search wave stops the producers (tests
+  // shrink it: pomcp_debug_set_spin_limit)
+  const int spin_max = p.spin_max > 0 ? p.spin_max : kSpinMax;
+  bool sp_off = false;   // the producers were stopped (a late hand-off): compute every step
   for (int it = 0; it < num_sims && run; ++it) {
     // ------------------------------------------------ start (mcts.py:286-287)
     uint4 pr = pf;                                         // belief.py:55
@@ -513,29 +521,35 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
     // counters are this simulation's
     bool spv = false;
     int sp_base = 0, pidx = 0;
-    if (NP > 0) {
+    if (NP > 0 && !sp_off) {
       const int slot = it % kSpecSlots;
       int spins = 0;
       while (lds_acquire(&sp_hdr[8 * slot]) != it + 1) {
-        if (++spins > kSpinMax) {   // bounded: a broken hand-off fails the search, never hangs
+        if (++spins > spin_max) {
+          // the hand-off is late (a slow producer): stop the producers and run
+          // the rest of the launch without them -- a slower search, the same
+          // results (no slot is read after this)
 #ifdef POMCP_SPIN_DEBUG
           if (lane == 0)
             printf("search wave: sim %d slot %d seq %d next %d consumed %d\n", it, slot,
                    sp_hdr[8 * slot], sp_ctl[SP_NEXT], sp_ctl[SP_CONSUMED]);
 #endif
-          err = POMCP_E_HIP;
-          run = false;
+          if (lane == 0) lds_release(&sp_ctl[SP_STOP], 1);
+          sp_off = true;
           break;
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      if (!run) break;
-      const uint32_t oc = p.other == 0 ? s0s.ctr : s1s.ctr;
-      spv = uniu((uint32_t)sp_hdr[8 * slot + 1]) == sd.ctr && uniu((uint32_t)sp_hdr[8 * slot + 2]) == oc;
-      sp_base = slot * NE;
-      pr = make_uint4((uint32_t)sp_hdr[8 * slot + 4], (uint32_t)sp_hdr[8 * slot + 5],
-                      (uint32_t)sp_hdr[8 * slot + 6], 0u);   // the producer's draw of it
+      if (!sp_off) {
+        const uint32_t oc = p.other == 0 ? s0s.ctr : s1s.ctr;
+        spv = uniu((uint32_t)sp_hdr[8 * slot + 1]) == sd.ctr && uniu((uint32_t)sp_hdr[8 * slot + 2]) == oc;
+        sp_base = slot * NE;
+        pr = make_uint4((uint32_t)sp_hdr[8 * slot + 4], (uint32_t)sp_hdr[8 * slot + 5],
+                        (uint32_t)sp_hdr[8 * slot + 6], 0u);   // the producer's draw of it
+      }
     }
+    if (NP > 0 && sp_off)   // the particle the producer would have drawn (belief.py:55)
+      pr = particle(uniform_int(philox_word(seed, tkey, S_BELIEF, bctr0 + (uint32_t)it), (uint32_t)bsize));
     int t = (int)pr.x;
     uint32_t s0 = pr.y, s1 = pr.z;
     int blk = root_blk, nv = root_visits;
@@ -873,10 +887,10 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
     ++root_visits;                                          // mcts.py:288
     max_depth = depth > max_depth ? depth : max_depth;
     ++sims;
-    if (NP > 0) {
-      if (lane == 0) lds_release(&sp_ctl[SP_CONSUMED], it + 1);   // the slot is free
+    if (NP > 0 && !sp_off) {
       // the next simulation's counters off the prediction (this one terminated
-      // early): re-base the producers
+      // early): re-base the producers -- before the slot is released, so the
+      // producer it frees builds its slot from the new prediction
       const uint32_t oc = p.other == 0 ? s0s.ctr : s1s.ctr;
       if (sd.ctr != (uint32_t)(syn_m + (it + 1 - syn_k) * dm) ||
           oc != (uint32_t)(syn_o + (it + 1 - syn_k) * d1)) {
@@ -889,6 +903,7 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
           lds_release(&sp_ctl[SP_SYNC_K], syn_k);
         }
       }
+      if (lane == 0) lds_release(&sp_ctl[SP_CONSUMED], it + 1);   // the slot is free
     }
     PT_MARK(9);
     __builtin_amdgcn_wave_barrier();

@@ -228,10 +228,12 @@ SIGNATURES = [
 DEBUG_SIGNATURES = [
     ("pomcp_debug_fp_selftest", C.c_int, [_PD, _PD, C.c_int32, _PD]),
     ("pomcp_debug_exp", C.c_int, [_PD, C.c_int32, _PD]),
+    ("pomcp_debug_fast_recip", C.c_int, [_PD, C.c_int32, _PD]),
     ("pomcp_debug_host_exp", C.c_int, [_PD, C.c_int32, _PD]),
     ("pomcp_debug_phase_timing", C.c_int,
      [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32, C.POINTER(C.c_int32)]),
     ("pomcp_debug_set_inline_slots", C.c_int, [C.c_void_p, C.c_int32]),
+    ("pomcp_debug_set_spin_limit", C.c_int, [C.c_void_p, C.c_int32]),
     ("intmcp_debug_set_softmax_slack", C.c_int, [C.c_void_p, C.c_float]),
     ("intmcp_debug_exact_draws", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
 ]

@@ -50,6 +50,29 @@ def test_device_fp64_is_correctly_rounded():
     assert np.array_equal(out[:, 3], (a - b) / (a + b))
 
 
+def test_fast_ucb_reciprocals_error_bound():
+    """k_search's fast UCB scores use rcp_nr(range) and rsq_nr(n) (hardware
+    estimates + two Newton steps); their exact fallback assumes each within a
+    few ulp.  Checked here against correctly rounded 1/x and
+    1/sqrt(x) on every visit count up to 2^20 and on random positive doubles:
+    at most 4 ulp (the fallback assumes < 16)."""
+    import ctypes as C
+    from posggym_baselines_amd import _native as N
+    rng = np.random.default_rng(1)
+    x = np.concatenate([np.arange(1, 1 << 20, dtype=np.float64),
+                        np.exp(rng.uniform(-30, 30, 1 << 18)), rng.uniform(1e-3, 4.0, 1 << 18)])
+    out = np.zeros(2 * len(x))
+    P = C.POINTER(C.c_double)
+    assert N.load().pomcp_debug_fast_recip(x.ctypes.data_as(P), len(x), out.ctypes.data_as(P)) == 0
+    out = out.reshape(-1, 2)
+
+    def ulps(got, exact):
+        return np.abs(got - exact) / np.spacing(np.abs(exact))
+
+    assert ulps(out[:, 0], 1.0 / x).max() <= 4.0
+    assert ulps(out[:, 1], 1.0 / np.sqrt(x)).max() <= 4.0
+
+
 @pytest.mark.parametrize("case", EPISODE_CASES)
 def test_gpu_matches_reference_goldens(case):
     data = load(case)
@@ -502,3 +525,25 @@ def test_deep_tree_beyond_the_lds_pool():
     for b in range(len(seeds)):
         assert got[b] == exp[b], f"tree {b} (env seed {seeds[b]})"
     assert max(u[0] for k, u in usage) > 300   # blocks in use: beyond the LDS pool
+
+
+def test_late_step_tree_handoff_falls_back():
+    """k_search_lds with its step-tree producers (wave_tree): when a hand-off is
+    late the search wave stops the producers and computes the rest of the
+    launch itself -- never an error.  With the wait bounded at one poll, most
+    searches fall back at once; 12 planners over 3 real steps stay bit-exact
+    against the oracle."""
+    from gpu_util import batched_episodes
+    from oracle.run import oracle_episode
+    S, K = 256, 3
+    seeds, exp = [], []
+    s = 700
+    while len(seeds) < 12:
+        trace, recs = oracle_episode(TEST_CFG, S, s, tree=len(seeds), max_steps=K)
+        if trace["len"] >= K and all(r["searched"] and r["num_sims"] > 0 for r in recs):
+            seeds.append(s)
+            exp.append(recs)
+        s += 1
+    got = batched_episodes(TEST_CFG, S, seeds, K, spin_limit=1)
+    for b in range(len(seeds)):
+        assert got[b] == exp[b], f"tree {b} (env seed {seeds[b]})"

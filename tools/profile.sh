@@ -5,7 +5,9 @@
 set -e
 TAG=${1:-r1}
 shift || true
-ARGS="$@"
+# --no-sub: only the named configuration's launches (the default bench run appends
+# secondary-configuration records whose kernels would mix into the trace)
+ARGS="--no-sub $@"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
