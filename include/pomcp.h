@@ -362,6 +362,13 @@ int pomcp_pe_obs(const pomcp_pe_grid* g, const uint32_t state[2], uint64_t obs_k
 int pomcp_philox_words(uint64_t seed, uint32_t tree, uint32_t stream, uint32_t first, int32_t n,
                        uint32_t* out);
 
+/* ---- Host math.log table -------------------------------------------------
+ * out[k] = log(first + k) with the host C library's log (the function
+ * Python's math.log calls: mcts.py:534's log(N) bit for bit), 0.0 for 0; the
+ * planner's pomcp_config.log_table at C speed (wall-clock arenas ask for tens
+ * of millions of entries). */
+int pomcp_host_log_table(int64_t first, int64_t n, double* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cmath>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -960,6 +961,21 @@ int pomcp_philox_words(uint64_t seed, uint32_t tree, uint32_t stream, uint32_t f
                        uint32_t* out) {
   if (n < 0 || (n > 0 && !out)) return POMCP_E_INVALID;
   for (int32_t k = 0; k < n; ++k) out[k] = philox_word(seed, tree, stream, first + (uint32_t)k);
+  return POMCP_OK;
+}
+
+// ---------------------------------------------------------- host log(N) table
+
+// out[i] = log((double)i) for i in [first, first + n), out[0] of i = 0 is 0.0:
+// the host C library's log, the function Python's math.log calls for a float
+// (Modules/mathmodule.c), so the table is math.log's bit for bit at C speed
+// (tests/test_host_exp.py checks it against math.log).
+int pomcp_host_log_table(int64_t first, int64_t n, double* out) {
+  if (first < 0 || n < 0 || (n > 0 && !out)) return POMCP_E_INVALID;
+  for (int64_t k = 0; k < n; ++k) {
+    const int64_t i = first + k;
+    out[k] = i == 0 ? 0.0 : std::log((double)i);
+  }
   return POMCP_OK;
 }
 

@@ -224,6 +224,7 @@ SIGNATURES = [
     ("pomcp_pe_obs", C.c_int, [C.POINTER(PomcpPeGrid), _PU32, _PU64]),
     ("pomcp_philox_words", C.c_int, [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int32,
                                      _PU32]),
+    ("pomcp_host_log_table", C.c_int, [C.c_int64, C.c_int64, _PD]),
 ]
 DEBUG_SIGNATURES = [
     ("pomcp_debug_fp_selftest", C.c_int, [_PD, _PD, C.c_int32, _PD]),

@@ -87,7 +87,12 @@ def plan_wallclock_capacities(config, step_limit: int, num_trees: int = 1, num_a
     """Capacities of a wall-clock (num_sims=None) engine; returns (capacities,
     per-search simulation bound)."""
     levels = min(config.depth_limit, step_limit) + 1
-    per_sim = num_actions * 128 + 16 * min(levels, 64)   # block + particle records, worst case
+    # block + particle records, worst case; batches of up to 256 trees run on the
+    # wave-per-tree kernel, whose per-tree scratch log holds one more 12 B record
+    # per level (k_search_lds, allocated on its first search)
+    per_sim = num_actions * 128 + 16 * min(levels, 64)
+    if num_trees <= 256:
+        per_sim += 12 * min(levels, 64)
     sims = math.ceil(config.search_time_limit * WALL_CLOCK_SIMS_PER_S)
     sims = min(sims, WALL_CLOCK_HBM_BUDGET // (2 * per_sim * max(1, num_trees)))
     ovf = 1 << 16
@@ -108,11 +113,16 @@ _LOG_TABLE = np.zeros(1, dtype=np.float64)
 def log_table(n: int) -> np.ndarray:
     """[0.0, log(1), .., log(n-1)] with the host's math.log (the reference's
     UCB term, mcts.py:534), bit for bit; one cached table per process, grown on
-    demand (wall-clock arenas ask for tens of millions of entries)."""
+    demand (wall-clock arenas ask for tens of millions of entries).  Computed
+    by pomcp_host_log_table: the C library's log, which math.log calls for a
+    float (tests/test_host_exp.py pins the two equal)."""
     global _LOG_TABLE
     if len(_LOG_TABLE) < n:
         m = len(_LOG_TABLE)
-        ext = np.fromiter(map(math.log, range(m, n)), dtype=np.float64, count=n - m)
+        ext = np.empty(n - m, dtype=np.float64)
+        rc = N.load().pomcp_host_log_table(m, n - m, ext.ctypes.data_as(C.POINTER(C.c_double)))
+        if rc != N.POMCP_OK:
+            raise N.PomcpError(rc, "pomcp_host_log_table failed")
         _LOG_TABLE = np.concatenate([_LOG_TABLE, ext])
     return _LOG_TABLE[:n]
 

@@ -73,3 +73,24 @@ def test_exp_table_is_the_hosts():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_exp_table.py"),
                         "--check-only"], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_host_log_table_equals_math_log():
+    """The planner's log(N) table (engine.log_table, mcts.py:534's
+    math.log(N)) comes from pomcp_host_log_table, the C library's log: equal to
+    Python's math.log bit for bit on every N < 2^21, on a sample up to 2^31,
+    and across an offset start."""
+    from posggym_baselines_amd import _native as N
+    lib = N.load()
+    P = C.POINTER(C.c_double)
+    n = 1 << 21
+    out = np.zeros(n)
+    assert lib.pomcp_host_log_table(0, n, out.ctypes.data_as(P)) == 0
+    ref = np.array([0.0] + [math.log(i) for i in range(1, n)])
+    assert np.array_equal(out.view(np.uint64), ref.view(np.uint64))
+    rng = np.random.default_rng(3)
+    for first in rng.integers(1, 2**31 - 4096, 64):
+        seg = np.zeros(4096)
+        assert lib.pomcp_host_log_table(int(first), 4096, seg.ctypes.data_as(P)) == 0
+        exp = np.array([math.log(int(first) + k) for k in range(4096)])
+        assert np.array_equal(seg.view(np.uint64), exp.view(np.uint64))
