@@ -619,7 +619,7 @@ struct ImPair {
         if (i < nr && q[i].x == 0u) zero = i;
       if (zero >= 0) return im_order(x.info, zero);
       const double log_n = logn(x.visits);
-#ifndef IM_ABLATE_SELECT
+#if !defined(IM_ABLATE_SELECT) && !defined(POMCP_EXACT_SELECT)
       // Fast scores first, the exact ones only for near-ties of different
       // statistics: as k_search's select_action (pomcp_search.hip), in
       // registration order

@@ -348,6 +348,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
           }
           a = af;
           exact = amb;
+#ifdef POMCP_EXACT_SELECT   // measurement builds only (A/B): the exact scores always
+          exact = true;
+#endif
         }
         if (exact) {
 #pragma unroll
@@ -362,13 +365,58 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
       } else {                             // PUCB, mcts.py:502-527
         const double noise = 1.0 / (double)A;
         const double sqrt_n = sqrt((double)nv);
+        double cp[A];   // c * prior (exact: the same operations as the reference)
 #pragma unroll
-        for (int q = 0; q < A; ++q) {
-          const double prior = (TM != 0 ? ap[q] : 1.0 / (double)A) * (1.0 - p.pucb_f) + p.pucb_f * noise;
-          const int n = (int)st[q].x;
-          const double v = hilo_d(st[q].z, st[q].w);
-          const double nvq = nz ? (v - mm_min) / range : v;
-          sc[q] = (n > 0 ? nvq : 0.0) + p.c * prior * (sqrt_n / (double)(1 + n));
+        for (int q = 0; q < A; ++q)
+          cp[q] = p.c * ((TM != 0 ? ap[q] : 1.0 / (double)A) * (1.0 - p.pucb_f) + p.pucb_f * noise);
+#ifndef POMCP_EXACT_SELECT
+        {   // fast scores, the exact ones for near-ties (as UCB above); equal
+            // statistics here include the prior (type-based priors differ)
+          const double rr = nz ? rcp_nr(range) : 1.0;
+          double sf[A], mg[A];
+#pragma unroll
+          for (int q = 0; q < A; ++q) {
+            const int n = (int)st[q].x;
+            const double v = hilo_d(st[q].z, st[q].w);
+            const double qf = n > 0 ? (nz ? (v - mm_min) * rr : v) : 0.0;
+            const double ef = cp[q] * (sqrt_n * rcp_nr((double)(1 + n)));
+            sf[q] = qf + ef;
+            mg[q] = __builtin_fabs(qf) + __builtin_fabs(ef);
+          }
+          int af = 0;
+          double bf = sf[0], bm = mg[0], bp = cp[0];
+          uint4 sb = st[0];
+#pragma unroll
+          for (int q = 1; q < A; ++q) {
+            if (sf[q] > bf) {
+              bf = sf[q];
+              bm = mg[q];
+              af = q;
+            }
+          }
+#pragma unroll
+          for (int q = 1; q < A; ++q) {
+            sb = sel4(q == af, st[q], sb);
+            bp = q == af ? cp[q] : bp;
+          }
+          bool amb = false;
+#pragma unroll
+          for (int q = 0; q < A; ++q) {
+            const bool same = st[q].x == sb.x && st[q].z == sb.z && st[q].w == sb.w && cp[q] == bp;
+            amb |= q != af && !same && !(bf - sf[q] > 1e-12 * (mg[q] + bm));
+          }
+          a = af;
+          exact = amb;
+        }
+#endif
+        if (exact) {
+#pragma unroll
+          for (int q = 0; q < A; ++q) {
+            const int n = (int)st[q].x;
+            const double v = hilo_d(st[q].z, st[q].w);
+            const double nvq = nz ? (v - mm_min) / range : v;
+            sc[q] = (n > 0 ? nvq : 0.0) + cp[q] * (sqrt_n / (double)(1 + n));
+          }
         }
       }
       if (exact) {

@@ -5,17 +5,17 @@
 # update()-inclusive PursuitEvasion step
 set -o pipefail
 O=gpurun_out/r4d; mkdir -p $O
-POMCP_LIB_PATH=$PWD/variants/lib_upd.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_root_parallel.py tests/test_gpu_dist.py tests/test_gpu_intmcp.py -k "lane or fast_ucb or root or dist or intmcp or pairs or softmax" -x -q --timeout 300 --timeout-method thread > $O/test.log 2>&1 || { tail -30 $O/test.log; exit 1; }
+POMCP_LIB_PATH=$PWD/variants/lib_upd.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_potmmcp.py tests/test_gpu_mcts_policies.py -k "lane or potmmcp or base_planner" -x -q --timeout 300 --timeout-method thread > $O/test.log 2>&1 || { tail -30 $O/test.log; exit 1; }
 tail -2 $O/test.log
-for n in cur2 upd cur2 upd; do
+for n in exact upd exact upd; do
   echo "== $n" >> $O/exp.log
   POMCP_LIB_PATH=$PWD/variants/lib_$n.so timeout -k 10 300 python bench.py --no-cpu-baseline --no-sub --steps 3 --warmup 1 >> $O/exp.log 2>&1 || exit 1
 done
-for n in cur2 upd; do
+for n in upd; do
   echo "== pe_$n" >> $O/exp.log
   POMCP_LIB_PATH=$PWD/variants/lib_$n.so timeout -k 10 300 python bench.py --no-cpu-baseline --no-sub --steps 2 --warmup 1 --env PursuitEvasion-v1 --update-step --trees 16384 >> $O/exp.log 2>&1 || exit 1
 done
-for n in cur2 upd cur2 upd; do
+for n in exact upd exact upd; do
   echo "== im_$n" >> $O/exp.log
   POMCP_LIB_PATH=$PWD/variants/lib_$n.so timeout -k 10 300 python bench.py --no-cpu-baseline --planner intmcp --steps 3 --warmup 1 >> $O/exp.log 2>&1 || exit 1
 done
