@@ -387,15 +387,27 @@ class _Planner:
 
 
 class OracleINTMCP:
-    """``INTMCP.initialize(model, ego, config, 1, None)`` with fixed simulation
-    counts per level.  ``step(obs)`` follows ``intmcp.py:115-140``."""
+    """``INTMCP.initialize(model, ego, config, nesting_level, None)`` with fixed
+    simulation counts per level, nesting level 1 (a level-1 planner over the
+    other agent's level-0 planner) or 0 (one level-0 planner: the other agent
+    acts by its own ``self._rng.choice``, intmcp.py:750-753).  ``step(obs)``
+    follows ``intmcp.py:115-140``.  The planners' ``random.Random(seed)`` are
+    streams in construction order (the lowest level first, intmcp.py:964-986):
+    S_BELIEF_NESTED, then S_BELIEF."""
 
-    def __init__(self, model, agent_id, cfg, streams: Streams):
+    def __init__(self, model, agent_id, cfg, streams: Streams, nesting_level: int = 1):
         assert cfg.num_sims is not None
+        if nesting_level not in (0, 1):
+            raise NotImplementedError("nesting levels 0 and 1")
         other = model.possible_agents[1 - model.possible_agents.index(agent_id)]
-        # construction order of INTMCP.initialize: the nested planner first
-        self.nested = _Planner(model, other, cfg, 0, streams, S_BELIEF_NESTED)
-        self.top = _Planner(model, agent_id, cfg, 1, streams, S_BELIEF, nested=self.nested)
+        if nesting_level == 0:
+            self.nested = None
+            self.top = _Planner(model, agent_id, cfg, 0, streams, S_BELIEF_NESTED)
+        else:
+            # construction order of INTMCP.initialize: the nested planner first
+            self.nested = _Planner(model, other, cfg, 0, streams, S_BELIEF_NESTED)
+            self.top = _Planner(model, agent_id, cfg, 1, streams, S_BELIEF, nested=self.nested)
+        self.nesting_level = nesting_level
         self.cfg = cfg
         self.model = model
         self.stats = {}
@@ -411,7 +423,8 @@ class OracleINTMCP:
         self.stats = {"searched": True}
         top.update(top.last_action, obs)
         top.search_depth = 0
-        self.nested.search_depth = 0
+        if self.nested is not None:
+            self.nested.search_depth = 0
         top.last_action = top.get_action(self.cfg.num_sims)
         return top.last_action
 

@@ -181,12 +181,14 @@ def reference_episode(cfg_kwargs, num_sims, env_seed, ego="0", grid=None,
 
 
 # ----------------------------------------------------------------- I-NTMCP
-def make_reference_intmcp(model, agent_id, cfg_kwargs, num_sims, streams):
-    """``INTMCP.initialize(model, agent_id, config, 1, None)`` wired to ``streams``
-    with ``num_sims`` simulations per nesting level (intmcp.py:385-399: the
-    wrapped top-level ``_nested_sim`` jumps the fake clock after num_sims calls).
-    ``random.Random(seed)`` is called once per planner, the nested planner first
-    (intmcp.py:964-986): first call -> S_BELIEF_NESTED, second -> S_BELIEF."""
+def make_reference_intmcp(model, agent_id, cfg_kwargs, num_sims, streams, nesting_level=1):
+    """``INTMCP.initialize(model, agent_id, config, nesting_level, None)`` wired
+    to ``streams`` with ``num_sims`` simulations per nesting level
+    (intmcp.py:385-399: the wrapped top-level ``_nested_sim`` jumps the fake
+    clock after num_sims calls).  ``random.Random(seed)`` is called once per
+    planner, the lowest level first (intmcp.py:964-986): first call ->
+    S_BELIEF_NESTED, second -> S_BELIEF (nesting level 0: the one planner's is
+    S_BELIEF_NESTED)."""
     P = import_reference()
     import posggym_baselines.planning.intmcp as im
     import posggym_baselines.planning.belief as B
@@ -216,8 +218,9 @@ def make_reference_intmcp(model, agent_id, cfg_kwargs, num_sims, streams):
     if kw.get("known_bounds") is not None:
         kw["known_bounds"] = KnownBounds(*kw["known_bounds"])
     config = P.MCTSConfig(**kw)
-    planner = P.INTMCP.initialize(model, agent_id, config, nesting_level=1, search_policies=None)
-    assert len(made) == 2
+    planner = P.INTMCP.initialize(model, agent_id, config, nesting_level=nesting_level,
+                                  search_policies=None)
+    assert len(made) == nesting_level + 1
     inner = planner._nested_sim
     count = [0]
 
@@ -258,10 +261,15 @@ def reference_intmcp_record(planner, searched, action):
         return rec
     root = _walk(planner.root, planner.history)
     other = [i for i in model.possible_agents if i != planner.agent_id][0]
+    kids = [(int(c.action), c.visits, c.value, c.total_value) for c in root.get_child_nodes()]
+    st = planner.step_statistics
+    if planner.nesting_level == 0:   # no other-agent histories (intmcp_record of the oracle)
+        parts = [(p.t, model.pack_words(p.state), ()) for p in root.belief.particles]
+        return intmcp_record(rec, int(st["num_sims"]), int(st["search_depth"]), root.visits, kids,
+                             st["min_value"], st["max_value"], parts, [])
     nested = planner.other_agent_policies[other]
     parts = [(p.t, model.pack_words(p.state), _hist_key(model, p.history.get_agent_history(other)))
              for p in root.belief.particles]
-    kids = [(int(c.action), c.visits, c.value, c.total_value) for c in root.get_child_nodes()]
     nested_nodes = []
     seen = []
     for p in root.belief.particles:
@@ -282,14 +290,14 @@ def reference_intmcp_record(planner, searched, action):
 
 
 def reference_intmcp_episode(cfg_kwargs, num_sims, env_seed, ego="0", tree=0, max_steps=50,
-                             env="Driving-v1"):
+                             env="Driving-v1", nesting_level=1):
     from oracle.envs import make_model
     from oracle.episode import run_episode
     from oracle.rng import Streams
 
     streams = Streams(cfg_kwargs.get("seed") or 0, tree)
     model = make_model(env, streams)
-    planner = make_reference_intmcp(model, ego, cfg_kwargs, num_sims, streams)
+    planner = make_reference_intmcp(model, ego, cfg_kwargs, num_sims, streams, nesting_level)
     planner.reset()
     records = []
 

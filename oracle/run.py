@@ -70,12 +70,12 @@ def oracle_first_step(cfg_kwargs, num_sims, tree, env_seed, rekey=None, env="Dri
 
 
 # ----------------------------------------------------------------- I-NTMCP
-def make_oracle_intmcp(cfg_kwargs, num_sims, ego="0", tree=0, env="Driving-v1"):
+def make_oracle_intmcp(cfg_kwargs, num_sims, ego="0", tree=0, env="Driving-v1", nesting_level=1):
     from oracle.intmcp import OracleINTMCP
     streams = Streams(cfg_kwargs.get("seed") or 0, tree)
     model = make_model(env, streams)
     cfg = OracleConfig(num_sims=num_sims, **cfg_kwargs)
-    return OracleINTMCP(model, ego, cfg, streams)
+    return OracleINTMCP(model, ego, cfg, streams, nesting_level)
 
 
 def oracle_intmcp_record(p, searched, action):
@@ -85,8 +85,12 @@ def oracle_intmcp_record(p, searched, action):
         return rec
     top, nested = p.top, p.nested
     tr, n = top.tree, top.cur
-    parts = [(q[2], p.model.pack_words(q[0]), p.history(nested.tree, q[1])) for q in tr.belief[n]]
     kids = [(a,) + tuple(tr.stats[(n, a)][:3]) for a in tr.order[n]]
+    if nested is None:   # nesting level 0: no other-agent histories
+        parts = [(q[1], p.model.pack_words(q[0]), ()) for q in tr.belief[n]]
+        return intmcp_record(rec, top.num_sims, top.search_depth, tr.visits[n], kids,
+                             top.mm_min, top.mm_max, parts, [])
+    parts = [(q[2], p.model.pack_words(q[0]), p.history(nested.tree, q[1])) for q in tr.belief[n]]
     nested_nodes, seen = [], []
     for q in tr.belief[n]:
         if q[1] in seen:
@@ -102,8 +106,9 @@ def oracle_intmcp_record(p, searched, action):
 
 
 def oracle_intmcp_episode(cfg_kwargs, num_sims, env_seed, ego="0", tree=0, max_steps=50,
-                          env="Driving-v1"):
-    p = make_oracle_intmcp(cfg_kwargs, num_sims, ego=ego, tree=tree, env=env)
+                          env="Driving-v1", nesting_level=1):
+    p = make_oracle_intmcp(cfg_kwargs, num_sims, ego=ego, tree=tree, env=env,
+                           nesting_level=nesting_level)
     p.reset()
     records = []
 

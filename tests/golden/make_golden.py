@@ -90,18 +90,38 @@ INTMCP_CASES = {
 }
 
 
+# I-NTMCP nesting_level=0 (intmcp.py:950-994 with no nested planner: the other
+# agent acts by the planner's own self._rng.choice, intmcp.py:750-753);
+# search_time_limit = 0.1 * (nesting_level + 1) as tests/planning/test_intmcp.py
+INTMCP0_CFG = dict(TEST_CFG, search_time_limit=0.1, state_belief_only=False)
+INTMCP0_CASES = {
+    "intmcp0_ucb": ({}, 64, [(40, 40), (41, 41)], "0", 50, "Driving-v1"),
+    "intmcp0_ego1_uniform": ({"action_selection": "uniform"}, 48, [(42, 42)], "1", 50,
+                             "Driving-v1"),
+    "intmcp0_deep": ({"discount": 0.99, "epsilon": 0.01}, 16, [(43, 43)], "0", 20, "Driving-v1"),
+    "intmcp0_pe": ({}, 48, [(44, 44)], "0", 100, "PursuitEvasion-v1"),
+}
+
+
 def run_intmcp_case(name):
-    over, num_sims, pairs, ego, max_steps, env = INTMCP_CASES[name]
+    if name in INTMCP0_CASES:
+        over, num_sims, pairs, ego, max_steps, env = INTMCP0_CASES[name]
+        base, level = INTMCP0_CFG, 0
+    else:
+        over, num_sims, pairs, ego, max_steps, env = INTMCP_CASES[name]
+        base, level = INTMCP_CFG, 1
     out = {"case": name, "env": env, "num_sims": num_sims, "ego": ego, "max_steps": max_steps,
            "episodes": []}
+    if level != 1:
+        out["nesting_level"] = level
     for seed, env_seed in pairs:
-        cfg = dict(INTMCP_CFG)
+        cfg = dict(base)
         cfg.update(over)
         cfg["seed"] = seed
         tr, rr = reference_intmcp_episode(cfg, num_sims, env_seed, ego=ego, max_steps=max_steps,
-                                          env=env)
+                                          env=env, nesting_level=level)
         to, ro = oracle_intmcp_episode(cfg, num_sims, env_seed, ego=ego, max_steps=max_steps,
-                                       env=env)
+                                       env=env, nesting_level=level)
         if tr != to or rr != ro:
             raise SystemExit(f"oracle disagrees with reference in case {name} seed {seed}")
         out["episodes"].append({"config": dict(cfg), "env_seed": env_seed, "trace": tr,
@@ -362,7 +382,8 @@ def main(only=None, out_dir=HERE):
         _write(out_dir, name, data)
         n = sum(len(e["records"]) for e in data["episodes"])
         print(f"{name}: {len(data['episodes'])} episodes, {n} records")
-    for name in INTMCP_CASES if only is None else (only if isinstance(only, list) else ()):
+    for name in (list(INTMCP_CASES) + list(INTMCP0_CASES) if only is None
+                 else (only if isinstance(only, list) else ())):
         data = run_intmcp_case(name)
         _write(out_dir, name, data)
         n = sum(len(e["records"]) for e in data["episodes"])

@@ -34,3 +34,7 @@ def cfg_kwargs(cfg):
 IPOMCP_CASES = ["ipomcp_ucb", "ipomcp_pucb_ego1"]
 
 INTMCP_CASES = ["intmcp_ucb", "intmcp_ego1", "intmcp_uniform", "intmcp_deep", "intmcp_pe"]
+
+# I-NTMCP nesting_level=0 (tests/golden/make_golden.py INTMCP0_CASES): a single
+# level-0 tree whose other agent acts uniformly (intmcp.py:750-753)
+INTMCP0_CASES = ["intmcp0_ucb", "intmcp0_ego1_uniform", "intmcp0_deep", "intmcp0_pe"]

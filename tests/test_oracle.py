@@ -73,17 +73,20 @@ def test_oracle_matches_reference_goldens(case):
 
 
 @pytest.mark.parametrize("case", ["intmcp_ucb", "intmcp_ego1", "intmcp_uniform", "intmcp_deep",
-                                  "intmcp_pe"])
+                                  "intmcp_pe", "intmcp0_ucb", "intmcp0_ego1_uniform",
+                                  "intmcp0_deep", "intmcp0_pe"])
 def test_intmcp_oracle_matches_reference_goldens(case):
-    """I-NTMCP nesting 1 (BASELINE config 5): the oracle restatement against the
-    real reference planner's records (root children, beliefs with the other
-    agent's histories, the level-0 nodes of every history in the belief)."""
+    """I-NTMCP nesting 1 (BASELINE config 5) and nesting 0: the oracle
+    restatement against the real reference planner's records (root children,
+    beliefs with the other agent's histories, the level-0 nodes of every history
+    in the belief; at nesting 0 the single tree and its belief)."""
     from oracle.run import oracle_intmcp_episode
     data = load(case)
     for ep in data["episodes"]:
         trace, records = oracle_intmcp_episode(ep["config"], data["num_sims"], ep["env_seed"],
                                                ego=data["ego"], max_steps=data["max_steps"],
-                                               env=case_env(data))
+                                               env=case_env(data),
+                                               nesting_level=data.get("nesting_level", 1))
         assert trace == ep["trace"]
         for t, (got, exp) in enumerate(zip(records, ep["records"])):
             assert got == exp, f"{case} step {t}"
