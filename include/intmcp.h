@@ -5,7 +5,9 @@
  * INTMCP.initialize(model, ego, config, nesting_level=1, search_policies=None)
  * (intmcp.py:949-994): the ego's level-1 tree and the other agent's level-0
  * tree, random search policies.  One planner pair per "tree" index; many
- * pairs per call (a batched launch).  Paths relative to
+ * pairs per call (a batched launch).  nesting_level = 0: one level-0 planner
+ * per index (its tree is tree 1 of the diagnostics below; the other agent acts
+ * by the planner's own random choice, intmcp.py:750-753).  Paths relative to
  * posggym_baselines/planning/ in the reference.
  *
  * Same conventions as pomcp.h (plain pointers, POMCP_* status codes, a
@@ -25,7 +27,7 @@ extern "C" {
 typedef struct intmcp_config {
   pomcp_config base;              /* MCTSConfig + model + tables (num_trees = planner pairs) */
   int32_t state_belief_only;      /* MCTSConfig.state_belief_only (test config: 0) */
-  int32_t pad;
+  int32_t nesting_level;          /* 1 or 0 (INTMCP.initialize's nesting_level) */
   int64_t max_nodes;              /* obs nodes per tree */
   int64_t max_stats;              /* action-node statistics entries per tree (A per expanded node) */
   int64_t max_log;                /* particle log records per tree (16 B) */
@@ -68,13 +70,15 @@ int intmcp_update(intmcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_k
                   int32_t* root_absorbing_out);
 /* intmcp_update action of a pair to leave untouched (its episode has ended). */
 #define INTMCP_SKIP (-2)
-/* INTMCP.get_action (intmcp.py:368-408) with num_sims simulations per nesting level. */
+/* INTMCP.get_action (intmcp.py:368-408) with num_sims simulations per nesting level
+ * (nesting level 0: num_sims at level 0). */
 int intmcp_search(intmcp_ctx* ctx, int32_t num_sims_per_level, int32_t* actions_out);
 /* One chunk of get_action: level0_sims simulations at level 0 then
  * level1_sims at level 1.  flags: INTMCP_BEGIN resets the step's counters,
  * INTMCP_FINAL runs _final_action_selection (actions_out is then valid).  The
  * reference's wall-clock loop (per-level time budget) is a sequence of chunks;
- * intmcp_search(n) == intmcp_search_levels(n, n, BEGIN | FINAL). */
+ * intmcp_search(n) == intmcp_search_levels(n, n, BEGIN | FINAL) (nesting level 0:
+ * (n, 0); level1_sims > 0 is POMCP_E_INVALID there). */
 #define INTMCP_BEGIN 1
 #define INTMCP_FINAL 2
 int intmcp_search_levels(intmcp_ctx* ctx, int32_t level0_sims, int32_t level1_sims, int32_t flags,

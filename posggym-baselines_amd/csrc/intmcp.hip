@@ -1,5 +1,8 @@
 // I-NTMCP, nesting level 1, two agents: the ego's level-1 tree and the other
-// agent's level-0 tree, ONE planner pair per lane.
+// agent's level-0 tree, ONE planner pair per lane.  Nesting level 0
+// (ImParams::nest0): the planner's own level-0 tree alone, held as tree 1 --
+// the tree a level-1 pair keeps for its other agent -- with the planner as
+// that tree's agent (p.other) and one support entry, the root belief.
 //
 // Replaces posggym_baselines/planning/intmcp.py:198-517, 547-593, 634-862 as
 // built by INTMCP.initialize(model, ego, config, 1, None) (random search
@@ -127,7 +130,8 @@ struct IHdr {
 
 struct ImParams {
   int32_t B, A, ego, other, sel, depth_limit, step_limit, n_target, extra, has_kb,
-      state_belief_only, pad;
+      state_belief_only,
+      nest0;            // nesting level 0: only tree 1, whose agent (p.other) is the planner
   double discount, c, limit_factor, kb_min, kb_max;
   int64_t Nn, Ns, Nl, H, Nr, Nsp;   // per tree: nodes, stat entries, log records, hash slots;
                                     // per pair: root belief, support particles
@@ -590,6 +594,8 @@ struct ImPair {
   // ------------------------------------------------------------- selection
   // the agent of tree k: k = 0 the ego, k = 1 the other agent
   __device__ int agent(int k) const { return k == 0 ? p.ego : p.other; }
+  // the planner's own tree: 0 (nesting level 1), 1 (nesting level 0)
+  __device__ int top() const { return p.nest0 ? 1 : 0; }
 
   // {visits, -, value} of the registered children of node x, in registration
   // order, from the node's view
@@ -1345,6 +1351,68 @@ __device__ void ImPair<Env>::clear_old_beliefs(int cur_t) {
   }
 }
 
+// INTMCP.update (intmcp.py:198-300) of a nesting-level-0 planner (tree 1, the
+// planner p.other): its root belief is support entry 0 -- the support
+// {root: 1.0} the level-1 update hands a level-0 planner, so the same
+// materialisation and reinvigoration run (_initial_nested_update /
+// _nested_update with dist = {cur: 1.0}, intmcp.py:216-300)
+template <class Env, bool kWave>
+__device__ void im_update_nest0(ImPair<Env>& P, const typename Env::Model& sm, uint64_t obs,
+                                int action) {
+  const ImParams& p = P.p;
+  auto draw_model = [&](uint32_t n) { return P.d_model(n); };
+  const int sel = P.h.sup_sel ^ 1;
+  ISup* tab = P.sup_tab(sel);
+  if (P.N(1, P.h.cur).t == 0) {
+    const int node = P.child(1, 0, p.A, obs);
+    if (node < 0) return;
+    uint32_t s0, s1;   // the probe draw of sample_agent_initial_state(obs[first])
+    if (!Env::sample_agent_initial(sm, p.other, obs, draw_model, &s0, &s1)) P.fail(POMCP_E_INVALID);
+    P.traverse(1, node);
+    uint2* pp = P.sup_parts(sel);
+    int m = 0;
+    while (P.h.err == 0 && (double)m < 1.0 * (double)p.n_target) {
+      if (m >= p.Nsp) {
+        P.fail(POMCP_E_ARENA);
+        break;
+      }
+      Env::sample_agent_initial(sm, p.other, obs, draw_model, &s0, &s1);
+      pp[m++] = make_uint2(s0, s1);
+    }
+    tab[0] = ISup{node, 0, m, m};
+    P.h.cur = node;
+    P.h.root_size = m;
+    P.h.sup_sel = sel;
+    P.h.n_sup = 1;
+    P.h.sup_used = m;
+    return;
+  }
+  const int node = (action >= 0 && action < p.A) ? P.child(1, P.h.cur, action, obs) : -1;
+  if (node < 0) {
+    P.fail(POMCP_E_NOT_FOUND);
+    return;
+  }
+  P.traverse(1, node);
+  // its belief: the log records of `node` in insertion order, then the
+  // reinvigoration from the parent's (the previous root's, entry 0 of the
+  // previous table)
+  tab[0].node = node;
+  P.prob[0] = 1.0;
+  im_extract_support<Env, kWave>(P, sel, 1);
+  if (P.h.err != 0) return;
+  P.h.pad = P.h.n_sup;
+  P.mark_support(sel ^ 1, P.h.pad, true);
+  if (!im_absorbing(P.N(1, node).info))
+    P.reinvig_nested(node, action, obs, (int)ceil(1.0 * (double)p.n_target), sel, 0);
+  P.mark_support(sel ^ 1, P.h.pad, false);
+  P.h.cur = node;
+  P.h.root_size = tab[0].size;
+  P.h.sup_sel = sel;
+  P.h.n_sup = 1;
+  P.h.sup_used = tab[0].off + tab[0].cap;
+  if (P.h.err == 0) P.template clear_old_beliefs<kWave>(P.N(1, node).t);
+}
+
 // INTMCP.update (intmcp.py:198-300) for every pair.
 // kWave (few pairs: the drop-in's one): a wave per pair, its 64 lanes running
 // the same pair in lockstep (identical state, identical stores) and sharing
@@ -1358,14 +1426,18 @@ __global__ __launch_bounds__(64) void k_im_update(ImParams p) {
   if (b >= p.B) return;
   ImPair<Env> P(p, sm, b);
   const uint64_t obs = p.in_obs[b];
+  const int T = P.top();
   if (p.in_actions[b] == kImSkip) {   // a pair whose episode has ended: untouched
-    p.out[2 * b] = im_absorbing(P.N(0, P.h.cur).info) ? 1 : 0;
+    p.out[2 * b] = im_absorbing(P.N(T, P.h.cur).info) ? 1 : 0;
     p.out[2 * b + 1] = P.h.err;
     return;
   }
   P.h.num_sims = 0;         // the step's counters (intmcp.py:114-136 resets them first)
   P.h.search_depth = 0;
-  if (P.h.err == 0 && !im_absorbing(P.N(0, P.h.cur).info)) {
+  if (p.nest0) {
+    if (P.h.err == 0 && !im_absorbing(P.N(1, P.h.cur).info))
+      im_update_nest0<Env, kWave>(P, sm, obs, p.in_actions[b]);
+  } else if (P.h.err == 0 && !im_absorbing(P.N(0, P.h.cur).info)) {
     auto draw_model = [&](uint32_t n) { return P.d_model(n); };
     const double* prob = P.prob;
     int nsup = 0;
@@ -1500,7 +1572,7 @@ __global__ __launch_bounds__(64) void k_im_update(ImParams p) {
   }
   P.h.pad = 0;
   P.store();
-  p.out[2 * b] = im_absorbing(P.N(0, P.h.cur).info) ? 1 : 0;
+  p.out[2 * b] = im_absorbing(P.N(T, P.h.cur).info) ? 1 : 0;
   p.out[2 * b + 1] = P.h.err;
 }
 
@@ -1539,16 +1611,18 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
     P.h.search_depth = 0;
   }
   const int root = P.h.cur;
+  const int T = P.top();
+  if (p.nest0) sims1 = 0;   // one level: the planner's own tree
   int action = 0;
-  if (P.h.err == 0 && !im_absorbing(P.N(0, root).info) && P.N(0, root).t > 0) {
+  if (P.h.err == 0 && !im_absorbing(P.N(T, root).info) && P.N(T, root).t > 0) {
     uint4* rb = P.root_buf(P.h.root_sel);
     // _nested_sim(history, level, top_level=True) of the level-1 planner
     // (intmcp.py:410-442) starts with traverse + expand of the root: no draws,
     // and no-ops once done, so they run once per launch.  The depleted-root
     // branch cannot be reached with a valid configuration.
     if (sims0 + sims1 > 0) {
-      P.traverse(0, root);
-      if (im_nreg(P.N(0, root).info) == 0) P.expand(0, root);
+      P.traverse(T, root);
+      if (im_nreg(P.N(T, root).info) == 0) P.expand(T, root);
       if (P.h.root_size == 0 || P.h.root_size < p.extra) P.fail(POMCP_E_UNSUPPORTED);
     }
     const ISup* const stab = P.sup_tab(P.h.sup_sel);
@@ -1561,8 +1635,9 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
       uint4 hp_next = make_uint4(0, 0, 0, 0);
       ISup e_next = {0, 0, 0, 0};
       if (num_sims > 0) {
-        hp_next = rb[P.d_bel(1, (uint32_t)P.h.root_size)];
-        if (level == 0) e_next = stab[hp_next.w];
+        // nesting level 0: every simulation starts at the root, support entry 0
+        if (!p.nest0) hp_next = rb[P.d_bel(1, (uint32_t)P.h.root_size)];
+        if (level == 0) e_next = stab[p.nest0 ? 0u : hp_next.w];
         if (level == 1) {   // the root's view, kept current by the backups (ImPair::rv)
           P.rv_put(P.view(0, root));
           P.rv_root = root;
@@ -1571,14 +1646,14 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
       for (int s = 0; s < num_sims && P.h.err == 0; ++s) {
         const uint4 hp = hp_next;
         const ISup e = e_next;
-        if (s + 1 < num_sims) {
+        if (s + 1 < num_sims && !p.nest0) {
           hp_next = rb[P.d_bel(1, (uint32_t)P.h.root_size)];
           if (level == 0) e_next = stab[hp_next.w];
         }
         if (level == 0) {
           // the level-0 planner's _nested_sim at the particle's history: its
           // node + statistics and the support particle in one round trip
-          const int n = (int)hp.z;
+          const int n = p.nest0 ? root : (int)hp.z;
           if (e.size == 0) {
             P.fail(POMCP_E_UNSUPPORTED);   // depleted level-0 node (unreachable)
             break;
@@ -1596,8 +1671,9 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
             for (int q = 0; q < ImPair<Env>::kNA; ++q) v.sh[q] = make_uint4(0, 0, 0, 0);
           }
           IM_MARK_P(IP_START);
-          P.simulate(1, q.x, q.y, 0u, n, v);
+          const int d = P.simulate(1, q.x, q.y, 0u, n, v);
           P.N(1, n).visits = v.x.visits + 1;   // (simulate writes no INode of its start)
+          if (p.nest0 && d > P.h.search_depth) P.h.search_depth = d;
         } else {
           const auto v = P.rv_get();
           IM_MARK_P(IP_START);
@@ -1620,7 +1696,7 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
       return;
     }
     // max_value_action_selection (intmcp.py:718-732)
-    const INode x = P.N(0, root);
+    const INode x = P.N(T, root);
     const int nr = im_nreg(x.info);
     if (nr == 0) {
       action = (int)P.d_sel((uint32_t)p.A);
@@ -1629,7 +1705,7 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
       int ties[6], nt = 0;
       for (int i = 0; i < nr; ++i) {
         const int a = im_order(x.info, i);
-        const uint32_t* const hd = P.H(0, root, a);
+        const uint32_t* const hd = P.H(T, root, a);
         const double v = hilo_d(hd[1], hd[2]);
         if (v == mx) {
           ties[nt++] = a;
@@ -1658,7 +1734,7 @@ __global__ __launch_bounds__(64) void k_im_synthetic(ImParams p, uint64_t env_se
   for (int k = 0; k < 5; ++k) env.ctr[k] = 0;
   uint32_t s0, s1;
   Env::sample_initial(sm, [&](uint32_t n) { return env.model(n); }, &s0, &s1);
-  p.out_obs[b] = Env::obs_key(sm, p.ego, s0, s1);
+  p.out_obs[b] = Env::obs_key(sm, p.nest0 ? p.other : p.ego, s0, s1);
 }
 
 }  // namespace pb

@@ -19,13 +19,15 @@ struct intmcp_ctx {
   intmcp_root_stats* dev_rstats = nullptr;   // device staging of intmcp_get_root_stats
 };
 
-// intmcp_root_stats of every pair's level-1 root (was a host loop with two
-// synchronous copies per pair: seconds at 65,536 pairs)
+// intmcp_root_stats of every pair's planner root (the level-1 root; at nesting
+// level 0 the root of tree 1) (was a host loop with two synchronous copies per
+// pair: seconds at 65,536 pairs)
 __global__ __launch_bounds__(64) void k_im_root_stats(ImParams d, intmcp_root_stats* out) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= d.B) return;
   const IHdr h = d.hdr[t];
-  const char* const blk = d.nodes + im_node_off(d.Nn, d.B, t, 0, h.cur);
+  const int T = d.nest0 ? 1 : 0;
+  const char* const blk = d.nodes + im_node_off(d.Nn, d.B, t, T, h.cur);
   const INode node = *reinterpret_cast<const INode*>(blk);
   intmcp_root_stats o;
   memset(&o, 0, sizeof(o));
@@ -52,8 +54,8 @@ __global__ __launch_bounds__(64) void k_im_root_stats(ImParams d, intmcp_root_st
       }
     }
   }
-  o.min_value = h.mm_min[0];
-  o.max_value = h.mm_max[0];
+  o.min_value = h.mm_min[T];
+  o.max_value = h.mm_max[T];
   for (int k = 0; k < 2; ++k) {
     o.n_nodes[k] = h.n_nodes[k];
     o.n_log[k] = h.n_log[k];
@@ -154,6 +156,8 @@ int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, in
   if (c.action_selection != POMCP_SEL_UCB && c.action_selection != POMCP_SEL_UNIFORM)
     return bad(POMCP_E_UNSUPPORTED, "I-NTMCP pucb reads self.action_space (intmcp.py:645): ucb / uniform only");
   if (c.ego_agent < 0 || c.ego_agent > 1 || c.num_trees < 1) return bad(POMCP_E_INVALID, "ego / pairs");
+  if (cfg->nesting_level != 0 && cfg->nesting_level != 1)
+    return bad(POMCP_E_UNSUPPORTED, "nesting levels 0 and 1");
   if (c.depth_limit < 0 || c.step_limit < 0 || c.num_particles < 1) return bad(POMCP_E_INVALID, "limits");
   if (cfg->max_nodes < 2 || cfg->max_nodes >= (1ll << 28) || cfg->max_stats < c.num_actions ||
       cfg->max_log < 1 || cfg->hash_slots < 16 || (cfg->hash_slots & (cfg->hash_slots - 1)) ||
@@ -195,8 +199,10 @@ int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, in
   d.fast_slack = IM_FAST_SLACK;
   d.B = c.num_trees;
   d.A = c.num_actions;
-  d.ego = c.ego_agent;
-  d.other = 1 - c.ego_agent;
+  // nesting level 0: the planner's tree is tree 1, whose agent is p.other
+  d.nest0 = cfg->nesting_level == 0 ? 1 : 0;
+  d.ego = d.nest0 ? 1 - c.ego_agent : c.ego_agent;
+  d.other = 1 - d.ego;
   d.sel = c.action_selection;
   d.depth_limit = c.depth_limit;
   d.step_limit = c.step_limit;
@@ -349,6 +355,10 @@ int intmcp_search_levels(intmcp_ctx* ctx, int32_t level0_sims, int32_t level1_si
                          int32_t flags, int32_t* actions_out) {
   if (!ctx || level0_sims < 0 || level1_sims < 0 || (flags & ~(kImBegin | kImFinal)))
     return POMCP_E_INVALID;
+  if (ctx->ip.nest0 && level1_sims > 0) {
+    ctx->err = "search_levels: nesting level 0 has no level-1 simulations";
+    return POMCP_E_INVALID;
+  }
   IM_TRY(ctx, hipSetDevice(ctx->device));
   IM_LAUNCH(ctx, k_im_search, dim3(im_blocks(ctx->ip.B)), dim3(64), ctx->ip, (int)level0_sims,
             (int)level1_sims, (int)flags);
@@ -368,7 +378,8 @@ int intmcp_search_levels(intmcp_ctx* ctx, int32_t level0_sims, int32_t level1_si
 
 int intmcp_search(intmcp_ctx* ctx, int32_t num_sims, int32_t* actions_out) {
   if (!ctx || num_sims < 0) return POMCP_E_INVALID;
-  return intmcp_search_levels(ctx, num_sims, num_sims, kImBegin | kImFinal, actions_out);
+  return intmcp_search_levels(ctx, num_sims, ctx->ip.nest0 ? 0 : num_sims, kImBegin | kImFinal,
+                              actions_out);
 }
 
 int intmcp_get_root_stats(intmcp_ctx* ctx, intmcp_root_stats* out) {

@@ -246,7 +246,7 @@ class IntmcpConfig(C.Structure):
     _fields_ = [
         ("base", PomcpConfig),
         ("state_belief_only", C.c_int32),
-        ("pad", C.c_int32),
+        ("nesting_level", C.c_int32),
         ("max_nodes", C.c_int64),
         ("max_stats", C.c_int64),
         ("max_log", C.c_int64),

@@ -1,6 +1,6 @@
 """I-NTMCP drop-in: the reference's ``INTMCP`` API (``intmcp.py:22-994``) at
-nesting level 1 with two agents, both planners' trees, beliefs and generative
-model on the GPU (``include/intmcp.h``, ``csrc/intmcp.hip``).
+nesting levels 1 and 0 with two agents, the planners' trees, beliefs and
+generative model on the GPU (``include/intmcp.h``, ``csrc/intmcp.hip``).
 
 Public surface kept from the reference: ``INTMCP.initialize(model,
 ego_agent_id, config, nesting_level, search_policies)``, ``step(obs)``,
@@ -13,7 +13,7 @@ same device state), ``search_policies``, ``action_spaces``, ``step_limit``,
 ``BatchedINTMCP`` runs many independent planner pairs in one launch (BASELINE
 config 5: nested trees as a batched launch).
 
-Scope (DESIGN.md "I-NTMCP"): nesting level 1, random search policies
+Scope (DESIGN.md "I-NTMCP"): nesting levels 0 and 1, random search policies
 (``search_policies=None``), ``ucb`` / ``uniform`` selection (the reference's
 ``pucb_action_selection`` reads ``self.action_space``, which INTMCP does not
 define, ``intmcp.py:645``).  The reinvigoration of a depleted root during the
@@ -139,7 +139,7 @@ class IntmcpEngine:
 
     def __init__(self, model, agent_id, config, num_pairs=1, capacities=None, num_sims=None,
                  searches=None, device=None, stream=None, tree_key_base=0, seed=None,
-                 wall_clock=False):
+                 wall_clock=False, nesting_level=1):
         lib = N.load()
         model = engine_model(model)   # posggym-style models by spec.id + kwargs
         if len(model.possible_agents) != 2:
@@ -152,6 +152,9 @@ class IntmcpEngine:
         self._emodel = engine_model(model)
         self.config = config
         self.num_pairs = int(num_pairs)
+        if nesting_level not in (0, 1):
+            raise NotImplementedError("the GPU I-NTMCP engine runs nesting levels 0 and 1")
+        self.nesting_level = int(nesting_level)
         self.ego = model.possible_agents.index(agent_id)
         self.A = model.action_spaces[agent_id].n
         other = model.possible_agents[1 - self.ego]
@@ -167,7 +170,7 @@ class IntmcpEngine:
         self.wall_clock_sims = None
         if capacities is None and wall_clock:
             capacities, self.wall_clock_sims = plan_intmcp_wallclock_capacities(
-                config, step_limit, self.A)
+                config, step_limit, self.A, self.nesting_level)
         if capacities is None:
             sims = num_sims if num_sims is not None else (config.num_sims or 1024)
             budget = searches if searches is not None else (
@@ -208,6 +211,7 @@ class IntmcpEngine:
         c.discount_pow_size = len(self._dpow)
         model.configure_engine(c)
         ic.state_belief_only = 1 if config.state_belief_only else 0
+        ic.nesting_level = self.nesting_level
         ic.max_nodes = capacities.max_nodes
         ic.max_stats = capacities.max_stats
         ic.max_log = capacities.max_log
@@ -295,7 +299,13 @@ class IntmcpEngine:
         return max(0, room)
 
     def root_belief(self, pair=0):
-        """Level-1 root particles as (v0, v1, level-0 node) u32 rows."""
+        """Level-1 root particles as (v0, v1, level-0 node) u32 rows; at
+        nesting level 0 the planner's root particles as (v0, v1) rows."""
+        if self.nesting_level == 0:
+            ent, parts = self.support(pair)
+            if len(ent) == 0:
+                return parts[:0]
+            return parts[int(ent[0]["off"]):int(ent[0]["off"]) + int(ent[0]["size"])]
         n = C.c_int32()
         self._check(self._lib.intmcp_get_root_belief(self._ctx, pair, None, 0, C.byref(n)),
                     "get_root_belief")
@@ -396,8 +406,8 @@ class INTMCP:
     def __init__(self, model, agent_id: str, config: MCTSConfig, nesting_level: int,
                  other_agent_policies=None, search_policies=None, *,
                  num_sims: Optional[int] = None):
-        if nesting_level != 1:
-            raise NotImplementedError("the GPU I-NTMCP engine runs nesting level 1")
+        if nesting_level not in (0, 1):
+            raise NotImplementedError("the GPU I-NTMCP engine runs nesting levels 0 and 1")
         if search_policies is not None and not all(
                 isinstance(p, RandomSearchPolicy) for p in search_policies.values()):
             raise NotImplementedError("only RandomSearchPolicy search policies run in-kernel")
@@ -413,11 +423,13 @@ class INTMCP:
         self.action_spaces = {i: list(range(model.action_spaces[i].n))
                               for i in model.possible_agents}
         other = [i for i in model.possible_agents if i != agent_id][0]
-        self.other_agent_policies = {other: _NestedPlanner(self, other)}
+        # intmcp.py:971-981: a level-0 planner models no other agent
+        self.other_agent_policies = {other: _NestedPlanner(self, other)} if nesting_level else {}
         self._num_sims = num_sims if num_sims is not None else config.num_sims
         self._engine = IntmcpEngine(model, agent_id, config, num_pairs=1,
                                     num_sims=self._num_sims,
-                                    wall_clock=self._num_sims is None)
+                                    wall_clock=self._num_sims is None,
+                                    nesting_level=nesting_level)
         self.step_limit = self._engine.step_limit
         self._logger = logging.getLogger()
         self._last_action = None
@@ -542,7 +554,8 @@ class INTMCP:
         return int(st.action)
 
     def root_belief(self):
-        """Level-1 root particles as (v0, v1, level-0 node id) rows."""
+        """Root particles: (v0, v1, level-0 node id) rows at nesting level 1,
+        (v0, v1) rows at nesting level 0."""
         return self._engine.root_belief(0)
 
     def close(self):
@@ -563,7 +576,7 @@ class BatchedINTMCP:
 
     def __init__(self, model, agent_id, config: MCTSConfig, num_pairs: int, num_sims: int, *,
                  searches: int = 1, capacities=None, stream=None, tree_key_base: int = 0,
-                 device: Optional[int] = None):
+                 device: Optional[int] = None, nesting_level: int = 1):
         if capacities is None:
             step_limit = config.step_limit or model.spec.max_episode_steps
             capacities = plan_intmcp_capacities(config, step_limit, num_sims, searches,
@@ -572,7 +585,8 @@ class BatchedINTMCP:
         self.num_sims = num_sims
         self.engine = IntmcpEngine(model, agent_id, config, num_pairs=num_pairs,
                                    capacities=capacities, stream=stream,
-                                   tree_key_base=tree_key_base, device=device)
+                                   tree_key_base=tree_key_base, device=device,
+                                   nesting_level=nesting_level)
         self.engine.reset()
 
     def init_synthetic(self, env_seed_base: int = 1000):

@@ -156,6 +156,13 @@ def intmcp_state_record(eng, pair, searched, action):
     n1 = eng.nodes(pair, 1)
     s1 = eng.stats(pair, 1)
     ent, sparts = eng.support(pair)
+    kids = [(int(st.child_action[i]), int(st.child_visits[i]), st.child_values[i],
+             st.child_totals[i]) for i in range(st.num_children)]
+    if eng.nesting_level == 0:   # the planner's tree (tree 1), its root belief = support entry 0
+        t_root = int(n1[int(ent[0]["node"])]["t"])
+        parts = [(t_root, (int(q[0]), int(q[1])), ()) for q in eng.root_belief(pair)]
+        return intmcp_record(rec, int(st.num_sims), int(st.search_depth), int(st.root_visits),
+                             kids, st.min_value, st.max_value, parts, [])
     rows = eng.root_belief(pair)
 
     def history(n):
@@ -169,8 +176,6 @@ def intmcp_state_record(eng, pair, searched, action):
     # the root's t: every root particle's other-agent history has that length
     t_root = int(n1[int(rows[0][2])]["t"]) if len(rows) else 0
     parts = [(t_root, (int(r[0]), int(r[1])), history(int(r[2]))) for r in rows]
-    kids = [(int(st.child_action[i]), int(st.child_visits[i]), st.child_values[i],
-             st.child_totals[i]) for i in range(st.num_children)]
     nested, seen = [], []
     for r in rows:
         m = int(r[2])
@@ -207,12 +212,13 @@ def _exact_draws(ctx):
 
 
 def gpu_intmcp_episode(cfg_kwargs, num_sims, env_seed, ego="0", max_steps=50, env="Driving-v1",
-                       softmax_slack=None, exact=None):
+                       softmax_slack=None, exact=None, nesting_level=1):
     """softmax_slack: the fast softmax bound's widening (None: the product's);
     the exact-path draws of the episode are appended to `exact` (a list)."""
     from posggym_baselines_amd.planning import INTMCP
     model = product_model(env)
-    planner = INTMCP.initialize(model, ego, product_config(cfg_kwargs, num_sims), 1, None)
+    planner = INTMCP.initialize(model, ego, product_config(cfg_kwargs, num_sims), nesting_level,
+                                None)
     if softmax_slack is not None:
         _softmax_debug(planner._engine._ctx, softmax_slack)
     planner.reset()
@@ -232,7 +238,7 @@ def gpu_intmcp_episode(cfg_kwargs, num_sims, env_seed, ego="0", max_steps=50, en
 
 
 def batched_intmcp_episodes(cfg_kwargs, num_sims, env_seeds, steps, env="Driving-v1", ego="0",
-                            softmax_slack=None, exact=None):
+                            softmax_slack=None, exact=None, nesting_level=1):
     """Lockstep I-NTMCP episodes of len(env_seeds) planner pairs in ONE engine
     (pair b = tree key b, env seed env_seeds[b]), at most `steps` real steps;
     a pair whose episode ended is skipped (INTMCP_SKIP).  Per-pair record lists
@@ -246,7 +252,7 @@ def batched_intmcp_episodes(cfg_kwargs, num_sims, env_seeds, steps, env="Driving
     model = product_model(env)
     B = len(env_seeds)
     bp = BatchedINTMCP(model, ego, product_config(cfg_kwargs, num_sims), B, num_sims,
-                       searches=steps)
+                       searches=steps, nesting_level=nesting_level)
     if softmax_slack is not None:
         _softmax_debug(bp.engine._ctx, softmax_slack)
     envs = []

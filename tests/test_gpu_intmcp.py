@@ -9,20 +9,23 @@ import pytest
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
 
-from golden_util import INTMCP_CASES, cfg_kwargs, load
+from golden_util import INTMCP0_CASES, INTMCP_CASES, cfg_kwargs, load
 from gpu_util import gpu_intmcp_episode
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("case", INTMCP_CASES)
+@pytest.mark.parametrize("case", INTMCP_CASES + INTMCP0_CASES)
 def test_gpu_intmcp_matches_reference_goldens(case):
+    """Nesting level 1 (intmcp_*) and 0 (intmcp0_*: the planner's own tree,
+    the other agent acting by the planner's random choice)."""
     data = load(case)
     for ep in data["episodes"]:
         kw = cfg_kwargs(ep["config"])
         trace, records = gpu_intmcp_episode(kw, data["num_sims"], ep["env_seed"],
                                             ego=data["ego"], max_steps=data["max_steps"],
-                                            env=data["env"])
+                                            env=data["env"],
+                                            nesting_level=data.get("nesting_level", 1))
         assert len(records) == len(ep["records"]), case
         for t, (got, exp) in enumerate(zip(records, ep["records"])):
             assert got == exp, f"{case} env_seed {ep['env_seed']} step {t}"
@@ -260,3 +263,35 @@ def test_search_split_over_launches_equals_one_launch():
         e.update(acts, keys)
     one.close()
     split.close()
+
+
+@pytest.mark.parametrize("env,ego", [("Driving-v1", "0"), ("PursuitEvasion-v1", "1")])
+def test_gpu_intmcp_nesting0_batched_pairs_match_oracle(env, ego):
+    """Nesting level 0, many planners in one launch: every planner's records
+    against the oracle (oracle/intmcp.py, pinned at nesting 0 by the
+    intmcp0_* goldens) with that planner's tree key."""
+    from gpu_util import batched_intmcp_episodes
+    from oracle.run import oracle_intmcp_episode
+    B, sims, steps = 6, 40, 8
+    seeds = [300 + b for b in range(B)]
+    got = batched_intmcp_episodes(TEST_CFG, sims, seeds, steps, env=env, ego=ego,
+                                  nesting_level=0)
+    for b in range(B):
+        _, exp = oracle_intmcp_episode(TEST_CFG, sims, seeds[b], ego=ego, tree=b,
+                                       max_steps=steps, env=env, nesting_level=0)
+        assert len(got[b]) == len(exp), b
+        for t, (g, e) in enumerate(zip(got[b], exp)):
+            assert g == e, f"{env} pair {b} step {t}"
+
+
+def test_intmcp_nesting0_rejects_level1_simulations():
+    import ctypes as C
+    from gpu_util import product_config, product_model
+    from posggym_baselines_amd import _native as N
+    from posggym_baselines_amd.planning import INTMCP
+    planner = INTMCP.initialize(product_model("Driving-v1"), "0", product_config(TEST_CFG, 16),
+                                0, None)
+    assert planner.other_agent_policies == {}
+    rc = N.load().intmcp_search_levels(planner._engine._ctx, 4, 4, N.INTMCP_BEGIN, None)
+    assert rc == N.POMCP_E_INVALID
+    planner.close()

@@ -5,7 +5,7 @@
 # update()-inclusive PursuitEvasion step
 set -o pipefail
 O=gpurun_out/r4d; mkdir -p $O
-POMCP_LIB_PATH=$PWD/variants/lib_upd.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_potmmcp.py tests/test_gpu_mcts_policies.py -k "lane or potmmcp or base_planner" -x -q --timeout 300 --timeout-method thread > $O/test.log 2>&1 || { tail -30 $O/test.log; exit 1; }
+timeout -k 10 700 python -u -m pytest tests/test_gpu_intmcp.py tests/test_gpu_parity.py tests/test_gpu_potmmcp.py tests/test_gpu_mcts_policies.py -k "intmcp or lane or potmmcp or base_planner" -x -v --timeout 300 --timeout-method thread > $O/test.log 2>&1 || { tail -30 $O/test.log; exit 1; }
 tail -2 $O/test.log
 for n in exact upd exact upd; do
   echo "== $n" >> $O/exp.log
