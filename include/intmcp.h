@@ -101,6 +101,15 @@ int intmcp_get_stats(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int
 int intmcp_get_support(intmcp_ctx* ctx, int32_t pair, int32_t* entries, int32_t capacity_entries,
                        int32_t* n_entries, uint32_t* particles, int32_t capacity_particles,
                        int32_t* n_particles);
+/* INTMCP.initialize's search_policies (intmcp.py:956-971): the search policy of
+ * agent `agent` at nesting level `level` -- NULL: RandomSearchPolicy
+ * (Discrete.sample(), the default), else the num_actions probabilities of a
+ * SearchPolicyWrapper(FixedDistributionPolicy), drawn as random.choices on the
+ * agent's action stream.  It draws the rollout actions of that level's planner
+ * (intmcp.py:547-593) and, at level 1, the other agent's action at a history
+ * its level-0 tree has not visited (intmcp.py:778-780).  Takes effect at the
+ * next search; every pair of the context. */
+int intmcp_set_search_policy(intmcp_ctx* ctx, int32_t level, int32_t agent, const double* probs);
 /* Synthetic roots (as pomcp_synthetic_obs). */
 int intmcp_synthetic_obs(intmcp_ctx* ctx, uint64_t env_seed_base, uint64_t* obs_keys_out);
 

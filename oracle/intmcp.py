@@ -89,8 +89,14 @@ class _Tree:
 class _Planner:
     """One INTMCP instance (``intmcp.py:22-111``)."""
 
-    def __init__(self, model, agent_id, cfg, level, streams, rng_stream, nested=None):
+    def __init__(self, model, agent_id, cfg, level, streams, rng_stream, nested=None,
+                 search_probs=None):
         self.model = model
+        # search_policies of this level (intmcp.py:956-971): agent id -> None
+        # (RandomSearchPolicy: Discrete.sample()) or the action distribution of a
+        # SearchPolicyWrapper(FixedDistributionPolicy), drawn as random.choices on
+        # the agent's action stream (oracle/ref_harness.py wires it so)
+        self.search_probs = dict(search_probs or {})
         self.agent_id = agent_id
         self.ego = model.possible_agents.index(agent_id)
         self.other_id = model.possible_agents[1 - self.ego]
@@ -180,14 +186,21 @@ class _Planner:
         return best[self.s.randint(S_SELECT, len(best))]
 
     # ---------------------------------------------- other agent (level 1 only)
-    def sample_action(self, n):
+    def _policy_action(self, agent_id, probs):
+        if probs is None:
+            return self.s.randint(S_ACT_BASE + int(agent_id), self.model.action_spaces[agent_id].n)
+        return StreamRandom(self.s, S_ACT_BASE + int(agent_id)).choices(range(len(probs)),
+                                                                       weights=probs)[0]
+
+    def sample_action(self, n, caller_probs=None):
         """``INTMCP.sample_action`` of the level-0 planner (``intmcp.py:763-791``)
         for the node of the other agent's history."""
         tr = self.tree
         tr.traverse(n)
         if tr.visits[n] == 0 or len(tr.order[n]) == 0:
-            # search_policy.sample_action -> model.action_spaces[j].sample()
-            return self.s.randint(S_ACT_BASE + self.ego, self.A)
+            # the caller's search_policies[j].sample_action (intmcp.py:780):
+            # model.action_spaces[j].sample(), or a fixed distribution's draw
+            return self._policy_action(self.agent_id, caller_probs)
         sq = math.sqrt(tr.visits[n])
         probs = [math.exp(tr.stats[(n, a)][0] / sq) for a in tr.order[n]]
         total = sum(probs)
@@ -197,7 +210,7 @@ class _Planner:
     def _other_action(self, particle):                   # intmcp.py:602-615, 891-905
         if self.level == 0 or self.cfg.state_belief_only:
             return self.s.randint(self.rng_stream, self.A_other)   # self._rng.choice
-        return self.nested.sample_action(particle[1])
+        return self.nested.sample_action(particle[1], self.search_probs.get(self.other_id))
 
     def _joint(self, ego_action, other_action):
         ja = {}
@@ -292,7 +305,8 @@ class _Planner:
         k = 0
         state, t = hps[0], hps[-1]
         while depth <= cfg.depth_limit and t <= self.step_limit:
-            ja = {i: self.model.action_spaces[i].sample() for i in self.model.possible_agents}
+            ja = {i: self._policy_action(i, self.search_probs.get(i))
+                  for i in self.model.possible_agents}
             ts = self.model.step(state, ja)
             ret += cfg.discount ** k * ts.rewards[self.agent_id]
             if (ts.terminations[self.agent_id] or ts.truncations[self.agent_id]
@@ -395,18 +409,25 @@ class OracleINTMCP:
     streams in construction order (the lowest level first, intmcp.py:964-986):
     S_BELIEF_NESTED, then S_BELIEF."""
 
-    def __init__(self, model, agent_id, cfg, streams: Streams, nesting_level: int = 1):
+    def __init__(self, model, agent_id, cfg, streams: Streams, nesting_level: int = 1,
+                 search_probs=None):
+        """search_probs: {level: {agent id: None or action probabilities}}
+        (the search_policies of INTMCP.initialize; None: all random)."""
         assert cfg.num_sims is not None
         if nesting_level not in (0, 1):
             raise NotImplementedError("nesting levels 0 and 1")
+        sp = search_probs or {}
         other = model.possible_agents[1 - model.possible_agents.index(agent_id)]
         if nesting_level == 0:
             self.nested = None
-            self.top = _Planner(model, agent_id, cfg, 0, streams, S_BELIEF_NESTED)
+            self.top = _Planner(model, agent_id, cfg, 0, streams, S_BELIEF_NESTED,
+                                search_probs=sp.get(0))
         else:
             # construction order of INTMCP.initialize: the nested planner first
-            self.nested = _Planner(model, other, cfg, 0, streams, S_BELIEF_NESTED)
-            self.top = _Planner(model, agent_id, cfg, 1, streams, S_BELIEF, nested=self.nested)
+            self.nested = _Planner(model, other, cfg, 0, streams, S_BELIEF_NESTED,
+                                   search_probs=sp.get(0))
+            self.top = _Planner(model, agent_id, cfg, 1, streams, S_BELIEF, nested=self.nested,
+                                search_probs=sp.get(1))
         self.nesting_level = nesting_level
         self.cfg = cfg
         self.model = model

@@ -181,14 +181,18 @@ def reference_episode(cfg_kwargs, num_sims, env_seed, ego="0", grid=None,
 
 
 # ----------------------------------------------------------------- I-NTMCP
-def make_reference_intmcp(model, agent_id, cfg_kwargs, num_sims, streams, nesting_level=1):
-    """``INTMCP.initialize(model, agent_id, config, nesting_level, None)`` wired
-    to ``streams`` with ``num_sims`` simulations per nesting level
+def make_reference_intmcp(model, agent_id, cfg_kwargs, num_sims, streams, nesting_level=1,
+                          search_probs=None):
+    """``INTMCP.initialize(model, agent_id, config, nesting_level, search_policies)``
+    wired to ``streams`` with ``num_sims`` simulations per nesting level
     (intmcp.py:385-399: the wrapped top-level ``_nested_sim`` jumps the fake
     clock after num_sims calls).  ``random.Random(seed)`` is called once per
     planner, the lowest level first (intmcp.py:964-986): first call ->
     S_BELIEF_NESTED, second -> S_BELIEF (nesting level 0: the one planner's is
-    S_BELIEF_NESTED)."""
+    S_BELIEF_NESTED).  search_probs: None (``search_policies=None``: random at
+    every level) or {level: {agent: None | probs}} -> ``RandomSearchPolicy`` /
+    ``SearchPolicyWrapper(FixedDistributionPolicy)`` drawing on the agent's
+    action stream (``S_ACT_BASE + agent``, the stream ``Discrete.sample()`` uses)."""
     P = import_reference()
     import posggym_baselines.planning.intmcp as im
     import posggym_baselines.planning.belief as B
@@ -218,8 +222,25 @@ def make_reference_intmcp(model, agent_id, cfg_kwargs, num_sims, streams, nestin
     if kw.get("known_bounds") is not None:
         kw["known_bounds"] = KnownBounds(*kw["known_bounds"])
     config = P.MCTSConfig(**kw)
+    search_policies = None
+    if search_probs is not None:
+        import posggym_baselines.planning.search_policy as sp_mod
+        from oracle.rng import S_ACT_BASE
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                        "posggym-baselines_amd"))
+        from posggym_baselines_amd.planning.policies import FixedDistributionPolicy
+
+        def policy(i, probs):
+            if probs is None:
+                return P.RandomSearchPolicy(model, i)
+            return sp_mod.SearchPolicyWrapper(FixedDistributionPolicy(
+                model, i, "search", probs, StreamRandom(streams, S_ACT_BASE + int(i))))
+
+        search_policies = {lv: {i: policy(i, search_probs.get(lv, {}).get(i))
+                                for i in model.possible_agents}
+                           for lv in range(nesting_level + 1)}
     planner = P.INTMCP.initialize(model, agent_id, config, nesting_level=nesting_level,
-                                  search_policies=None)
+                                  search_policies=search_policies)
     assert len(made) == nesting_level + 1
     inner = planner._nested_sim
     count = [0]
@@ -290,14 +311,15 @@ def reference_intmcp_record(planner, searched, action):
 
 
 def reference_intmcp_episode(cfg_kwargs, num_sims, env_seed, ego="0", tree=0, max_steps=50,
-                             env="Driving-v1", nesting_level=1):
+                             env="Driving-v1", nesting_level=1, search_probs=None):
     from oracle.envs import make_model
     from oracle.episode import run_episode
     from oracle.rng import Streams
 
     streams = Streams(cfg_kwargs.get("seed") or 0, tree)
     model = make_model(env, streams)
-    planner = make_reference_intmcp(model, ego, cfg_kwargs, num_sims, streams, nesting_level)
+    planner = make_reference_intmcp(model, ego, cfg_kwargs, num_sims, streams, nesting_level,
+                                    search_probs)
     planner.reset()
     records = []
 

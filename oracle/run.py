@@ -70,12 +70,13 @@ def oracle_first_step(cfg_kwargs, num_sims, tree, env_seed, rekey=None, env="Dri
 
 
 # ----------------------------------------------------------------- I-NTMCP
-def make_oracle_intmcp(cfg_kwargs, num_sims, ego="0", tree=0, env="Driving-v1", nesting_level=1):
+def make_oracle_intmcp(cfg_kwargs, num_sims, ego="0", tree=0, env="Driving-v1", nesting_level=1,
+                       search_probs=None):
     from oracle.intmcp import OracleINTMCP
     streams = Streams(cfg_kwargs.get("seed") or 0, tree)
     model = make_model(env, streams)
     cfg = OracleConfig(num_sims=num_sims, **cfg_kwargs)
-    return OracleINTMCP(model, ego, cfg, streams, nesting_level)
+    return OracleINTMCP(model, ego, cfg, streams, nesting_level, search_probs)
 
 
 def oracle_intmcp_record(p, searched, action):
@@ -106,9 +107,9 @@ def oracle_intmcp_record(p, searched, action):
 
 
 def oracle_intmcp_episode(cfg_kwargs, num_sims, env_seed, ego="0", tree=0, max_steps=50,
-                          env="Driving-v1", nesting_level=1):
+                          env="Driving-v1", nesting_level=1, search_probs=None):
     p = make_oracle_intmcp(cfg_kwargs, num_sims, ego=ego, tree=tree, env=env,
-                           nesting_level=nesting_level)
+                           nesting_level=nesting_level, search_probs=search_probs)
     p.reset()
     records = []
 

@@ -161,8 +161,16 @@ struct ImParams {
   // path runs on most draws, intmcp_debug_set_softmax_slack), and the exact-path
   // draws are counted when exact_draws is set (tests only)
   float fast_slack;
-  int32_t pad2;
+  // search policies (INTMCP search_policies, intmcp.py:956-971) of tree k's
+  // planner for agent i: sp_fixed[k][i] = 0 RandomSearchPolicy
+  // (Discrete.sample()), 1 a fixed distribution drawn as random.choices
+  // (sp_cum / sp_tot, pomcp_device.h tm_choice) on the agent's action stream;
+  // sp_any: some table is fixed (else the draws stay the plain uniform ones)
+  int32_t sp_any;
   unsigned long long* exact_draws;
+  int32_t sp_fixed[2][2];
+  double sp_cum[2][2][kImMaxA];
+  double sp_tot[2][2];
 };
 
 // Phase timing (diagnostics build, -DPOMCP_PHASE_TIMING): per-lane s_memtime
@@ -411,6 +419,12 @@ struct ImPair {
   __device__ __forceinline__ uint32_t d_model(uint32_t n) { return uniform_int(draw(2, S_MODEL), n); }
   __device__ __forceinline__ uint32_t d_act(int agent, uint32_t n) {   // model.action_spaces[agent].sample()
     return agent == 0 ? uniform_int(draw(3, S_ACT_BASE), n) : uniform_int(draw(4, S_ACT_BASE + 1), n);
+  }
+  // search_policies[agent].sample_action of tree k's planner
+  __device__ __forceinline__ uint32_t d_pol(int k, int agent) {
+    if (!p.sp_any || !p.sp_fixed[k][agent]) return d_act(agent, (uint32_t)p.A);
+    const uint32_t w = agent == 0 ? draw(3, S_ACT_BASE) : draw(4, S_ACT_BASE + 1);
+    return (uint32_t)tm_choice(p.sp_cum[k][agent], p.sp_tot[k][agent], p.A, w);
   }
 
   // ---------------------------------------------------------------- trees
@@ -718,7 +732,7 @@ struct ImPair {
     }
     const INode& x = v.x;
     const int nr = im_nreg(x.info);
-    if (x.visits == 0 || nr == 0) return (int)d_act(p.other, (uint32_t)p.A);
+    if (x.visits == 0 || nr == 0) return (int)d_pol(0, p.other);   // the level-1 caller's policy
     uint4 q[kImMaxA];
     child_stats(v, nr, q);
     const double d = d_sel_float();   // random.choices' random() (the stream's only draw here)
@@ -847,8 +861,8 @@ struct ImPair {
     int kk = 0;
     const int me = agent(k);
     while (depth <= p.depth_limit && t <= p.step_limit) {
-      const uint32_t a0 = d_act(0, (uint32_t)p.A);
-      const uint32_t a1 = d_act(1, (uint32_t)p.A);
+      const uint32_t a0 = d_pol(k, 0);
+      const uint32_t a1 = d_pol(k, 1);
       const uint32_t j = Env::kStepDraws ? d_model(2) : 0u;
       uint32_t n0, n1;
       double r;

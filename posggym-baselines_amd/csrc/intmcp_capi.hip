@@ -539,6 +539,43 @@ int intmcp_debug_set_softmax_slack(intmcp_ctx* ctx, float slack) {
   return POMCP_OK;
 }
 
+int intmcp_set_search_policy(intmcp_ctx* ctx, int32_t level, int32_t agent, const double* probs) {
+  if (!ctx || agent < 0 || agent > 1) return POMCP_E_INVALID;
+  const int top = ctx->ip.nest0 ? 0 : 1;   // the planner's nesting level
+  if (level < 0 || level > top) {
+    ctx->err = "set_search_policy: no planner at level " + std::to_string(level);
+    return POMCP_E_INVALID;
+  }
+  const int k = top - level;               // tree 0 = level 1; the level-0 planner's is tree 1
+  const int tree = ctx->ip.nest0 ? 1 : k;
+  ImParams& d = ctx->ip;
+  if (probs == nullptr) {
+    d.sp_fixed[tree][agent] = 0;
+  } else {
+    // random.choices' cumulative weights, summed left to right as
+    // itertools.accumulate does, and total = cum[-1] + 0.0
+    double acc = 0.0;
+    for (int a = 0; a < d.A; ++a) {
+      if (!(probs[a] >= 0.0)) {
+        ctx->err = "set_search_policy: negative or NaN weight";
+        return POMCP_E_INVALID;
+      }
+      acc = a == 0 ? probs[0] : acc + probs[a];
+      d.sp_cum[tree][agent][a] = acc;
+    }
+    if (!(acc > 0.0)) {
+      ctx->err = "set_search_policy: weights sum to zero";
+      return POMCP_E_INVALID;
+    }
+    d.sp_tot[tree][agent] = acc + 0.0;
+    d.sp_fixed[tree][agent] = 1;
+  }
+  d.sp_any = 0;
+  for (int t = 0; t < 2; ++t)
+    for (int i = 0; i < 2; ++i) d.sp_any |= d.sp_fixed[t][i];
+  return POMCP_OK;
+}
+
 int intmcp_debug_exact_draws(intmcp_ctx* ctx, uint64_t* count) {
   if (!ctx || !count) return POMCP_E_INVALID;
   *count = 0;

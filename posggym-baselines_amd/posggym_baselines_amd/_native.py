@@ -306,6 +306,7 @@ INTMCP_SIGNATURES = [
     ("intmcp_get_support", C.c_int,
      [_CTX, C.c_int32, _P32, C.c_int32, _P32, _PU32, C.c_int32, _P32]),
     ("intmcp_synthetic_obs", C.c_int, [_CTX, C.c_uint64, _PU64]),
+    ("intmcp_set_search_policy", C.c_int, [_CTX, C.c_int32, C.c_int32, _PD]),
     ("intmcp_debug_phase_timing", C.c_int, [_CTX, C.c_void_p, C.c_int32, _P32]),
 ]
 

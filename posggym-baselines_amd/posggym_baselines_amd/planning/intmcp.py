@@ -13,8 +13,11 @@ same device state), ``search_policies``, ``action_spaces``, ``step_limit``,
 ``BatchedINTMCP`` runs many independent planner pairs in one launch (BASELINE
 config 5: nested trees as a batched launch).
 
-Scope (DESIGN.md "I-NTMCP"): nesting levels 0 and 1, random search policies
-(``search_policies=None``), ``ucb`` / ``uniform`` selection (the reference's
+Scope (DESIGN.md "I-NTMCP"): nesting levels 0 and 1, random or
+fixed-distribution search policies (``RandomSearchPolicy`` /
+``SearchPolicyWrapper(FixedDistributionPolicy)`` per level and agent: they draw
+the rollouts and the other agent's action at an unvisited history; the node
+priors they give only matter to PUCB), ``ucb`` / ``uniform`` selection (the reference's
 ``pucb_action_selection`` reads ``self.action_space``, which INTMCP does not
 define, ``intmcp.py:645``).  The reinvigoration of a depleted root during the
 search (``intmcp.py:426-431``) cannot run under a valid configuration (the
@@ -267,6 +270,20 @@ class IntmcpEngine:
                                             out.ctypes.data_as(C.POINTER(C.c_int32))), "search")
         return out
 
+    def set_search_policy(self, level, agent_index, probs=None):
+        """``search_policies[level][agent]``: None (random) or a fixed action
+        distribution (``intmcp_set_search_policy``)."""
+        ptr = None
+        if probs is not None:
+            self._sp_keep = getattr(self, "_sp_keep", [])
+            arr = np.ascontiguousarray(np.asarray(probs, dtype=np.float64))
+            if arr.shape != (self.A,):
+                raise ValueError(f"search policy: {self.A} action probabilities expected")
+            self._sp_keep.append(arr)
+            ptr = arr.ctypes.data_as(C.POINTER(C.c_double))
+        self._check(self._lib.intmcp_set_search_policy(self._ctx, int(level), int(agent_index), ptr),
+                    "set_search_policy")
+
     def search_levels(self, level0_sims, level1_sims, flags, fetch=False):
         out = np.zeros(self.num_pairs, dtype=np.int32) if fetch else None
         ptr = out.ctypes.data_as(C.POINTER(C.c_int32)) if fetch else None
@@ -408,17 +425,24 @@ class INTMCP:
                  num_sims: Optional[int] = None):
         if nesting_level not in (0, 1):
             raise NotImplementedError("the GPU I-NTMCP engine runs nesting levels 0 and 1")
-        if search_policies is not None and not all(
-                isinstance(p, RandomSearchPolicy) for p in search_policies.values()):
-            raise NotImplementedError("only RandomSearchPolicy search policies run in-kernel")
+        from posggym_baselines_amd.planning.ipomcp import search_policy_probs
         assert agent_id in model.possible_agents
+        # {level: {agent: policy}} (INTMCP.initialize) or one {agent: policy}
+        # dict for every level
+        if search_policies is not None and not all(
+                isinstance(v, dict) for v in search_policies.values()):
+            search_policies = {lv: search_policies for lv in range(nesting_level + 1)}
+        self._search_probs = {
+            lv: {i: search_policy_probs(model, i, pol) for i, pol in pols.items()}
+            for lv, pols in (search_policies or {}).items()}
         self.model = model
         self._emodel = engine_model(model)
         self.agent_id = agent_id
         self.config = config
         self.nesting_level = nesting_level
         self.num_agents = len(model.possible_agents)
-        self.search_policies = search_policies or {
+        # this planner's own level's policies (intmcp.py:985: search_policies[nesting_level])
+        self.search_policies = (search_policies or {}).get(nesting_level) or {
             i: RandomSearchPolicy(model, i) for i in model.possible_agents}
         self.action_spaces = {i: list(range(model.action_spaces[i].n))
                               for i in model.possible_agents}
@@ -430,6 +454,11 @@ class INTMCP:
                                     num_sims=self._num_sims,
                                     wall_clock=self._num_sims is None,
                                     nesting_level=nesting_level)
+        for lv, probs in self._search_probs.items():
+            if lv > nesting_level:
+                continue
+            for i, pr in probs.items():
+                self._engine.set_search_policy(lv, model.possible_agents.index(i), pr)
         self.step_limit = self._engine.step_limit
         self._logger = logging.getLogger()
         self._last_action = None
@@ -443,16 +472,10 @@ class INTMCP:
     @classmethod
     def initialize(cls, model, ego_agent_id: str, config: MCTSConfig, nesting_level: int,
                    search_policies=None, *, num_sims: Optional[int] = None) -> "INTMCP":
-        """``intmcp.py:949-994``; ``search_policies`` is ``{level: {agent: policy}}``."""
-        if search_policies is not None:
-            flat = {}
-            for level_pols in search_policies.values():
-                for i, p in level_pols.items():
-                    if not isinstance(p, RandomSearchPolicy):
-                        raise NotImplementedError(
-                            "only RandomSearchPolicy search policies run in-kernel")
-                    flat[i] = p
-            search_policies = flat
+        """``intmcp.py:949-994``; ``search_policies`` is ``{level: {agent: policy}}``
+        (None: ``RandomSearchPolicy`` everywhere); a policy is a
+        ``RandomSearchPolicy`` or a ``SearchPolicyWrapper(FixedDistributionPolicy)``
+        (others raise ``NotImplementedError``)."""
         return cls(model, ego_agent_id, config, nesting_level, None, search_policies,
                    num_sims=num_sims)
 
@@ -560,7 +583,8 @@ class INTMCP:
 
     def close(self):
         for p in self.search_policies.values():
-            p.close()
+            if hasattr(p, "close"):
+                p.close()
         self._engine.close()
 
     def __str__(self):

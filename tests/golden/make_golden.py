@@ -103,8 +103,28 @@ INTMCP0_CASES = {
 }
 
 
+# I-NTMCP with caller-supplied search policies (intmcp.py:956-971):
+# {level: {agent: probs}} -> SearchPolicyWrapper(FixedDistributionPolicy) on
+# the agent's action stream, RandomSearchPolicy for the agents left out.
+# (nesting level, search_probs, num_sims, [(seed, env_seed)], ego, max_steps, env)
+INTMCP_SP_CASES = {
+    "intmcp_sp_ucb": (1, {1: {"0": [0.1, 0.4, 0.2, 0.2, 0.1], "1": [0.5, 0.1, 0.1, 0.2, 0.1]},
+                          0: {"1": [0.05, 0.05, 0.3, 0.3, 0.3]}},
+                      48, [(50, 50)], "0", 30, "Driving-v1"),
+    "intmcp0_sp_ego1": (0, {0: {"1": [0.1, 0.4, 0.2, 0.2, 0.1], "0": [0.3, 0.0, 0.1, 0.5, 0.1]}},
+                        48, [(51, 51)], "1", 50, "Driving-v1"),
+    "intmcp_sp_pe": (1, {1: {"1": [0.25, 0.25, 0.4, 0.1]},
+                         0: {"0": [0.1, 0.2, 0.3, 0.4], "1": [0.7, 0.1, 0.1, 0.1]}},
+                     32, [(52, 52)], "1", 100, "PursuitEvasion-v1"),
+}
+
+
 def run_intmcp_case(name):
-    if name in INTMCP0_CASES:
+    sp = None
+    if name in INTMCP_SP_CASES:
+        level, sp, num_sims, pairs, ego, max_steps, env = INTMCP_SP_CASES[name]
+        over, base = {}, (INTMCP0_CFG if level == 0 else INTMCP_CFG)
+    elif name in INTMCP0_CASES:
         over, num_sims, pairs, ego, max_steps, env = INTMCP0_CASES[name]
         base, level = INTMCP0_CFG, 0
     else:
@@ -114,16 +134,23 @@ def run_intmcp_case(name):
            "episodes": []}
     if level != 1:
         out["nesting_level"] = level
+    if sp is not None:   # JSON keys are strings: levels as "0" / "1"
+        out["search_probs"] = {str(lv): v for lv, v in sp.items()}
     for seed, env_seed in pairs:
         cfg = dict(base)
         cfg.update(over)
         cfg["seed"] = seed
         tr, rr = reference_intmcp_episode(cfg, num_sims, env_seed, ego=ego, max_steps=max_steps,
-                                          env=env, nesting_level=level)
+                                          env=env, nesting_level=level, search_probs=sp)
         to, ro = oracle_intmcp_episode(cfg, num_sims, env_seed, ego=ego, max_steps=max_steps,
-                                       env=env, nesting_level=level)
+                                       env=env, nesting_level=level, search_probs=sp)
         if tr != to or rr != ro:
             raise SystemExit(f"oracle disagrees with reference in case {name} seed {seed}")
+        if sp is not None:   # the policies must matter: the random-policy run differs
+            _, r0 = oracle_intmcp_episode(cfg, num_sims, env_seed, ego=ego, max_steps=max_steps,
+                                          env=env, nesting_level=level)
+            if r0 == ro:
+                raise SystemExit(f"case {name}: the search policies change no record")
         out["episodes"].append({"config": dict(cfg), "env_seed": env_seed, "trace": tr,
                                 "records": rr})
     return out
@@ -382,7 +409,7 @@ def main(only=None, out_dir=HERE):
         _write(out_dir, name, data)
         n = sum(len(e["records"]) for e in data["episodes"])
         print(f"{name}: {len(data['episodes'])} episodes, {n} records")
-    for name in (list(INTMCP_CASES) + list(INTMCP0_CASES) if only is None
+    for name in (list(INTMCP_CASES) + list(INTMCP0_CASES) + list(INTMCP_SP_CASES) if only is None
                  else (only if isinstance(only, list) else ())):
         data = run_intmcp_case(name)
         _write(out_dir, name, data)

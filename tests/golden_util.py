@@ -38,3 +38,12 @@ INTMCP_CASES = ["intmcp_ucb", "intmcp_ego1", "intmcp_uniform", "intmcp_deep", "i
 # I-NTMCP nesting_level=0 (tests/golden/make_golden.py INTMCP0_CASES): a single
 # level-0 tree whose other agent acts uniformly (intmcp.py:750-753)
 INTMCP0_CASES = ["intmcp0_ucb", "intmcp0_ego1_uniform", "intmcp0_deep", "intmcp0_pe"]
+
+# I-NTMCP with fixed-distribution search policies (make_golden.py INTMCP_SP_CASES)
+INTMCP_SP_CASES = ["intmcp_sp_ucb", "intmcp0_sp_ego1", "intmcp_sp_pe"]
+
+
+def search_probs(data):
+    """A golden's {level: {agent: probs}} with integer levels (None if absent)."""
+    sp = data.get("search_probs")
+    return None if sp is None else {int(lv): v for lv, v in sp.items()}

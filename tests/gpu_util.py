@@ -211,14 +211,29 @@ def _exact_draws(ctx):
     return int(n.value)
 
 
+def intmcp_search_policies(model, search_probs):
+    """{level: {agent: probs}} -> the product's INTMCP.initialize search_policies
+    (SearchPolicyWrapper(FixedDistributionPolicy) / RandomSearchPolicy)."""
+    if search_probs is None:
+        return None
+    from posggym_baselines_amd.planning.policies import FixedDistributionPolicy
+    from posggym_baselines_amd.planning.search_policy import (RandomSearchPolicy,
+                                                               SearchPolicyWrapper)
+    return {lv: {i: (RandomSearchPolicy(model, i) if pols.get(i) is None else
+                     SearchPolicyWrapper(FixedDistributionPolicy(model, i, "search", pols[i])))
+                 for i in model.possible_agents}
+            for lv, pols in search_probs.items()}
+
+
 def gpu_intmcp_episode(cfg_kwargs, num_sims, env_seed, ego="0", max_steps=50, env="Driving-v1",
-                       softmax_slack=None, exact=None, nesting_level=1):
+                       softmax_slack=None, exact=None, nesting_level=1, search_probs=None):
     """softmax_slack: the fast softmax bound's widening (None: the product's);
-    the exact-path draws of the episode are appended to `exact` (a list)."""
+    the exact-path draws of the episode are appended to `exact` (a list);
+    search_probs: {level: {agent: probs}} fixed-distribution search policies."""
     from posggym_baselines_amd.planning import INTMCP
     model = product_model(env)
     planner = INTMCP.initialize(model, ego, product_config(cfg_kwargs, num_sims), nesting_level,
-                                None)
+                                intmcp_search_policies(model, search_probs))
     if softmax_slack is not None:
         _softmax_debug(planner._engine._ctx, softmax_slack)
     planner.reset()

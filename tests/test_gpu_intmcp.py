@@ -9,23 +9,25 @@ import pytest
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
 
-from golden_util import INTMCP0_CASES, INTMCP_CASES, cfg_kwargs, load
+from golden_util import INTMCP0_CASES, INTMCP_CASES, INTMCP_SP_CASES, cfg_kwargs, load, search_probs
 from gpu_util import gpu_intmcp_episode
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("case", INTMCP_CASES + INTMCP0_CASES)
+@pytest.mark.parametrize("case", INTMCP_CASES + INTMCP0_CASES + INTMCP_SP_CASES)
 def test_gpu_intmcp_matches_reference_goldens(case):
     """Nesting level 1 (intmcp_*) and 0 (intmcp0_*: the planner's own tree,
-    the other agent acting by the planner's random choice)."""
+    the other agent acting by the planner's random choice); *_sp_*: fixed-
+    distribution search policies per level and agent."""
     data = load(case)
     for ep in data["episodes"]:
         kw = cfg_kwargs(ep["config"])
         trace, records = gpu_intmcp_episode(kw, data["num_sims"], ep["env_seed"],
                                             ego=data["ego"], max_steps=data["max_steps"],
                                             env=data["env"],
-                                            nesting_level=data.get("nesting_level", 1))
+                                            nesting_level=data.get("nesting_level", 1),
+                                            search_probs=search_probs(data))
         assert len(records) == len(ep["records"]), case
         for t, (got, exp) in enumerate(zip(records, ep["records"])):
             assert got == exp, f"{case} env_seed {ep['env_seed']} step {t}"

@@ -1,7 +1,8 @@
 """Oracle pinning: the CPU restatement against the reference's golden vectors."""
 import pytest
 
-from golden_util import EPISODE_CASES, IPOMCP_CASES, case_env, case_max_steps, cfg_kwargs, load
+from golden_util import (EPISODE_CASES, IPOMCP_CASES, case_env, case_max_steps, cfg_kwargs, load,
+                         search_probs)
 from oracle.pomcp import OracleConfig
 from oracle.rng import Streams, StreamRandom, philox4x32_10
 from oracle.run import oracle_episode
@@ -74,7 +75,8 @@ def test_oracle_matches_reference_goldens(case):
 
 @pytest.mark.parametrize("case", ["intmcp_ucb", "intmcp_ego1", "intmcp_uniform", "intmcp_deep",
                                   "intmcp_pe", "intmcp0_ucb", "intmcp0_ego1_uniform",
-                                  "intmcp0_deep", "intmcp0_pe"])
+                                  "intmcp0_deep", "intmcp0_pe", "intmcp_sp_ucb",
+                                  "intmcp0_sp_ego1", "intmcp_sp_pe"])
 def test_intmcp_oracle_matches_reference_goldens(case):
     """I-NTMCP nesting 1 (BASELINE config 5) and nesting 0: the oracle
     restatement against the real reference planner's records (root children,
@@ -86,7 +88,8 @@ def test_intmcp_oracle_matches_reference_goldens(case):
         trace, records = oracle_intmcp_episode(ep["config"], data["num_sims"], ep["env_seed"],
                                                ego=data["ego"], max_steps=data["max_steps"],
                                                env=case_env(data),
-                                               nesting_level=data.get("nesting_level", 1))
+                                               nesting_level=data.get("nesting_level", 1),
+                                               search_probs=search_probs(data))
         assert trace == ep["trace"]
         for t, (got, exp) in enumerate(zip(records, ep["records"])):
             assert got == exp, f"{case} step {t}"
