@@ -1,4 +1,4 @@
-"""I-NTMCP hot path (nesting level 1, two agents) — CPU restatement (pure Python).
+"""I-NTMCP hot path (nesting levels 0-2, two agents) — CPU restatement (pure Python).
 
 TEST INFRASTRUCTURE (see ``oracle/__init__.py``).
 
@@ -31,6 +31,7 @@ from oracle.rng import S_ACT_BASE, S_BELIEF, S_SELECT, Streams, StreamRandom
 
 INF = float("inf")
 S_BELIEF_NESTED = 3   # the level-0 planner's random.Random(config.seed) (intmcp.py:66)
+S_BELIEF_MID = 5      # nesting level 2: the level-1 planner's random.Random(config.seed)
 
 
 class _Tree:
@@ -335,12 +336,20 @@ class _Planner:
             self.search_depth = max(self.search_depth, d)
 
     # --------------------------------------------------------------- update
-    def _nested_dist(self, n):                           # intmcp.py:334-362
-        b = self.tree.belief[n]
-        counts = {}
-        for p in b:
-            counts[p[1]] = counts.get(p[1], 0) + 1
-        return {h: 0 + 1.0 * (c / len(b)) for h, c in counts.items()}
+    def _nested_dist(self, dist):                        # intmcp.py:334-362
+        """The other agent's history distribution: every history of every
+        particle of the dist's nodes, weighted prob * count / size, in first-
+        occurrence order."""
+        out = {}
+        for n, prob in dist.items():
+            self.tree.traverse(n)
+            b = self.tree.belief[n]
+            counts = {}
+            for p in b:
+                counts[p[1]] = counts.get(p[1], 0) + 1
+            for h, c in counts.items():
+                out[h] = out.get(h, 0) + prob * (c / len(b))
+        return out
 
     def _initial_nested_update(self, dist):              # intmcp.py:216-268
         tr, m = self.tree, self.model
@@ -363,7 +372,7 @@ class _Planner:
                     parts.append((state, nid, 1))
             tr.belief[n] = parts
         if self.level > 0:
-            self.nested._initial_nested_update(self._nested_dist(next(iter(dist))))
+            self.nested._initial_nested_update(self._nested_dist(dist))
 
     def _nested_update(self, dist):                      # intmcp.py:270-300
         tr = self.tree
@@ -375,7 +384,7 @@ class _Planner:
             p, a = tr.parent[n]
             self._reinvigorate(n, a, tr.obs[n], math.ceil(prob * target))
         if self.level > 0:
-            self.nested._nested_update(self._nested_dist(next(iter(dist))))
+            self.nested._nested_update(self._nested_dist(dist))
 
     def update(self, action, obs):                       # intmcp.py:198-214
         tr = self.tree
@@ -414,20 +423,27 @@ class OracleINTMCP:
         """search_probs: {level: {agent id: None or action probabilities}}
         (the search_policies of INTMCP.initialize; None: all random)."""
         assert cfg.num_sims is not None
-        if nesting_level not in (0, 1):
-            raise NotImplementedError("nesting levels 0 and 1")
+        if nesting_level not in (0, 1, 2):
+            raise NotImplementedError("nesting levels 0-2")
         sp = search_probs or {}
-        other = model.possible_agents[1 - model.possible_agents.index(agent_id)]
-        if nesting_level == 0:
-            self.nested = None
-            self.top = _Planner(model, agent_id, cfg, 0, streams, S_BELIEF_NESTED,
-                                search_probs=sp.get(0))
-        else:
-            # construction order of INTMCP.initialize: the nested planner first
-            self.nested = _Planner(model, other, cfg, 0, streams, S_BELIEF_NESTED,
-                                   search_probs=sp.get(0))
-            self.top = _Planner(model, agent_id, cfg, 1, streams, S_BELIEF, nested=self.nested,
-                                search_probs=sp.get(1))
+        ids = model.possible_agents
+        ego = ids.index(agent_id)
+        # construction order of INTMCP.initialize (intmcp.py:964-986): the
+        # lowest level first; level 0 draws on S_BELIEF_NESTED, the top planner
+        # on S_BELIEF (nesting 0: the one planner is level 0), a middle level-1
+        # planner on S_BELIEF_MID.  Level k models agent ego if L - k is even.
+        planners = []
+        below = None
+        for level in range(nesting_level + 1):
+            who = ids[ego if (nesting_level - level) % 2 == 0 else 1 - ego]
+            stream = (S_BELIEF_NESTED if level == 0 else
+                      S_BELIEF if level == nesting_level else S_BELIEF_MID)
+            below = _Planner(model, who, cfg, level, streams, stream, nested=below,
+                             search_probs=sp.get(level))
+            planners.append(below)
+        self.planners = planners                       # by level
+        self.top = planners[-1]
+        self.nested = planners[-2] if nesting_level > 0 else None
         self.nesting_level = nesting_level
         self.cfg = cfg
         self.model = model

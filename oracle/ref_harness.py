@@ -196,11 +196,16 @@ def make_reference_intmcp(model, agent_id, cfg_kwargs, num_sims, streams, nestin
     P = import_reference()
     import posggym_baselines.planning.intmcp as im
     import posggym_baselines.planning.belief as B
-    from oracle.intmcp import S_BELIEF_NESTED
+    from oracle.intmcp import S_BELIEF_MID, S_BELIEF_NESTED
     from oracle.rng import S_BELIEF, S_SELECT, StreamRandom
 
     select = StreamRandom(streams, S_SELECT)
-    order = [StreamRandom(streams, S_BELIEF_NESTED), StreamRandom(streams, S_BELIEF)]
+    # lowest level first: level 0, [level 1 of a nesting-2 planner], the top
+    order = [StreamRandom(streams, S_BELIEF_NESTED)]
+    if nesting_level == 2:
+        order.append(StreamRandom(streams, S_BELIEF_MID))
+    if nesting_level > 0:
+        order.append(StreamRandom(streams, S_BELIEF))
     made = []
 
     def new_random(seed=None):
@@ -291,23 +296,38 @@ def reference_intmcp_record(planner, searched, action):
     nested = planner.other_agent_policies[other]
     parts = [(p.t, model.pack_words(p.state), _hist_key(model, p.history.get_agent_history(other)))
              for p in root.belief.particles]
-    nested_nodes = []
-    seen = []
+    def node(n):
+        nparts = [(q.t, model.pack_words(q.state)) for q in n.belief.particles]
+        nkids = [(int(c.action), c.visits, c.value) for c in n.get_child_nodes()]
+        return (n.visits, nkids, nparts)
+
+    nested_nodes, seen, seen_nodes = [], [], []
     for p in root.belief.particles:
         h = p.history.get_agent_history(other)
         if h in seen:
             continue
         seen.append(h)
         n = _walk(nested.root, h)
-        if n is None:
-            nested_nodes.append((_hist_key(model, h), None))
-            continue
-        nparts = [(q.t, model.pack_words(q.state)) for q in n.belief.particles]
-        nkids = [(int(c.action), c.visits, c.value) for c in n.get_child_nodes()]
-        nested_nodes.append((_hist_key(model, h), (n.visits, nkids, nparts)))
+        seen_nodes.append(n)
+        nested_nodes.append((_hist_key(model, h), None if n is None else node(n)))
+    nested2 = None
+    if planner.nesting_level == 2:   # the third tree (the ego's level 0)
+        low = nested.other_agent_policies[planner.agent_id]
+        seqs, nodes2, seen2 = [], [], []
+        for n in seen_nodes:
+            seq = []
+            for q in ([] if n is None else n.belief.particles):
+                h2 = q.history.get_agent_history(planner.agent_id)
+                seq.append(_hist_key(model, h2))
+                if h2 not in seen2:
+                    seen2.append(h2)
+                    n2 = _walk(low.root, h2)
+                    nodes2.append((_hist_key(model, h2), None if n2 is None else node(n2)))
+            seqs.append(seq)
+        nested2 = (seqs, nodes2)
     st = planner.step_statistics
     return intmcp_record(rec, int(st["num_sims"]), int(st["search_depth"]), root.visits, kids,
-                         st["min_value"], st["max_value"], parts, nested_nodes)
+                         st["min_value"], st["max_value"], parts, nested_nodes, nested2=nested2)
 
 
 def reference_intmcp_episode(cfg_kwargs, num_sims, env_seed, ego="0", tree=0, max_steps=50,

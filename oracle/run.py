@@ -92,18 +92,34 @@ def oracle_intmcp_record(p, searched, action):
         return intmcp_record(rec, top.num_sims, top.search_depth, tr.visits[n], kids,
                              top.mm_min, top.mm_max, parts, [])
     parts = [(q[2], p.model.pack_words(q[0]), p.history(nested.tree, q[1])) for q in tr.belief[n]]
+
+    def node(pl, m):
+        t = pl.tree
+        nkids = [(a, t.stats[(m, a)][0], t.stats[(m, a)][1]) for a in t.order[m]]
+        nparts = [(r[-1], p.model.pack_words(r[0])) for r in t.belief[m]]
+        return (t.visits[m], nkids, nparts)
+
     nested_nodes, seen = [], []
     for q in tr.belief[n]:
         if q[1] in seen:
             continue
         seen.append(q[1])
-        nt = nested.tree
-        m = q[1]
-        nkids = [(a, nt.stats[(m, a)][0], nt.stats[(m, a)][1]) for a in nt.order[m]]
-        nparts = [(r[1], p.model.pack_words(r[0])) for r in nt.belief[m]]
-        nested_nodes.append((p.history(nt, m), (nt.visits[m], nkids, nparts)))
+        nested_nodes.append((p.history(nested.tree, q[1]), node(nested, q[1])))
+    nested2 = None
+    if p.nesting_level == 2:   # the third tree: histories carried by the second tree's particles
+        low = p.planners[0]
+        seqs, nodes2, seen2 = [], [], []
+        for m in seen:
+            seq = []
+            for r in nested.tree.belief[m]:
+                seq.append(p.history(low.tree, r[1]))
+                if r[1] not in seen2:
+                    seen2.append(r[1])
+                    nodes2.append((p.history(low.tree, r[1]), node(low, r[1])))
+            seqs.append(seq)
+        nested2 = (seqs, nodes2)
     return intmcp_record(rec, top.num_sims, top.search_depth, tr.visits[n], kids,
-                         top.mm_min, top.mm_max, parts, nested_nodes)
+                         top.mm_min, top.mm_max, parts, nested_nodes, nested2=nested2)
 
 
 def oracle_intmcp_episode(cfg_kwargs, num_sims, env_seed, ego="0", tree=0, max_steps=50,

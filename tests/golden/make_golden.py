@@ -103,6 +103,18 @@ INTMCP0_CASES = {
 }
 
 
+# I-NTMCP nesting_level=2: the ego's level-2 tree over the other agent's
+# level-1 planner over the ego's level-0 planner (intmcp.py:950-994 recursion,
+# _nested_sim dispatch intmcp.py:434-436); search_time_limit = 0.1 * 3
+INTMCP2_CFG = dict(TEST_CFG, search_time_limit=0.3, state_belief_only=False)
+INTMCP2_CASES = {
+    "intmcp2_ucb": ({}, 32, [(60, 60)], "0", 25, "Driving-v1"),
+    "intmcp2_ego1_uniform": ({"action_selection": "uniform"}, 24, [(61, 61)], "1", 20,
+                             "Driving-v1"),
+    "intmcp2_pe": ({}, 24, [(62, 62)], "1", 30, "PursuitEvasion-v1"),
+}
+
+
 # I-NTMCP with caller-supplied search policies (intmcp.py:956-971):
 # {level: {agent: probs}} -> SearchPolicyWrapper(FixedDistributionPolicy) on
 # the agent's action stream, RandomSearchPolicy for the agents left out.
@@ -116,6 +128,10 @@ INTMCP_SP_CASES = {
     "intmcp_sp_pe": (1, {1: {"1": [0.25, 0.25, 0.4, 0.1]},
                          0: {"0": [0.1, 0.2, 0.3, 0.4], "1": [0.7, 0.1, 0.1, 0.1]}},
                      32, [(52, 52)], "1", 100, "PursuitEvasion-v1"),
+    "intmcp2_sp_ucb": (2, {2: {"0": [0.1, 0.4, 0.2, 0.2, 0.1]},
+                           1: {"0": [0.2, 0.2, 0.2, 0.3, 0.1], "1": [0.5, 0.1, 0.1, 0.2, 0.1]},
+                           0: {"1": [0.05, 0.05, 0.3, 0.3, 0.3]}},
+                       24, [(66, 66)], "0", 20, "Driving-v1"),
 }
 
 
@@ -123,7 +139,10 @@ def run_intmcp_case(name):
     sp = None
     if name in INTMCP_SP_CASES:
         level, sp, num_sims, pairs, ego, max_steps, env = INTMCP_SP_CASES[name]
-        over, base = {}, (INTMCP0_CFG if level == 0 else INTMCP_CFG)
+        over, base = {}, (INTMCP0_CFG, INTMCP_CFG, INTMCP2_CFG)[level]
+    elif name in INTMCP2_CASES:
+        over, num_sims, pairs, ego, max_steps, env = INTMCP2_CASES[name]
+        base, level = INTMCP2_CFG, 2
     elif name in INTMCP0_CASES:
         over, num_sims, pairs, ego, max_steps, env = INTMCP0_CASES[name]
         base, level = INTMCP0_CFG, 0
@@ -409,7 +428,8 @@ def main(only=None, out_dir=HERE):
         _write(out_dir, name, data)
         n = sum(len(e["records"]) for e in data["episodes"])
         print(f"{name}: {len(data['episodes'])} episodes, {n} records")
-    for name in (list(INTMCP_CASES) + list(INTMCP0_CASES) + list(INTMCP_SP_CASES) if only is None
+    for name in (list(INTMCP_CASES) + list(INTMCP0_CASES) + list(INTMCP2_CASES)
+                 + list(INTMCP_SP_CASES) if only is None
                  else (only if isinstance(only, list) else ())):
         data = run_intmcp_case(name)
         _write(out_dir, name, data)

@@ -40,7 +40,10 @@ INTMCP_CASES = ["intmcp_ucb", "intmcp_ego1", "intmcp_uniform", "intmcp_deep", "i
 INTMCP0_CASES = ["intmcp0_ucb", "intmcp0_ego1_uniform", "intmcp0_deep", "intmcp0_pe"]
 
 # I-NTMCP with fixed-distribution search policies (make_golden.py INTMCP_SP_CASES)
-INTMCP_SP_CASES = ["intmcp_sp_ucb", "intmcp0_sp_ego1", "intmcp_sp_pe"]
+INTMCP_SP_CASES = ["intmcp_sp_ucb", "intmcp0_sp_ego1", "intmcp_sp_pe", "intmcp2_sp_ucb"]
+
+# I-NTMCP nesting_level=2 (make_golden.py INTMCP2_CASES): three trees
+INTMCP2_CASES = ["intmcp2_ucb", "intmcp2_ego1_uniform", "intmcp2_pe"]
 
 
 def search_probs(data):
