@@ -1103,7 +1103,7 @@ int pomcp_debug_set_spin_limit(pomcp_ctx* ctx, int32_t polls) {
 // Debug: per-wave phase cycles of k_search (diagnostics build only).
 int pomcp_debug_phase_timing(pomcp_ctx* ctx, uint64_t* out, int32_t capacity, int32_t* count) {
   if (!ctx || !count) return POMCP_E_INVALID;
-#ifndef POMCP_PHASE_TIMING
+#if !defined(POMCP_PHASE_TIMING) && !defined(PB_CLOG_TIMING)
   (void)out;
   (void)capacity;
   *count = 0;

@@ -419,13 +419,21 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_extract(DevParams p) {
   __syncthreads();
   const WaveLog wl(p.plog, p.Np, sw, p.tm);
   const uint32_t n = p.wlog[sw];
-  for (uint32_t base = 0; base < n; base += kWave * kLogWaves) {
+  constexpr uint32_t T = kWave * kLogWaves;
+  // the next pass's records are loaded while this pass runs
+  LogRec rn = {0xFFFFFFFFu, 0u, 0u};
+  uint32_t auxn = 0u;   // type-based: the particle's other-agent policy
+  if (threadIdx.x < n) {
+    rn = wl.load(threadIdx.x);
+    if (p.tm) auxn = wl.aux[threadIdx.x];
+  }
+  for (uint32_t base = 0; base < n; base += T) {
     const uint32_t i = base + (uint32_t)threadIdx.x;
-    LogRec r = {0xFFFFFFFFu, 0u, 0u};
-    uint32_t aux = 0u;   // type-based: the particle's other-agent policy
-    if (i < n) {
-      r = wl.load(i);
-      if (p.tm) aux = wl.aux[i];
+    const LogRec r = rn;
+    const uint32_t aux = auxn;
+    if (i + T < n) {
+      rn = wl.load(i + T);
+      if (p.tm) auxn = wl.aux[i + T];
     }
     const uint32_t l = r.id >> kIdBits;
     const bool m = i < n && want[l] == r.id;
@@ -638,6 +646,14 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
 // order (the alive blocks in ascending old order), which lets one ascending pass
 // decide reachability and move blocks in place.
 
+// Ordering of a workgroup's own global stores before its later (L1-bypassing,
+// ld_agent) loads: every tree (and every search wave's log) is owned by ONE
+// workgroup, so workgroup scope suffices.  (__threadfence() is agent scope: on
+// gfx950 its release writes back the XCD's whole L2 (buffer_wbl2) -- it was
+// 49% of k_compact_log, tools/clog_timing.py.)  The next kernel sees
+// everything: the end of a kernel releases at agent scope.
+__device__ __forceinline__ void wg_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+
 __device__ __forceinline__ int32_t ld_agent(const int32_t* p) {   // bypass the (stale) L1
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -669,7 +685,7 @@ __global__ __launch_bounds__(256) void k_compact(DevParams p) {
   // 1. parent of every block: the inline child slots of each block, then the
   //    live overflow entries
   for (int b = lane; b < nb; b += kWave) cpar[b] = -1;
-  __threadfence();
+  wg_fence();
   for (int b = lane; b < nb; b += kWave) {
     const uint4* blk = reinterpret_cast<const uint4*>(an + (int64_t)b * bstride);
     for (int a = 0; a < A; ++a) {
@@ -686,7 +702,7 @@ __global__ __launch_bounds__(256) void k_compact(DevParams p) {
     const uint64_t key = (uint64_t)w0.x | ((uint64_t)w0.y << 32);
     if ((uint32_t)(key >> kEpochShift) == epoch && (int)w1.x >= 0) cpar[(int)w1.x] = (int)(w0.z / (uint32_t)A);
   }
-  __threadfence();
+  wg_fence();
   // 2. reachability and the new numbering (ascending), alive list into cpar
   for (int b = lane; b < (R < 0 ? nb : R); b += kWave) cmap[b] = -1;
   int m = 0;
@@ -710,9 +726,9 @@ __global__ __launch_bounds__(256) void k_compact(DevParams p) {
     if (in) cmap[b] = alive ? idx : -1;
     if (alive) cpar[idx] = b;   // idx <= b: entries of this and later chunks already read
     m += __popcll(mk);
-    __threadfence();
+    wg_fence();
   }
-  __threadfence();
+  wg_fence();
   // 3. move the alive blocks down (in place, ascending), remapping the child
   //    block of every valid inline slot.  8 blocks per pass: all of a pass's
   //    parts are loaded before any is stored (a destination may be a source
@@ -749,7 +765,7 @@ __global__ __launch_bounds__(256) void k_compact(DevParams p) {
 #pragma unroll
     for (int q = 0; q < kPer; ++q)
       if (dst[q] >= 0) reinterpret_cast<uint4*>(an + (int64_t)dst[q] * bstride)[prt[q]] = v[q];
-    __threadfence();
+    wg_fence();
   }
   // 4. overflow map: live entries of alive action nodes are copied out (with the
   //    new action node and child block), the generation is bumped, and they are
@@ -788,7 +804,7 @@ __global__ __launch_bounds__(256) void k_compact(DevParams p) {
     clear_ovf(p, tree, lane);
     ne = 1u;
   }
-  __threadfence();
+  wg_fence();
   for (int i = 0; i < nlive; ++i) {
     const uint4 w0 = reinterpret_cast<const uint4*>(otmp + i)[0];
     const uint4 w1 = reinterpret_cast<const uint4*>(otmp + i)[1];
@@ -807,7 +823,7 @@ __global__ __launch_bounds__(256) void k_compact(DevParams p) {
           reinterpret_cast<uint4*>(e)[1] = make_uint4(w1.x, w1.y, 0u, 0u);
           onew[w1.z] = (int32_t)(p.ovf_base + b * kBucket + (uint32_t)L);
         }
-        __threadfence();
+        wg_fence();
         break;
       }
       b = (b + 1) & p.bucket_mask;
@@ -841,6 +857,32 @@ __device__ __forceinline__ uint64_t ld_agent_u64(const uint64_t* p) {
 // 64 kLogWaves consecutive records, one per thread; all of them are loaded
 // before any is stored, and a kept record goes to a place at or before its
 // own, so the log is filtered in place.
+// Section timing of k_compact_log (diagnostics builds, -DPB_CLOG_TIMING): thread
+// 0's s_memtime deltas per section and per-workgroup counters into
+// p.timing[search wave][16] (tools/clog_timing.py).
+#ifdef PB_CLOG_TIMING
+#define CL_MARK(s)                                                  \
+  do {                                                              \
+    if (t == 0) {                                                   \
+      __builtin_amdgcn_s_waitcnt(0);                                \
+      const uint64_t now_ = __builtin_amdgcn_s_memtime();           \
+      clt[s] += now_ - cl_last;                                     \
+      cl_last = now_;                                               \
+    }                                                               \
+  } while (0)
+#define CL_CNT(s, f)                                                \
+  do {                                                              \
+    const uint64_t m_ = __ballot(f);                                \
+    if (lane == 0 && m_) atomicAdd(&clc[s], (uint32_t)__popcll(m_)); \
+  } while (0)
+#else
+#define CL_MARK(s) \
+  do {             \
+  } while (0)
+#define CL_CNT(s, f) \
+  do {               \
+  } while (0)
+#endif
 template <class Env>
 __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
   __shared__ typename Env::Model sm;
@@ -859,6 +901,12 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
   __shared__ int32_t ovres[T];      // per thread: its overflow entry (-1: map full)
   __shared__ uint32_t ovd[5][T];    // per thread: tree lane, action node, key lo / hi, done
   __shared__ uint64_t fpl[T];       // the pass's children (flag word addresses), thread order
+#ifdef PB_CLOG_TIMING
+  uint64_t clt[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t cl_last = __builtin_amdgcn_s_memtime();
+  __shared__ uint32_t clc[8];
+  if (t < 8) clc[t] = 0u;
+#endif
   if (w == 0) {
     const int mytree = sw * kWave + lane;
     kept[lane] = 0;
@@ -888,20 +936,30 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
   const uint32_t A = (uint32_t)p.A;
   const int64_t bstride = blk_stride_lines(p.lines);
   uint32_t out = 0;
+  // the records of the next pass are loaded while this one runs (a pass's stores
+  // land below base + T, the next pass reads from base + T on)
+  LogRec rn = {0u, 0u, 0u};
+  uint32_t auxn = 0u;
+  if ((uint32_t)t < n) {
+    rn = wl.load(t);
+    if (p.tm) auxn = wl.aux[t];
+  }
   for (uint32_t base = 0; base < n; base += T) {
     const uint32_t i = base + (uint32_t)t;
-    LogRec r = {0u, 0u, 0u};
-    uint32_t aux = 0u;
+    LogRec r = rn;
+    uint32_t aux = auxn;
+    if (i + T < n) {
+      rn = wl.load(i + T);
+      if (p.tm) auxn = wl.aux[i + T];
+    }
     bool keep = false, mat = false;
     uint32_t l = 0u, nani = 0u;
     uint64_t okey = 0ull;
     int done = 0;
     int32_t nid = -1;
     int32_t* vis = nullptr;   // the node's visits (zeroed by k_compact): + 1 per record
-    const int tree = sw * kWave + (int)((i < n ? wl.id[i] : 0u) >> kIdBits);
+    const int tree = sw * kWave + (int)((i < n ? r.id : 0u) >> kIdBits);
     if (i < n) {
-      r = wl.load(i);
-      if (p.tm) aux = wl.aux[i];
       l = r.id >> kIdBits;
       const uint32_t id = r.id & kIdMask;
       keep = true;
@@ -931,6 +989,9 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
         keep = nid >= 0 || mat;
       }
     }
+    CL_MARK(0);
+    CL_CNT(0, i < n);
+    CL_CNT(1, mat);
     // ---- deferred records: find or insert the child
     if (__syncthreads_or(mat ? 1 : 0)) {
       uint32_t* flagw = nullptr;   // the word holding the child's absorbing flag ...
@@ -971,11 +1032,43 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
           flagw = reinterpret_cast<uint32_t*>(sl0 + ks) + 1;
           fbit = 1u << 31;
         } else {
-          need_ovf = true;
+          // an overflow child made by an earlier pass (or by the search): every
+          // thread looks its own up (read-only probe in insertion order: a bucket
+          // holding the key, else the first bucket with a free entry ends it)
+          OvfSlot* const ovf = p.ovf + (int64_t)tree * p.H;
+          const uint32_t epoch = (uint32_t)p.hdr[tree].epoch;   // k_compact's generation
+          const uint64_t key = okey | ((uint64_t)epoch << kEpochShift);
+          uint32_t b = ovf_hash(nani, okey) & p.bucket_mask;
+          int32_t jid = -1;
+          for (uint32_t probe = 0; probe <= p.bucket_mask; ++probe) {
+            bool free = false;
+#pragma unroll 4
+            for (int e = 0; e < kBucket; ++e) {
+              OvfSlot* const ep = ovf + (int64_t)b * kBucket + e;
+              const uint64_t sk = ld_agent_u64(&ep->key);
+              const uint32_t san = ld_agent_u32(&ep->an);
+              const bool live = (uint32_t)(sk >> kEpochShift) == epoch;
+              if (jid < 0 && live && sk == key && san == nani) jid = (int32_t)(b * kBucket + (uint32_t)e);
+              free |= !live;
+            }
+            if (jid >= 0 || free) break;
+            b = (b + 1) & p.bucket_mask;
+          }
+          if (jid >= 0) {
+            nid = (int32_t)(p.ovf_base + (uint32_t)jid);
+            vis = &ovf[jid].visits;
+            flagw = &ovf[jid].flags;
+            fbit = 1u;
+          } else {
+            need_ovf = true;   // a new child: inserted below, in log order
+          }
         }
       }
-      // overflow map: the pass's such records in thread (= log) order, one at a
-      // time, by wave 0 (its 16 lanes probe a bucket)
+      // overflow map: the pass's records of NEW overflow children (and of the
+      // ones inserted earlier in the same pass), in thread (= log) order, one at
+      // a time, by wave 0 (its 16 lanes probe a bucket)
+      CL_MARK(1);
+      CL_CNT(2, need_ovf);
       int novf = 0;
       const int opos = wg_rank(need_ovf, &novf);
       if (need_ovf) {
@@ -1020,7 +1113,7 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
                   reinterpret_cast<uint4*>(e)[1] = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
                   atomicAdd(&made[jl], 1);
                 }
-                __threadfence();
+                wg_fence();
                 jid = (int32_t)(b * kBucket + (uint32_t)L);
               }
               b = (b + 1) & p.bucket_mask;
@@ -1043,6 +1136,7 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
           }
         }
       }
+      CL_MARK(2);
       // the absorbing flag of each child = that of its last arrival: the pass's
       // children in thread order; the last thread naming a child sets it
       int nf = 0;
@@ -1058,7 +1152,9 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
           else atomicAnd(flagw, ~fbit);
         }
       }
-      __threadfence();   // the pass's inserts and flags land before the next pass's
+      wg_fence();   // the pass's inserts and flags land before the next pass's
+      CL_MARK(3);
+      CL_CNT(3, flagw != nullptr);
     }
     if (act[l] && i < n) {
       if (vis != nullptr) atomicAdd(vis, 1);
@@ -1072,8 +1168,16 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
       if (p.tm) wl.aux[out + (uint32_t)at] = aux;
     }
     out += (uint32_t)nk;
+    CL_MARK(4);
+    CL_CNT(4, keep);
   }
   __syncthreads();
+#ifdef PB_CLOG_TIMING
+  if (t == 0 && p.timing != nullptr) {
+    for (int q = 0; q < 5; ++q) p.timing[sw * 16 + q] = clt[q];
+    for (int q = 0; q < 5; ++q) p.timing[sw * 16 + 8 + q] = clc[q];
+  }
+#endif
   if (w == 0) {
     const int mytree = sw * kWave + lane;
     if (mytree < p.B) {
