@@ -7,7 +7,10 @@
  * tree, random search policies.  One planner pair per "tree" index; many
  * pairs per call (a batched launch).  nesting_level = 0: one level-0 planner
  * per index (its tree is tree 1 of the diagnostics below; the other agent acts
- * by the planner's own random choice, intmcp.py:750-753).  Paths relative to
+ * by the planner's own random choice, intmcp.py:750-753).  nesting_level = 2:
+ * three trees per index -- tree 0 the planner's (level 2), tree 1 the other
+ * agent's level-1 planner, tree 2 the level-0 planner of the planner's agent
+ * (INTMCP.initialize's recursion, intmcp.py:950-994).  Paths relative to
  * posggym_baselines/planning/ in the reference.
  *
  * Same conventions as pomcp.h (plain pointers, POMCP_* status codes, a
@@ -27,7 +30,7 @@ extern "C" {
 typedef struct intmcp_config {
   pomcp_config base;              /* MCTSConfig + model + tables (num_trees = planner pairs) */
   int32_t state_belief_only;      /* MCTSConfig.state_belief_only (test config: 0) */
-  int32_t nesting_level;          /* 1 or 0 (INTMCP.initialize's nesting_level) */
+  int32_t nesting_level;          /* 0, 1 or 2 (INTMCP.initialize's nesting_level) */
   int64_t max_nodes;              /* obs nodes per tree */
   int64_t max_stats;              /* action-node statistics entries per tree (A per expanded node) */
   int64_t max_log;                /* particle log records per tree (16 B) */
@@ -91,7 +94,8 @@ int intmcp_get_root_belief(intmcp_ctx* ctx, int32_t pair, uint32_t* out, int32_t
  * visits i32, t i32, stats i32, -, obs key u64; info = parent action:3 |
  * absorbing:1 | path_ok:1 | registered:3 | registration order 6 x 3 bits) and
  * statistics entries (32 B: visits i32, -, value f64, total f64, agg f64 = 0: not kept);
- * tree 0 = level 1, tree 1 = level 0. */
+ * tree 0 = the planner's (top) level, tree 1 the level below, tree 2 (nesting
+ * level 2) level 0. */
 int intmcp_get_nodes(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int32_t capacity,
                      int32_t* count);
 int intmcp_get_stats(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int32_t capacity,
@@ -101,6 +105,22 @@ int intmcp_get_stats(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int
 int intmcp_get_support(intmcp_ctx* ctx, int32_t pair, int32_t* entries, int32_t capacity_entries,
                        int32_t* n_entries, uint32_t* particles, int32_t capacity_particles,
                        int32_t* n_particles);
+/* Nesting level 2: the level-1 (middle, tree 1) planner's materialised beliefs
+ * of the histories in the top root belief: entries (node, offset, size,
+ * capacity) and their (v0, v1, level-0 node id) particles.  POMCP_E_INVALID at
+ * other nesting levels.  (intmcp_get_support is always the level-0 tree's.) */
+int intmcp_get_mid_support(intmcp_ctx* ctx, int32_t pair, int32_t* entries, int32_t capacity_entries,
+                           int32_t* n_entries, uint32_t* particles, int32_t capacity_particles,
+                           int32_t* n_particles);
+/* One chunk of get_action at one nesting level (level <= the planner's):
+ * `sims` simulations at `level` (intmcp.py:385-392; the wall-clock loop of a
+ * nesting-level-2 planner is a sequence of these).  flags as
+ * intmcp_search_levels. */
+int intmcp_search_level(intmcp_ctx* ctx, int32_t level, int32_t sims, int32_t flags,
+                        int32_t* actions_out);
+/* Arena counters of every pair: out[pair][tree][{nodes, log records, stats}]
+ * for trees 0..2 (zeros for a tree the nesting level does not have), B x 9. */
+int intmcp_get_tree_counts(intmcp_ctx* ctx, int32_t* out);
 /* INTMCP.initialize's search_policies (intmcp.py:956-971): the search policy of
  * agent `agent` at nesting level `level` -- NULL: RandomSearchPolicy
  * (Discrete.sample(), the default), else the num_actions probabilities of a

@@ -57,7 +57,8 @@ constexpr int64_t kImRec = 32;                              // {total f64, 2 x {
 constexpr int64_t kImRecs = 6 * kImRec;                     // records of actions 0..5 (kImMaxA)
 constexpr int64_t kImBlock = kImLine + kImRecs;             // 320 B per node (packed extraction ABI)
 // Nodes are interleaved by wavefront: per wave [2 trees][Nn] slabs of W nodes
-// (W = 64, fewer in a last partial wave), each slab = the W node lines then
+// (W = 64, fewer in a last partial wave; nt trees: [nt trees][Nn] at nesting
+// level 2), each slab = the W node lines then
 // the W nodes' records ([W][128 B] [W][192 B]), so the pairs of a wave keep
 // node n of their trees side by side (a view load is W whole lines) and a
 // wave's loads spread over the slabs in use, not over 64 separate per-pair
@@ -71,9 +72,10 @@ __host__ __device__ __forceinline__ int64_t im_node_stride(int B, int b) {   // 
   return (int64_t)im_wave_width(B, b) * kImBlock;
 }
 // node n's line (tree k of pair b)
-__host__ __device__ __forceinline__ int64_t im_node_off(int64_t Nn, int B, int b, int k, int64_t n) {
+__host__ __device__ __forceinline__ int64_t im_node_off(int64_t Nn, int B, int b, int k, int64_t n,
+                                                       int nt) {
   const int64_t w0 = b - b % kWave;
-  return w0 * 2 * Nn * kImBlock + ((int64_t)k * Nn + n) * im_node_stride(B, b) + (b - w0) * kImLine;
+  return w0 * nt * Nn * kImBlock + ((int64_t)k * Nn + n) * im_node_stride(B, b) + (b - w0) * kImLine;
 }
 // a node's action records, relative to its line
 __host__ __device__ __forceinline__ int64_t im_rec_delta(int B, int b) {
@@ -118,20 +120,29 @@ struct ISup {           // a materialised level-0 belief
   int32_t node, off, size, cap;
 };
 
+// Trees of a pair: nesting level 1 -- tree 0 (the planner's level-1 tree) and
+// tree 1 (the other agent's level-0 tree); nesting level 2 (ImParams::nt = 3)
+// -- tree 0 (level 2, the planner), tree 1 (level 1, the other agent), tree 2
+// (level 0, the planner's agent again).  Tree k models agent ego if k is even.
+// The bottom tree (nt - 1) is the level-0 one: its beliefs are the "support"
+// (sup / supp); at nesting level 2 the middle tree's beliefs are sup1 / supp1.
+constexpr int kImMaxT = 3;
 struct IHdr {
-  int32_t n_nodes[2], n_stats[2], n_log[2];
+  int32_t n_nodes[kImMaxT], n_stats[kImMaxT], n_log[kImMaxT];
   int32_t cur, root_sel, root_size, sup_sel, n_sup, sup_used, err, last_action;
   int32_t num_sims, search_depth, sims_done, pad;
-  double mm_min[2], mm_max[2];
+  int32_t sup1_sel, n_sup1, sup1_used, pad1;   // nesting level 2: the middle tree's beliefs
+  double mm_min[kImMaxT], mm_max[kImMaxT];
   uint64_t seed;
   uint32_t tree_key;
-  uint32_t ctr[6];      // belief (level 1), select, model, act0, act1, belief (level 0)
+  uint32_t ctr[7];      // belief (top), select, model, act0, act1, belief (level 0), belief (middle)
 };
 
 struct ImParams {
   int32_t B, A, ego, other, sel, depth_limit, step_limit, n_target, extra, has_kb,
       state_belief_only,
-      nest0;            // nesting level 0: only tree 1, whose agent (p.other) is the planner
+      nest0,            // nesting level 0: only tree 1, whose agent (p.other) is the planner
+      nt;               // trees per pair in the arenas: 2 (nesting levels 0, 1) or 3 (level 2)
   double discount, c, limit_factor, kb_min, kb_max;
   int64_t Nn, Ns, Nl, H, Nr, Nsp;   // per tree: nodes, stat entries, log records, hash slots;
                                     // per pair: root belief, support particles
@@ -139,11 +150,14 @@ struct ImParams {
   char* nodes;          // node lines + action records (kImBlock B a node), wave-interleaved:
                         // im_node_off, im_rec_delta
   int64_t nstride;      // kImBlock (the packed block size of the extraction ABI)
-  IHash* hash;          // [B][2][H] obs children beyond a record's inline slots
-  IRec* log;            // [B][2][Nl]
+  IHash* hash;          // [B][nt][H] obs children beyond a record's inline slots
+  IRec* log;            // [B][nt][Nl]
   uint4* root;          // [B][2][Nr] {v0, v1, nested, support slot}
-  ISup* sup;            // [B][2][Nr]
+  ISup* sup;            // [B][2][Nr] the bottom (level-0) tree's beliefs
   uint2* supp;          // [B][2][Nsp]
+  ISup* sup1;           // [B][2][Nr] nesting level 2: the middle tree's beliefs ...
+  uint4* supp1;         // [B][2][Nsp] ... {v0, v1, level-0 node, its support slot}
+  double* prob1;        // [B][Nr] nesting level 2: the middle tree's history distribution
   int4* path;           // [B][kImPath][3] path of the running simulation (deep levels)
   double* prob;         // [B][Nr] support probabilities (update scratch)
   const double* logtab;
@@ -168,9 +182,9 @@ struct ImParams {
   // sp_any: some table is fixed (else the draws stay the plain uniform ones)
   int32_t sp_any;
   unsigned long long* exact_draws;
-  int32_t sp_fixed[2][2];
-  double sp_cum[2][2][kImMaxA];
-  double sp_tot[2][2];
+  int32_t sp_fixed[kImMaxT][2];
+  double sp_cum[kImMaxT][2][kImMaxA];
+  double sp_tot[kImMaxT][2];
 };
 
 // Phase timing (diagnostics build, -DPOMCP_PHASE_TIMING): per-lane s_memtime
@@ -211,24 +225,29 @@ __host__ __device__ __forceinline__ int im_nreg(uint32_t info) { return (int)((i
 __host__ __device__ __forceinline__ int im_order(uint32_t info, int k) { return (int)((info >> (8 + 3 * k)) & 7u); }
 __device__ __forceinline__ bool im_has_stats(uint32_t info) { return (info & kImStatsBit) != 0u; }
 
-// One planner pair (lane): pointers, counters, RNG.
-template <class Env>
+// One planner pair (lane): pointers, counters, RNG.  NT: trees per pair
+// (== ImParams::nt: 2, or 3 at nesting level 2).
+template <class Env, int NT = 2>
 struct ImPair {
   using Model = typename Env::Model;
   static constexpr int kNA = Env::kA;   // == p.A (intmcp_create checks num_actions)
+  static constexpr int kBot = NT - 1;   // the level-0 tree
   const ImParams& p;
   const Model& m;
   int pair;
-  char* nb[2];     // node blocks of the level-1 (0) and level-0 (1) trees
+  char* nb[NT];    // node blocks of tree k (0: the planner's)
   int64_t ns;      // node n -> n + 1 (im_node_stride)
   int64_t ro;      // node line -> its action records (im_rec_delta)
-  IHash* hs[2];
-  IRec* lg[2];
+  IHash* hs[NT];
+  IRec* lg[NT];
   uint4* rootb;   // [2][Nr]
-  ISup* sup;      // [2][Nr]
+  ISup* sup;      // [2][Nr] the level-0 tree's beliefs
   uint2* supp;    // [2][Nsp]
+  ISup* sup1;     // [2][Nr] nesting level 2: the middle tree's beliefs
+  uint4* supp1;   // [2][Nsp]
   int4* path;
   double* prob;   // [Nr]
+  double* prob1;  // [Nr] nesting level 2
   IHdr h;
   // k_im_search only: math.log(N) for N < lt_n staged in LDS, and the level-1
   // root's view (this lane's column of an [kImRootWords][64] uint4 array),
@@ -246,7 +265,7 @@ struct ImPair {
   // wave waits on a load anyway; draw() consumes it.  Each stream is consumed
   // in order, so results are unchanged; stored counters exclude a computed but
   // unconsumed word (la_pend).
-  uint32_t la_w[6];
+  uint32_t la_w[7];
   uint32_t la_pend = 0u;
 #ifdef POMCP_PHASE_TIMING
   uint64_t pt[kImPhases] = {};
@@ -254,21 +273,31 @@ struct ImPair {
 #endif
 
   __device__ ImPair(const ImParams& pp, const Model& mm, int b) : p(pp), m(mm), pair(b) {
-    for (int k = 0; k < 2; ++k) {
-      nb[k] = p.nodes + im_node_off(p.Nn, p.B, b, k, 0);
-      hs[k] = p.hash + ((int64_t)b * 2 + k) * p.H;
-      lg[k] = p.log + ((int64_t)b * 2 + k) * p.Nl;
+    for (int k = 0; k < NT; ++k) {
+      nb[k] = p.nodes + im_node_off(p.Nn, p.B, b, k, 0, NT);
+      hs[k] = p.hash + ((int64_t)b * NT + k) * p.H;
+      lg[k] = p.log + ((int64_t)b * NT + k) * p.Nl;
     }
     ns = im_node_stride(p.B, b);
     ro = im_rec_delta(p.B, b);
     rootb = p.root + (int64_t)b * 2 * p.Nr;
     sup = p.sup + (int64_t)b * 2 * p.Nr;
     supp = p.supp + (int64_t)b * 2 * p.Nsp;
+    if constexpr (NT == 3) {
+      sup1 = p.sup1 + (int64_t)b * 2 * p.Nr;
+      supp1 = p.supp1 + (int64_t)b * 2 * p.Nsp;
+      prob1 = p.prob1 + (int64_t)b * p.Nr;
+    } else {
+      sup1 = nullptr;
+      supp1 = nullptr;
+      prob1 = nullptr;
+    }
     path = p.path + (int64_t)b * kImPath * 3;
     prob = p.prob + (int64_t)b * p.Nr;
     h = p.hdr[b];
     dp = p.dpow;
   }
+  static constexpr int kCtrs = NT == 3 ? 7 : 6;   // RNG streams in use
   __device__ __forceinline__ uint32_t ctr_stored(int q) const { return h.ctr[q] - ((la_pend >> q) & 1u); }
   // intmcp.py:326-330 (_prune_traverse's clear_belief at every update): the
   // particles of nodes more than two steps behind the current one are dropped
@@ -282,7 +311,7 @@ struct ImPair {
   __device__ void store() {
     IHdr o = h;
 #pragma unroll
-    for (int q = 0; q < 6; ++q) o.ctr[q] = ctr_stored(q);
+    for (int q = 0; q < kCtrs; ++q) o.ctr[q] = ctr_stored(q);
     p.hdr[pair] = o;
   }
   // what a search changes (k_im_search): the other fields need not stay live
@@ -290,7 +319,7 @@ struct ImPair {
   __device__ void store_search() {
     IHdr& o = p.hdr[pair];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < NT; ++k) {
       o.n_nodes[k] = h.n_nodes[k];
       o.n_stats[k] = h.n_stats[k];
       o.n_log[k] = h.n_log[k];
@@ -298,7 +327,7 @@ struct ImPair {
       o.mm_max[k] = h.mm_max[k];
     }
 #pragma unroll
-    for (int q = 0; q < 6; ++q) o.ctr[q] = ctr_stored(q);
+    for (int q = 0; q < kCtrs; ++q) o.ctr[q] = ctr_stored(q);
     o.err = h.err;
     o.last_action = h.last_action;
     o.num_sims = h.num_sims;
@@ -400,10 +429,10 @@ struct ImPair {
     return philox_word(h.seed, h.tree_key, stream, h.ctr[slot]++);
   }
   __device__ __forceinline__ void la_fill() {
-    constexpr uint32_t st[6] = {S_BELIEF, S_SELECT, S_MODEL, S_ACT_BASE, S_ACT_BASE + 1,
-                                S_BELIEF_NESTED};
+    constexpr uint32_t st[7] = {S_BELIEF, S_SELECT, S_MODEL, S_ACT_BASE, S_ACT_BASE + 1,
+                                S_BELIEF_NESTED, S_BELIEF_MID};
 #pragma unroll
-    for (int q = 0; q < 6; ++q) {
+    for (int q = 0; q < kCtrs; ++q) {
       if (q == 2 && !Env::kStepDraws) continue;
       if (!((la_pend >> q) & 1u)) {
         la_w[q] = philox_word(h.seed, h.tree_key, st[q], h.ctr[q]++);
@@ -411,8 +440,13 @@ struct ImPair {
       }
     }
   }
-  __device__ __forceinline__ uint32_t d_bel(int level, uint32_t n) {   // planner random.Random(seed)
-    return level == 1 ? uniform_int(draw(0, S_BELIEF), n) : uniform_int(draw(5, S_BELIEF_NESTED), n);
+  // tree k's planner's random.Random(seed): the top planner's S_BELIEF, the
+  // level-0 planner's S_BELIEF_NESTED, a middle (level-1, nesting 2) planner's
+  // S_BELIEF_MID (the oracle's streams, oracle/intmcp.py OracleINTMCP)
+  __device__ __forceinline__ uint32_t d_bel(int k, uint32_t n) {
+    if (k == kBot) return uniform_int(draw(5, S_BELIEF_NESTED), n);
+    if (k == 0) return uniform_int(draw(0, S_BELIEF), n);
+    return uniform_int(draw(6, S_BELIEF_MID), n);
   }
   __device__ __forceinline__ uint32_t d_sel(uint32_t n) { return uniform_int(draw(1, S_SELECT), n); }
   __device__ __forceinline__ double d_sel_float() { return uniform_float(draw(1, S_SELECT)); }
@@ -607,7 +641,7 @@ struct ImPair {
 
   // ------------------------------------------------------------- selection
   // the agent of tree k: k = 0 the ego, k = 1 the other agent
-  __device__ int agent(int k) const { return k == 0 ? p.ego : p.other; }
+  __device__ int agent(int k) const { return (k & 1) == 0 ? p.ego : p.other; }
   // the planner's own tree: 0 (nesting level 1), 1 (nesting level 0)
   __device__ int top() const { return p.nest0 ? 1 : 0; }
 
@@ -711,28 +745,29 @@ struct ImPair {
     return nxt;
   }
 
-  // INTMCP.sample_action of the level-0 planner (intmcp.py:763-791) at node n
-  __device__ int sample_action(int n) {
-    View v = view(1, n);                // node + statistics: one round trip
-    return sample_action(n, v, -1, nullptr);
+  // INTMCP.sample_action (intmcp.py:763-791) of tree j's planner (the level
+  // below its caller's, tree j - 1) at node n
+  __device__ int sample_action(int j, int n) {
+    View v = view(j, n);                // node + statistics: one round trip
+    return sample_action(j, n, v, -1, nullptr);
   }
   // pn / pnx: a node the caller holds current (the previous level's history
   // node: usually n's parent), so the traverse of a fresh history node
   // registers it at its parent without reading either
-  __device__ int sample_action(int n, View& v, int pn = -1, INode* pnx = nullptr) {
+  __device__ int sample_action(int j, int n, View& v, int pn = -1, INode* pnx = nullptr) {
     if (n > 0 && !im_path_ok(v.x.info)) {
-      if (pnx != nullptr && v.x.parent == pn) {   // traverse(1, n), first step known
-        reg_known(1, pn, (int)im_paction(v.x.info), *pnx);
-        N(1, n).info = v.x.info | (1u << 4);
-        if (pn > 0 && !im_path_ok(pnx->info)) traverse(1, pn);
+      if (pnx != nullptr && v.x.parent == pn) {   // traverse(j, n), first step known
+        reg_known(j, pn, (int)im_paction(v.x.info), *pnx);
+        N(j, n).info = v.x.info | (1u << 4);
+        if (pn > 0 && !im_path_ok(pnx->info)) traverse(j, pn);
       } else {
-        traverse(1, n);         // registers n's path at its ancestors; n itself
+        traverse(j, n);         // registers n's path at its ancestors; n itself
       }
       v.x.info |= 1u << 4;      // only gains the path_ok bit (no reload)
     }
     const INode& x = v.x;
     const int nr = im_nreg(x.info);
-    if (x.visits == 0 || nr == 0) return (int)d_pol(0, p.other);   // the level-1 caller's policy
+    if (x.visits == 0 || nr == 0) return (int)d_pol(j - 1, agent(j));   // the caller's policy
     uint4 q[kImMaxA];
     child_stats(v, nr, q);
     const double d = d_sel_float();   // random.choices' random() (the stream's only draw here)
@@ -816,8 +851,8 @@ struct ImPair {
 
   // the other agent's action from a particle of tree k (intmcp.py:602-615)
   __device__ int other_action(int k, uint32_t nested) {
-    if (k == 1 || p.state_belief_only) return (int)d_bel(k == 0 ? 1 : 0, (uint32_t)p.A);
-    return sample_action((int)nested);
+    if (k == kBot || p.state_belief_only) return (int)d_bel(k, (uint32_t)p.A);
+    return sample_action(k + 1, (int)nested);
   }
 
   // joint step for tree k's agent; the next particle's other-agent node
@@ -829,9 +864,9 @@ struct ImPair {
     Env::step(m, me, s0, s1, (uint32_t)a_self, (uint32_t)a_other, j, n0, n1, r, done);
     *okey = Env::obs_key(m, me, *n0, *n1);
     *nested_out = 0;
-    if (k == 0) {
-      const uint64_t ok = Env::obs_key(m, p.other, *n0, *n1);
-      const int c = child(1, (int)nested, a_other, ok);
+    if (k < kBot) {   // the other agent's history extension in tree k + 1
+      const uint64_t ok = Env::obs_key(m, agent(k + 1), *n0, *n1);
+      const int c = child(k + 1, (int)nested, a_other, ok);
       *nested_out = c < 0 ? 0u : (uint32_t)c;
     }
   }
@@ -900,8 +935,8 @@ struct ImPair {
     INode pnx;                 // the previous level's history node, as it is now
     int pn = -1;
     int roll_t = -1;           // >= 0: the descent ended at a leaf of this t
-    if (k == 0 && !p.state_belief_only) {   // the first level's history view, in flight
-      nv = view(1, (int)nested);            // while the root selection runs
+    if (k < kBot && !p.state_belief_only) {   // the first level's history view, in flight
+      nv = view(k + 1, (int)nested);          // while the root selection runs
       have_nv = true;
       la_fill();                            // (the RNG words, while it is in flight)
     }
@@ -927,11 +962,11 @@ struct ImPair {
         sa = sel4(q == a, v.sh[q], sa);
       // the other agent's action (intmcp.py:602-615): at level 1 its
       // history node's view was loaded when the previous level created it
-      const bool nested_k = k == 0 && !p.state_belief_only;
+      const bool nested_k = k < kBot && !p.state_belief_only;
       int ao;
       if (nested_k) {
-        if (!have_nv) nv = view(1, (int)nested);
-        ao = sample_action((int)nested, nv, pn, pn >= 0 ? &pnx : nullptr);
+        if (!have_nv) nv = view(k + 1, (int)nested);
+        ao = sample_action(k + 1, (int)nested, nv, pn, pn >= 0 ? &pnx : nullptr);
         pn = (int)nested;   // the next level's history node is a child of this one
         pnx = nv.x;
       } else {
@@ -941,7 +976,7 @@ struct ImPair {
       // (nested, ao), in flight during the step
       IM_MARK(IP_OTHER);
       Rec rn;
-      if (k == 0) rn = rec(1, (int)nested, ao);
+      if (k < kBot) rn = rec(k + 1, (int)nested, ao);
       uint32_t n0, n1, nn = 0u;
       double r;
       int done;
@@ -949,7 +984,7 @@ struct ImPair {
       const uint32_t j = Env::kStepDraws ? d_model(2) : 0u;
       Env::step(m, me, s0, s1, (uint32_t)a, (uint32_t)ao, j, &n0, &n1, &r, &done);
       const uint64_t okey = Env::obs_key(m, me, n0, n1);
-      const uint64_t ok = k == 0 ? Env::obs_key(m, p.other, n0, n1) : 0ull;
+      const uint64_t ok = k < kBot ? Env::obs_key(m, agent(k + 1), n0, n1) : 0ull;
       IM_MARK(IP_STEP);
       // the child (a, obs): found in the record, its view loaded; created,
       // its view is known (the descent writes its INode below).  Then, at
@@ -962,13 +997,13 @@ struct ImPair {
       if (c < 0) return depth;
       View cv;
       if (!created) cv = view(k, c);
-      if (k == 0) {
+      if (k < kBot) {
         bool ncr;
         INode nx;
-        const int cn = child_rec(1, (int)nested, ao, ok, rn, &ncr, nested_k ? nv.x.t : -1, &nx);
+        const int cn = child_rec(k + 1, (int)nested, ao, ok, rn, &ncr, nested_k ? nv.x.t : -1, &nx);
         nn = cn < 0 ? 0u : (uint32_t)cn;
         if (nested_k) {   // the next level's other-agent view (no wait)
-          nv = ncr ? fresh_view(nx) : view(1, (int)nn);
+          nv = ncr ? fresh_view(nx) : view(k + 1, (int)nn);
           have_nv = true;
         }
       }
@@ -1046,22 +1081,25 @@ struct ImPair {
   __device__ uint4* root_buf(int sel) { return rootb + (int64_t)sel * p.Nr; }
   __device__ ISup* sup_tab(int sel) { return sup + (int64_t)sel * p.Nr; }
   __device__ uint2* sup_parts(int sel) { return supp + (int64_t)sel * p.Nsp; }
+  __device__ ISup* sup1_tab(int sel) { return sup1 + (int64_t)sel * p.Nr; }
+  __device__ uint4* sup1_parts(int sel) { return supp1 + (int64_t)sel * p.Nsp; }
 
-  // the slot of level-0 node n in support table `sel` (count entries): the
+  // the slot of node n of tree k in the belief table tab (count entries): the
   // node's `support` field while the caller has that table's slots marked
-  // (mark_support), else a scan
-  __device__ int find_support(int sel, int n, int count) {
-    const uint32_t s = C(1, n).support;
-    if (s != kImNoSupport) return (int)s < count && sup_tab(sel)[s].node == n ? (int)s : -1;
-    const ISup* t = sup_tab(sel);
+  // (mark_slots), else a scan
+  __device__ int find_slot(int k, const ISup* tab, int n, int count) {
+    const uint32_t s = C(k, n).support;
+    if (s != kImNoSupport) return (int)s < count && tab[s].node == n ? (int)s : -1;
     for (int i = 0; i < count; ++i)
-      if (t[i].node == n) return i;
+      if (tab[i].node == n) return i;
     return -1;
   }
-  __device__ void mark_support(int sel, int count, bool on) {
-    const ISup* t = sup_tab(sel);
-    for (int i = 0; i < count; ++i) C(1, t[i].node).support = on ? (uint32_t)i : kImNoSupport;
+  __device__ void mark_slots(int k, const ISup* tab, int count, bool on) {
+    for (int i = 0; i < count; ++i) C(k, tab[i].node).support = on ? (uint32_t)i : kImNoSupport;
   }
+  // the level-0 tree's support table `sel`
+  __device__ int find_support(int sel, int n, int count) { return find_slot(kBot, sup_tab(sel), n, count); }
+  __device__ void mark_support(int sel, int count, bool on) { mark_slots(kBot, sup_tab(sel), count, on); }
 
   // BeliefRejectionSampler (belief.py:145-194, use_rejected_samples=True) for a
   // level-1 node n: parent particles from the previous root buffer; appends to
@@ -1086,7 +1124,7 @@ struct ImPair {
     // accepted go to [base, base + to_add), rejected to [base + to_add, ...)
     while (count < to_add && (double)attempts < limit) {
       ++attempts;
-      const uint4 hp = par[d_bel(1, (uint32_t)psize)];
+      const uint4 hp = par[d_bel(0, (uint32_t)psize)];
       const int ao = other_action(0, hp.z);
       uint32_t n0, n1, nn;
       double r;
@@ -1112,7 +1150,7 @@ struct ImPair {
     ISup& e = sup_tab(sel)[si];
     const int to_add = target - e.size;
     if (to_add <= 0) return;
-    const int par = N(1, n).parent;
+    const int par = N(kBot, n).parent;
     const int pi = find_support(sel ^ 1, par, h.pad);   // previous support count in pad
     if (pi < 0) {
       fail(POMCP_E_UNSUPPORTED);   // parent belief not materialised
@@ -1134,13 +1172,13 @@ struct ImPair {
     const int base = e.size;
     while (count < to_add && (double)attempts < limit) {
       ++attempts;
-      const uint2 hp = pp[d_bel(0, (uint32_t)pe.size)];
-      const int ao = (int)d_bel(0, (uint32_t)p.A);      // self._rng.choice (level 0)
+      const uint2 hp = pp[d_bel(kBot, (uint32_t)pe.size)];
+      const int ao = (int)d_bel(kBot, (uint32_t)p.A);   // self._rng.choice (level 0)
       uint32_t n0, n1, nn;
       double r;
       int done;
       uint64_t k2;
-      step(1, hp.x, hp.y, 0u, action, ao, &n0, &n1, &r, &done, &k2, &nn);
+      step(kBot, hp.x, hp.y, 0u, action, ao, &n0, &n1, &r, &done, &k2, &nn);
       const uint2 rec = make_uint2(n0, n1);
       if (k2 == okey) {
         cur[base + count++] = rec;
@@ -1153,22 +1191,74 @@ struct ImPair {
     for (int q = 0; q < fill; ++q) cur[base + count + q] = cur[base + to_add + q];
     e.size = base + count + fill;
   }
+
+  // nesting level 2: the same for a node of the middle (level-1) tree, whose
+  // particles carry the level-0 history (intmcp.py:815-862 at level 1: the
+  // other agent acts by the level-0 planner's sample_action, the particle's
+  // history extends in the level-0 tree); parents in the previous middle table
+  // (h.pad1 entries), appends to entry `si` of table `sel`
+  __device__ void reinvig_mid(int n, int action, uint64_t okey, int target, int sel, int si) {
+    ISup& e = sup1_tab(sel)[si];
+    const int to_add = target - e.size;
+    if (to_add <= 0) return;
+    const int par = N(1, n).parent;
+    const int pi = find_slot(1, sup1_tab(sel ^ 1), par, h.pad1);
+    if (pi < 0) {
+      fail(POMCP_E_UNSUPPORTED);   // parent belief not materialised
+      return;
+    }
+    const ISup pe = sup1_tab(sel ^ 1)[pi];
+    if (pe.size <= 0) {
+      fail(POMCP_E_STATE);
+      return;
+    }
+    const uint4* pp = sup1_parts(sel ^ 1) + pe.off;
+    uint4* cur = sup1_parts(sel) + e.off;
+    if (e.size + 2 * to_add > e.cap) {
+      fail(POMCP_E_ARENA);
+      return;
+    }
+    const double limit = p.limit_factor * (double)to_add;
+    int count = 0, attempts = 0, nrej = 0;
+    const int base = e.size;
+    while (count < to_add && (double)attempts < limit) {
+      ++attempts;
+      const uint4 hp = pp[d_bel(1, (uint32_t)pe.size)];
+      const int ao = other_action(1, hp.z);
+      uint32_t n0, n1, nn;
+      double r;
+      int done;
+      uint64_t k2;
+      step(1, hp.x, hp.y, hp.z, action, ao, &n0, &n1, &r, &done, &k2, &nn);
+      const uint4 rec = make_uint4(n0, n1, nn, 0u);
+      if (k2 == okey) {
+        cur[base + count++] = rec;
+      } else if (nrej < to_add) {
+        cur[base + to_add + nrej++] = rec;
+      }
+      if (h.err != 0) return;
+    }
+    int fill = to_add - count;
+    if (fill > nrej) fill = nrej;
+    for (int q = 0; q < fill; ++q) cur[base + count + q] = cur[base + to_add + q];
+    e.size = base + count + fill;
+  }
 };
 
-// Level-0 support of the root belief: distinct other-agent nodes in
-// first-occurrence order with probability count / size (intmcp.py:334-362);
-// writes support slots into the root buffer's .w.
+// The history distribution of a belief (intmcp.py:334-362 for one node of
+// probability 1): the distinct tree-k nodes named by the particles rb[0, size)
+// (.z) in first-occurrence order, probability count / size; writes each
+// particle's slot into .w.  (At nesting level 1: tree 1 from the level-1 root
+// belief; at level 2: tree 1 from the level-2 root belief.)
 // kWave: the 64 lanes of the wave run the same pair (k_im_update's wave mode,
 // every lane holding the same state) and share the scans: 64 records per
 // step, grouped per node / slot in lane order, so the result (first-occurrence
 // order, insertion order per slot) is the serial loop's.
 __device__ __forceinline__ uint64_t im_lanes_below() { return (1ull << (threadIdx.x & 63)) - 1ull; }
 
-template <class Env, bool kWave = false>
-__device__ void im_support(ImPair<Env>& P, int sel, int size, int* nsup) {
-  double* prob = P.prob;
-  uint4* rb = P.root_buf(P.h.root_sel);
-  ISup* tab = P.sup_tab(sel);
+template <class Env, int NT, bool kWave = false>
+__device__ void im_support(ImPair<Env, NT>& P, int k, ISup* tab, double* prob, uint4* rb, int size,
+                           int* nsup) {
   int n = 0;
   // node -> slot through the nodes' `support` field (kImNoSupport outside a
   // materialisation), not a scan of the table per particle: O(size), not
@@ -1183,12 +1273,12 @@ __device__ void im_support(ImPair<Env>& P, int sel, int size, int* nsup) {
         const int lead = __ffsll((long long)todo) - 1;
         const int ln = __shfl(nodeid, lead);
         const uint64_t peers = __ballot(on && nodeid == ln);
-        int s = (int)P.C(1, ln).support;
-        if (P.C(1, ln).support == kImNoSupport) {
+        int s = (int)P.C(k, ln).support;
+        if (P.C(k, ln).support == kImNoSupport) {
           s = n++;
           tab[s].node = ln;
           tab[s].size = 0;
-          P.C(1, ln).support = (uint32_t)s;
+          P.C(k, ln).support = (uint32_t)s;
         }
         tab[s].size += __popcll(peers);
         if (on && nodeid == ln) rb[i].w = (uint32_t)s;
@@ -1198,18 +1288,18 @@ __device__ void im_support(ImPair<Env>& P, int sel, int size, int* nsup) {
   } else {
     for (int i = 0; i < size; ++i) {
       const int nodeid = (int)rb[i].z;
-      int s = (int)P.C(1, nodeid).support;
-      if (P.C(1, nodeid).support == kImNoSupport) {
+      int s = (int)P.C(k, nodeid).support;
+      if (P.C(k, nodeid).support == kImNoSupport) {
         s = n++;
         tab[s].node = nodeid;
         tab[s].size = 0;   // count for now
-        P.C(1, nodeid).support = (uint32_t)s;
+        P.C(k, nodeid).support = (uint32_t)s;
       }
       tab[s].size += 1;
       rb[i].w = (uint32_t)s;
     }
   }
-  for (int q = 0; q < n; ++q) P.C(1, tab[q].node).support = kImNoSupport;
+  for (int q = 0; q < n; ++q) P.C(k, tab[q].node).support = kImNoSupport;
   for (int q = 0; q < n; ++q) {
     prob[q] = 0.0 + 1.0 * ((double)tab[q].size / (double)size);
     tab[q].size = 0;
@@ -1217,18 +1307,75 @@ __device__ void im_support(ImPair<Env>& P, int sel, int size, int* nsup) {
   *nsup = n;
 }
 
-// Materialise the level-0 support beliefs from the level-0 log (insertion
-// order), leaving `slack` free slots per entry for reinvigoration.
-template <class Env, bool kWave = false>
-__device__ void im_extract_support(ImPair<Env>& P, int sel, int nsup) {
-  ISup* tab = P.sup_tab(sel);
-  for (int q = 0; q < nsup; ++q) P.C(1, tab[q].node).support = (uint32_t)q;
+// Nesting level 2: get_nested_history_dist (intmcp.py:334-362) of the middle
+// tree's distribution (n1 entries of table t1, probabilities p1, particles
+// parts1 with the level-0 node in .z): for each entry in order, each distinct
+// level-0 node of its particles (first occurrence) gains p1 x count / size;
+// the nodes in first-occurrence order over all entries.  Writes the bottom
+// table `tab` (sizes zeroed) and `prob`, and each particle's slot into .w.
+// (A lane per pair, or the wave's lanes in lockstep on the same pair.)
+template <class Env, int NT>
+__device__ void im_support_nested(ImPair<Env, NT>& P, const ISup* t1, const double* p1, int n1,
+                                  uint4* parts1, ISup* tab, double* prob, int* nsup) {
+  constexpr int kB = NT - 1;
+  int n = 0;
+  for (int q = 0; q < n1; ++q) {
+    const ISup e = t1[q];
+    if (e.size <= 0) continue;   // (an empty belief contributes nothing; the reference divides by 0)
+    // counts of this entry's nodes: tab[].cap as the per-entry counter
+    const int first = n;
+    for (int i = 0; i < e.size; ++i) {
+      const int m = (int)parts1[e.off + i].z;
+      int s = (int)P.C(kB, m).support;
+      if (P.C(kB, m).support == kImNoSupport) {
+        s = n++;
+        tab[s].node = m;
+        tab[s].size = 0;
+        tab[s].cap = 0;
+        prob[s] = 0.0;
+        P.C(kB, m).support = (uint32_t)s;
+      }
+      if (tab[s].cap == 0) tab[s].off = -1;   // not yet counted in this entry
+      tab[s].cap += 1;
+      parts1[e.off + i].w = (uint32_t)s;
+    }
+    // add in first-occurrence order within the entry (the reference's dict order
+    // of h_count); the sum for each node runs over the entries in order
+    for (int i = 0; i < e.size; ++i) {
+      const int s = (int)parts1[e.off + i].w;
+      if (tab[s].off == -1) {
+        prob[s] = (s >= first ? 0.0 : prob[s]) + p1[q] * ((double)tab[s].cap / (double)e.size);
+        tab[s].off = 0;
+        tab[s].cap = 0;
+      }
+    }
+  }
+  for (int q = 0; q < n; ++q) {
+    P.C(kB, tab[q].node).support = kImNoSupport;
+    tab[q].size = 0;
+    tab[q].off = 0;
+    tab[q].cap = 0;
+  }
+  *nsup = n;
+}
+
+// Materialise the beliefs of tree k's table entries (nsup, probabilities
+// prob) from that tree's log (insertion order), leaving room per entry for the
+// reinvigoration (accepted + rejected).  Part: uint2 {v0, v1} (the level-0
+// tree) or uint4 {v0, v1, level-0 node, -} (the middle tree at nesting 2).
+__device__ __forceinline__ void im_part(uint2* d, const IRec& r) { *d = make_uint2(r.v0, r.v1); }
+__device__ __forceinline__ void im_part(uint4* d, const IRec& r) { *d = make_uint4(r.v0, r.v1, r.nested, 0u); }
+
+template <class Env, int NT, bool kWave = false, class Part>
+__device__ void im_extract_support(ImPair<Env, NT>& P, int k, ISup* tab, Part* parts,
+                                   const double* prob, int nsup) {
+  for (int q = 0; q < nsup; ++q) P.C(k, tab[q].node).support = (uint32_t)q;
   for (int q = 0; q < nsup; ++q) tab[q].cap = 0;
-  const int nlog = P.h.n_log[1];
+  const int nlog = P.h.n_log[k];
   if constexpr (kWave) {
     for (int base = 0; base < nlog; base += kWave64) {
       const int i = base + (int)(threadIdx.x & 63);
-      const uint32_t s = i < nlog ? P.C(1, P.lg[1][i].node).support : kImNoSupport;
+      const uint32_t s = i < nlog ? P.C(k, P.lg[k][i].node).support : kImNoSupport;
       uint64_t todo = __ballot(s != kImNoSupport);
       while (todo) {
         const uint32_t ls = (uint32_t)__shfl((int)s, __ffsll((long long)todo) - 1);
@@ -1239,7 +1386,7 @@ __device__ void im_extract_support(ImPair<Env>& P, int sel, int nsup) {
     }
   } else {
     for (int i = 0; i < nlog; ++i) {
-      const uint32_t s = P.C(1, P.lg[1][i].node).support;
+      const uint32_t s = P.C(k, P.lg[k][i].node).support;
       if (s != kImNoSupport) tab[s].cap += 1;
     }
   }
@@ -1247,42 +1394,41 @@ __device__ void im_extract_support(ImPair<Env>& P, int sel, int nsup) {
   for (int q = 0; q < nsup; ++q) {   // room for the reinvigoration (accepted + rejected)
     tab[q].off = off;
     tab[q].size = 0;
-    tab[q].cap += 2 * (int)ceil(P.prob[q] * (double)P.p.n_target) + 2;
+    tab[q].cap += 2 * (int)ceil(prob[q] * (double)P.p.n_target) + 2;
     off += tab[q].cap;
   }
   if (off > P.p.Nsp) {
     P.fail(POMCP_E_ARENA);
-    for (int q = 0; q < nsup; ++q) P.C(1, tab[q].node).support = kImNoSupport;
+    for (int q = 0; q < nsup; ++q) P.C(k, tab[q].node).support = kImNoSupport;
     return;
   }
-  uint2* parts = P.sup_parts(sel);
   if constexpr (kWave) {
     for (int base = 0; base < nlog; base += kWave64) {
       const int i = base + (int)(threadIdx.x & 63);
       IRec r{0u, 0u, 0u, 0u};
       uint32_t s = kImNoSupport;
       if (i < nlog) {
-        r = P.lg[1][i];
-        s = P.C(1, r.node).support;
+        r = P.lg[k][i];
+        s = P.C(k, r.node).support;
       }
       uint64_t todo = __ballot(s != kImNoSupport);
       while (todo) {   // each slot of the batch: its records in lane (= insertion) order
         const uint32_t ls = (uint32_t)__shfl((int)s, __ffsll((long long)todo) - 1);
         const uint64_t peers = __ballot(s == ls);
         const int at = tab[ls].off + tab[ls].size;
-        if (s == ls) parts[at + __popcll(peers & im_lanes_below())] = make_uint2(r.v0, r.v1);
+        if (s == ls) im_part(parts + at + __popcll(peers & im_lanes_below()), r);
         tab[ls].size += __popcll(peers);
         todo &= ~peers;
       }
     }
   } else {
     for (int i = 0; i < nlog; ++i) {
-      const IRec r = P.lg[1][i];
-      const uint32_t s = P.C(1, r.node).support;
-      if (s != kImNoSupport) parts[tab[s].off + tab[s].size++] = make_uint2(r.v0, r.v1);
+      const IRec r = P.lg[k][i];
+      const uint32_t s = P.C(k, r.node).support;
+      if (s != kImNoSupport) im_part(parts + tab[s].off + tab[s].size++, r);
     }
   }
-  for (int q = 0; q < nsup; ++q) P.C(1, tab[q].node).support = kImNoSupport;
+  for (int q = 0; q < nsup; ++q) P.C(k, tab[q].node).support = kImNoSupport;
 }
 
 // Every obs-child map slot empty ({0, 0, -1}), grid-stride over all pairs'
@@ -1302,7 +1448,7 @@ __global__ __launch_bounds__(64) void k_im_reset(ImParams p) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= p.B) return;
   IHdr h = p.hdr[b];
-  for (int k = 0; k < 2; ++k) {   // (the hash tables: k_im_clear_hash, all lanes)
+  for (int k = 0; k < p.nt; ++k) {   // (the hash tables: k_im_clear_hash, all lanes)
     INode r;
     r.parent = -1;
     r.info = 1u << 4;   // path_ok
@@ -1312,7 +1458,7 @@ __global__ __launch_bounds__(64) void k_im_reset(ImParams p) {
     o.okey = 0;
     o.stats = -1;
     o.support = kImNoSupport;
-    char* const line = p.nodes + im_node_off(p.Nn, p.B, b, k, 0);
+    char* const line = p.nodes + im_node_off(p.Nn, p.B, b, k, 0, p.nt);
     *reinterpret_cast<INode*>(line) = r;
     *reinterpret_cast<ICold*>(line + kImCold) = o;
     h.n_nodes[k] = 1;
@@ -1333,13 +1479,17 @@ __global__ __launch_bounds__(64) void k_im_reset(ImParams p) {
   h.search_depth = 0;
   h.sims_done = 0;
   h.pad = 0;
+  h.sup1_sel = 0;
+  h.n_sup1 = 0;
+  h.sup1_used = 0;
+  h.pad1 = 0;
   p.hdr[b] = h;
 }
 
-template <class Env>
+template <class Env, int NT>
 template <bool kWave>
-__device__ void ImPair<Env>::clear_old_beliefs(int cur_t) {
-  for (int k = 0; k < 2; ++k) {
+__device__ void ImPair<Env, NT>::clear_old_beliefs(int cur_t) {
+  for (int k = 0; k < NT; ++k) {
     const int n = h.n_log[k];
     int out = 0;
     if constexpr (kWave) {   // 64 records per step; the chunk is loaded before it is stored
@@ -1412,7 +1562,7 @@ __device__ void im_update_nest0(ImPair<Env>& P, const typename Env::Model& sm, u
   // previous table)
   tab[0].node = node;
   P.prob[0] = 1.0;
-  im_extract_support<Env, kWave>(P, sel, 1);
+  im_extract_support<Env, 2, kWave>(P, 1, P.sup_tab(sel), P.sup_parts(sel), P.prob, 1);
   if (P.h.err != 0) return;
   P.h.pad = P.h.n_sup;
   P.mark_support(sel ^ 1, P.h.pad, true);
@@ -1425,6 +1575,237 @@ __device__ void im_update_nest0(ImPair<Env>& P, const typename Env::Model& sm, u
   P.h.n_sup = 1;
   P.h.sup_used = tab[0].off + tab[0].cap;
   if (P.h.err == 0) P.template clear_old_beliefs<kWave>(P.N(1, node).t);
+}
+
+// The level-0 (bottom, tree kBot) planner's initial beliefs
+// (_initial_nested_update, intmcp.py:216-268, at level 0) for the nsup entries
+// of table `sel` with probabilities prob: the probe draw of
+// sample_agent_initial_state(obs of the first history), then per entry
+// ceil-free `len(parts) < prob x target` draws.  Returns the particles used.
+template <class Env, int NT>
+__device__ int im_initial_bottom(ImPair<Env, NT>& P, const typename Env::Model& sm, int sel, int nsup,
+                                 const double* prob) {
+  constexpr int kB = NT - 1;
+  const ImParams& p = P.p;
+  auto draw_model = [&](uint32_t n) { return P.d_model(n); };
+  ISup* tab = P.sup_tab(sel);
+  uint32_t s0, s1;
+  const int who = P.agent(kB);
+  Env::sample_agent_initial(sm, who, P.C(kB, tab[0].node).okey, draw_model, &s0, &s1);   // probe
+  int off = 0;
+  for (int q = 0; q < nsup && P.h.err == 0; ++q) {
+    P.traverse(kB, tab[q].node);
+    const uint64_t oq = P.C(kB, tab[q].node).okey;
+    tab[q].off = off;
+    tab[q].size = 0;
+    uint2* pp = P.sup_parts(sel) + off;
+    int m = 0;
+    while ((double)m < prob[q] * (double)p.n_target) {
+      if (off + m >= p.Nsp) {
+        P.fail(POMCP_E_ARENA);
+        break;
+      }
+      Env::sample_agent_initial(sm, who, oq, draw_model, &s0, &s1);
+      pp[m++] = make_uint2(s0, s1);
+    }
+    tab[q].size = m;
+    tab[q].cap = m;
+    off += m;
+  }
+  return off;
+}
+
+// The top tree's new root belief at a re-root to `node`: its particle-log
+// records in insertion order (rb, returns the count)
+template <class Env, int NT, bool kWave>
+__device__ int im_extract_root(ImPair<Env, NT>& P, int node, uint4* rb) {
+  const ImParams& p = P.p;
+  int n = 0;
+  const int nlog = P.h.n_log[0];
+  if constexpr (kWave) {
+    for (int base = 0; base < nlog; base += kWave64) {
+      const int i = base + (int)(threadIdx.x & 63);
+      IRec r{0u, 0u, 0u, 0u};
+      if (i < nlog) r = P.lg[0][i];
+      const bool hit = i < nlog && (int)r.node == node;
+      const uint64_t m = __ballot(hit);
+      if (n + __popcll(m) > p.Nr) {
+        P.fail(POMCP_E_ARENA);
+        break;
+      }
+      if (hit) rb[n + __popcll(m & im_lanes_below())] = make_uint4(r.v0, r.v1, r.nested, 0u);
+      n += __popcll(m);
+    }
+  } else {
+    for (int i = 0; i < nlog; ++i) {
+      const IRec r = P.lg[0][i];
+      if ((int)r.node == node) {
+        if (n >= p.Nr) {
+          P.fail(POMCP_E_ARENA);
+          break;
+        }
+        rb[n++] = make_uint4(r.v0, r.v1, r.nested, 0u);
+      }
+    }
+  }
+  return n;
+}
+
+// INTMCP.update (intmcp.py:198-300) of a nesting-level-2 planner: tree 0's
+// re-root (or initial belief) and reinvigoration, then the middle planner's
+// (tree 1) _initial_nested_update / _nested_update over the history
+// distribution of the new root belief, then the level-0 planner's (tree 2)
+// over the middle beliefs' nested distribution (get_nested_history_dist,
+// intmcp.py:334-362, summed over every node of the distribution) -- the
+// oracle's order (oracle/intmcp.py _Planner.update / _nested_update).
+template <class Env, bool kWave>
+__device__ void im_update_nest2(ImPair<Env, 3>& P, const typename Env::Model& sm, uint64_t obs,
+                                int action) {
+  const ImParams& p = P.p;
+  auto draw_model = [&](uint32_t n) { return P.d_model(n); };
+  const bool initial = P.N(0, P.h.cur).t == 0;
+  int node, n = 0;
+  if (initial) {   // _initial_nested_update, level 2
+    node = P.child(0, 0, p.A, obs);
+    if (node < 0) return;
+    P.traverse(0, node);
+    uint32_t s0, s1;
+    if (!Env::sample_agent_initial(sm, p.ego, obs, draw_model, &s0, &s1)) P.fail(POMCP_E_INVALID);
+    P.h.root_sel ^= 1;
+    uint4* rb = P.root_buf(P.h.root_sel);
+    while (P.h.err == 0 && (double)n < 1.0 * (double)p.n_target) {
+      if (n >= p.Nr) {
+        P.fail(POMCP_E_ARENA);
+        break;
+      }
+      Env::sample_agent_initial(sm, p.ego, obs, draw_model, &s0, &s1);
+      const uint64_t ok = Env::obs_key(sm, p.other, s0, s1);
+      const int c = P.child(1, 0, p.A, ok);
+      rb[n++] = make_uint4(s0, s1, (uint32_t)(c < 0 ? 0 : c), 0u);
+    }
+  } else {         // _nested_update, level 2: re-root to (action, obs)
+    node = (action >= 0 && action < p.A) ? P.child(0, P.h.cur, action, obs) : -1;
+    if (node < 0) {
+      P.fail(POMCP_E_NOT_FOUND);
+      return;
+    }
+    P.traverse(0, node);
+    const int prev_size = P.h.root_size;
+    P.h.root_sel ^= 1;
+    n = im_extract_root<Env, 3, kWave>(P, node, P.root_buf(P.h.root_sel));
+    P.h.pad = prev_size;
+    if (!im_absorbing(P.N(0, node).info) && P.h.err == 0)
+      P.reinvig_top(node, action, obs, p.n_target, &n);   // ceil(1.0 * target)
+  }
+  P.h.cur = node;
+  P.h.root_size = n;
+  if (P.h.err != 0 || n == 0) return;
+  // ---- the middle (level-1) planner: the root belief's history distribution
+  const int sel1 = P.h.sup1_sel ^ 1;
+  ISup* t1 = P.sup1_tab(sel1);
+  uint4* q1 = P.sup1_parts(sel1);
+  int n1 = 0;
+  im_support<Env, 3, kWave>(P, 1, t1, P.prob1, P.root_buf(P.h.root_sel), n, &n1);
+  if (initial) {   // _initial_nested_update, level 1
+    uint32_t s0, s1;
+    Env::sample_agent_initial(sm, p.other, P.C(1, t1[0].node).okey, draw_model, &s0, &s1);   // probe
+    int off = 0;
+    for (int q = 0; q < n1 && P.h.err == 0; ++q) {
+      P.traverse(1, t1[q].node);
+      const uint64_t oq = P.C(1, t1[q].node).okey;
+      t1[q].off = off;
+      int m = 0;
+      while ((double)m < P.prob1[q] * (double)p.n_target) {
+        if (off + m >= p.Nsp) {
+          P.fail(POMCP_E_ARENA);
+          break;
+        }
+        Env::sample_agent_initial(sm, p.other, oq, draw_model, &s0, &s1);
+        const uint64_t ok = Env::obs_key(sm, p.ego, s0, s1);
+        const int c = P.child(2, 0, p.A, ok);
+        q1[off + m++] = make_uint4(s0, s1, (uint32_t)(c < 0 ? 0 : c), 0u);
+      }
+      t1[q].size = m;
+      t1[q].cap = m;
+      off += m;
+    }
+    P.h.sup1_used = off;
+  } else {         // _nested_update, level 1
+    im_extract_support<Env, 3, kWave>(P, 1, t1, q1, P.prob1, n1);
+    if (P.h.err != 0) return;
+    P.h.pad1 = P.h.n_sup1;   // the previous middle table (parents)
+    P.mark_slots(1, P.sup1_tab(sel1 ^ 1), P.h.pad1, true);
+    for (int q = 0; q < n1 && P.h.err == 0; ++q) {
+      const int m = t1[q].node;
+      P.traverse(1, m);
+      if (im_absorbing(P.N(1, m).info)) continue;
+      const int tq = (int)ceil(P.prob1[q] * (double)p.n_target);
+      P.reinvig_mid(m, (int)im_paction(P.N(1, m).info), P.C(1, m).okey, tq, sel1, q);
+    }
+    P.mark_slots(1, P.sup1_tab(sel1 ^ 1), P.h.pad1, false);
+    int used = 0;
+    for (int q = 0; q < n1; ++q) used = max(used, t1[q].off + t1[q].cap);
+    P.h.sup1_used = used;
+  }
+  P.h.sup1_sel = sel1;
+  P.h.n_sup1 = n1;
+  if (P.h.err != 0) return;
+  // ---- the level-0 planner: the middle beliefs' nested history distribution
+  const int sel = P.h.sup_sel ^ 1;
+  ISup* tab = P.sup_tab(sel);
+  int n2 = 0;
+  im_support_nested<Env, 3>(P, t1, P.prob1, n1, q1, tab, P.prob, &n2);
+  if (n2 == 0) {
+    P.fail(POMCP_E_STATE);
+    return;
+  }
+  if (initial) {
+    P.h.sup_used = im_initial_bottom<Env, 3>(P, sm, sel, n2, P.prob);
+  } else {
+    im_extract_support<Env, 3, kWave>(P, 2, tab, P.sup_parts(sel), P.prob, n2);
+    if (P.h.err != 0) return;
+    P.h.pad = P.h.n_sup;   // previous support count (parents)
+    P.mark_support(sel ^ 1, P.h.pad, true);
+    for (int q = 0; q < n2 && P.h.err == 0; ++q) {
+      const int m = tab[q].node;
+      P.traverse(2, m);
+      if (im_absorbing(P.N(2, m).info)) continue;
+      const int tq = (int)ceil(P.prob[q] * (double)p.n_target);
+      P.reinvig_nested(m, (int)im_paction(P.N(2, m).info), P.C(2, m).okey, tq, sel, q);
+    }
+    P.mark_support(sel ^ 1, P.h.pad, false);
+    int used = 0;
+    for (int q = 0; q < n2; ++q) used = max(used, tab[q].off + tab[q].cap);
+    P.h.sup_used = used;
+  }
+  P.h.sup_sel = sel;
+  P.h.n_sup = n2;
+  if (P.h.err == 0) P.template clear_old_beliefs<kWave>(P.N(0, node).t);
+}
+
+// k_im_update at nesting level 2 (three trees per pair; as k_im_update)
+template <class Env, bool kWave>
+__global__ __launch_bounds__(64) void k_im_update3(ImParams p) {
+  __shared__ typename Env::Model sm;
+  stage_model(p.model, sm);
+  const int b = kWave ? (int)blockIdx.x : (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (b >= p.B) return;
+  ImPair<Env, 3> P(p, sm, b);
+  const uint64_t obs = p.in_obs[b];
+  if (p.in_actions[b] == kImSkip) {
+    p.out[2 * b] = im_absorbing(P.N(0, P.h.cur).info) ? 1 : 0;
+    p.out[2 * b + 1] = P.h.err;
+    return;
+  }
+  P.h.num_sims = 0;
+  P.h.search_depth = 0;
+  if (P.h.err == 0 && !im_absorbing(P.N(0, P.h.cur).info))
+    im_update_nest2<Env, kWave>(P, sm, obs, p.in_actions[b]);
+  P.h.pad = 0;
+  P.h.pad1 = 0;
+  P.store();
+  p.out[2 * b] = im_absorbing(P.N(0, P.h.cur).info) ? 1 : 0;
+  p.out[2 * b + 1] = P.h.err;
 }
 
 // INTMCP.update (intmcp.py:198-300) for every pair.
@@ -1480,7 +1861,7 @@ __global__ __launch_bounds__(64) void k_im_update(ImParams p) {
         if (P.h.err == 0 && n > 0) {
           // level 0: support of the histories, their initial beliefs
           const int sel = P.h.sup_sel ^ 1;
-          im_support<Env, kWave>(P, sel, n, &nsup);
+          im_support<Env, 2, kWave>(P, 1, P.sup_tab(sel), P.prob, P.root_buf(P.h.root_sel), n, &nsup);
           ISup* tab = P.sup_tab(sel);
           const uint64_t o0 = P.C(1, tab[0].node).okey;
           Env::sample_agent_initial(sm, p.other, o0, draw_model, &s0, &s1);   // probe
@@ -1557,8 +1938,8 @@ __global__ __launch_bounds__(64) void k_im_update(ImParams p) {
         // level 0: support of the new root belief, materialised + reinvigorated
         if (P.h.err == 0 && n > 0) {
           const int sel = P.h.sup_sel ^ 1;
-          im_support<Env, kWave>(P, sel, n, &nsup);
-          im_extract_support<Env, kWave>(P, sel, nsup);
+          im_support<Env, 2, kWave>(P, 1, P.sup_tab(sel), P.prob, P.root_buf(P.h.root_sel), n, &nsup);
+          im_extract_support<Env, 2, kWave>(P, 1, P.sup_tab(sel), P.sup_parts(sel), P.prob, nsup);
           ISup* tab = P.sup_tab(sel);
           P.h.pad = P.h.n_sup;   // previous support count (parents)
           P.mark_support(sel ^ 1, P.h.pad, true);   // parents found by node, not by scan
@@ -1650,7 +2031,7 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
       ISup e_next = {0, 0, 0, 0};
       if (num_sims > 0) {
         // nesting level 0: every simulation starts at the root, support entry 0
-        if (!p.nest0) hp_next = rb[P.d_bel(1, (uint32_t)P.h.root_size)];
+        if (!p.nest0) hp_next = rb[P.d_bel(0, (uint32_t)P.h.root_size)];
         if (level == 0) e_next = stab[p.nest0 ? 0u : hp_next.w];
         if (level == 1) {   // the root's view, kept current by the backups (ImPair::rv)
           P.rv_put(P.view(0, root));
@@ -1661,7 +2042,7 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
         const uint4 hp = hp_next;
         const ISup e = e_next;
         if (s + 1 < num_sims && !p.nest0) {
-          hp_next = rb[P.d_bel(1, (uint32_t)P.h.root_size)];
+          hp_next = rb[P.d_bel(0, (uint32_t)P.h.root_size)];
           if (level == 0) e_next = stab[hp_next.w];
         }
         if (level == 0) {
@@ -1672,7 +2053,7 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
             P.fail(POMCP_E_UNSUPPORTED);   // depleted level-0 node (unreachable)
             break;
           }
-          const uint2 q = sparts[e.off + P.d_bel(0, (uint32_t)e.size)];
+          const uint2 q = sparts[e.off + P.d_bel(1, (uint32_t)e.size)];
           auto v = P.view(1, n);
           P.la_fill();   // the RNG words, while the start node's view is in flight
           if (n > 0 && !im_path_ok(v.x.info)) {
@@ -1720,6 +2101,133 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
       for (int i = 0; i < nr; ++i) {
         const int a = im_order(x.info, i);
         const uint32_t* const hd = P.H(T, root, a);
+        const double v = hilo_d(hd[1], hd[2]);
+        if (v == mx) {
+          ties[nt++] = a;
+        } else if (v > mx) {
+          mx = v;
+          ties[0] = a;
+          nt = 1;
+        }
+      }
+      action = ties[P.d_sel((uint32_t)nt)];
+    }
+  }
+  if (flags & kImFinal) P.h.last_action = action;
+  P.store_search();
+}
+
+// INTMCP.get_action (intmcp.py:368-408) at nesting level 2: sims[l]
+// simulations at level l = 0, 1, 2 in turn.  Every simulation samples a root
+// particle of the top planner (its stream); below level 2 it dispatches down
+// the levels (_nested_sim, intmcp.py:410-442): the middle planner's
+// traverse + expand of the particle's history node, a particle of its belief
+// (the middle stream), and at level 0 the same again in the level-0 tree; the
+// planner whose level is the search level runs _simulate.  (Correctness
+// first: a plain serial lane per pair, no lookahead of the next particle.)
+template <class Env>
+__global__ __launch_bounds__(64) void k_im_search3(ImParams p, int sims0, int sims1, int sims2,
+                                                   int flags) {
+  __shared__ typename Env::Model sm;
+  __shared__ double slog[kImLogLds];
+  __shared__ uint4 srv[kImRootWords * kWave];
+  __shared__ double sdp[kImDpowLds];
+  __shared__ uint64_t sexp[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) sexp[i] = kHostExpTab[i];
+  const int ltn = p.logtab_n < kImLogLds ? (int)p.logtab_n : kImLogLds;
+  for (int i = threadIdx.x; i < ltn; i += blockDim.x) slog[i] = p.logtab[i];
+  const bool dp_lds = p.dpow_n <= kImDpowLds;
+  if (dp_lds)
+    for (int i = threadIdx.x; i < p.dpow_n; i += blockDim.x) sdp[i] = p.dpow[i];
+  stage_model(p.model, sm);   // (synchronises)
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= p.B) return;
+  ImPair<Env, 3> P(p, sm, b);
+  P.lt_lds = slog;
+  P.lt_n = ltn;
+  P.rv = srv + threadIdx.x;
+  if (dp_lds) P.dp = sdp;
+  P.exp_tab = sexp;
+  if (flags & kImBegin) {
+    P.h.num_sims = 0;
+    P.h.search_depth = 0;
+  }
+  const int root = P.h.cur;
+  int action = 0;
+  if (P.h.err == 0 && !im_absorbing(P.N(0, root).info) && P.N(0, root).t > 0) {
+    const uint4* const rb = P.root_buf(P.h.root_sel);
+    if (sims0 + sims1 + sims2 > 0) {   // the top planner's _nested_sim head (no draws)
+      P.traverse(0, root);
+      if (im_nreg(P.N(0, root).info) == 0) P.expand(0, root);
+      if (P.h.root_size == 0 || P.h.root_size < p.extra) P.fail(POMCP_E_UNSUPPORTED);
+    }
+    const ISup* const t1 = P.sup1_tab(P.h.sup1_sel);
+    const uint4* const q1s = P.sup1_parts(P.h.sup1_sel);
+    const ISup* const t2 = P.sup_tab(P.h.sup_sel);
+    const uint2* const q2s = P.sup_parts(P.h.sup_sel);
+    for (int level = 0; level < 3 && P.h.err == 0; ++level) {
+      const int num_sims = level == 0 ? sims0 : level == 1 ? sims1 : sims2;
+      if (level == 2 && num_sims > 0) {   // the root's view, kept current by the backups
+        P.rv_put(P.view(0, root));
+        P.rv_root = root;
+      }
+      for (int s = 0; s < num_sims && P.h.err == 0; ++s) {
+        const uint4 hp = rb[P.d_bel(0, (uint32_t)P.h.root_size)];
+        if (level == 2) {
+          const auto v = P.rv_get();
+          const int d = P.simulate(0, hp.x, hp.y, hp.z, root, v);
+          P.N(0, root).visits = v.x.visits + 1;
+          P.rv[0].z = (uint32_t)(v.x.visits + 1);
+          if (d > P.h.search_depth) P.h.search_depth = d;
+        } else {
+          // the middle planner's _nested_sim at the particle's history
+          const int n1 = (int)hp.z;
+          const ISup e1 = t1[hp.w];
+          P.traverse(1, n1);
+          if (im_nreg(P.N(1, n1).info) == 0) P.expand(1, n1);
+          if (e1.size == 0) {
+            P.fail(POMCP_E_UNSUPPORTED);   // depleted node (not reached by the goldens)
+            break;
+          }
+          const uint4 q1 = q1s[e1.off + P.d_bel(1, (uint32_t)e1.size)];
+          if (level == 1) {
+            auto v = P.view(1, n1);
+            P.simulate(1, q1.x, q1.y, q1.z, n1, v);
+            P.N(1, n1).visits = v.x.visits + 1;
+          } else {   // ... and the level-0 planner's at the middle particle's history
+            const int n2 = (int)q1.z;
+            const ISup e2 = t2[q1.w];
+            P.traverse(2, n2);
+            if (im_nreg(P.N(2, n2).info) == 0) P.expand(2, n2);
+            if (e2.size == 0) {
+              P.fail(POMCP_E_UNSUPPORTED);
+              break;
+            }
+            const uint2 q2 = q2s[e2.off + P.d_bel(2, (uint32_t)e2.size)];
+            auto v = P.view(2, n2);
+            P.simulate(2, q2.x, q2.y, 0u, n2, v);
+            P.N(2, n2).visits = v.x.visits + 1;
+          }
+        }
+        P.h.num_sims += 1;
+      }
+    }
+    if (!(flags & kImFinal) || P.h.err != 0) {
+      if (P.h.err != 0 && (flags & kImFinal)) P.h.last_action = -1;
+      P.store_search();
+      return;
+    }
+    // max_value_action_selection (intmcp.py:718-732)
+    const INode x = P.N(0, root);
+    const int nr = im_nreg(x.info);
+    if (nr == 0) {
+      action = (int)P.d_sel((uint32_t)p.A);
+    } else {
+      double mx = -__builtin_inf();
+      int ties[6], nt = 0;
+      for (int i = 0; i < nr; ++i) {
+        const int a = im_order(x.info, i);
+        const uint32_t* const hd = P.H(0, root, a);
         const double v = hilo_d(hd[1], hd[2]);
         if (v == mx) {
           ties[nt++] = a;

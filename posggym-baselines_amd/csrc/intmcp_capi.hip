@@ -27,7 +27,7 @@ __global__ __launch_bounds__(64) void k_im_root_stats(ImParams d, intmcp_root_st
   if (t >= d.B) return;
   const IHdr h = d.hdr[t];
   const int T = d.nest0 ? 1 : 0;
-  const char* const blk = d.nodes + im_node_off(d.Nn, d.B, t, T, h.cur);
+  const char* const blk = d.nodes + im_node_off(d.Nn, d.B, t, T, h.cur, d.nt);
   const INode node = *reinterpret_cast<const INode*>(blk);
   intmcp_root_stats o;
   memset(&o, 0, sizeof(o));
@@ -110,7 +110,7 @@ static int im_copy(intmcp_ctx* ctx, T* dst, const T* src, size_t n) {
 static int im_copy_blocks(intmcp_ctx* ctx, std::vector<char>& out, int pair, int tree, int n) {
   out.resize((size_t)n * kImBlock);
   if (n == 0) return POMCP_OK;
-  const char* line0 = ctx->ip.nodes + im_node_off(ctx->ip.Nn, ctx->ip.B, pair, tree, 0);
+  const char* line0 = ctx->ip.nodes + im_node_off(ctx->ip.Nn, ctx->ip.B, pair, tree, 0, ctx->ip.nt);
   const size_t ns = (size_t)im_node_stride(ctx->ip.B, pair);
   IM_TRY(ctx, hipMemcpy2DAsync(out.data(), kImBlock, line0, ns, kImLine, n, hipMemcpyDeviceToHost,
                                ctx->stream));
@@ -156,8 +156,8 @@ int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, in
   if (c.action_selection != POMCP_SEL_UCB && c.action_selection != POMCP_SEL_UNIFORM)
     return bad(POMCP_E_UNSUPPORTED, "I-NTMCP pucb reads self.action_space (intmcp.py:645): ucb / uniform only");
   if (c.ego_agent < 0 || c.ego_agent > 1 || c.num_trees < 1) return bad(POMCP_E_INVALID, "ego / pairs");
-  if (cfg->nesting_level != 0 && cfg->nesting_level != 1)
-    return bad(POMCP_E_UNSUPPORTED, "nesting levels 0 and 1");
+  if (cfg->nesting_level < 0 || cfg->nesting_level > 2)
+    return bad(POMCP_E_UNSUPPORTED, "nesting levels 0, 1 and 2");
   if (c.depth_limit < 0 || c.step_limit < 0 || c.num_particles < 1) return bad(POMCP_E_INVALID, "limits");
   if (cfg->max_nodes < 2 || cfg->max_nodes >= (1ll << 28) || cfg->max_stats < c.num_actions ||
       cfg->max_log < 1 || cfg->hash_slots < 16 || (cfg->hash_slots & (cfg->hash_slots - 1)) ||
@@ -201,6 +201,7 @@ int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, in
   d.A = c.num_actions;
   // nesting level 0: the planner's tree is tree 1, whose agent is p.other
   d.nest0 = cfg->nesting_level == 0 ? 1 : 0;
+  d.nt = cfg->nesting_level == 2 ? 3 : 2;   // nesting level 2: a third (level-0) tree
   d.ego = d.nest0 ? 1 - c.ego_agent : c.ego_agent;
   d.other = 1 - d.ego;
   d.sel = c.action_selection;
@@ -235,12 +236,16 @@ int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, in
   } while (0)
   IM_ALLOC(hdr, IHdr, B);
   d.nstride = kImBlock;   // node blocks (intmcp.hip), interleaved by wave: im_node_off
-  IM_ALLOC(nodes, char, B * 2 * d.Nn * d.nstride);
-  IM_ALLOC(hash, IHash, B * 2 * d.H);
-  IM_ALLOC(log, IRec, B * 2 * d.Nl);
+  IM_ALLOC(nodes, char, B * d.nt * d.Nn * d.nstride);
+  IM_ALLOC(hash, IHash, B * d.nt * d.H);
+  IM_ALLOC(log, IRec, B * d.nt * d.Nl);
   IM_ALLOC(root, uint4, B * 2 * d.Nr);
   IM_ALLOC(sup, ISup, B * 2 * d.Nr);
   IM_ALLOC(supp, uint2, B * 2 * d.Nsp);
+  const bool mid = d.nt == 3;   // the middle planner's beliefs and distribution
+  IM_ALLOC(sup1, ISup, mid ? B * 2 * d.Nr : 1);
+  IM_ALLOC(supp1, uint4, mid ? B * 2 * d.Nsp : 1);
+  IM_ALLOC(prob1, double, mid ? B * d.Nr : 1);
   IM_ALLOC(path, int4, B * kImPath * 3);
   IM_ALLOC(prob, double, B * d.Nr);
   IM_ALLOC(logtab, double, c.log_table_size);
@@ -290,9 +295,9 @@ int intmcp_reset(intmcp_ctx* ctx) {
   IM_TRY(ctx, hipSetDevice(ctx->device));
   // node lines and records start zeroed: statistics and inline child slots
   // need no initialising writes (intmcp.hip, kImBlock)
-  IM_TRY(ctx, hipMemsetAsync(ctx->ip.nodes, 0, (size_t)ctx->ip.B * 2 * ctx->ip.Nn * kImBlock,
+  IM_TRY(ctx, hipMemsetAsync(ctx->ip.nodes, 0, (size_t)ctx->ip.B * ctx->ip.nt * ctx->ip.Nn * kImBlock,
                              ctx->stream));
-  const int64_t slots = (int64_t)ctx->ip.B * 2 * ctx->ip.H;
+  const int64_t slots = (int64_t)ctx->ip.B * ctx->ip.nt * ctx->ip.H;
   const int64_t cblocks = std::min<int64_t>((slots + 255) / 256, 256 * 64);
   hipLaunchKernelGGL(k_im_clear_hash, dim3((unsigned)cblocks), dim3(256), 0, ctx->stream, ctx->ip.hash,
                      slots);
@@ -328,7 +333,15 @@ int intmcp_update(intmcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_k
   // shared by the wave's lanes (k_im_update kWave); a lane per pair otherwise
   const bool wave = B <= 1024;
   const dim3 ugrid(wave ? (unsigned)B : (unsigned)im_blocks(B));
-  if (ctx->cfg.base.env_id == POMCP_ENV_PURSUIT_EVASION) {
+  if (ctx->ip.nt == 3) {   // nesting level 2
+    if (ctx->cfg.base.env_id == POMCP_ENV_PURSUIT_EVASION) {
+      if (wave) hipLaunchKernelGGL((k_im_update3<EnvPursuitEvasion, true>), ugrid, dim3(64), 0, ctx->stream, ctx->ip);
+      else hipLaunchKernelGGL((k_im_update3<EnvPursuitEvasion, false>), ugrid, dim3(64), 0, ctx->stream, ctx->ip);
+    } else {
+      if (wave) hipLaunchKernelGGL((k_im_update3<EnvDriving, true>), ugrid, dim3(64), 0, ctx->stream, ctx->ip);
+      else hipLaunchKernelGGL((k_im_update3<EnvDriving, false>), ugrid, dim3(64), 0, ctx->stream, ctx->ip);
+    }
+  } else if (ctx->cfg.base.env_id == POMCP_ENV_PURSUIT_EVASION) {
     if (wave) hipLaunchKernelGGL((k_im_update<EnvPursuitEvasion, true>), ugrid, dim3(64), 0, ctx->stream, ctx->ip);
     else hipLaunchKernelGGL((k_im_update<EnvPursuitEvasion, false>), ugrid, dim3(64), 0, ctx->stream, ctx->ip);
   } else {
@@ -351,6 +364,9 @@ static int im_fetch_hdr(intmcp_ctx* ctx) {
   return POMCP_OK;
 }
 
+// one launch of sims[l] simulations at level l (l = 0, 1, 2 in turn)
+static int im_search3(intmcp_ctx* ctx, const int32_t sims[3], int32_t flags, int32_t* actions_out);
+
 int intmcp_search_levels(intmcp_ctx* ctx, int32_t level0_sims, int32_t level1_sims,
                          int32_t flags, int32_t* actions_out) {
   if (!ctx || level0_sims < 0 || level1_sims < 0 || (flags & ~(kImBegin | kImFinal)))
@@ -358,6 +374,10 @@ int intmcp_search_levels(intmcp_ctx* ctx, int32_t level0_sims, int32_t level1_si
   if (ctx->ip.nest0 && level1_sims > 0) {
     ctx->err = "search_levels: nesting level 0 has no level-1 simulations";
     return POMCP_E_INVALID;
+  }
+  if (ctx->ip.nt == 3) {
+    const int32_t sims[3] = {level0_sims, level1_sims, 0};
+    return im_search3(ctx, sims, flags, actions_out);
   }
   IM_TRY(ctx, hipSetDevice(ctx->device));
   IM_LAUNCH(ctx, k_im_search, dim3(im_blocks(ctx->ip.B)), dim3(64), ctx->ip, (int)level0_sims,
@@ -376,10 +396,48 @@ int intmcp_search_levels(intmcp_ctx* ctx, int32_t level0_sims, int32_t level1_si
   return POMCP_OK;
 }
 
+static int im_search3(intmcp_ctx* ctx, const int32_t sims[3], int32_t flags, int32_t* actions_out) {
+  IM_TRY(ctx, hipSetDevice(ctx->device));
+  IM_LAUNCH(ctx, k_im_search3, dim3(im_blocks(ctx->ip.B)), dim3(64), ctx->ip, (int)sims[0],
+            (int)sims[1], (int)sims[2], (int)flags);
+  IM_TRY(ctx, hipGetLastError());
+  if (!actions_out) return POMCP_OK;
+  int rc = im_fetch_hdr(ctx);
+  if (rc != POMCP_OK) return rc;
+  for (int t = 0; t < ctx->ip.B; ++t) {
+    if (ctx->host_hdr[t].err != 0) {
+      ctx->err = "search: pair " + std::to_string(t) + ": status " + std::to_string(ctx->host_hdr[t].err);
+      return ctx->host_hdr[t].err;
+    }
+    actions_out[t] = ctx->host_hdr[t].last_action;
+  }
+  return POMCP_OK;
+}
+
 int intmcp_search(intmcp_ctx* ctx, int32_t num_sims, int32_t* actions_out) {
   if (!ctx || num_sims < 0) return POMCP_E_INVALID;
+  if (ctx->ip.nt == 3) {
+    const int32_t sims[3] = {num_sims, num_sims, num_sims};
+    return im_search3(ctx, sims, kImBegin | kImFinal, actions_out);
+  }
   return intmcp_search_levels(ctx, num_sims, ctx->ip.nest0 ? 0 : num_sims, kImBegin | kImFinal,
                               actions_out);
+}
+
+int intmcp_search_level(intmcp_ctx* ctx, int32_t level, int32_t sims, int32_t flags,
+                        int32_t* actions_out) {
+  if (!ctx || sims < 0 || (flags & ~(kImBegin | kImFinal))) return POMCP_E_INVALID;
+  const int top = ctx->ip.nest0 ? 0 : ctx->ip.nt - 1;   // the planner's nesting level
+  if (level < 0 || level > top) {
+    ctx->err = "search_level: no level " + std::to_string(level);
+    return POMCP_E_INVALID;
+  }
+  if (ctx->ip.nt == 3) {
+    int32_t s[3] = {0, 0, 0};
+    s[level] = sims;
+    return im_search3(ctx, s, flags, actions_out);
+  }
+  return intmcp_search_levels(ctx, level == 0 ? sims : 0, level == 1 ? sims : 0, flags, actions_out);
 }
 
 int intmcp_get_root_stats(intmcp_ctx* ctx, intmcp_root_stats* out) {
@@ -431,7 +489,8 @@ int intmcp_get_root_belief(intmcp_ctx* ctx, int32_t pair, uint32_t* out, int32_t
 
 int intmcp_get_nodes(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int32_t capacity,
                      int32_t* count) {
-  if (!ctx || !count || pair < 0 || pair >= ctx->ip.B || tree < 0 || tree > 1) return POMCP_E_INVALID;
+  if (!ctx || !count || pair < 0 || pair >= ctx->ip.B || tree < 0 || tree >= ctx->ip.nt)
+    return POMCP_E_INVALID;
   int rc = im_fetch_hdr(ctx);
   if (rc != POMCP_OK) return rc;
   const int n = ctx->host_hdr[pair].n_nodes[tree];
@@ -463,7 +522,8 @@ int intmcp_get_nodes(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int
 
 int intmcp_get_stats(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int32_t capacity,
                      int32_t* count) {
-  if (!ctx || !count || pair < 0 || pair >= ctx->ip.B || tree < 0 || tree > 1) return POMCP_E_INVALID;
+  if (!ctx || !count || pair < 0 || pair >= ctx->ip.B || tree < 0 || tree >= ctx->ip.nt)
+    return POMCP_E_INVALID;
   int rc = im_fetch_hdr(ctx);
   if (rc != POMCP_OK) return rc;
   const int n = ctx->host_hdr[pair].n_stats[tree];
@@ -541,12 +601,12 @@ int intmcp_debug_set_softmax_slack(intmcp_ctx* ctx, float slack) {
 
 int intmcp_set_search_policy(intmcp_ctx* ctx, int32_t level, int32_t agent, const double* probs) {
   if (!ctx || agent < 0 || agent > 1) return POMCP_E_INVALID;
-  const int top = ctx->ip.nest0 ? 0 : 1;   // the planner's nesting level
+  const int top = ctx->ip.nest0 ? 0 : ctx->ip.nt - 1;   // the planner's nesting level
   if (level < 0 || level > top) {
     ctx->err = "set_search_policy: no planner at level " + std::to_string(level);
     return POMCP_E_INVALID;
   }
-  const int k = top - level;               // tree 0 = level 1; the level-0 planner's is tree 1
+  const int k = top - level;               // tree 0 = the top level; the level-0 planner's is the last
   const int tree = ctx->ip.nest0 ? 1 : k;
   ImParams& d = ctx->ip;
   if (probs == nullptr) {
@@ -571,7 +631,7 @@ int intmcp_set_search_policy(intmcp_ctx* ctx, int32_t level, int32_t agent, cons
     d.sp_fixed[tree][agent] = 1;
   }
   d.sp_any = 0;
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < kImMaxT; ++t)
     for (int i = 0; i < 2; ++i) d.sp_any |= d.sp_fixed[t][i];
   return POMCP_OK;
 }
@@ -604,6 +664,54 @@ int intmcp_get_support(intmcp_ctx* ctx, int32_t pair, int32_t* entries, int32_t 
     rc = im_copy(ctx, reinterpret_cast<uint2*>(particles),
                  ctx->ip.supp + ((int64_t)pair * 2 + h.sup_sel) * ctx->ip.Nsp, (size_t)h.sup_used);
     if (rc != POMCP_OK) return rc;
+  }
+  return POMCP_OK;
+}
+
+int intmcp_get_mid_support(intmcp_ctx* ctx, int32_t pair, int32_t* entries, int32_t capacity_entries,
+                           int32_t* n_entries, uint32_t* particles, int32_t capacity_particles,
+                           int32_t* n_particles) {
+  if (!ctx || !n_entries || !n_particles || pair < 0 || pair >= ctx->ip.B) return POMCP_E_INVALID;
+  if (ctx->ip.nt != 3) {
+    ctx->err = "get_mid_support: nesting level 2 only";
+    return POMCP_E_INVALID;
+  }
+  int rc = im_fetch_hdr(ctx);
+  if (rc != POMCP_OK) return rc;
+  const IHdr& h = ctx->host_hdr[pair];
+  *n_entries = h.n_sup1;
+  *n_particles = h.sup1_used;
+  if (entries && capacity_entries >= h.n_sup1) {
+    rc = im_copy(ctx, reinterpret_cast<ISup*>(entries),
+                 ctx->ip.sup1 + ((int64_t)pair * 2 + h.sup1_sel) * ctx->ip.Nr, (size_t)h.n_sup1);
+    if (rc != POMCP_OK) return rc;
+  }
+  if (particles && capacity_particles >= h.sup1_used) {
+    std::vector<uint4> buf((size_t)h.sup1_used);
+    rc = im_copy(ctx, buf.data(), ctx->ip.supp1 + ((int64_t)pair * 2 + h.sup1_sel) * ctx->ip.Nsp,
+                 (size_t)h.sup1_used);
+    if (rc != POMCP_OK) return rc;
+    for (int i = 0; i < h.sup1_used; ++i) {
+      particles[3 * i] = buf[i].x;
+      particles[3 * i + 1] = buf[i].y;
+      particles[3 * i + 2] = buf[i].z;
+    }
+  }
+  return POMCP_OK;
+}
+
+int intmcp_get_tree_counts(intmcp_ctx* ctx, int32_t* out) {
+  if (!ctx || !out) return POMCP_E_INVALID;
+  int rc = im_fetch_hdr(ctx);
+  if (rc != POMCP_OK) return rc;
+  for (int t = 0; t < ctx->ip.B; ++t) {
+    const IHdr& h = ctx->host_hdr[t];
+    for (int k = 0; k < 3; ++k) {
+      const bool on = k < ctx->ip.nt;
+      out[9 * t + 3 * k] = on ? h.n_nodes[k] : 0;
+      out[9 * t + 3 * k + 1] = on ? h.n_log[k] : 0;
+      out[9 * t + 3 * k + 2] = on ? h.n_stats[k] : 0;
+    }
   }
   return POMCP_OK;
 }

@@ -305,6 +305,10 @@ INTMCP_SIGNATURES = [
     ("intmcp_get_stats", C.c_int, [_CTX, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, _P32]),
     ("intmcp_get_support", C.c_int,
      [_CTX, C.c_int32, _P32, C.c_int32, _P32, _PU32, C.c_int32, _P32]),
+    ("intmcp_get_mid_support", C.c_int,
+     [_CTX, C.c_int32, _P32, C.c_int32, _P32, _PU32, C.c_int32, _P32]),
+    ("intmcp_search_level", C.c_int, [_CTX, C.c_int32, C.c_int32, C.c_int32, _P32]),
+    ("intmcp_get_tree_counts", C.c_int, [_CTX, _P32]),
     ("intmcp_synthetic_obs", C.c_int, [_CTX, C.c_uint64, _PU64]),
     ("intmcp_set_search_policy", C.c_int, [_CTX, C.c_int32, C.c_int32, _PD]),
     ("intmcp_debug_phase_timing", C.c_int, [_CTX, C.c_void_p, C.c_int32, _P32]),
@@ -339,6 +343,8 @@ def load():
     for name, res, args in SIGNATURES + DEBUG_SIGNATURES + INTMCP_SIGNATURES:
         if (name, res, args) in DEBUG_SIGNATURES and not hasattr(lib, name):
             continue   # diagnostics: optional in libraries built from older sources
+        if os.environ.get("POMCP_LIB_PATH") and not hasattr(lib, name):
+            continue   # an explicitly chosen (measurement) library built from older sources
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -1,5 +1,5 @@
 """I-NTMCP drop-in: the reference's ``INTMCP`` API (``intmcp.py:22-994``) at
-nesting levels 1 and 0 with two agents, the planners' trees, beliefs and
+nesting levels 0, 1 and 2 with two agents, the planners' trees, beliefs and
 generative model on the GPU (``include/intmcp.h``, ``csrc/intmcp.hip``).
 
 Public surface kept from the reference: ``INTMCP.initialize(model,
@@ -13,7 +13,7 @@ same device state), ``search_policies``, ``action_spaces``, ``step_limit``,
 ``BatchedINTMCP`` runs many independent planner pairs in one launch (BASELINE
 config 5: nested trees as a batched launch).
 
-Scope (DESIGN.md "I-NTMCP"): nesting levels 0 and 1, random or
+Scope (DESIGN.md "I-NTMCP"): nesting levels 0, 1 and 2, random or
 fixed-distribution search policies (``RandomSearchPolicy`` /
 ``SearchPolicyWrapper(FixedDistributionPolicy)`` per level and agent: they draw
 the rollouts and the other agent's action at an unvisited history; the node
@@ -64,11 +64,16 @@ class IntmcpCapacities:
     max_support_particles: int  # materialised level-0 particles (8 B, x2)
     log_table_size: int
     discount_pow_size: int
+    trees: int = 2              # trees per pair: 3 at nesting level 2
 
     def bytes_per_pair(self, num_actions: int = 5) -> int:
-        return (2 * (self.max_nodes * INTMCP_NODE_BYTES + self.max_log * 16
-                     + self.hash_slots * 16) + 4 * self.max_root_belief * 16
-                + 2 * self.max_support_particles * 8 + self.max_root_belief * 8)
+        b = (self.trees * (self.max_nodes * INTMCP_NODE_BYTES + self.max_log * 16
+                           + self.hash_slots * 16) + 4 * self.max_root_belief * 16
+             + 2 * self.max_support_particles * 8 + self.max_root_belief * 8)
+        if self.trees == 3:   # the middle planner's beliefs (entries, 16 B particles, distribution)
+            b += 2 * self.max_root_belief * 16 + 2 * self.max_support_particles * 16 \
+                + self.max_root_belief * 8
+        return b
 
 
 def _next_pow2(n: int) -> int:
@@ -76,7 +81,7 @@ def _next_pow2(n: int) -> int:
 
 
 def plan_intmcp_capacities(config, step_limit: int, num_sims: int, searches: int,
-                           num_actions: int) -> IntmcpCapacities:
+                           num_actions: int, nesting_level: int = 1) -> IntmcpCapacities:
     """Worst-case sizes for ``searches`` steps of ``num_sims`` simulations per level.
 
     Per step and tree: every simulation steps at most ``L = min(depth_limit,
@@ -91,15 +96,22 @@ def plan_intmcp_capacities(config, step_limit: int, num_sims: int, searches: int
     target = config.num_particles + config.extra_particles
     lf = config.reinvigoration_sample_limit_factor
     reinv = int(math.ceil(lf * target)) + target
-    per_step = 2 * S * L + 2 * reinv + 2 * target + 8
+    levels = 3 if nesting_level == 2 else 2   # (nesting 0 keeps the level-1 sizing)
+    per_step = levels * S * L + 2 * reinv + 2 * target + 8
+    if nesting_level == 2:   # the middle planner's reinvigorations extend level-0 histories
+        per_step += 2 * reinv * 8
     nodes = searches * per_step + 16
     nr = S * L + 4 * target + 64
     nsp = S * L + 2 * nr + 4 * target + 64
-    total_sims = 2 * S * searches
+    if nesting_level == 2:   # every root history's middle belief, and its level-0 histories'
+        nr += 8 * target
+        nsp = levels * S * L + 8 * nr + 8 * target + 64
+    total_sims = levels * S * searches
     return IntmcpCapacities(
         max_nodes=nodes, max_stats=num_actions * nodes, max_log=nodes,
         hash_slots=_next_pow2(2 * nodes), max_root_belief=nr, max_support_particles=nsp,
-        log_table_size=total_sims + 2, discount_pow_size=min(L, 4096) + 2)
+        log_table_size=total_sims + 2, discount_pow_size=min(L, 4096) + 2,
+        trees=3 if nesting_level == 2 else 2)
 
 
 # Wall-clock sizing.  One pair's simulation rate alone on the GPU (one lane,
@@ -121,12 +133,13 @@ def plan_intmcp_wallclock_capacities(config, step_limit: int, num_actions: int,
     per_level = config.search_time_limit / (nesting_level + 1)
     sims = max(64, math.ceil(per_level * INTMCP_WALL_CLOCK_SIMS_PER_S))
     searches = (step_limit if step_limit < INT32_MAX else 100) + 1
-    caps = plan_intmcp_capacities(config, step_limit, sims, searches, num_actions)
-    # per node and pair: two trees x (320 B node + 16 B log record + <=64 B of
+    caps = plan_intmcp_capacities(config, step_limit, sims, searches, num_actions, nesting_level)
+    # per node and pair: the trees x (320 B node + 16 B log record + <=64 B of
     # hash slots); per-search arrays (root belief, support) keep their worst case
-    per_node = 2 * (INTMCP_NODE_BYTES + 16 + 64)
-    fixed = caps.bytes_per_pair(num_actions) - caps.max_nodes * 2 * INTMCP_NODE_BYTES \
-        - caps.max_log * 2 * 16 - caps.hash_slots * 2 * 16
+    nt = caps.trees
+    per_node = nt * (INTMCP_NODE_BYTES + 16 + 64)
+    fixed = caps.bytes_per_pair(num_actions) - caps.max_nodes * nt * INTMCP_NODE_BYTES \
+        - caps.max_log * nt * 16 - caps.hash_slots * nt * 16
     nodes = (INTMCP_WALL_CLOCK_HBM_BUDGET - fixed) // per_node
     nodes = max(1 << 16, min(caps.max_nodes, nodes, _INTMCP_ID_LIMIT))
     caps.max_nodes = caps.max_log = nodes
@@ -155,8 +168,8 @@ class IntmcpEngine:
         self._emodel = engine_model(model)
         self.config = config
         self.num_pairs = int(num_pairs)
-        if nesting_level not in (0, 1):
-            raise NotImplementedError("the GPU I-NTMCP engine runs nesting levels 0 and 1")
+        if nesting_level not in (0, 1, 2):
+            raise NotImplementedError("the GPU I-NTMCP engine runs nesting levels 0, 1 and 2")
         self.nesting_level = int(nesting_level)
         self.ego = model.possible_agents.index(agent_id)
         self.A = model.action_spaces[agent_id].n
@@ -178,7 +191,8 @@ class IntmcpEngine:
             sims = num_sims if num_sims is not None else (config.num_sims or 1024)
             budget = searches if searches is not None else (
                 (step_limit if step_limit < INT32_MAX else 100) + 1)
-            capacities = plan_intmcp_capacities(config, step_limit, sims, budget, self.A)
+            capacities = plan_intmcp_capacities(config, step_limit, sims, budget, self.A,
+                                                self.nesting_level)
         self.capacities = capacities
         ic = N.IntmcpConfig()
         c = ic.base
@@ -284,6 +298,21 @@ class IntmcpEngine:
         self._check(self._lib.intmcp_set_search_policy(self._ctx, int(level), int(agent_index), ptr),
                     "set_search_policy")
 
+    def search_level(self, level, sims, flags, fetch=False):
+        """One chunk of ``sims`` simulations at nesting ``level`` (``intmcp_search_level``)."""
+        out = np.zeros(self.num_pairs, dtype=np.int32) if fetch else None
+        ptr = out.ctypes.data_as(C.POINTER(C.c_int32)) if fetch else None
+        self._check(self._lib.intmcp_search_level(self._ctx, int(level), int(sims), int(flags), ptr),
+                    "search_level")
+        return out
+
+    def tree_counts(self):
+        """[pairs][3 trees][nodes, log records, stats] (``intmcp_get_tree_counts``)."""
+        out = np.zeros((self.num_pairs, 3, 3), dtype=np.int32)
+        self._check(self._lib.intmcp_get_tree_counts(self._ctx, out.ctypes.data_as(C.POINTER(C.c_int32))),
+                    "get_tree_counts")
+        return out
+
     def search_levels(self, level0_sims, level1_sims, flags, fetch=False):
         out = np.zeros(self.num_pairs, dtype=np.int32) if fetch else None
         ptr = out.ctypes.data_as(C.POINTER(C.c_int32)) if fetch else None
@@ -306,8 +335,16 @@ class IntmcpEngine:
         target = cfg.num_particles + cfg.extra_particles
         reinv = int(math.ceil(cfg.reinvigoration_sample_limit_factor * target)) + target
         reserve = 2 * reinv + 2 * target + 8        # plan_intmcp_capacities' per-update share
-        st = self._stats if stats is None else stats
         room = INT32_MAX
+        if getattr(self, "nesting_level", 1) == 2:   # three trees: intmcp_get_tree_counts
+            cnt = self.tree_counts()
+            for p in range(self.num_pairs):
+                for t in range(3):
+                    left = min(caps.max_nodes - cnt[p, t, 0], caps.max_log - cnt[p, t, 1],
+                               (caps.max_stats - cnt[p, t, 2]) // self.A) - reserve
+                    room = min(room, left // L)
+            return max(0, int(room))
+        st = self._stats if stats is None else stats
         for p in range(self.num_pairs):
             for t in range(2):
                 left = min(caps.max_nodes - st[p].n_nodes[t], caps.max_log - st[p].n_log[t],
@@ -341,11 +378,26 @@ class IntmcpEngine:
         return out[:n.value]
 
     def nodes(self, pair=0, tree=0):
-        """Obs nodes of one tree (0: level 1, 1: level 0) as a structured array."""
+        """Obs nodes of one tree (0: the planner's level, then one level down per
+        tree) as a structured array."""
         return self._records(self._lib.intmcp_get_nodes, pair, tree, N.INTMCP_NODE_DTYPE)
 
     def stats(self, pair=0, tree=0):
         return self._records(self._lib.intmcp_get_stats, pair, tree, N.INTMCP_STAT_DTYPE)
+
+    def mid_support(self, pair=0):
+        """Nesting level 2: the middle (level-1) planner's materialised beliefs:
+        (entries, (v0, v1, level-0 node) particles)."""
+        ne, npart = C.c_int32(), C.c_int32()
+        self._check(self._lib.intmcp_get_mid_support(self._ctx, pair, None, 0, C.byref(ne), None, 0,
+                                                     C.byref(npart)), "get_mid_support")
+        ent = np.zeros(max(ne.value, 1), dtype=N.INTMCP_SUPPORT_DTYPE)
+        parts = np.zeros(3 * max(npart.value, 1), dtype=np.uint32)
+        self._check(self._lib.intmcp_get_mid_support(
+            self._ctx, pair, ent.ctypes.data_as(C.POINTER(C.c_int32)), ne.value, C.byref(ne),
+            parts.ctypes.data_as(C.POINTER(C.c_uint32)), npart.value, C.byref(npart)),
+            "get_mid_support")
+        return ent[:ne.value], parts[:3 * npart.value].reshape(-1, 3)
 
     def support(self, pair=0):
         """The materialised level-0 beliefs: (entries, (v0, v1) particles)."""
@@ -386,16 +438,18 @@ class RootView:
 
 
 class _NestedPlanner:
-    """The level-0 planner of the other agent (``other_agent_policies[j]``):
-    a view of the device state shared with the level-1 planner."""
+    """A lower-level planner (``other_agent_policies[j]``, and its own at
+    nesting level 2): a view of the device state shared with the top planner."""
 
-    def __init__(self, parent, agent_id):
+    def __init__(self, parent, agent_id, nesting_level=0):
         self._parent = parent
         self.model = parent.model
         self.agent_id = agent_id
         self.config = parent.config
-        self.nesting_level = 0
-        self.other_agent_policies = {}
+        self.nesting_level = nesting_level
+        below = [i for i in parent.model.possible_agents if i != agent_id][0]
+        self.other_agent_policies = ({below: _NestedPlanner(parent, below, nesting_level - 1)}
+                                     if nesting_level > 0 else {})
         self.step_statistics = {"reinvigoration_time": 0.0}
 
     def reset(self):
@@ -423,8 +477,8 @@ class INTMCP:
     def __init__(self, model, agent_id: str, config: MCTSConfig, nesting_level: int,
                  other_agent_policies=None, search_policies=None, *,
                  num_sims: Optional[int] = None):
-        if nesting_level not in (0, 1):
-            raise NotImplementedError("the GPU I-NTMCP engine runs nesting levels 0 and 1")
+        if nesting_level not in (0, 1, 2):
+            raise NotImplementedError("the GPU I-NTMCP engine runs nesting levels 0, 1 and 2")
         from posggym_baselines_amd.planning.ipomcp import search_policy_probs
         assert agent_id in model.possible_agents
         # {level: {agent: policy}} (INTMCP.initialize) or one {agent: policy}
@@ -447,8 +501,10 @@ class INTMCP:
         self.action_spaces = {i: list(range(model.action_spaces[i].n))
                               for i in model.possible_agents}
         other = [i for i in model.possible_agents if i != agent_id][0]
-        # intmcp.py:971-981: a level-0 planner models no other agent
-        self.other_agent_policies = {other: _NestedPlanner(self, other)} if nesting_level else {}
+        # intmcp.py:971-981: a level-0 planner models no other agent; a level-2
+        # planner's other agent is a level-1 planner modelling this agent at level 0
+        self.other_agent_policies = ({other: _NestedPlanner(self, other, nesting_level - 1)}
+                                     if nesting_level else {})
         self._num_sims = num_sims if num_sims is not None else config.num_sims
         self._engine = IntmcpEngine(model, agent_id, config, num_pairs=1,
                                     num_sims=self._num_sims,
@@ -557,13 +613,12 @@ class INTMCP:
                     if n <= 0:
                         self.step_statistics["arena_full"] = True
                         break
-                    sims = (n, 0) if level == 0 else (0, n)
-                    self._engine.search_levels(sims[0], sims[1], flags)
+                    self._engine.search_level(level, n, flags)
                     flags = 0
                     room = self._engine.headroom(self._engine.root_stats())   # synchronises
                     done += n
                     chunk = min(chunk * 2, 4096)
-            self._engine.search_levels(0, 0, flags | N.INTMCP_FINAL)
+            self._engine.search_level(0, 0, flags | N.INTMCP_FINAL)
         st = self._engine.root_stats()[0]
         search_time = time.time() - start
         self._min_value, self._max_value = st.min_value, st.max_value
@@ -604,7 +659,7 @@ class BatchedINTMCP:
         if capacities is None:
             step_limit = config.step_limit or model.spec.max_episode_steps
             capacities = plan_intmcp_capacities(config, step_limit, num_sims, searches,
-                                                model.action_spaces[agent_id].n)
+                                                model.action_spaces[agent_id].n, nesting_level)
         self.num_pairs = num_pairs
         self.num_sims = num_sims
         self.engine = IntmcpEngine(model, agent_id, config, num_pairs=num_pairs,

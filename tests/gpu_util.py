@@ -165,35 +165,60 @@ def intmcp_state_record(eng, pair, searched, action):
                              kids, st.min_value, st.max_value, parts, [])
     rows = eng.root_belief(pair)
 
-    def history(n):
+    def history(nodes, n):
         out = []
         while n != 0:
-            a = int(n1[n]["info"]) & 7
-            out.append((-1 if a == A else a, int(n1[n]["okey"])))
-            n = int(n1[n]["parent"])
+            a = int(nodes[n]["info"]) & 7
+            out.append((-1 if a == A else a, int(nodes[n]["okey"])))
+            n = int(nodes[n]["parent"])
         return tuple(reversed(out))
 
+    def node(nodes, stats, n, ent_, parts_):
+        """(visits, registered children, particles) of node n, its particles
+        from its materialised belief entry"""
+        nd = nodes[n]
+        nk = [(a, int(stats[int(nd["stats"]) + a]["visits"]),
+               float(stats[int(nd["stats"]) + a]["value"]))
+              for a in node_order(int(nd["info"])) if a < A]
+        hit = [e for e in ent_ if int(e["node"]) == n]
+        rows_ = []
+        if hit:
+            e = hit[0]
+            rows_ = parts_[int(e["off"]):int(e["off"]) + int(e["size"])]
+        return (int(nd["visits"]), nk, [(int(nd["t"]), (int(q[0]), int(q[1]))) for q in rows_]), rows_
+
+    # the middle tree's beliefs at nesting level 2 (tree 1), else the level-0 support
+    mid = eng.nesting_level == 2
+    ent1, parts1 = eng.mid_support(pair) if mid else (ent, sparts)
     # the root's t: every root particle's other-agent history has that length
     t_root = int(n1[int(rows[0][2])]["t"]) if len(rows) else 0
-    parts = [(t_root, (int(r[0]), int(r[1])), history(int(r[2]))) for r in rows]
-    nested, seen = [], []
+    parts = [(t_root, (int(r[0]), int(r[1])), history(n1, int(r[2]))) for r in rows]
+    nested, seen, mrows = [], [], []
     for r in rows:
         m = int(r[2])
         if m in seen:
             continue
         seen.append(m)
-        nd = n1[m]
-        nk = [(a, int(s1[int(nd["stats"]) + a]["visits"]), float(s1[int(nd["stats"]) + a]["value"]))
-              for a in node_order(int(nd["info"])) if a < A]
-        hit = [e for e in ent if int(e["node"]) == m]
-        npart = []
-        if hit:
-            e = hit[0]
-            npart = [(int(nd["t"]), (int(q[0]), int(q[1])))
-                     for q in sparts[int(e["off"]):int(e["off"]) + int(e["size"])]]
-        nested.append((history(m), (int(nd["visits"]), nk, npart)))
+        nd, rows_ = node(n1, s1, m, ent1, parts1)
+        nested.append((history(n1, m), nd))
+        mrows.append(rows_)
+    nested2 = None
+    if mid:   # the third tree: histories carried by the middle beliefs' particles
+        n2 = eng.nodes(pair, 2)
+        s2 = eng.stats(pair, 2)
+        seqs, nodes2, seen2 = [], [], []
+        for rows_ in mrows:
+            seq = []
+            for q in rows_:
+                h2 = int(q[2])
+                seq.append(history(n2, h2))
+                if h2 not in seen2:
+                    seen2.append(h2)
+                    nodes2.append((history(n2, h2), node(n2, s2, h2, ent, sparts)[0]))
+            seqs.append(seq)
+        nested2 = (seqs, nodes2)
     return intmcp_record(rec, int(st.num_sims), int(st.search_depth), int(st.root_visits), kids,
-                         st.min_value, st.max_value, parts, nested)
+                         st.min_value, st.max_value, parts, nested, nested2=nested2)
 
 
 def _softmax_debug(ctx, slack):

@@ -9,15 +9,14 @@ import pytest
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
 
-from golden_util import INTMCP0_CASES, INTMCP_CASES, INTMCP_SP_CASES, cfg_kwargs, load, search_probs
+from golden_util import (INTMCP0_CASES, INTMCP2_CASES, INTMCP_CASES, INTMCP_SP_CASES, cfg_kwargs,
+                         load, search_probs)
 from gpu_util import gpu_intmcp_episode
 
 pytestmark = pytest.mark.gpu
 
 
-# nesting level 2 (intmcp2_*) is pinned in the oracle only (tests/test_oracle.py)
-@pytest.mark.parametrize("case", INTMCP_CASES + INTMCP0_CASES
-                         + [c for c in INTMCP_SP_CASES if not c.startswith("intmcp2")])
+@pytest.mark.parametrize("case", INTMCP_CASES + INTMCP0_CASES + INTMCP2_CASES + INTMCP_SP_CASES)
 def test_gpu_intmcp_matches_reference_goldens(case):
     """Nesting level 1 (intmcp_*) and 0 (intmcp0_*: the planner's own tree,
     the other agent acting by the planner's random choice); *_sp_*: fixed-
@@ -161,13 +160,13 @@ def test_device_softmax_exp_equals_math_exp():
     assert len(bad) == 0, [(x[i].hex(), out[i].hex(), ref[i].hex()) for i in bad[:5]]
 
 
-def _wall_clock_episode(time_limit, env_seed, max_steps):
+def _wall_clock_episode(time_limit, env_seed, max_steps, nesting_level=1):
     from gpu_util import product_model
     from oracle.episode import run_episode
     from posggym_baselines_amd.planning import INTMCP, MCTSConfig
     model = product_model("Driving-v1")
     cfg = MCTSConfig(**dict(TEST_CFG, search_time_limit=time_limit))   # num_sims=None
-    planner = INTMCP.initialize(model, "0", cfg, 1, None)
+    planner = INTMCP.initialize(model, "0", cfg, nesting_level, None)
     planner.reset()
     steps = []
 
@@ -199,6 +198,20 @@ def test_wall_clock_episode_half_second():
         assert 64 < st["num_sims"] <= 2 * ceiling
         assert 0 < st["child_visits"] <= st["visits"]
     print("I-NTMCP wall-clock sims per step:", [st["num_sims"] for st in steps])
+
+
+def test_wall_clock_nesting2_episode():
+    """Nesting level 2 in the reference's default mode: the time limit split
+    over three levels, chunks per level (intmcp_search_level) within the
+    headroom of all three trees (intmcp_get_tree_counts), no arena failure."""
+    trace, steps, ceiling = _wall_clock_episode(0.6, 43, 8, nesting_level=2)
+    assert len(steps) >= 2
+    for st in steps:
+        assert not st.get("arena_full")
+        assert 0.5 <= st["search_time"] < 2.5
+        assert 3 <= st["num_sims"] <= 3 * ceiling
+        assert 0 < st["child_visits"] <= st["visits"]
+    print("I-NTMCP nesting-2 wall-clock sims per step:", [st["num_sims"] for st in steps])
 
 
 def test_wall_clock_small_arena_stops_early(monkeypatch):
@@ -299,3 +312,57 @@ def test_intmcp_nesting0_rejects_level1_simulations():
     rc = N.load().intmcp_search_levels(planner._engine._ctx, 4, 4, N.INTMCP_BEGIN, None)
     assert rc == N.POMCP_E_INVALID
     planner.close()
+
+
+@pytest.mark.parametrize("env,ego", [("Driving-v1", "0"), ("PursuitEvasion-v1", "1")])
+def test_gpu_intmcp_nesting2_batched_pairs_match_oracle(env, ego):
+    """Nesting level 2 (three trees per pair), many planners in one launch:
+    every planner's records against the oracle (oracle/intmcp.py, pinned at
+    nesting 2 by the intmcp2_* goldens) with that planner's tree key."""
+    from gpu_util import batched_intmcp_episodes
+    from oracle.run import oracle_intmcp_episode
+    B, sims, steps = 5, 24, 6
+    seeds = [400 + b for b in range(B)]
+    got = batched_intmcp_episodes(TEST_CFG, sims, seeds, steps, env=env, ego=ego,
+                                  nesting_level=2)
+    for b in range(B):
+        _, exp = oracle_intmcp_episode(TEST_CFG, sims, seeds[b], ego=ego, tree=b,
+                                       max_steps=steps, env=env, nesting_level=2)
+        assert len(got[b]) == len(exp), b
+        for t, (g, e) in enumerate(zip(got[b], exp)):
+            assert g == e, f"{env} pair {b} step {t}"
+
+
+def test_intmcp_nesting2_search_level_chunks_equal_one_search():
+    """Nesting level 2: get_action as chunks per level (intmcp_search_level, the
+    wall-clock loop's launches) is bit-identical to one launch of all three
+    levels."""
+    import numpy as np
+    from gpu_util import intmcp_state_record, product_config, product_model
+    from posggym_baselines_amd import _native as N
+    from posggym_baselines_amd.planning.intmcp import BatchedINTMCP
+    model = product_model("Driving-v1")
+    cfg = product_config(TEST_CFG, 30)
+    one = BatchedINTMCP(model, "0", cfg, 4, 30, searches=3, nesting_level=2)
+    split = BatchedINTMCP(model, "0", cfg, 4, 30, searches=3, nesting_level=2)
+    keys = one.init_synthetic(500)
+    split.init_synthetic(500)
+    for step in range(2):
+        a1 = one.search()
+        e = split.engine
+        e.search_level(0, 7, N.INTMCP_BEGIN)
+        e.search_level(0, 23, 0)
+        e.search_level(1, 30, 0)
+        e.search_level(2, 11, 0)
+        a2 = e.search_level(2, 19, N.INTMCP_FINAL, fetch=True)
+        assert np.array_equal(a1, a2), step
+        for b in range(4):
+            assert e.root_stats()[b].num_sims == 90
+            r1 = intmcp_state_record(one.engine, b, True, int(a1[b]))
+            r2 = intmcp_state_record(e, b, True, int(a2[b]))
+            assert r1 == r2, (step, b)
+        acts = np.asarray(a1, dtype=np.int32)
+        one.engine.update(acts, keys)
+        e.update(acts, keys)
+    one.close()
+    split.close()
