@@ -519,7 +519,8 @@ def run_pomcp(dev, *, env, B, S, K, base_cfg, tm, steps, warmup, seed=0, max_blo
         pc = plan_capacities(cfg, step_limit, S, 1, reroot=True, max_blocks=mb,
                              overflow_slots=1024)
         nprobe = min(B, 1024)
-        probe = BatchedPOMCP(model, "0", cfg, nprobe, S, capacities=pc, device=dev)
+        probe = BatchedPOMCP(model, "0", cfg, nprobe, S, capacities=pc, device=dev,
+                             defer_cutoff=False)
         try:
             probe.init_synthetic(1000)
             acts = probe.search()
@@ -539,7 +540,11 @@ def run_pomcp(dev, *, env, B, S, K, base_cfg, tm, steps, warmup, seed=0, max_blo
         caps = plan_capacities(cfg, step_limit, S, 1, reroot=False, max_blocks=mb,
                                overflow_slots=1024)
     stream = torch.cuda.Stream(device=dev)
+    # an update()-inclusive step re-roots after every search: the episode
+    # planners' eager cut-off lookup (POMCP drop-in; pomcp_set_defer_cutoff);
+    # a search-only step (restore) re-searches the same roots: deferred records
     bp = BatchedPOMCP(model, "0", cfg, B, S, capacities=caps, stream=stream.cuda_stream,
+                      defer_cutoff=not update_step,
                       device=dev, type_policies=type_policies(model) if tm else None)
     try:
         bp.init_synthetic(1000)

@@ -180,6 +180,16 @@ typedef enum pomcp_search_kernel {
 int pomcp_set_search_kernel(pomcp_ctx* ctx, int32_t kind);
 /* The kernel the next search will use (POMCP_SEARCH_LANE or _WAVE). */
 int32_t pomcp_search_kernel_used(const pomcp_ctx* ctx);
+/* Cut-off children in the lane kernel (k_search): on = 1 (the default) a
+ * simulation's arrival at a child beyond the depth / step limits
+ * (mcts.py:315) is recorded against its action node and the child is
+ * materialised at the next re-root (pomcp_update) -- one slot line less per
+ * simulation, the cheaper choice when a tree is searched several times per
+ * re-root (batched search throughput); on = 0 looks the child up during the
+ * search (as the wave kernel always does) -- the cheaper choice when every
+ * search is followed by a re-root (an episode planner).  Same results either
+ * way (only node labels differ). */
+int pomcp_set_defer_cutoff(pomcp_ctx* ctx, int32_t on);
 
 /* Copy every tree's pomcp_root_stats of the last search to host. */
 int pomcp_get_root_stats(pomcp_ctx* ctx, pomcp_root_stats* out);

@@ -251,6 +251,7 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
   d.bucket_mask = (uint32_t)(c.overflow_slots / kBucket - 1);
   d.ovf_base = (uint32_t)(c.max_blocks * c.num_actions * kSlots + 1);
   d.cut_base = d.ovf_base + (uint32_t)c.overflow_slots;
+  d.defer = 1;   // deferred cut-off records (pomcp_set_defer_cutoff)
   d.islots = kSlots;
   d.tm = c.type_based;
   d.lines = blk_lines(d.A, d.tm);
@@ -460,6 +461,12 @@ int pomcp_set_search_kernel(pomcp_ctx* ctx, int32_t kind) {
 
 int32_t pomcp_search_kernel_used(const pomcp_ctx* ctx) {
   return ctx ? resolve_search_kind(ctx) : POMCP_E_INVALID;
+}
+
+int pomcp_set_defer_cutoff(pomcp_ctx* ctx, int32_t on) {
+  if (!ctx || (on != 0 && on != 1)) return POMCP_E_INVALID;
+  ctx->dp.defer = on;
+  return POMCP_OK;
 }
 
 // The wave search with step-tree producer waves (pomcp_search_lds.hip) when

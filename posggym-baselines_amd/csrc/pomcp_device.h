@@ -216,6 +216,7 @@ struct DevParams {
   int32_t spin_max;     // k_search_lds: polls of a late step-tree hand-off before the search
                         // wave runs on without producers (0: the default; tests shrink it)
   int32_t tm;           // type-based search (POTMMCP): tmt, prior lines, log aux
+  int32_t defer;        // k_search: defer cut-off children to the re-root (pomcp_set_defer_cutoff)
   const TmTables* tmt;
   TreeHdr* hdr;
   Line* an;             // [B][Nb][lines] action blocks

@@ -718,7 +718,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
           double r;
           int done;
           uint64_t okey;
+#ifdef POMCP_ABLATE_ROOTSTEP   // ablation build only (measurement): no root-level model step
+          n0 = s0;
+          n1 = s1;
+          r = 0.0;
+          done = 0;
+          okey = (uint64_t)ao;
+#else
           tree_step(a, ao, j, &n0, &n1, &r, &done, &okey);
+#endif
           bool match;
           const int ks = find_slot(sl, okey, &match);
           const uint32_t ani = (uint32_t)(root_blk * A + a);
@@ -831,11 +839,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         // (pomcp_device.h: no slot read or write; the re-root materialises the
         // children that survive it).  TM looks it up: the node's prior moves
         // on arrivals at existing children (potmmcp.py:255-264).
-#ifdef POMCP_EAGER_CUT   // measurement builds only (A/B): the round-3 eager lookup
-        constexpr bool skipc = false;
-#else
-        const bool skipc = TM == 0 && (depth + 1 > p.depth_limit || t + 1 > p.step_limit);
-#endif
+        // (p.defer = 0, pomcp_set_defer_cutoff: the eager lookup -- cheaper re-roots)
+        const bool skipc = TM == 0 && p.defer && (depth + 1 > p.depth_limit || t + 1 > p.step_limit);
         uint4 sl[kSlots];
   #pragma unroll
         for (int q = 0; q < kSlots; ++q) sl[q] = make_uint4(0, 0, 0, 0);

@@ -197,6 +197,7 @@ SIGNATURES = [
     ("pomcp_search_continue", C.c_int, [_CTX, C.c_int32]),
     ("pomcp_set_search_kernel", C.c_int, [_CTX, C.c_int32]),
     ("pomcp_search_kernel_used", C.c_int32, [_CTX]),
+    ("pomcp_set_defer_cutoff", C.c_int, [_CTX, C.c_int32]),
     ("pomcp_get_root_stats", C.c_int, [_CTX, C.POINTER(PomcpRootStats)]),
     ("pomcp_set_root_belief", C.c_int, [_CTX, C.c_int32, _PU32, C.c_int32]),
     ("pomcp_get_root_belief", C.c_int, [_CTX, C.c_int32, _PU32, C.c_int32, _P32]),

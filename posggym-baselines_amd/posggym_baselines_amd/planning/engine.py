@@ -219,6 +219,10 @@ class PomcpEngine:
         kind = os.environ.get("POMCP_SEARCH_KERNEL", "auto")
         if kind != "auto" and not (self.type_based and kind == "wave"):
             self.set_search_kernel(kind)
+        # deferral override (tests): POMCP_DEFER_CUTOFF=0|1
+        if os.environ.get("POMCP_DEFER_CUTOFF") in ("0", "1"):
+            self.set_defer_cutoff(os.environ["POMCP_DEFER_CUTOFF"] == "1")
+            self._defer_forced = True
 
     # ------------------------------------------------------------------
     def close(self):
@@ -285,6 +289,17 @@ class PomcpEngine:
         a wave per tree, tree in LDS); same results, different speed."""
         k = {"auto": N.SEARCH_AUTO, "lane": N.SEARCH_LANE, "wave": N.SEARCH_WAVE}[kind]
         self._check(self._lib.pomcp_set_search_kernel(self._ctx, k), "set_search_kernel")
+
+    def set_defer_cutoff(self, on):
+        """Defer cut-off children to the re-root (True, the default: batched search
+        throughput) or look them up during the search (False: one search per
+        re-root, the episode planners); same results (``pomcp_set_defer_cutoff``).
+        A process-wide POMCP_DEFER_CUTOFF override (tests) wins."""
+        if getattr(self, "_defer_forced", False):
+            return
+        if not hasattr(self._lib, "pomcp_set_defer_cutoff"):
+            return   # an explicitly chosen measurement library from older sources (always defers)
+        self._check(self._lib.pomcp_set_defer_cutoff(self._ctx, 1 if on else 0), "set_defer_cutoff")
 
     def search_kernel(self):
         """The kernel the next search uses: "lane" or "wave"."""

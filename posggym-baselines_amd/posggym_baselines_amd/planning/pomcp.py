@@ -111,6 +111,10 @@ class POMCP:
         self._engine = PomcpEngine(model, agent_id, config, num_trees=self._K,
                                    num_sims=per, tree_key_base=self._rank * self._K,
                                    wall_clock=per is None, type_policies=type_policies)
+        # an episode planner re-roots after every search: look cut-off children
+        # up during the search rather than materialising them at every re-root
+        # (pomcp_set_defer_cutoff; same results, DESIGN.md §4 "Deferred records")
+        self._engine.set_defer_cutoff(False)
         self.step_limit = self._engine.step_limit
         self._logger = logging.getLogger()
         self._last_action = None
@@ -307,7 +311,11 @@ class BatchedPOMCP:
 
     def __init__(self, model, agent_id, config: MCTSConfig, num_trees: int, num_sims: int,
                  *, searches: int = 1, reroot: bool = False, capacities=None, stream=None,
-                 tree_key_base: int = 0, device: Optional[int] = None, type_policies=None):
+                 tree_key_base: int = 0, device: Optional[int] = None, type_policies=None,
+                 defer_cutoff: bool = True):
+        """defer_cutoff: defer cut-off children to the re-root (the default: the
+        trees are searched several times per re-root, e.g. restore()); False
+        when every search is followed by an update (``pomcp_set_defer_cutoff``)."""
         from posggym_baselines_amd.planning.engine import plan_capacities
         if capacities is None:
             step_limit = config.step_limit or model.spec.max_episode_steps
@@ -319,6 +327,7 @@ class BatchedPOMCP:
                                   capacities=capacities, stream=stream,
                                   tree_key_base=tree_key_base, device=device,
                                   type_policies=type_policies)
+        self.engine.set_defer_cutoff(defer_cutoff)
         self.engine.reset()
 
     def init_synthetic(self, env_seed_base: int = 1000):

@@ -13,17 +13,21 @@ from oracle.run import make_oracle, oracle_record
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["lane", "wave", "wave_tree", "wave_plain"])
+@pytest.fixture(autouse=True, params=["lane", "lane_eager", "wave", "wave_tree", "wave_plain"])
 def search_kernel(request, monkeypatch):
     """Every parity test runs on every search kernel: k_search (a tree per lane,
-    tree in HBM) and k_search_lds (a wave per tree, tree in LDS) -- with its
-    step-tree producer waves as the engine picks them ("wave"), forced on for
-    any depth limit ("wave_tree") and off ("wave_plain"); they must give the
-    same bits as the reference / oracle."""
-    kind, _, tree = request.param.partition("_")
+    tree in HBM) with cut-off children deferred to the re-root ("lane") and
+    looked up during the search ("lane_eager", pomcp_set_defer_cutoff) and
+    k_search_lds (a wave per tree, tree in LDS) -- with its step-tree producer
+    waves as the engine picks them ("wave"), forced on for any depth limit
+    ("wave_tree") and off ("wave_plain"); they must give the same bits as the
+    reference / oracle."""
+    kind, _, mode = request.param.partition("_")
     monkeypatch.setenv("POMCP_SEARCH_KERNEL", kind)
-    if tree:
-        monkeypatch.setenv("POMCP_STEP_TREE", "1" if tree == "tree" else "0")
+    if mode == "eager":
+        monkeypatch.setenv("POMCP_DEFER_CUTOFF", "0")
+    elif mode:
+        monkeypatch.setenv("POMCP_STEP_TREE", "1" if mode == "tree" else "0")
     return kind
 
 SQRT2 = math.sqrt(2)

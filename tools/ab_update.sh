@@ -12,7 +12,7 @@ if [ -n "$K" ]; then
 fi
 for n in "$@" "$@"; do
   echo "== $n" >> $O/exp.log
-  POMCP_LIB_PATH=$PWD/variants/lib_$n.so timeout -k 10 300 python bench.py --no-cpu-baseline --no-sub --steps 2 --warmup 1 --env PursuitEvasion-v1 --update-step --trees 32768 >> $O/exp.log 2>&1 || exit 1
+  POMCP_LIB_PATH=$PWD/variants/lib_$n.so timeout -k 10 300 python bench.py --no-cpu-baseline --no-sub --steps 2 --warmup 1 --env ${ENV:-PursuitEvasion-v1} --update-step --trees ${TREES:-32768} >> $O/exp.log 2>&1 || exit 1
 done
 python3 - $O/exp.log <<'PY'
 import json, sys

@@ -21,7 +21,7 @@ O=gpurun_out/ablate_$2
 mkdir -p $O
 for n in ${VARIANTS:-base philox3 nosel nobelief nolog base}; do
   echo "== $n" >> $O/exp.log
-  POMCP_LIB_PATH=$PWD/variants/lib_$n.so timeout -k 10 300 python bench.py --no-cpu-baseline --steps 2 --warmup 1 >> $O/exp.log 2>&1 || exit 1
+  POMCP_LIB_PATH=$PWD/variants/lib_$n.so timeout -k 10 300 python bench.py --no-cpu-baseline --no-sub --steps 2 --warmup 1 >> $O/exp.log 2>&1 || exit 1
 done
 python3 - $O/exp.log <<'PY'
 import json, sys

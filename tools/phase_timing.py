@@ -15,7 +15,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = "/tmp/libpomcp_hip_timing.so"
+LIB = os.environ.get("PT_PREBUILT") or "/tmp/libpomcp_hip_timing.so"
 os.environ["POMCP_LIB_PATH"] = LIB
 sys.path[:0] = [ROOT, os.path.join(ROOT, "posggym-baselines_amd")]
 NAMES = ["start+root (LDS)", "level: stats line wait", "level: selection",
@@ -35,9 +35,10 @@ def main():
     ap.add_argument("--kernel", default="lane", choices=["lane", "wave"])
     args = ap.parse_args()
     os.environ["POMCP_SEARCH_KERNEL"] = args.kernel
-    env = dict(os.environ, POMCP_EXTRA_FLAGS="-DPOMCP_PHASE_TIMING")
-    subprocess.run([sys.executable, "-c", "from posggym_baselines_amd import build; build.build(force=True)"],
-                   check=True, env=env, cwd=os.path.join(ROOT, "posggym-baselines_amd"))
+    if not os.environ.get("PT_PREBUILT"):   # else LIB was built beforehand (on the CPU side)
+        env = dict(os.environ, POMCP_EXTRA_FLAGS="-DPOMCP_PHASE_TIMING")
+        subprocess.run([sys.executable, "-c", "from posggym_baselines_amd import build; build.build(force=True)"],
+                       check=True, env=env, cwd=os.path.join(ROOT, "posggym-baselines_amd"))
     import numpy as np
     from posggym_baselines_amd import _native as N
     from posggym_baselines_amd.envs import DrivingModel
