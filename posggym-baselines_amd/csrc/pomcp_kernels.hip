@@ -392,21 +392,42 @@ __global__ __launch_bounds__(256) void k_reroot_child(DevParams p) {
 // Re-root, step 2: one WORKGROUP (kLogWaves waves) per SEARCH wave scans that
 // wave's shared log once, in order, and appends each record of a wanted child
 // to its tree's new root belief ({root_t + 1, v0, v1}), preserving insertion
-// order per tree.  A pass reads 64 kLogWaves consecutive records (one per
-// thread); a record's place is its tree's count so far + the matches of the
-// same tree in the earlier waves of the pass + its rank in its own wave.  (One
-// wave per log took ~0.3 s at 65,536 trees x 65,536 simulations: one
-// dependent round trip per 64 records.)
+// order per tree.  A pass reads kLogRecs x 64 kLogWaves consecutive records
+// (sub-pass j: record base + j T + thread); a record's place is its tree's
+// count before the pass + the same tree's matches earlier in the pass
+// (earlier sub-passes, then earlier waves of its sub-pass) + its rank in its
+// wave (same_lane_mask: 6 ballots, no loop).  All of a pass's loads are issued
+// together and the next pass's while it runs.  (One wave per log took ~0.3 s
+// at 65,536 trees x 65,536 simulations: one dependent round trip per 64
+// records.)
 constexpr int kLogWaves = 4;
+constexpr int kLogRecs = 4;   // records per thread per pass
+
+// The lanes whose 6-bit key equals this lane's, among the active ones (a
+// match-any on the tree lane of a log record: 6 ballots).
+__device__ __forceinline__ uint64_t same_lane_mask(uint32_t key, bool active) {
+  uint64_t m = __ballot(active);
+#pragma unroll
+  for (int b = 0; b < 6; ++b) {
+    const bool bit = ((key >> b) & 1u) != 0u;
+    const uint64_t bb = __ballot(bit);
+    m &= bit ? bb : ~bb;
+  }
+  return m;
+}
+
 __global__ __launch_bounds__(64 * kLogWaves) void k_extract(DevParams p) {
+  constexpr uint32_t T = kWave * kLogWaves;
+  constexpr int R = kLogRecs;
   const int sw = blockIdx.x;   // search wave
   const int lane = lane_id();
   const int w = (int)(threadIdx.x >> 6);
+  const uint64_t below = (1ull << lane) - 1ull;
   __shared__ uint32_t want[kWave];
   __shared__ int32_t cnt[kWave];
   __shared__ uint32_t tval[kWave];
   __shared__ int64_t dst[kWave];
-  __shared__ int32_t wc[kLogWaves][kWave];   // this pass's matches per wave and tree
+  __shared__ int32_t wc[R][kLogWaves][kWave];   // this pass's matches per sub-pass, wave and tree
   if (w == 0) {
     const int tree = sw * kWave + lane;
     const bool valid = tree < p.B;
@@ -416,53 +437,69 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_extract(DevParams p) {
     tval[lane] = (uint32_t)h.root_t + 1u;
     dst[lane] = ((int64_t)tree * 2 + (h.belief_sel ^ 1)) * p.Nr;
   }
+  for (int q = (int)threadIdx.x; q < R * kLogWaves * kWave; q += (int)T) (&wc[0][0][0])[q] = 0;
   __syncthreads();
   const WaveLog wl(p.plog, p.Np, sw, p.tm);
   const uint32_t n = p.wlog[sw];
-  constexpr uint32_t T = kWave * kLogWaves;
-  // the next pass's records are loaded while this pass runs
-  LogRec rn = {0xFFFFFFFFu, 0u, 0u};
-  uint32_t auxn = 0u;   // type-based: the particle's other-agent policy
-  if (threadIdx.x < n) {
-    rn = wl.load(threadIdx.x);
-    if (p.tm) auxn = wl.aux[threadIdx.x];
-  }
-  for (uint32_t base = 0; base < n; base += T) {
-    const uint32_t i = base + (uint32_t)threadIdx.x;
-    const LogRec r = rn;
-    const uint32_t aux = auxn;
-    if (i + T < n) {
-      rn = wl.load(i + T);
-      if (p.tm) auxn = wl.aux[i + T];
+  LogRec rn[R];
+  uint32_t auxn[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const uint32_t i = (uint32_t)j * T + threadIdx.x;
+    rn[j] = LogRec{0xFFFFFFFFu, 0u, 0u};
+    auxn[j] = 0u;   // type-based: the particle's other-agent policy
+    if (i < n) {
+      rn[j] = wl.load(i);
+      if (p.tm) auxn[j] = wl.aux[i];
     }
-    const uint32_t l = r.id >> kIdBits;
-    const bool m = i < n && want[l] == r.id;
-    wc[w][lane] = 0;
-    __builtin_amdgcn_wave_barrier();
-    // ranks in this wave, in lane order (matches are few: one child per tree)
-    int rank = 0;
-    uint64_t mask = __ballot(m);
-    while (mask) {
-      const int j = __ffsll((long long)mask) - 1;
-      mask &= mask - 1ull;
-      const int lj = __builtin_amdgcn_readlane((int)l, j);
-      if (lane == j) {
-        rank = wc[w][lj];
-        wc[w][lj] = rank + 1;
+  }
+  for (uint32_t base = 0; base < n; base += (uint32_t)R * T) {
+    LogRec r[R];
+    uint32_t aux[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      r[j] = rn[j];
+      aux[j] = auxn[j];
+      const uint32_t i2 = base + (uint32_t)(R + j) * T + threadIdx.x;   // the next pass
+      if (i2 < n) {
+        rn[j] = wl.load(i2);
+        if (p.tm) auxn[j] = wl.aux[i2];
       }
-      __builtin_amdgcn_wave_barrier();
+    }
+    bool m[R];
+    uint32_t l[R];
+    int rank[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const uint32_t i = base + (uint32_t)j * T + threadIdx.x;
+      l[j] = r[j].id >> kIdBits;
+      m[j] = i < n && want[l[j]] == r[j].id;
+      const uint64_t same = same_lane_mask(l[j], m[j]);
+      rank[j] = __popcll(same & below);
+      if (m[j] && (same >> lane) == 1ull) wc[j][w][l[j]] = __popcll(same);   // the tree's last lane
     }
     __syncthreads();
-    if (m) {
-      int pos = cnt[l] + rank;
-      for (int v = 0; v < w; ++v) pos += wc[v][l];
-      if (pos < p.Nr) p.belief[dst[l] + pos] = make_uint4(tval[l], r.v0, r.v1, aux);
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      if (m[j]) {
+        const int lj = (int)l[j];
+        int pos = cnt[lj] + rank[j];
+        for (int jj = 0; jj < j; ++jj)
+          for (int v = 0; v < kLogWaves; ++v) pos += wc[jj][v][lj];
+        for (int v = 0; v < w; ++v) pos += wc[j][v][lj];
+        if (pos < p.Nr) p.belief[dst[lj] + pos] = make_uint4(tval[lj], r[j].v0, r[j].v1, aux[j]);
+      }
     }
     __syncthreads();
     if (w == 0) {
       int add = 0;
 #pragma unroll
-      for (int v = 0; v < kLogWaves; ++v) add += wc[v][lane];
+      for (int j = 0; j < R; ++j)
+#pragma unroll
+        for (int v = 0; v < kLogWaves; ++v) {
+          add += wc[j][v][lane];
+          wc[j][v][lane] = 0;
+        }
       cnt[lane] += add;
     }
     __syncthreads();
@@ -935,64 +972,14 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
   const uint32_t n = p.wlog[sw];
   const uint32_t A = (uint32_t)p.A;
   const int64_t bstride = blk_stride_lines(p.lines);
-  uint32_t out = 0;
-  // the records of the next pass are loaded while this one runs (a pass's stores
-  // land below base + T, the next pass reads from base + T on)
-  LogRec rn = {0u, 0u, 0u};
-  uint32_t auxn = 0u;
-  if ((uint32_t)t < n) {
-    rn = wl.load(t);
-    if (p.tm) auxn = wl.aux[t];
-  }
-  for (uint32_t base = 0; base < n; base += T) {
-    const uint32_t i = base + (uint32_t)t;
-    LogRec r = rn;
-    uint32_t aux = auxn;
-    if (i + T < n) {
-      rn = wl.load(i + T);
-      if (p.tm) auxn = wl.aux[i + T];
-    }
-    bool keep = false, mat = false;
-    uint32_t l = 0u, nani = 0u;
-    uint64_t okey = 0ull;
-    int done = 0;
-    int32_t nid = -1;
-    int32_t* vis = nullptr;   // the node's visits (zeroed by k_compact): + 1 per record
-    const int tree = sw * kWave + (int)((i < n ? r.id : 0u) >> kIdBits);
-    if (i < n) {
-      l = r.id >> kIdBits;
-      const uint32_t id = r.id & kIdMask;
-      keep = true;
-      if (act[l]) {
-        if (id >= p.cut_base) {   // deferred record: its child is materialised below
-          const uint32_t ani = id - p.cut_base;
-          const int nb = ld_agent(p.cmap + (int64_t)tree * p.Nb + (int)(ani / A));
-          if (nb >= 0) {
-            mat = true;
-            nani = (uint32_t)nb * A + ani % A;
-            okey = Env::obs_key(sm, p.ego, r.v0, r.v1);
-            done = Env::done_of(p.ego, r.v0, r.v1);
-          }
-        } else if (id >= p.ovf_base) {
-          nid = ld_agent(p.ovf_new + (int64_t)tree * p.H + (id - p.ovf_base));
-          if (nid >= 0) vis = &p.ovf[(int64_t)tree * p.H + ((uint32_t)nid - p.ovf_base)].visits;
-        } else if (id >= 1u) {
-          const uint32_t ani = (id - 1u) / kSlots, k = (id - 1u) % kSlots;
-          const int nb = ld_agent(p.cmap + (int64_t)tree * p.Nb + (int)(ani / A));
-          if (nb >= 0) {
-            nid = (int32_t)(((uint32_t)nb * A + ani % A) * kSlots + k + 1u);
-            uint4* const bp = reinterpret_cast<uint4*>(p.an + tree_base_lines(tree, p.Nb, p.lines) +
-                                                       (int64_t)nb * bstride);
-            vis = reinterpret_cast<int32_t*>(bp + part_slot((int)(ani % A), (int)k)) + 3;
-          }
-        }
-        keep = nid >= 0 || mat;
-      }
-    }
-    CL_MARK(0);
-    CL_CNT(0, i < n);
-    CL_CNT(1, mat);
-    // ---- deferred records: find or insert the child
+  constexpr int R = kLogRecs;
+  const uint64_t below = (1ull << lane) - 1ull;
+  __shared__ int32_t ksum[R][kLogWaves];   // kept records per sub-pass and wave
+  // A deferred record's child, found or inserted (inline slots by CAS, else the
+  // overflow map in log order) and its absorbing flag set by the last arrival
+  // of the sub-pass; every thread calls it (workgroup barriers inside)
+  auto mat_block = [&](bool mat, int tree, uint32_t l, uint32_t nani, uint64_t okey, int done,
+                       int32_t& nid, int32_t*& vis, bool& keep) {
     if (__syncthreads_or(mat ? 1 : 0)) {
       uint32_t* flagw = nullptr;   // the word holding the child's absorbing flag ...
       uint32_t fbit = 0u;          // ... and its bit
@@ -1156,20 +1143,137 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
       CL_MARK(3);
       CL_CNT(3, flagw != nullptr);
     }
-    if (act[l] && i < n) {
-      if (vis != nullptr) atomicAdd(vis, 1);
-      if (keep) r.id = (uint32_t)nid | (l << kIdBits);
+  };
+  uint32_t out = 0;
+  // a pass = kLogRecs sub-passes of T records (sub-pass j: record base + j T +
+  // t), all loaded before any is stored, the next pass's loaded while this one
+  // runs; a kept record lands at or before its own place (in-place filter)
+  LogRec rn[R];
+  uint32_t auxn[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const uint32_t i = (uint32_t)(j * T + t);
+    rn[j] = LogRec{0u, 0u, 0u};
+    auxn[j] = 0u;
+    if (i < n) {
+      rn[j] = wl.load(i);
+      if (p.tm) auxn[j] = wl.aux[i];
     }
-    if (keep) atomicAdd(&kept[l], 1);
-    int nk = 0;
-    const int at = wg_rank(keep, &nk);   // (every thread has loaded its record)
-    if (keep) {
-      wl.store(out + (uint32_t)at, r);
-      if (p.tm) wl.aux[out + (uint32_t)at] = aux;
+  }
+  for (uint32_t base = 0; base < n; base += (uint32_t)(R * T)) {
+    LogRec r[R];
+    uint32_t aux[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      r[j] = rn[j];
+      aux[j] = auxn[j];
+      const uint32_t i2 = base + (uint32_t)((R + j) * T + t);
+      if (i2 < n) {
+        rn[j] = wl.load(i2);
+        if (p.tm) auxn[j] = wl.aux[i2];
+      }
     }
-    out += (uint32_t)nk;
+    bool keep[R], mat[R];
+    uint32_t l[R], nani[R];
+    uint64_t okey[R];
+    int done[R], tree[R];
+    int32_t nid[R];
+    int32_t* vis[R];   // the node's visits (zeroed by k_compact): + 1 per record
+    bool any_mat = false;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const uint32_t i = base + (uint32_t)(j * T + t);
+      keep[j] = false;
+      mat[j] = false;
+      l[j] = 0u;
+      nani[j] = 0u;
+      okey[j] = 0ull;
+      done[j] = 0;
+      nid[j] = -1;
+      vis[j] = nullptr;
+      tree[j] = sw * kWave + (int)((i < n ? r[j].id : 0u) >> kIdBits);
+      if (i < n) {
+        l[j] = r[j].id >> kIdBits;
+        const uint32_t id = r[j].id & kIdMask;
+        keep[j] = true;
+        if (act[l[j]]) {
+          if (id >= p.cut_base) {   // deferred record: its child is materialised below
+            const uint32_t ani = id - p.cut_base;
+            const int nb = p.cmap[(int64_t)tree[j] * p.Nb + (int)(ani / A)];
+            if (nb >= 0) {
+              mat[j] = true;
+              nani[j] = (uint32_t)nb * A + ani % A;
+              okey[j] = Env::obs_key(sm, p.ego, r[j].v0, r[j].v1);
+              done[j] = Env::done_of(p.ego, r[j].v0, r[j].v1);
+            }
+          } else if (id >= p.ovf_base) {
+            nid[j] = p.ovf_new[(int64_t)tree[j] * p.H + (id - p.ovf_base)];
+            if (nid[j] >= 0) vis[j] = &p.ovf[(int64_t)tree[j] * p.H + ((uint32_t)nid[j] - p.ovf_base)].visits;
+          } else if (id >= 1u) {
+            const uint32_t ani = (id - 1u) / kSlots, k = (id - 1u) % kSlots;
+            const int nb = p.cmap[(int64_t)tree[j] * p.Nb + (int)(ani / A)];
+            if (nb >= 0) {
+              nid[j] = (int32_t)(((uint32_t)nb * A + ani % A) * kSlots + k + 1u);
+              uint4* const bp = reinterpret_cast<uint4*>(p.an + tree_base_lines(tree[j], p.Nb, p.lines) +
+                                                         (int64_t)nb * bstride);
+              vis[j] = reinterpret_cast<int32_t*>(bp + part_slot((int)(ani % A), (int)k)) + 3;
+            }
+          }
+          keep[j] = nid[j] >= 0 || mat[j];
+        }
+      }
+      any_mat |= mat[j];
+      CL_CNT(0, i < n);
+      CL_CNT(1, mat[j]);
+    }
+    CL_MARK(0);
+    // deferred records: the sub-passes in log order (cmap / ovf_new are
+    // k_compact's output: plain loads; slots and the overflow map change
+    // here: ld_agent)
+    if (__syncthreads_or(any_mat ? 1 : 0)) {
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+        mat_block(mat[j], tree[j], l[j], nani[j], okey[j], done[j], nid[j], vis[j], keep[j]);
+    }
+    // visits, relabelling, per-tree counts, the pass's places
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const uint32_t i = base + (uint32_t)(j * T + t);
+      if (i < n && act[l[j]]) {
+        if (vis[j] != nullptr) atomicAdd(vis[j], 1);
+        if (keep[j]) r[j].id = (uint32_t)nid[j] | (l[j] << kIdBits);
+      }
+      const uint64_t same = same_lane_mask(l[j], keep[j]);
+      if (keep[j] && (same >> lane) == 1ull) atomicAdd(&kept[l[j]], __popcll(same));
+    }
+    uint64_t mk[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      mk[j] = __ballot(keep[j]);
+      if (lane == 0) ksum[j][w] = __popcll(mk[j]);
+    }
+    __syncthreads();
+    int tot = 0;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      int pre = 0, tj = 0;
+#pragma unroll
+      for (int v = 0; v < kLogWaves; ++v) {
+        pre += v < w ? ksum[j][v] : 0;
+        tj += ksum[j][v];
+      }
+      if (keep[j]) {
+        const uint32_t at = out + (uint32_t)(tot + pre + __popcll(mk[j] & below));
+        wl.store(at, r[j]);
+        if (p.tm) wl.aux[at] = aux[j];
+      }
+      tot += tj;
+    }
+    out += (uint32_t)tot;
+    __syncthreads();   // (ksum is rewritten by the next pass)
+#pragma unroll
+    for (int j = 0; j < R; ++j) CL_CNT(4, keep[j]);
     CL_MARK(4);
-    CL_CNT(4, keep);
   }
   __syncthreads();
 #ifdef PB_CLOG_TIMING
