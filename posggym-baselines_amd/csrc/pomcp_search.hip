@@ -71,6 +71,10 @@ __host__ __device__ constexpr int rc_stats(int a) { return a; }
 __host__ __device__ constexpr int rc_slot(int a, int k) { return kMaxA + a * kSlots + k; }
 
 constexpr int kRegPath = 3;  // levels 1..kRegPath held in registers (deeper ones in p.path)
+#ifndef PB_BQ_LEVELS
+#define PB_BQ_LEVELS 3
+#endif
+constexpr int kBq = PB_BQ_LEVELS;   // levels 1..kBq: backup stores queued (pomcp_search.hip q_flush)
 constexpr int kPre = 2 + kMaxA;   // node line parts read by a level: visits, node, {value, total}
 
 // One level (depth >= 1) of the running simulation's path: {block << 3 |
@@ -475,6 +479,44 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   int lf_b = -1;
   uint32_t lf_nv = 0;
   double lf_ln = 0.0;
+  // A simulation's backup writes of its register-path levels (node line bytes
+  // 0..31 and the action's {value, total}) wait in registers and are stored
+  // right after the NEXT simulation's first node-line load is issued: vmcnt
+  // completes in order on gfx950, so stores issued before that load made its
+  // wait also wait for their acknowledgements (as the particle-log record,
+  // DESIGN.md §4 "Deferred backup stores").  That load may read the level-1
+  // node the queue writes (a node is at one depth: only queue entry 0, the
+  // level-1 node, can be it): its line is patched from the entry (fw_*) when
+  // the level pass consumes it.  Queue entry l = path level l + 1.
+  int q_n = 0;                      // queued levels (0..kBq)
+  int q_b[kBq];                     // block
+  uint32_t q_a[kBq];                // action
+  uint4 q_s1[kBq], q_vt[kBq];       // node line part 1 as written, {value, total}
+  uint32_t q_v[kBq];                // action a's visits (node line word a, a < 4)
+  bool fw_on = false;               // the next level pass is depth 1: patch its line if fw_b
+  int fw_b = -1;
+  uint32_t fw_a = 0, fw_v = 0;
+  uint4 fw_s1 = make_uint4(0, 0, 0, 0), fw_vt = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int l = 0; l < kBq; ++l) {
+    q_b[l] = -1;
+    q_a[l] = 0u;
+    q_v[l] = 0u;
+    q_s1[l] = make_uint4(0, 0, 0, 0);
+    q_vt[l] = make_uint4(0, 0, 0, 0);
+  }
+  auto q_flush = [&]() {
+#pragma unroll
+    for (int l = 0; l < kBq; ++l) {
+      if (l < q_n) {
+        char* const lp = an + (int64_t)q_b[l] * blk_bytes;   // the node line
+        if (q_a[l] < 4u) reinterpret_cast<uint32_t*>(lp)[q_a[l]] = q_v[l];
+        reinterpret_cast<uint4*>(lp)[1] = q_s1[l];
+        reinterpret_cast<uint4*>(lp)[part_vt((int)q_a[l])] = q_vt[l];
+      }
+    }
+    q_n = 0;
+  };
   auto logtab = [&](int n) { return p.logtab[n < p.logtab_n ? n : 0]; };
 
   if (!valid || err != 0 || root_abs) phase = TP_DONE;   // mcts.py:270-272
@@ -645,6 +687,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   // A done arrival at a child that has a block (rare: it was expanded by an
   // earlier, non-terminal arrival): ObsNode.visits += 1 in its node line.
   auto bump_node = [&](int cb) {
+    q_flush();   // (rare) its line may be queued
     uint4* const c1 = reinterpret_cast<uint4*>(an + (int64_t)cb * blk_bytes) + 1;
     const uint4 x = *c1;
     const double ln = logtab((int)x.y + 2);
@@ -793,6 +836,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         }
       }
       root_logn = logtab(root_visits + 1);   // the next simulation's (no wait)
+      // the previous simulation's backup stores, after this one's first
+      // node-line load (descend); entry 0 forwards to it
+      fw_on = q_n > 0 && phase == TP_LEVEL;
+      fw_b = q_b[0];
+      fw_a = q_a[0];
+      fw_v = q_v[0];
+      fw_s1 = q_s1[0];
+      fw_vt = q_vt[0];
+      q_flush();
       PT_MARK(0);
     }
     // refill the lookahead words the root level consumed while the first level's
@@ -810,6 +862,17 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         PT_MARK(8);
         // the node line, prefetched by descend(): this arrival's N (its visits
         // + 1) and math.log(N) are in it
+        if (fw_on) {   // the line loaded before the previous backup's stores (q_flush)
+          fw_on = false;
+          if (blk == fw_b) {
+            const uint32_t a4 = fw_a;
+            pre[0] = make_uint4(a4 == 0u ? fw_v : pre[0].x, a4 == 1u ? fw_v : pre[0].y,
+                                a4 == 2u ? fw_v : pre[0].z, a4 == 3u ? fw_v : pre[0].w);
+            pre[1] = fw_s1;
+#pragma unroll
+            for (int q = 2; q < kPre; ++q) pre[q] = sel4(q == part_vt((int)a4), fw_vt, pre[q]);
+          }
+        }
         nvis = (int)pre[1].y + 1;
         const double log_n = hilo_d(pre[1].z, pre[1].w);
         const double lnx = logtab(nvis + 1);   // written back by the backup (no wait here)
@@ -973,7 +1036,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
     // ------------------------------------------------------ backup
     if (phase == TP_BACKUP) {                                // mcts.py:374-381
       double gr = ret;
-      auto level = [&](const PathEntry& pe) {
+      // ql >= 0: a register-path level, its stores queued as entry ql
+      auto level = [&](const PathEntry& pe, int ql) {
         const uint4 e0 = pe.e0, e1 = pe.e1, e2 = pe.e2;
         const double r = hilo_d(e0.z, e0.w);
         gr = (e0.x >> 31) ? r : r + p.discount * gr;
@@ -984,19 +1048,35 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         const double value = value0 + delta / (double)n;
         const uint32_t ba = e0.x & 0x7FFFFFFFu;
         const uint32_t a = ba & 7u;
-        char* const lp = an + (int64_t)(ba >> 3) * blk_bytes;   // the node line
-        if (a < 4u) reinterpret_cast<uint32_t*>(lp)[a] = (uint32_t)n;
-        reinterpret_cast<uint4*>(lp)[1] = make_uint4(a == 4u ? (uint32_t)n : e2.x, e2.y, e2.z, e2.w);
-        reinterpret_cast<uint4*>(lp)[part_vt((int)a)] =
-            make_uint4((uint32_t)__double2loint(value), (uint32_t)__double2hiint(value),
-                       (uint32_t)__double2loint(total), (uint32_t)__double2hiint(total));
+        const uint4 s1w = make_uint4(a == 4u ? (uint32_t)n : e2.x, e2.y, e2.z, e2.w);
+        const uint4 vtw = make_uint4((uint32_t)__double2loint(value), (uint32_t)__double2hiint(value),
+                                     (uint32_t)__double2loint(total), (uint32_t)__double2hiint(total));
+        if (ql < 0 || ql >= kBq) {
+          char* const lp = an + (int64_t)(ba >> 3) * blk_bytes;   // the node line
+          if (a < 4u) reinterpret_cast<uint32_t*>(lp)[a] = (uint32_t)n;
+          reinterpret_cast<uint4*>(lp)[1] = s1w;
+          reinterpret_cast<uint4*>(lp)[part_vt((int)a)] = vtw;
+        } else {
+#pragma unroll
+          for (int l = 0; l < kBq; ++l) {
+            if (l == ql) {
+              q_b[l] = (int)(ba >> 3);
+              q_a[l] = a;
+              q_v[l] = (uint32_t)n;
+              q_s1[l] = s1w;
+              q_vt[l] = vtw;
+            }
+          }
+        }
         if (value > mm_max) mm_max = value;   // utils.py:29-32
         if (value < mm_min) mm_min = value;
       };
-      for (int l = plen - 1; l >= kRegPath; --l) level(path[l]);
+      for (int l = plen - 1; l >= kRegPath; --l) level(path[l], -1);
+      q_flush();   // (nothing queued: the START after the previous backup flushed)
 #pragma unroll
       for (int l = kRegPath - 1; l >= 0; --l)
-        if (l < plen) level(rpath[l]);
+        if (l < plen) level(rpath[l], l);
+      q_n = plen < kBq ? plen : kBq;
       if (lf_b >= 0) {   // the expanded leaf's own visits and log(N)
         reinterpret_cast<uint4*>(an + (int64_t)lf_b * blk_bytes)[1] =
             make_uint4(0u, lf_nv, (uint32_t)__double2loint(lf_ln), (uint32_t)__double2hiint(lf_ln));
@@ -1029,6 +1109,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   }
 #endif
 
+  q_flush();   // the last simulation's backup stores
   // ------------------------------------------------------------------ results
   {   // the wave's log length: every lane's appends of this launch
     uint32_t mine = valid ? (uint32_t)(n_log - log0) : 0u;

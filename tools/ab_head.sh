@@ -1,0 +1,25 @@
+#!/bin/bash
+# A/B of the headline bench line (Driving-v1 65,536 x 65,536, restore steps)
+# between library variants: tools/ab_head.sh TAG "pytest -k expr or ''" lib1 lib2 ...
+set -o pipefail
+export TMPDIR=/tmp
+T=$1; K=$2; shift 2
+O=gpurun_out/abh_$T; mkdir -p $O
+if [ -n "$K" ]; then
+  timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$K" > $O/test.log 2>&1 || { tail -30 $O/test.log; exit 1; }
+  tail -1 $O/test.log
+fi
+for n in "$@" "$@"; do
+  echo "== $n" >> $O/exp.log
+  POMCP_LIB_PATH=$PWD/variants/lib_$n.so timeout -k 10 300 python bench.py --no-cpu-baseline --no-sub --steps 3 --warmup 1 $BENCH_ARGS >> $O/exp.log 2>&1 || exit 1
+done
+python3 - $O/exp.log <<'PY'
+import json, sys
+name = None
+for line in open(sys.argv[1]):
+    if line.startswith("=="):
+        name = line.split()[1]
+    elif line.startswith("{"):
+        d = json.loads(line)
+        print(f"{name:8s} {d['value']/1e9:6.3f} G sims/s  kernel {d['roofline']['kernel_ms']:8.1f} ms frac {d['roofline']['frac']:.4f}")
+PY
