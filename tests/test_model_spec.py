@@ -77,3 +77,34 @@ def test_intmcp_wallclock_capacities_within_budget():
     assert eng.headroom(st) == (caps.max_nodes - 20 - reserve) // L
     st = [SimpleNamespace(n_nodes=[caps.max_nodes - reserve, 0], n_log=[0, 0], n_stats=[0, 0])]
     assert eng.headroom(st) == 0
+
+
+def test_intmcp_nesting2_capacities_and_headroom():
+    """Nesting level 2 (three trees per pair): the arenas and the bytes per pair
+    count the third tree and the middle planner's belief table; the wall-clock
+    budget still holds; the headroom takes the fullest of the three trees
+    (intmcp_get_tree_counts)."""
+    import numpy as np
+    from posggym_baselines_amd.planning import MCTSConfig
+    from posggym_baselines_amd.planning import intmcp as M
+    cfg = MCTSConfig(discount=0.95, c=1.4, truncated=False, search_time_limit=1.0)
+    c1 = M.plan_intmcp_capacities(cfg, 50, 256, 4, 5, nesting_level=1)
+    c2 = M.plan_intmcp_capacities(cfg, 50, 256, 4, 5, nesting_level=2)
+    assert c1.trees == 2 and c2.trees == 3
+    assert c2.max_nodes > c1.max_nodes and c2.max_root_belief > c1.max_root_belief
+    assert c2.bytes_per_pair(5) > 1.4 * c1.bytes_per_pair(5)
+    assert c2.log_table_size >= 3 * 256 * 4
+    caps, sims = M.plan_intmcp_wallclock_capacities(cfg, 50, 5, nesting_level=2)
+    assert caps.trees == 3 and sims == int(1.0 / 3 * M.INTMCP_WALL_CLOCK_SIMS_PER_S + 0.999)
+    assert caps.bytes_per_pair(5) <= M.INTMCP_WALL_CLOCK_HBM_BUDGET * 1.1
+    eng = object.__new__(M.IntmcpEngine)
+    eng.config, eng.capacities, eng.step_limit, eng.A, eng.num_pairs = cfg, caps, 50, 5, 1
+    eng.nesting_level = 2
+    L = min(cfg.depth_limit, 50) + 1
+    target = cfg.num_particles + cfg.extra_particles
+    reserve = 2 * (int(-(-cfg.reinvigoration_sample_limit_factor * target // 1)) + target) \
+        + 2 * target + 8
+    counts = np.zeros((1, 3, 3), dtype=np.int32)
+    counts[0, 2, 0] = 1000     # the level-0 tree holds the most nodes
+    eng.tree_counts = lambda: counts
+    assert eng.headroom() == (caps.max_nodes - 1000 - reserve) // L
