@@ -23,6 +23,9 @@
 
 using namespace pb;
 
+// k_search lives in pomcp_search_tu.hip (a translation unit of its own)
+const void* pb_search_kernel(int row, int e, int sel);
+
 static_assert(sizeof(pomcp_grid) == sizeof(DrvGrid), "grid layout");
 static_assert(sizeof(pomcp_pe_grid) == 1344, "pe grid layout");
 static_assert(sizeof(Line) == 128, "block line layout");
@@ -519,20 +522,11 @@ static int launch_search(pomcp_ctx* ctx, int32_t num_sims, int final_sel) {
   const int tpb = search_tpb(ctx->dp.B);
   const dim3 grid((unsigned)((ctx->dp.B + tpb - 1) / tpb)), block((unsigned)tpb);
   // kernel per (environment, selection rule, workgroup size); the action count is the model's
-  using KFn = void (*)(DevParams, int, int);
-#define PB_SEARCH_ROW(T, TM)                                                                      \
-  {{k_search<EnvDriving, POMCP_SEL_PUCB, 5, T, TM>, k_search<EnvDriving, POMCP_SEL_UCB, 5, T, TM>, \
-    k_search<EnvDriving, POMCP_SEL_UNIFORM, 5, T, TM>},                                           \
-   {k_search<EnvPursuitEvasion, POMCP_SEL_PUCB, 4, T, TM>,                                        \
-    k_search<EnvPursuitEvasion, POMCP_SEL_UCB, 4, T, TM>,                                         \
-    k_search<EnvPursuitEvasion, POMCP_SEL_UNIFORM, 4, T, TM>}}
-  static const KFn table[4][2][3] = {PB_SEARCH_ROW(kTPB, 0), PB_SEARCH_ROW(kTPBSmall, 0),
-                                     PB_SEARCH_ROW(kTPB, 1), PB_SEARCH_ROW(kTPBSmall, 1)};
-#undef PB_SEARCH_ROW
   const int e = ctx->dp.env == POMCP_ENV_PURSUIT_EVASION ? 1 : 0;
   const int row = (ctx->dp.tm ? 2 : 0) + (tpb == kTPB ? 0 : 1);
-  hipLaunchKernelGGL(table[row][e][ctx->dp.sel], grid, block, 0, ctx->stream, ctx->dp,
-                     (int)num_sims, final_sel);
+  int sims = (int)num_sims, fsel = final_sel;
+  void* args[] = {&ctx->dp, &sims, &fsel};
+  HIP_TRY(ctx, hipLaunchKernel(pb_search_kernel(row, e, ctx->dp.sel), grid, block, args, 0, ctx->stream));
   HIP_TRY(ctx, hipGetLastError());
   return POMCP_OK;
 }

@@ -1267,6 +1267,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   so->n_deferred = c_defer;
 }
 
+// Instantiated only in pomcp_search_tu.hip, the translation unit of its own
+// that k_search is compiled in (its scheduler flag, build.py); the C-ABI's
+// launcher takes the kernels from pb_search_kernel below.
+#ifdef PB_SEARCH_TU
 #define PB_SEARCH_INST(E, NA, T, TM)                                                 \
   template __global__ void k_search<E, POMCP_SEL_PUCB, NA, T, TM>(DevParams, int, int);  \
   template __global__ void k_search<E, POMCP_SEL_UCB, NA, T, TM>(DevParams, int, int);   \
@@ -1281,4 +1285,25 @@ PB_SEARCH_INST(EnvDriving, 5, kTPBSmall, 1)
 PB_SEARCH_INST(EnvPursuitEvasion, 4, kTPBSmall, 1)
 #undef PB_SEARCH_INST
 
+#endif  // PB_SEARCH_TU
+
 }  // namespace pb
+
+#ifdef PB_SEARCH_TU
+// The k_search instantiation launched for (row = 2 * TM + small workgroups,
+// environment, selection rule): pomcp_capi.hip launch_search.
+__attribute__((visibility("hidden"))) const void* pb_search_kernel(int row, int e, int sel) {
+  using namespace pb;
+  using KFn = void (*)(DevParams, int, int);
+#define PB_SEARCH_ROW(T, TM)                                                                      \
+  {{k_search<EnvDriving, POMCP_SEL_PUCB, 5, T, TM>, k_search<EnvDriving, POMCP_SEL_UCB, 5, T, TM>, \
+    k_search<EnvDriving, POMCP_SEL_UNIFORM, 5, T, TM>},                                           \
+   {k_search<EnvPursuitEvasion, POMCP_SEL_PUCB, 4, T, TM>,                                        \
+    k_search<EnvPursuitEvasion, POMCP_SEL_UCB, 4, T, TM>,                                         \
+    k_search<EnvPursuitEvasion, POMCP_SEL_UNIFORM, 4, T, TM>}}
+  static const KFn table[4][2][3] = {PB_SEARCH_ROW(kTPB, 0), PB_SEARCH_ROW(kTPBSmall, 0),
+                                     PB_SEARCH_ROW(kTPB, 1), PB_SEARCH_ROW(kTPBSmall, 1)};
+#undef PB_SEARCH_ROW
+  return reinterpret_cast<const void*>(table[row][e][sel]);
+}
+#endif  // PB_SEARCH_TU
