@@ -29,7 +29,8 @@ FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-f
          f"-I{INCLUDE}", "-Wall", "-Wno-unused-function"]
 # k_search's unit only (pomcp_search_tu.hip): LLVM's iterative ILP scheduler,
 # +2% simulations/s on the headline, -5% on k_im_search
-SEARCH_FLAGS = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
+SEARCH_FLAGS = (os.environ.get("POMCP_SEARCH_FLAGS") or
+                "-mllvm -amdgpu-sched-strategy=iterative-ilp").split()   # env: A/B builds only
 # diagnostics builds (e.g. POMCP_EXTRA_FLAGS=-DPOMCP_PHASE_TIMING with a separate
 # POMCP_LIB_PATH); never the default library
 FLAGS += os.environ.get("POMCP_EXTRA_FLAGS", "").split()
