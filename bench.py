@@ -38,6 +38,10 @@ for _p in (ROOT, os.path.join(ROOT, "posggym-baselines_amd")):
 # tree level stepped (node 8 + A x 12 child statistics + 84), per leaf expansion
 # (A x 20 + 4), per obs node created.  The per-action record is {visits,
 # value, total}: ActionNode.agg is not kept, so it is not counted.
+# The POMCP search's count is planning/engine.py search_bytes (the same
+# constants, and only the work the timed kernel does: no child lookup at a
+# deferred level, no child write at a cut-off level, from k_search's
+# n_deferred / n_cutoff counters); these are I-NTMCP's (run_intmcp).
 B_SIM, B_NEW_NODE = 16, 28
 B_LOG_APPEND = 16   # of b_level: the particle-log record (the root level's only HBM term)
 
@@ -46,8 +50,6 @@ def b_level(A):
     return 8 + 12 * A + 84
 
 
-def b_expand(A):
-    return 20 * A + 4
 HBM_PEAK_GBS = 8000.0
 
 
@@ -186,7 +188,9 @@ class _ClockSampler:
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs = rank processes (default: WORLD_SIZE, else 1); outside a "
+                         "torch.distributed launch N > 1 starts the N ranks itself")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--trees", type=int, default=65536)
@@ -219,6 +223,11 @@ def parse():
     ap.add_argument("--no-sub", action="store_true",
                     help="skip the secondary-configuration records (`sub`) the default run "
                          "appends after the headline (profiling runs)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend of N > 1 ranks: nccl (= RCCL over xGMI, the "
+                         "measurement) or gloo (tests: several ranks sharing one GPU)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="tests only (with --dist-backend gloo): every rank on GPU 0")
     ap.add_argument("--cpu-sample-sims", type=int, default=16384)
     ap.add_argument("--cpu-sample-trees", type=int, default=4)
     ap.add_argument("--cpu-procs", type=int, default=16,
@@ -243,7 +252,6 @@ TM_SPEC = {"ego": {"u": [0.2] * 5, "acc": [0.1, 0.5, 0.1, 0.2, 0.1],
                    "stay": [0.6, 0.1, 0.1, 0.1, 0.1]},
            "other": {"o_u": [0.2] * 5, "o_fast": [0.05, 0.7, 0.05, 0.1, 0.1]},
            "meta": {"o_u": {"u": 0.5, "acc": 0.25, "stay": 0.25}, "o_fast": {"stay": 0.7, "u": 0.3}}}
-B_TM_LEVEL = 16 * 5   # TM: a level reads the node's action_probs and writes their moving average
 
 
 def type_policies(model):
@@ -285,7 +293,20 @@ def _cpu_worker(job):
     return sims, sims / r["value"]
 
 
-PORT_VS_REFERENCE = 1.15   # 6.8 k vs 6.0 k sims/s per core
+def _port_vs_reference():
+    """The oracle port's speed relative to the real reference planner on the
+    same workload, one core each, as last measured where the reference imports
+    (tools/port_vs_reference.py -> profiles/port_vs_reference.json; the
+    reference never travels to the GPU box)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "port_vs_reference.json")) as f:
+            r = json.load(f)
+        return {"port_vs_reference_speed": r["port_vs_reference_speed"],
+                "port_vs_reference": {k: r[k] for k in ("port_sims_per_s", "reference_sims_per_s",
+                                                        "sims", "trees", "cpu", "measured")
+                                      if k in r}}
+    except (OSError, ValueError, KeyError):
+        return {"port_vs_reference_speed": None}
 
 
 def cpu_baseline_parallel(sims, procs, seed, env="Driving-v1", base=None):
@@ -311,7 +332,7 @@ def cpu_baseline_parallel(sims, procs, seed, env="Driving-v1", base=None):
                       f"{procs} processes x 1 thread",
             # the port against the real reference planner on the same workload,
             # one core each, measured where the reference imports
-            "port_vs_reference_speed": PORT_VS_REFERENCE}
+            **_port_vs_reference()}
 
 
 def b_other(A):
@@ -492,7 +513,7 @@ def main_intmcp(args):
 
 
 def run_pomcp(dev, *, env, B, S, K, base_cfg, tm, steps, warmup, seed=0, max_blocks=512,
-              world=1, rank=0, dist=None, update_step=False, clocks=False):
+              world=1, rank=0, dist=None, update_step=False, clocks=False, defer=None):
     """`steps` timed POMCP steps on B synthetic roots (S simulations each; K
     replica trees per planner, merged on the device).  A step is restore() +
     one k_search launch + the root-parallel exchange, or with `update_step` a
@@ -502,8 +523,9 @@ def run_pomcp(dev, *, env, B, S, K, base_cfg, tm, steps, warmup, seed=0, max_blo
     import torch
     from posggym_baselines_amd.envs import DrivingModel, PursuitEvasionModel
     from posggym_baselines_amd.planning import BatchedPOMCP, MCTSConfig
-    from posggym_baselines_amd.planning.engine import plan_capacities
-    from posggym_baselines_amd.planning.parallel import gather_buffer_tensor, merge_buffer_tensor
+    from posggym_baselines_amd.planning.engine import plan_capacities, search_bytes
+    from posggym_baselines_amd.planning.parallel import (gather_buffer_tensor, gather_records,
+                                                         merge_buffer_tensor)
     lib_sha = _lib_sha16()
     cfg = MCTSConfig(seed=seed, num_sims=S, **base_cfg)
     model = PursuitEvasionModel() if env == "PursuitEvasion-v1" else DrivingModel()
@@ -543,8 +565,9 @@ def run_pomcp(dev, *, env, B, S, K, base_cfg, tm, steps, warmup, seed=0, max_blo
     # an update()-inclusive step re-roots after every search: the episode
     # planners' eager cut-off lookup (POMCP drop-in; pomcp_set_defer_cutoff);
     # a search-only step (restore) re-searches the same roots: deferred records
+    defer = (not update_step) if defer is None else bool(defer)
     bp = BatchedPOMCP(model, "0", cfg, B, S, capacities=caps, stream=stream.cuda_stream,
-                      defer_cutoff=not update_step,
+                      defer_cutoff=defer,
                       device=dev, type_policies=type_policies(model) if tm else None)
     try:
         bp.init_synthetic(1000)
@@ -575,8 +598,8 @@ def run_pomcp(dev, *, env, B, S, K, base_cfg, tm, steps, warmup, seed=0, max_blo
                 # records (RCCL, same stream), then the device merge of each planner's
                 # world x K replicas in replica order (pomcp_merge_roots) -- the same
                 # FP64 sums and action on every rank
-                if world > 1:
-                    dist.all_gather_into_tensor(gather, merge)
+                if world > 1:   # RCCL: all_gather_into_tensor on this stream (gloo: via host)
+                    gather_records(merge, gather)
                 bp.engine.merge_roots(K, fetch=False, world=world if world > 1 else 0)
 
         for _ in range(warmup):
@@ -607,12 +630,11 @@ def run_pomcp(dev, *, env, B, S, K, base_cfg, tm, steps, warmup, seed=0, max_blo
             with torch.cuda.stream(stream):
                 bp.search(fetch=False)
             torch.cuda.synchronize()
-        st = bp.engine.root_stats()
+        st = list(bp.engine.root_stats())
         sims = sum(s.num_sims for s in st)          # counted by the kernel, last timed launch
         levels = sum(s.n_levels for s in st)
-        expands = sum(s.n_expansions for s in st)
-        new_nodes = sum(s.n_new_nodes for s in st)
         deferred = sum(s.n_deferred for s in st)
+        cutoff = sum(s.n_cutoff for s in st)
         rollout = sum(s.n_rollout_steps for s in st)
         blocks_used = max(s.n_blocks for s in st)
         log_used = max(s.n_log for s in st)
@@ -622,9 +644,8 @@ def run_pomcp(dev, *, env, B, S, K, base_cfg, tm, steps, warmup, seed=0, max_blo
                 raise SystemExit("merged action out of range")
     finally:
         bp.close()
-    alg_bytes = B_SIM * sims + b_level(A) * levels + b_expand(A) * expands + B_NEW_NODE * new_nodes
-    if tm:   # the action_probs of every stepped node (+ 8A written per leaf expansion)
-        alg_bytes += B_TM_LEVEL * levels + 8 * A * expands
+    # tm: + the action_probs of every stepped node (+ 8A written per leaf expansion)
+    alg_bytes = search_bytes(st, A, tm)
     # the root level of every simulation is served from LDS / registers except
     # its particle-log append: its other bytes never reach HBM
     root_levels = min(sims, levels)
@@ -652,17 +673,21 @@ def run_pomcp(dev, *, env, B, S, K, base_cfg, tm, steps, warmup, seed=0, max_blo
                        "(fixed distributions), " if tm else "")
                     + (f"{B // K} planner(s) x {K} replica trees merged on the device, "
                        if K > 1 else "")
+                    + ("cut-off children deferred to the re-root, " if defer and not tm else
+                       "cut-off children looked up during the search, ")
                     + ("each step = search + env step + update() (re-root, extraction, "
                        "reinvigoration, subtree compaction)" if update_step else
                        f"root-parallel all-gather over {world} GPU(s)"),
         "rollout_steps_per_sim": rollout / max(sims, 1),
         "deferred_levels_per_sim": deferred / max(sims, 1),
+        "cutoff_levels_per_sim": cutoff / max(sims, 1), "defer_cutoff": defer,
         "blocks_used": blocks_used, "log_used": log_used, "depth_limit": cfg.depth_limit,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "k_search" if B > 256 or K > 1 else "k_search_lds",
                      "kernel_ms": kernel_ms,
                      "alg_bytes_per_launch": alg_bytes,
+                     "alg_bytes_per_sim": alg_bytes / max(sims, 1),
                      # the same without the root level's LDS-served bytes
                      "alg_bytes_hbm_per_launch": alg_bytes_hbm,
                      "achieved_hbm": achieved_hbm, "frac_hbm": achieved_hbm / HBM_PEAK_GBS},
@@ -688,6 +713,8 @@ def _sub(name, r):
          "ms_per_step": r["ms_per_step"], "kernel": r["roofline"]["kernel"],
          "kernel_ms": r["roofline"]["kernel_ms"], "frac": r["roofline"]["frac"],
          "frac_hbm": r["roofline"]["frac_hbm"]}
+    if "defer_cutoff" in r:
+        d["defer_cutoff"] = r["defer_cutoff"]
     if "update_ms" in r:
         d["update_ms"] = r["update_ms"]
     return d
@@ -699,6 +726,9 @@ def sub_records(dev, seed):
     region) and 5, each with a few timed steps; a failure is recorded, never
     fatal to the headline line."""
     jobs = [
+        ("C2 headline workload, eager cut-off lookup (the POMCP drop-in's mode)",
+         lambda: run_pomcp(dev, env="Driving-v1", B=65536, S=65536, K=1, base_cfg=TEST_CFG,
+                           tm=False, steps=3, warmup=1, seed=seed, defer=False)),
         ("C2 exact single tree (1 x 65536 sims)",
          lambda: run_pomcp(dev, env="Driving-v1", B=1, S=65536, K=1, base_cfg=TEST_CFG, tm=False,
                            steps=3, warmup=1, seed=seed)),
@@ -724,15 +754,103 @@ def sub_records(dev, seed):
     return out
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_plan(n, argv, port, base_env=None):
+    """The N rank processes `python bench.py --gpus N ...` starts when it is not
+    already a torch.distributed rank: one process per GPU (the process-per-
+    worker shape of baseline_exps/run_planning_exps.py:378-380), each with the
+    env torch.distributed.run would give it.  Returns [(argv, env)] by rank."""
+    env0 = dict(os.environ if base_env is None else base_env)
+    env0.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only (RCCL)
+    plan = []
+    for r in range(n):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        plan.append(([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), env))
+    return plan
+
+
+def _gpu_count():
+    """Visible GPUs, counted without initialising the GPU in this process
+    (torch.cuda.device_count() does not on this image): the launcher starts its
+    rank processes afterwards and must never run GPU code itself."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def spawn_ranks(n, argv):
+    """`--gpus N > 1` outside a torch.distributed launch: check that N GPUs are
+    visible, start N rank processes (before this process touches the GPU), wait
+    for them and exit with the first failing rank's status (0 if all pass).
+    Rank 0 prints the JSON line; a rank that fails ends the others."""
+    have = _gpu_count()
+    if "--share-gpu" in argv and have >= 1:   # tests: ranks share GPU 0 (gloo)
+        have = n
+    if have < n:
+        print(f"bench.py: --gpus {n} needs {n} visible GPUs, this node has {have}: "
+              "nothing was run", file=sys.stderr, flush=True)
+        return 3
+    import signal
+    import subprocess
+    plan = launch_plan(n, argv, _free_port())
+
+    def _term(signum, frame):   # the launcher's own SIGTERM ends its ranks (finally below)
+        raise SystemExit(128 + signum)
+    signal.signal(signal.SIGTERM, _term)
+    procs = [subprocess.Popen(a, env=e) for a, e in plan]
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                r = p.poll()
+                if r is None:
+                    continue
+                live.remove(p)
+                if r != 0 and rc == 0:
+                    rc = r if r > 0 else 128 - r
+                    print(f"bench.py: rank {procs.index(p)} exited with {r}; stopping the "
+                          "other ranks", file=sys.stderr, flush=True)
+                    for q in live:
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+            p.wait()
+    return rc
+
+
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if world == 0 and (args.gpus or 1) > 1:
+        # not a torch.distributed rank: become the launcher of N ranks (no GPU
+        # work in this process, so no exec-after-GPU-init hazard)
+        if args.planner == "intmcp":
+            raise SystemExit("--planner intmcp is a single-GPU configuration (BASELINE config 5)")
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    world = world or 1
+    if args.gpus is None:
+        args.gpus = world
+    if args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one "
+                         "process per GPU (torch.distributed.run --nproc-per-node N ... "
+                         "--gpus N, or python bench.py --gpus N)")
     _smi_static()   # before anything touches the GPU
     if args.planner == "intmcp":
         return main_intmcp(args)
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     cpu = None
@@ -751,10 +869,26 @@ def main():
         cpu = cpu_baseline_parallel(sample, procs, args.seed, args.env, base_cfg)
     if rank == 0:
         _build_if_missing()
+    rccl_ranks = None
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if args.share_gpu:
+            if args.dist_backend != "gloo":
+                raise SystemExit("bench.py: --share-gpu needs --dist-backend gloo")
+            local = 0
+        if local >= torch.cuda.device_count():
+            raise SystemExit(f"bench.py: rank {rank} (LOCAL_RANK {local}) has no GPU: "
+                             f"{torch.cuda.device_count()} visible")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+        formed = dist.get_world_size()
+        if formed != world:
+            raise SystemExit(f"bench.py: the process group formed with {formed} ranks, "
+                             f"expected {world}")
+        rccl_ranks = formed if args.dist_backend == "nccl" else None
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
@@ -789,7 +923,11 @@ def main():
                    "sims_per_planner_step": S * K,
                    "rollout_steps_per_sim": r["rollout_steps_per_sim"],
                    "deferred_levels_per_sim": r["deferred_levels_per_sim"],
+                   "cutoff_levels_per_sim": r["cutoff_levels_per_sim"],
+                   "defer_cutoff": r["defer_cutoff"],
+                   "collective": (args.dist_backend if world > 1 else None),
                    "parallelism": f"root-parallel x{world}",
+                   "rccl_ranks": rccl_ranks,
                    "device": dict(_device_info(dev), during_run=r["clocks"]),
                    "lib_sha16": r["lib_sha"], "counted_sims_per_step": r["counted"],
                    "arena": {"max_blocks": caps.max_blocks,

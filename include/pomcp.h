@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define POMCP_ABI_VERSION 4
+#define POMCP_ABI_VERSION 5
 #define POMCP_MAX_ACTIONS 8
 #define POMCP_MAX_TYPE_POLICIES 8
 
@@ -118,12 +118,21 @@ typedef struct pomcp_root_stats {
   /* work counters (algorithmic-byte accounting) */
   int64_t n_levels;             /* tree levels stepped (mcts.py:330-381) */
   int64_t n_expansions;         /* leaf expansions (mcts.py:318-321) */
-  int64_t n_new_nodes;          /* obs nodes created (mcts.py:369) */
+  int64_t n_new_nodes;          /* obs nodes created (mcts.py:369); with deferred cut-off
+                                   records (pomcp_set_defer_cutoff) the children first
+                                   reached by those records are not included -- they are
+                                   created at the next re-root, if they survive it */
   int64_t n_rollout_steps;      /* model steps in _rollout (mcts.py:414-450) */
   int64_t n_probes;             /* obs-child hash bucket probes */
   int32_t n_obs_nodes, n_blocks, n_log;
   int32_t n_deferred;           /* levels whose child (beyond the depth / step limits) was
                                    not looked up: deferred records */
+  int32_t n_cutoff;             /* levels below the root whose child lies beyond the depth /
+                                   step limits (mcts.py:315), deferred or looked up; their
+                                   child slot is not rewritten (0: the wave kernel) */
+  int32_t n_exact_selects;      /* UCB / PUCB selections decided by the exact FP64 scores
+                                   (near-ties of the fast scores, DESIGN.md §4 "Fast
+                                   selection"; pomcp_debug_set_select_margin widens it) */
 } pomcp_root_stats;
 
 typedef struct pomcp_ctx pomcp_ctx;

@@ -39,6 +39,14 @@ int pomcp_debug_set_spin_limit(pomcp_ctx* ctx, int32_t polls);
  * this call on the exact-path draws are counted: intmcp_debug_exact_draws. */
 int intmcp_debug_set_softmax_slack(intmcp_ctx* ctx, float slack);
 int intmcp_debug_exact_draws(intmcp_ctx* ctx, uint64_t* count);
+/* k_search's fast UCB / PUCB selection (DESIGN.md §4 "Fast selection") takes
+ * the fast scores' leader unless an action with different statistics scores
+ * within `rel` of it relative to their magnitudes, and then decides with the
+ * exact FP64 scores (mcts.py:502-546).  rel >= 1e-12 (the default, above the
+ * fast scores' proven error) keeps results exact; a large rel (e.g. 1e-4)
+ * sends most selections down the exact path.  pomcp_root_stats.n_exact_selects
+ * counts them per tree and search. */
+int pomcp_debug_set_select_margin(pomcp_ctx* ctx, double rel);
 /* Only the first n (1..6) inline obs-child slots of each action node are used,
  * the overflow map holds the rest (tests of that path).  Before the first search. */
 int pomcp_debug_set_inline_slots(pomcp_ctx* ctx, int32_t n);

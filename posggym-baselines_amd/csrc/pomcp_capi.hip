@@ -16,6 +16,9 @@
 
 // Single translation unit: the kernels are compiled together with their launchers.
 #include "pomcp_kernels.hip"
+// the host-only entry points (environment models, RNG words, log / exp tables):
+// plain C++, also built on its own with the host sanitizers (tests/test_host_sanitize.py)
+#include "host_api.cpp"
 #include "pomcp_search.hip"
 #include "pomcp_search_lds.hip"
 #include "intmcp.hip"
@@ -53,6 +56,11 @@ struct pomcp_ctx {
   int search_kind = POMCP_SEARCH_AUTO;
   TmTables host_tm{};                    // type-based contexts (pomcp_set_type_policies)
   bool tm_set = false;
+  // a lane search with deferred cut-off records ran since the last update /
+  // reset / restore: the mode and the kernel stay fixed until the re-root
+  // materialises those children (a record's absorbing flag must not race an
+  // eager arrival's, mcts.py:370)
+  bool defer_pending = false;
 };
 
 // Wave-per-tree search (k_search_lds) for batches up to this many trees: one
@@ -66,10 +74,6 @@ constexpr int64_t kWaveSearchMaxScratch = (int64_t)4 << 30;
 // step-tree producers for depth limits up to this (use_step_tree)
 constexpr int kStepTreeMaxDepth = 8;
 
-static void make_model(const pomcp_grid* g, DrvModel* m) {
-  std::memcpy(&m->g, g, sizeof(DrvGrid));
-  build_model_tables(m->g, m);
-}
 
 // Launch `KERNEL<Env>` for the context's environment.
 #define PB_ENV_LAUNCH(ctx, KERNEL, grid, block, ...)                                          \
@@ -255,6 +259,7 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
   d.ovf_base = (uint32_t)(c.max_blocks * c.num_actions * kSlots + 1);
   d.cut_base = d.ovf_base + (uint32_t)c.overflow_slots;
   d.defer = 1;   // deferred cut-off records (pomcp_set_defer_cutoff)
+  d.sel_margin = 1e-12;   // fast-selection margin (pomcp_debug_set_select_margin)
   d.islots = kSlots;
   d.tm = c.type_based;
   d.lines = blk_lines(d.A, d.tm);
@@ -359,6 +364,7 @@ int pomcp_reset(pomcp_ctx* ctx) {
   hipLaunchKernelGGL(k_reset, dim3(grid_blocks(ctx->dp.B)), dim3(256), 0, ctx->stream, ctx->dp);
   HIP_TRY(ctx, hipGetLastError());
   ctx->have_snapshot = false;
+  ctx->defer_pending = false;
   return POMCP_OK;
 }
 
@@ -434,6 +440,7 @@ int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_key
   HIP_TRY(ctx, hipMemcpyAsync(ctx->host_upd.data(), ctx->dp.upd_out, sizeof(int32_t) * 2 * B,
                               hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->defer_pending = false;   // k_compact_log materialised the surviving deferred children
   if (root_absorbing_out)
     for (int t = 0; t < B; ++t) root_absorbing_out[t] = ctx->host_upd[2 * t];
   return first_tree_error(ctx, ctx->host_upd.data(), 2, 1, "update");
@@ -458,6 +465,15 @@ int pomcp_set_search_kernel(pomcp_ctx* ctx, int32_t kind) {
     return fail(ctx, POMCP_E_UNSUPPORTED, "set_search_kernel: wave search scratch too large");
   if (kind == POMCP_SEARCH_WAVE && ctx->dp.tm)
     return fail(ctx, POMCP_E_UNSUPPORTED, "set_search_kernel: the type-based search is lane-per-tree");
+  if (ctx->defer_pending) {
+    const int was = ctx->search_kind;
+    ctx->search_kind = kind;
+    const bool same = resolve_search_kind(ctx) == POMCP_SEARCH_LANE;
+    ctx->search_kind = was;
+    if (!same)
+      return fail(ctx, POMCP_E_STATE, "set_search_kernel: deferred cut-off records are pending "
+                                      "(update, reset or restore first)");
+  }
   ctx->search_kind = kind;
   return POMCP_OK;
 }
@@ -468,6 +484,9 @@ int32_t pomcp_search_kernel_used(const pomcp_ctx* ctx) {
 
 int pomcp_set_defer_cutoff(pomcp_ctx* ctx, int32_t on) {
   if (!ctx || (on != 0 && on != 1)) return POMCP_E_INVALID;
+  if (ctx->defer_pending && on != ctx->dp.defer)
+    return fail(ctx, POMCP_E_STATE, "set_defer_cutoff: deferred cut-off records are pending "
+                                    "(update, reset or restore first)");
   ctx->dp.defer = on;
   return POMCP_OK;
 }
@@ -528,6 +547,7 @@ static int launch_search(pomcp_ctx* ctx, int32_t num_sims, int final_sel) {
   void* args[] = {&ctx->dp, &sims, &fsel};
   HIP_TRY(ctx, hipLaunchKernel(pb_search_kernel(row, e, ctx->dp.sel), grid, block, args, 0, ctx->stream));
   HIP_TRY(ctx, hipGetLastError());
+  if (ctx->dp.defer && !ctx->dp.tm && num_sims > 0) ctx->defer_pending = true;
   return POMCP_OK;
 }
 
@@ -901,127 +921,7 @@ int pomcp_restore(pomcp_ctx* ctx) {
   hipLaunchKernelGGL(k_restore, dim3(grid_blocks(ctx->dp.B)), dim3(256), 0, ctx->stream, ctx->dp,
                      ctx->snap_hdr);
   HIP_TRY(ctx, hipGetLastError());
-  return POMCP_OK;
-}
-
-// ---------------------------------------------------------------- host model
-
-int pomcp_driving_sample_initial_state(const pomcp_grid* g, uint64_t seed, uint32_t tree,
-                                       uint32_t* model_ctr, uint32_t state_out[2]) {
-  if (!g || !model_ctr || !state_out) return POMCP_E_INVALID;
-  const DrvGrid& gg = *reinterpret_cast<const DrvGrid*>(g);
-  Streams s;
-  s.seed = seed;
-  s.tree = tree;
-  for (int k = 0; k < 5; ++k) s.ctr[k] = 0;
-  s.ctr[2] = *model_ctr;
-  drv_sample_initial_state2(gg, [&](uint32_t n) { return s.model(n); }, &state_out[0],
-                            &state_out[1]);
-  *model_ctr = s.ctr[2];
-  return POMCP_OK;
-}
-
-int pomcp_driving_step(const pomcp_grid* g, uint64_t seed, uint32_t tree, uint32_t* model_ctr,
-                       const uint32_t state[2], const int32_t actions[2], uint32_t next_out[2],
-                       double rewards_out[2], int32_t terminated_out[2],
-                       uint64_t obs_keys_out[2]) {
-  if (!g || !model_ctr || !state || !actions || !next_out) return POMCP_E_INVALID;
-  DrvModel m;
-  make_model(g, &m);
-  Streams s;
-  s.seed = seed;
-  s.tree = tree;
-  for (int k = 0; k < 5; ++k) s.ctr[k] = 0;
-  s.ctr[2] = *model_ctr;
-  const uint32_t j = s.model(2);   // execution-order shuffle
-  *model_ctr = s.ctr[2];
-  drv_step2_fast(m, state[0], state[1], actions[0], actions[1], j, &next_out[0], &next_out[1]);
-  for (int i = 0; i < 2; ++i) {
-    if (rewards_out) rewards_out[i] = drv_reward_fast(m, state[i], next_out[i]);
-    if (terminated_out) terminated_out[i] = veh_done(next_out[i]) ? 1 : 0;
-  }
-  if (obs_keys_out) {
-    obs_keys_out[0] = obs_key_fast(m, next_out[0], next_out[1]);
-    obs_keys_out[1] = obs_key_fast(m, next_out[1], next_out[0]);
-  }
-  return POMCP_OK;
-}
-
-int pomcp_driving_obs(const pomcp_grid* g, const uint32_t state[2], uint64_t obs_keys_out[2]) {
-  if (!g || !state || !obs_keys_out) return POMCP_E_INVALID;
-  DrvModel m;
-  make_model(g, &m);
-  obs_keys_out[0] = obs_key_fast(m, state[0], state[1]);
-  obs_keys_out[1] = obs_key_fast(m, state[1], state[0]);
-  return POMCP_OK;
-}
-
-// ---------------------------------------------------------- host RNG streams
-
-int pomcp_philox_words(uint64_t seed, uint32_t tree, uint32_t stream, uint32_t first, int32_t n,
-                       uint32_t* out) {
-  if (n < 0 || (n > 0 && !out)) return POMCP_E_INVALID;
-  for (int32_t k = 0; k < n; ++k) out[k] = philox_word(seed, tree, stream, first + (uint32_t)k);
-  return POMCP_OK;
-}
-
-// ---------------------------------------------------------- host log(N) table
-
-// out[i] = log((double)i) for i in [first, first + n), out[0] of i = 0 is 0.0:
-// the host C library's log, the function Python's math.log calls for a float
-// (Modules/mathmodule.c), so the table is math.log's bit for bit at C speed
-// (tests/test_host_exp.py checks it against math.log).
-int pomcp_host_log_table(int64_t first, int64_t n, double* out) {
-  if (first < 0 || n < 0 || (n > 0 && !out)) return POMCP_E_INVALID;
-  for (int64_t k = 0; k < n; ++k) {
-    const int64_t i = first + k;
-    out[k] = i == 0 ? 0.0 : std::log((double)i);
-  }
-  return POMCP_OK;
-}
-
-// ---------------------------------------------------------- host PursuitEvasion
-
-int pomcp_pe_sample_initial_state(const pomcp_pe_grid* g, uint64_t seed, uint32_t tree,
-                                  uint32_t* model_ctr, uint32_t state_out[2]) {
-  if (!g || !model_ctr || !state_out) return POMCP_E_INVALID;
-  PeModel m;
-  build_pe_model(*g, &m);
-  Streams s;
-  s.seed = seed;
-  s.tree = tree;
-  for (int k = 0; k < 5; ++k) s.ctr[k] = 0;
-  s.ctr[2] = *model_ctr;
-  pe_sample_initial_state(m, [&](uint32_t n) { return s.model(n); }, &state_out[0], &state_out[1]);
-  *model_ctr = s.ctr[2];
-  return POMCP_OK;
-}
-
-int pomcp_pe_step(const pomcp_pe_grid* g, const uint32_t state[2], const int32_t actions[2],
-                  uint32_t next_out[2], double rewards_out[2], int32_t terminated_out[2],
-                  uint64_t obs_keys_out[2]) {
-  if (!g || !state || !actions || !next_out || !rewards_out || !terminated_out || !obs_keys_out)
-    return POMCP_E_INVALID;
-  for (int i = 0; i < 2; ++i)
-    if (actions[i] < 0 || actions[i] > 3) return POMCP_E_INVALID;
-  PeModel m;
-  build_pe_model(*g, &m);
-  uint32_t prog, outcome;
-  pe_step(m, state[0], state[1], (uint32_t)actions[0], (uint32_t)actions[1], &next_out[0],
-          &next_out[1], &prog, &outcome);
-  for (int i = 0; i < 2; ++i) {
-    rewards_out[i] = pe_reward(m, i, state[0], prog, outcome);
-    terminated_out[i] = pe_done(next_out[0]) ? 1 : 0;
-    obs_keys_out[i] = pe_obs_key(m, i, next_out[0], next_out[1]);
-  }
-  return POMCP_OK;
-}
-
-int pomcp_pe_obs(const pomcp_pe_grid* g, const uint32_t state[2], uint64_t obs_keys_out[2]) {
-  if (!g || !state || !obs_keys_out) return POMCP_E_INVALID;
-  PeModel m;
-  build_pe_model(*g, &m);
-  for (int i = 0; i < 2; ++i) obs_keys_out[i] = pe_obs_key(m, i, state[0], state[1]);
+  ctx->defer_pending = false;   // back to the post-update roots: no records left
   return POMCP_OK;
 }
 
@@ -1076,17 +976,19 @@ int pomcp_debug_exp(const double* x, int32_t n, double* out) {
   return e == hipSuccess ? POMCP_OK : POMCP_E_HIP;
 }
 
-// Debug: the same host_exp on the host CPU (tests/test_host_exp.py compares it
-// with math.exp without a GPU).
-int pomcp_debug_host_exp(const double* x, int32_t n, double* out) {
-  if (!x || !out || n < 0) return POMCP_E_INVALID;
-  for (int32_t i = 0; i < n; ++i) out[i] = host_exp(x[i]);
-  return POMCP_OK;
-}
 
 // Debug: use only the first n (1..6) inline obs slots of every action node, so
 // the overflow map serves the rest (tests of that path: the models here rarely
 // give an action node more than 6 obs children).  Before the first search.
+// Debug: k_search's fast-selection margin (pomcp_debug.h); >= 1e-12 keeps
+// results exact, larger sends more selections to the exact FP64 scores
+// (counted in pomcp_root_stats.n_exact_selects).
+int pomcp_debug_set_select_margin(pomcp_ctx* ctx, double rel) {
+  if (!ctx || !(rel >= 1e-12) || !(rel <= 1.0)) return POMCP_E_INVALID;
+  ctx->dp.sel_margin = rel;
+  return POMCP_OK;
+}
+
 int pomcp_debug_set_inline_slots(pomcp_ctx* ctx, int32_t n) {
   if (!ctx || n < 1 || n > kSlots) return POMCP_E_INVALID;
   ctx->dp.islots = n;

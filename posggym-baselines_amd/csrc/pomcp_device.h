@@ -217,6 +217,7 @@ struct DevParams {
                         // wave runs on without producers (0: the default; tests shrink it)
   int32_t tm;           // type-based search (POTMMCP): tmt, prior lines, log aux
   int32_t defer;        // k_search: defer cut-off children to the re-root (pomcp_set_defer_cutoff)
+  double sel_margin;    // k_search: fast-selection margin (1e-12; pomcp_debug_set_select_margin)
   const TmTables* tmt;
   TreeHdr* hdr;
   Line* an;             // [B][Nb][lines] action blocks

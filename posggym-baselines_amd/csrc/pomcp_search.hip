@@ -75,6 +75,7 @@ constexpr int kRegPath = 3;  // levels 1..kRegPath held in registers (deeper one
 #define PB_BQ_LEVELS 3
 #endif
 constexpr int kBq = PB_BQ_LEVELS;   // levels 1..kBq: backup stores queued (pomcp_search.hip q_flush)
+static_assert(kBq >= 1 && kBq <= kRegPath, "only register-path levels are queued (level() passes ql = -1 below)");
 constexpr int kPre = 2 + kMaxA;   // node line parts read by a level: visits, node, {value, total}
 
 // One level (depth >= 1) of the running simulation's path: {block << 3 |
@@ -196,7 +197,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   uint32_t c_bel = h->ctr[0], c_sel = h->ctr[1], c_mod = h->ctr[2], c_a0 = h->ctr[3],
            c_a1 = h->ctr[4];
   const int log0 = n_log, blocks0 = n_blocks, nodes0 = n_nodes;
-  int c_rollout = 0, c_probes = 0, c_defer = 0;
+  int c_rollout = 0, c_probes = 0, c_cut = 0, c_exact = 0;
 #ifdef POMCP_PHASE_TIMING
   uint64_t pt[16];
   for (int i = 0; i < 16; ++i) pt[i] = 0;
@@ -348,7 +349,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
 #pragma unroll
           for (int q = 0; q < A; ++q) {
             const bool same = st[q].x == sb.x && st[q].z == sb.z && st[q].w == sb.w;
-            amb |= q != af && !same && !(bf - sf[q] > 1e-12 * (mg[q] + bm));
+            amb |= q != af && !same && !(bf - sf[q] > p.sel_margin * (mg[q] + bm));
           }
           a = af;
           exact = amb;
@@ -407,7 +408,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
 #pragma unroll
           for (int q = 0; q < A; ++q) {
             const bool same = st[q].x == sb.x && st[q].z == sb.z && st[q].w == sb.w && cp[q] == bp;
-            amb |= q != af && !same && !(bf - sf[q] > 1e-12 * (mg[q] + bm));
+            amb |= q != af && !same && !(bf - sf[q] > p.sel_margin * (mg[q] + bm));
           }
           a = af;
           exact = amb;
@@ -424,6 +425,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         }
       }
       if (exact) {
+        ++c_exact;   // (the stats' n_exact_selects: tests force and count this path)
         a = 0;
         double best = sc[0];
 #pragma unroll
@@ -903,7 +905,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         // children that survive it).  TM looks it up: the node's prior moves
         // on arrivals at existing children (potmmcp.py:255-264).
         // (p.defer = 0, pomcp_set_defer_cutoff: the eager lookup -- cheaper re-roots)
-        const bool skipc = TM == 0 && p.defer && (depth + 1 > p.depth_limit || t + 1 > p.step_limit);
+        const bool cutc = depth + 1 > p.depth_limit || t + 1 > p.step_limit;   // mcts.py:315
+        c_cut += cutc ? 1 : 0;   // (stats: n_cutoff, and n_deferred when deferring)
+        const bool skipc = TM == 0 && p.defer && cutc;
         uint4 sl[kSlots];
   #pragma unroll
         for (int q = 0; q < kSlots; ++q) sl[q] = make_uint4(0, 0, 0, 0);
@@ -928,7 +932,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         leaf_rc = -1;
         if (skipc) {
           cid = p.cut_base + ani;
-          ++c_defer;
         } else if (ks >= 0) {
           uint4 sk = sl[0];
   #pragma unroll
@@ -946,9 +949,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
           uint4* slot = const_cast<uint4*>(ap) + part_slot(a, ks);
           // the slot changes beyond its visit count, or its count is needed
           // (no block yet, within the limits): pomcp_device.h
-          const bool cut = depth + 1 > p.depth_limit || t + 1 > p.step_limit;   // mcts.py:315
           const bool flip = (sk.y >> 31) != (uint32_t)done;
-          if (!match || flip || (cblk < 0 && (done || !cut)))
+          if (!match || flip || (cblk < 0 && (done || !cutc)))
             *slot = make_uint4((uint32_t)nk, (uint32_t)(nk >> 32), (uint32_t)cblk, (uint32_t)cvis);
           if (match && cblk >= 0 && done) bump_node(cblk);
           cid = ani * kSlots + (uint32_t)ks + 1u;
@@ -1264,7 +1266,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   so->n_obs_nodes = n_nodes;
   so->n_blocks = n_blocks;
   so->n_log = n_log;
-  so->n_deferred = c_defer;
+  so->n_deferred = TM == 0 && p.defer ? c_cut : 0;
+  so->n_cutoff = c_cut;
+  so->n_exact_selects = c_exact;
 }
 
 // Instantiated only in pomcp_search_tu.hip, the translation unit of its own

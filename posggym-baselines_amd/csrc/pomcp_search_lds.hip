@@ -1028,6 +1028,8 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
     so->n_blocks = n_blocks;
     so->n_log = n_log;
     so->n_deferred = 0;
+    so->n_cutoff = 0;          // (not counted by this kernel)
+    so->n_exact_selects = 0;   // (this kernel's scores are always the exact ones)
   }
 }
 

@@ -11,7 +11,7 @@ import os
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.environ.get("POMCP_LIB_PATH") or os.path.join(LIB_DIR, "libpomcp_hip.so")
 
-POMCP_ABI_VERSION = 4
+POMCP_ABI_VERSION = 5
 POMCP_MAX_TYPE_POLICIES = 8
 POMCP_MAX_ACTIONS = 8
 POMCP_XREC_STATS = 6
@@ -142,6 +142,8 @@ class PomcpRootStats(C.Structure):
         ("n_blocks", C.c_int32),
         ("n_log", C.c_int32),
         ("n_deferred", C.c_int32),
+        ("n_cutoff", C.c_int32),
+        ("n_exact_selects", C.c_int32),
     ]
 
 
@@ -235,6 +237,7 @@ DEBUG_SIGNATURES = [
     ("pomcp_debug_phase_timing", C.c_int,
      [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32, C.POINTER(C.c_int32)]),
     ("pomcp_debug_set_inline_slots", C.c_int, [C.c_void_p, C.c_int32]),
+    ("pomcp_debug_set_select_margin", C.c_int, [C.c_void_p, C.c_double]),
     ("pomcp_debug_set_spin_limit", C.c_int, [C.c_void_p, C.c_int32]),
     ("intmcp_debug_set_softmax_slack", C.c_int, [C.c_void_p, C.c_float]),
     ("intmcp_debug_exact_draws", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),

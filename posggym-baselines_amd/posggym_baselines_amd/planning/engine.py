@@ -79,6 +79,40 @@ def plan_capacities(config, step_limit: int, num_sims: int, searches: int = 1,
 # pomcp_kernels.hip k_compact), and get_action stops launching chunks before
 # a chunk could overflow it (POMCP.get_action), so a time-limited episode never
 # fails with POMCP_E_ARENA.  HBM budget for all trees of one engine:
+# Algorithmic HBM bytes of a search (DESIGN.md §4 "Algorithmic
+# bytes"), from the kernel's own per-tree counters: per simulation its root
+# particle (16); per tree level stepped the node (8) + A action statistics
+# (12 each) + child lookup (16) + child visit / absorbing flag (8 + 4) +
+# particle record (16) + backup of {visits, value, total} (40); per leaf
+# expansion 20 A + 4; per obs node created 28.  Charged only for what the
+# kernel does: no lookup at a deferred level (no probe), no child write at a
+# cut-off level (mcts.py:315).  Type-based searches add the node's
+# action_probs (16 A per level, 8 A per expansion).  bench.py's roofline
+# numerator and step_statistics["hbm_bytes"] both come from here.
+B_SIM, B_NEW_NODE, B_LOOKUP, B_CHILD_WRITE = 16, 28, 16, 12
+
+
+def b_level(A: int) -> int:
+    return 8 + 12 * A + 84
+
+
+def b_expand(A: int) -> int:
+    return 20 * A + 4
+
+
+def search_bytes(stats, A: int, type_based: bool = False) -> int:
+    """Algorithmic bytes of the last search of the trees in `stats`
+    (pomcp_root_stats records)."""
+    tot = 0
+    for s in stats:
+        tot += (B_SIM * s.num_sims + b_level(A) * s.n_levels - B_LOOKUP * s.n_deferred
+                - B_CHILD_WRITE * s.n_cutoff + b_expand(A) * s.n_expansions
+                + B_NEW_NODE * s.n_new_nodes)
+        if type_based:
+            tot += 16 * A * s.n_levels + 8 * A * s.n_expansions
+    return int(tot)
+
+
 WALL_CLOCK_SIMS_PER_S = 1_000_000
 WALL_CLOCK_HBM_BUDGET = 64 << 30
 

@@ -43,7 +43,7 @@ import psutil
 from posggym_baselines_amd.envs import engine_model
 
 from posggym_baselines_amd.planning.config import MCTSConfig
-from posggym_baselines_amd.planning.engine import PomcpEngine
+from posggym_baselines_amd.planning.engine import PomcpEngine, search_bytes
 from posggym_baselines_amd.planning.other_policy import RandomOtherAgentPolicy
 from posggym_baselines_amd.planning.search_policy import RandomSearchPolicy, SearchPolicy
 from posggym_baselines_amd.planning.utils import PlanningStatTracker
@@ -162,6 +162,9 @@ class POMCP:
             "evaluation_time": 0.0, "policy_calls": 0, "inference_time": 0.0,
             "search_depth": 0, "num_sims": 0, "mem_usage": 0,
             "min_value": self._min_value, "max_value": self._max_value,
+            # the build's additions (SURVEY §5 metrics): the search's algorithmic
+            # HBM bytes on this rank (engine.search_bytes) and its simulations/s
+            "hbm_bytes": 0, "sims_per_s": 0.0,
         }
 
     # -------------------------------------------------------------- update
@@ -204,6 +207,7 @@ class POMCP:
         start = time.time()
         K, world = self._K, self._world
         exc, depth, n_sims = None, 0, 0
+        self._hbm = 0
         try:
             depth, n_sims = self._search(start)
         except Exception as e:  # noqa: BLE001 -- raised on every rank below
@@ -231,13 +235,16 @@ class POMCP:
             ctot = tuple(st.totals[:A])
             cval = tuple(t / v if v > 0 else 0.0 for t, v in zip(ctot, cv))
         search_time = time.time() - start
+        if self._hbm is None:   # this rank's replicas' algorithmic bytes (engine.search_bytes)
+            self._hbm = search_bytes(self._engine.root_stats(), A, self._engine.type_based)
         self._min_value, self._max_value = st.min_value, st.max_value
         self.root = dataclasses.replace(
             self.root, visits=visits, belief_size=belief_size, child_visits=cv,
             child_values=cval, child_totals=ctot)
         self.step_statistics.update(
             search_time=search_time, search_depth=max(depth, st.search_depth), num_sims=n_sims,
-            min_value=st.min_value, max_value=st.max_value)
+            min_value=st.min_value, max_value=st.max_value, hbm_bytes=self._hbm,
+            sims_per_s=n_sims / search_time if search_time > 0 else 0.0)
         return action
 
     def _device(self):
@@ -247,8 +254,11 @@ class POMCP:
         """This rank's simulations of one get_action; returns (search depth
         seen by the chunk loop, simulations run by this rank's replicas)."""
         K, depth = self._K, 0
+        A = len(self.action_space)
+        tb = self._engine.type_based
         if self._num_sims is not None:
             self._engine.search(self._per_replica, fetch=False)
+            self._hbm = None   # counted after the decision (errors surface in the merge first)
             return depth, self._per_replica * K
         # the wall-clock loop (mcts.py:285) as launches of growing chunks; the
         # final action choice is drawn once, after the last one.  A chunk is
@@ -268,6 +278,7 @@ class POMCP:
             self._engine.search(n, final=False)
             room = self._engine.headroom()    # synchronises
             depth = max(depth, self._depth())
+            self._hbm += search_bytes(self._engine.root_stats(), A, tb)   # this chunk's
             done += n
             chunk = min(chunk * 2, 4096)
         self._engine.search(0, fetch=False)

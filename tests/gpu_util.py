@@ -45,7 +45,9 @@ def stats_record(st, A, searched, action, rows):
 
 
 def gpu_episode(cfg_kwargs, num_sims, env_seed, ego="0", max_steps=50, env="Driving-v1",
-                planner_cls="POMCP"):
+                planner_cls="POMCP", select_margin=None, exact=None):
+    """select_margin: k_search's fast-selection margin (pomcp_debug_set_select_margin);
+    exact: a list that receives each search's n_exact_selects."""
     from posggym_baselines_amd.planning import (IPOMCP, POMCP, RandomOtherAgentPolicy,
                                                 RandomSearchPolicy)
     model = product_model(env)
@@ -55,6 +57,10 @@ def gpu_episode(cfg_kwargs, num_sims, env_seed, ego="0", max_steps=50, env="Driv
         planner = IPOMCP(model, ego, config, others, RandomSearchPolicy(model, ego))
     else:
         planner = POMCP(model, ego, config, RandomSearchPolicy(model, ego))
+    if select_margin is not None:
+        from posggym_baselines_amd import _native as N
+        assert N.load().pomcp_debug_set_select_margin(planner._engine._ctx,
+                                                      float(select_margin)) == 0
     planner.reset()
     records = []
     A = model.action_spaces[ego].n
@@ -67,6 +73,8 @@ def gpu_episode(cfg_kwargs, num_sims, env_seed, ego="0", max_steps=50, env="Driv
             return a
         rows = planner.root_belief()
         st = planner._engine.root_stats()[0]
+        if exact is not None:
+            exact.append(int(st.n_exact_selects))
         rec = stats_record(st, A, True, a, rows)
         rec["num_sims"] = int(planner.step_statistics["num_sims"])
         if rec["num_sims"] == 0:
@@ -89,21 +97,24 @@ def _arena_usage(engine):
 
 
 def batched_episodes(cfg_kwargs, num_sims, env_seeds, steps, capacities=None, usage=None,
-                     inline_slots=None, probes=None, spin_limit=None):
+                     inline_slots=None, probes=None, spin_limit=None, env="Driving-v1",
+                     select_margin=None, counters=None):
     """Lockstep episodes of len(env_seeds) independent planners in ONE engine
     (tree b = planner b, env seed env_seeds[b]), `steps` real steps each.
     Returns per-tree record lists in the oracle format.  inline_slots: use only
     that many inline obs slots per action node (pomcp_debug_set_inline_slots);
     probes: a list that receives each search's overflow-map probes; spin_limit:
-    k_search_lds's polls of a late step-tree hand-off (pomcp_debug_set_spin_limit)."""
+    k_search_lds's polls of a late step-tree hand-off (pomcp_debug_set_spin_limit);
+    select_margin: k_search's fast-selection margin (pomcp_debug_set_select_margin);
+    counters: a list that receives each search's summed (n_exact_selects,
+    n_deferred, n_cutoff)."""
     import numpy as np
-    from oracle.driving import DrivingModel as EnvModel
-    from oracle.driving import pack_obs
+    from oracle.envs import make_model
     from oracle.episode import ENV_TREE_BASE
     from oracle.rng import S_ENV_POLICY_BASE, Streams
-    from posggym_baselines_amd.envs import DrivingModel
     from posggym_baselines_amd.planning import BatchedPOMCP
-    model = DrivingModel()
+    model = product_model(env)
+    A = model.action_spaces["0"].n
     B = len(env_seeds)
     bp = BatchedPOMCP(model, "0", product_config(cfg_kwargs, num_sims), B, num_sims,
                       searches=steps, reroot=True, capacities=capacities)
@@ -113,16 +124,19 @@ def batched_episodes(cfg_kwargs, num_sims, env_seeds, steps, capacities=None, us
     if spin_limit is not None:
         from posggym_baselines_amd import _native as N
         assert N.load().pomcp_debug_set_spin_limit(bp.engine._ctx, int(spin_limit)) == 0
+    if select_margin is not None:
+        from posggym_baselines_amd import _native as N
+        assert N.load().pomcp_debug_set_select_margin(bp.engine._ctx, float(select_margin)) == 0
     envs = []
     for s in env_seeds:
         es = Streams(s, ENV_TREE_BASE)
-        env = EnvModel(es)
-        st = env.sample_initial_state()
-        envs.append([es, env, st, env.sample_initial_obs(st)])
+        e = make_model(env, es)
+        st = e.sample_initial_state()
+        envs.append([es, e, st, e.sample_initial_obs(st)])
     records = [[] for _ in range(B)]
     last = np.full(B, -1, dtype=np.int32)
     for t in range(steps):
-        keys = np.array([pack_obs(e[3]["0"]) for e in envs], dtype=np.uint64)
+        keys = np.array([e[1].pack_obs(e[3]["0"]) for e in envs], dtype=np.uint64)
         if usage is not None:
             usage.append(("before_update", _arena_usage(bp.engine)))
         bp.engine.update(last, keys)
@@ -132,11 +146,16 @@ def batched_episodes(cfg_kwargs, num_sims, env_seeds, steps, capacities=None, us
         stats = bp.engine.root_stats()
         if probes is not None:
             probes.append(sum(int(st.n_probes) for st in stats))
+        if counters is not None:
+            counters.append((sum(int(st.n_exact_selects) for st in stats),
+                             sum(int(st.n_deferred) for st in stats),
+                             sum(int(st.n_cutoff) for st in stats)))
         for b in range(B):
-            records[b].append(stats_record(stats[b], 5, True, actions[b], bp.engine.root_belief(b)))
-            es, env, st, obs = envs[b]
-            acts = {"0": int(actions[b]), "1": es.randint(S_ENV_POLICY_BASE + 1, 5)}
-            ts = env.step(st, acts)
+            records[b].append(stats_record(stats[b], A, True, actions[b], bp.engine.root_belief(b)))
+            es, e, st, obs = envs[b]
+            acts = {"0": int(actions[b]), "1": es.randint(S_ENV_POLICY_BASE + 1,
+                                                          e.action_spaces["1"].n)}
+            ts = e.step(st, acts)
             envs[b][2], envs[b][3] = ts.state, ts.observations
         last = actions.astype(np.int32)
     bp.close()

@@ -96,6 +96,10 @@ class _FakeEngine:
     def __init__(self, fail_update=False, fail_search=False):
         self.fail_update, self.fail_search = fail_update, fail_search
         self.wall_clock_sims = None
+        self.type_based = False
+
+    def root_stats(self):   # (the search's work counters: none here)
+        return []
 
     def update(self, actions, keys):
         if self.fail_update:

@@ -116,3 +116,25 @@ def test_tracker_fixture_covers_nan_and_max_reductions():
     assert any(len(ep["steps"]) == 0 for ep in log["episodes"])
     mem = [_dec(ep["get"]["mem_usage_mean"]) for ep in log["episodes"]]
     assert not all(np.isnan(mem))
+
+
+def test_port_vs_reference_measurement():
+    """tools/port_vs_reference.py (the cpu_baseline's tie to the real reference,
+    bench.py port_vs_reference_speed) runs here and agrees with the committed
+    record's order of magnitude; both planners choose the same actions."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from oracle.ref_harness import reference_available
+    if not reference_available():
+        pytest.skip("reference not importable here")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "port_vs_reference.py"),
+                        "--sims", "512", "--trees", "2", "--out", "-"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    assert 0.3 < got["port_vs_reference_speed"] < 3.0
+    rec = json.load(open(os.path.join(root, "profiles", "port_vs_reference.json")))
+    assert rec["sims"] >= 4096 and 0.5 < rec["port_vs_reference_speed"] < 2.0

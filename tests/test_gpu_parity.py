@@ -17,15 +17,17 @@ pytestmark = pytest.mark.gpu
 def search_kernel(request, monkeypatch):
     """Every parity test runs on every search kernel: k_search (a tree per lane,
     tree in HBM) with cut-off children deferred to the re-root ("lane") and
-    looked up during the search ("lane_eager", pomcp_set_defer_cutoff) and
+    looked up during the search ("lane_eager", pomcp_set_defer_cutoff) -- both
+    forced through POMCP_DEFER_CUTOFF, so they also hold for the POMCP episode
+    planners, which otherwise pick the eager lookup -- and
     k_search_lds (a wave per tree, tree in LDS) -- with its step-tree producer
     waves as the engine picks them ("wave"), forced on for any depth limit
     ("wave_tree") and off ("wave_plain"); they must give the same bits as the
     reference / oracle."""
     kind, _, mode = request.param.partition("_")
     monkeypatch.setenv("POMCP_SEARCH_KERNEL", kind)
-    if mode == "eager":
-        monkeypatch.setenv("POMCP_DEFER_CUTOFF", "0")
+    if kind == "lane":   # the override wins over the episode planners' eager choice
+        monkeypatch.setenv("POMCP_DEFER_CUTOFF", "0" if mode == "eager" else "1")
     elif mode:
         monkeypatch.setenv("POMCP_STEP_TREE", "1" if mode == "tree" else "0")
     return kind
@@ -122,12 +124,16 @@ def _oracle_first_step(cfg, num_sims, tree, env_seed, rekey=None, env="Driving-v
     return recs[0]
 
 
-def _batched_vs_oracle(cfg, num_trees, num_sims, check_trees, rekey=None, env="Driving-v1"):
+def _batched_vs_oracle(cfg, num_trees, num_sims, check_trees, rekey=None, env="Driving-v1",
+                       select_margin=None):
     from gpu_util import product_model
+    from posggym_baselines_amd import _native as N
     from posggym_baselines_amd.planning import BatchedPOMCP
     model = product_model(env)
     A = model.action_spaces["0"].n
     bp = BatchedPOMCP(model, "0", product_config(cfg, num_sims), num_trees, num_sims)
+    if select_margin is not None:
+        assert N.load().pomcp_debug_set_select_margin(bp.engine._ctx, float(select_margin)) == 0
     bp.init_synthetic(1000)
     if rekey is not None:
         bp.engine.rekey(rekey)
@@ -551,3 +557,154 @@ def test_late_step_tree_handoff_falls_back():
     got = batched_episodes(TEST_CFG, S, seeds, K, spin_limit=1)
     for b in range(len(seeds)):
         assert got[b] == exp[b], f"tree {b} (env seed {seeds[b]})"
+
+
+def _pe_oracle_episodes(cfg, S, K, B, s0):
+    from oracle.run import oracle_episode
+    seeds, exp = [], []
+    s = s0
+    while len(seeds) < B:   # planners whose episodes last >= K steps, searched every step
+        trace, recs = oracle_episode(cfg, S, s, tree=len(seeds), max_steps=K,
+                                     env="PursuitEvasion-v1")
+        if trace["len"] >= K and all(r["searched"] and r.get("num_sims") for r in recs):
+            seeds.append(s)
+            exp.append(recs)
+        s += 1
+    return seeds, exp
+
+
+@pytest.mark.parametrize("islots", [6, 2])
+def test_pursuit_evasion_batched_reroot(search_kernel, islots):
+    """PursuitEvasion-v1 planners over 5 real steps in one engine: re-root,
+    extraction, reinvigoration and subtree compaction after every search.  In
+    the "lane" mode the cut-off children are deferred and materialised by
+    k_compact_log from the records (Env::obs_key / Env::done_of of
+    PursuitEvasion), in "lane_eager" they are looked up during the search;
+    with 2 inline slots most children go through the overflow map (deferred
+    ones inserted by the re-root).  Bit-exact against the oracle every step."""
+    import os
+    from gpu_util import batched_episodes
+    cfg = dict(TEST_CFG, seed=11)
+    S, K, B = 160, 5, 40
+    seeds, exp = _pe_oracle_episodes(cfg, S, K, B, 8800)
+    counters = []
+    got = batched_episodes(cfg, S, seeds, K, env="PursuitEvasion-v1", inline_slots=islots,
+                           counters=counters)
+    for b in range(B):
+        assert got[b] == exp[b], f"tree {b} (env seed {seeds[b]})"
+    deferred = sum(c[1] for c in counters)
+    cut = sum(c[2] for c in counters)
+    if search_kernel == "lane":
+        if os.environ.get("POMCP_DEFER_CUTOFF") == "1":
+            assert deferred > 0 and deferred == cut, counters
+        else:
+            assert deferred == 0 and cut > 0, counters
+
+
+def test_exact_selection_fallback_fires_and_is_exact(search_kernel):
+    """k_search's fast UCB / PUCB selection falls back to the exact FP64 scores
+    near a tie (DESIGN.md §4 "Fast selection").  With the margin widened to
+    1e-4 (pomcp_debug_set_select_margin) that path decides a large share of the
+    selections; the reference goldens (UCB, PUCB, deep, PursuitEvasion), a
+    65,536-simulation search and re-rooting batched planners stay bit-exact and
+    the lane kernel counts the exact-path selections (n_exact_selects).  The
+    wave kernel always scores exactly (its count is 0)."""
+    from gpu_util import batched_episodes
+    from oracle.run import oracle_episode
+    lane = search_kernel == "lane"
+    for case in ("c1_ucb", "c1_pucb", "deep_ucb", "pe_evader_ucb", "pe_pursuer_pucb"):
+        data = load(case)
+        ep = data["episodes"][0]
+        exact = []
+        trace, records = gpu_episode(cfg_kwargs(ep["config"]), data["num_sims"], ep["env_seed"],
+                                     ego=data["ego"], max_steps=case_max_steps(case, data),
+                                     env=case_env(data), select_margin=1e-4, exact=exact)
+        assert records == ep["records"], case
+        assert trace == ep["trace"], case
+        assert (sum(exact) > 0) == lane, (case, exact)
+    stats = _batched_vs_oracle(TEST_CFG, 2, 65536, [0], select_margin=1e-4)
+    sel = sum(int(st.n_exact_selects) for st in stats)
+    assert (sel > 1000) == lane, sel
+    cfg = dict(TEST_CFG, action_selection="pucb", seed=4)
+    S, K = 128, 4
+    seeds, exp = [], []
+    s = 5100
+    while len(seeds) < 24:
+        trace, recs = oracle_episode(cfg, S, s, tree=len(seeds), max_steps=K)
+        if trace["len"] >= K and all(r["searched"] for r in recs):
+            seeds.append(s)
+            exp.append(recs)
+        s += 1
+    counters = []
+    got = batched_episodes(cfg, S, seeds, K, select_margin=1e-4, counters=counters)
+    assert got == exp
+    assert (sum(c[0] for c in counters) > 0) == lane, counters
+
+
+def test_select_margin_below_the_error_bound_is_rejected():
+    from gpu_util import product_model
+    from posggym_baselines_amd import _native as N
+    from posggym_baselines_amd.planning import BatchedPOMCP
+    bp = BatchedPOMCP(product_model("Driving-v1"), "0", product_config(TEST_CFG, 16), 3, 16)
+    lib = N.load()
+    assert lib.pomcp_debug_set_select_margin(bp.engine._ctx, 1e-13) == N.POMCP_E_INVALID
+    assert lib.pomcp_debug_set_select_margin(bp.engine._ctx, float("nan")) == N.POMCP_E_INVALID
+    assert lib.pomcp_debug_set_select_margin(bp.engine._ctx, 1e-12) == 0
+    bp.close()
+
+
+def test_mode_change_with_pending_deferred_records_is_refused(search_kernel):
+    """Deferred cut-off records take their absorbing flag from the last record at
+    the re-root; an eager arrival in between could be overwritten (mcts.py:370's
+    last arrival must win).  So while a lane search's deferred records are
+    pending, switching deferral or the kernel is refused (POMCP_E_STATE); an
+    update / restore / reset clears them."""
+    import numpy as np
+    from gpu_util import product_model
+    from posggym_baselines_amd import _native as N
+    from posggym_baselines_amd.planning import BatchedPOMCP
+    if search_kernel != "lane":
+        pytest.skip("lane kernel")
+    bp = BatchedPOMCP(product_model("Driving-v1"), "0", product_config(TEST_CFG, 64), 4, 64,
+                      searches=3, reroot=True, defer_cutoff=True)
+    bp.engine._defer_forced = False
+    bp.init_synthetic(1000)
+    lib, ctx = N.load(), bp.engine._ctx
+    assert lib.pomcp_set_defer_cutoff(ctx, 1) == 0
+    acts = bp.search()
+    assert sum(int(s.n_deferred) for s in bp.engine.root_stats()) > 0
+    assert lib.pomcp_set_defer_cutoff(ctx, 0) == N.POMCP_E_STATE
+    assert lib.pomcp_set_search_kernel(ctx, N.SEARCH_WAVE) == N.POMCP_E_STATE
+    assert lib.pomcp_set_defer_cutoff(ctx, 1) == 0            # no change: allowed
+    assert lib.pomcp_set_search_kernel(ctx, N.SEARCH_LANE) == 0
+    bp.engine.update(acts, bp.engine.synthetic_step(1000, acts))
+    assert lib.pomcp_set_defer_cutoff(ctx, 0) == 0
+    bp.search()
+    assert sum(int(s.n_deferred) for s in bp.engine.root_stats()) == 0
+    assert lib.pomcp_set_defer_cutoff(ctx, 1) == 0   # eager records: nothing pending
+    bp.close()
+
+
+def test_step_statistics_hbm_bytes_and_rate(search_kernel):
+    """the drop-in keeps the reference's step_statistics keys
+    (mcts.py:140-153) and adds hbm_bytes (the search's algorithmic bytes from
+    the kernel's counters, engine.search_bytes -- bench.py's roofline
+    numerator) and sims_per_s."""
+    from gpu_util import product_model
+    from posggym_baselines_amd.planning import POMCP, RandomSearchPolicy
+    from posggym_baselines_amd.planning.engine import b_level, search_bytes
+    model = product_model("Driving-v1")
+    S = 512
+    planner = POMCP(model, "0", product_config(TEST_CFG, S), RandomSearchPolicy(model, "0"))
+    planner.reset()
+    obs = model.sample_initial_obs(model.sample_initial_state())
+    planner.step(obs["0"])
+    st = planner.step_statistics
+    assert {"search_time", "update_time", "reinvigoration_time", "evaluation_time",
+            "policy_calls", "inference_time", "search_depth", "num_sims", "mem_usage",
+            "min_value", "max_value"} <= set(st)
+    rs = planner._engine.root_stats()
+    assert st["hbm_bytes"] == search_bytes(rs, 5) > 0
+    assert st["hbm_bytes"] >= 16 * S + (b_level(5) - 28) * int(rs[0].n_levels)
+    assert st["sims_per_s"] == pytest.approx(S / st["search_time"])
+    planner.close()
