@@ -608,12 +608,19 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   // ao: the other agent's action (mcts.py:331), j: the model's exec-order
   // shuffle draw; both are drawn before the selection (their streams are
   // independent of it) so that they overlap the statistics load.
+  // need_key = false: a deferred level (no child lookup, the record names the
+  // action node): the observation key is not computed -- the re-root derives
+  // it from the record's state (Env::obs_key in k_compact_log)
   auto tree_step = [&](int a, uint32_t ao, uint32_t j, uint32_t* n0, uint32_t* n1, double* r,
-                       int* done, uint64_t* okey) {
+                       int* done, uint64_t* okey, bool need_key) {
     PT_MARK(15);
     Env::step(sm, p.ego, s0, s1, (uint32_t)a, ao, j, n0, n1, r, done);
     PT_MARK(9);
-    *okey = Env::obs_key(sm, p.ego, *n0, *n1);
+    *okey = 0ull;
+#ifdef PB_NO_CUTKEY_SKIP   // A/B builds: the key computed at deferred levels too
+    need_key = true;
+#endif
+    if (need_key) *okey = Env::obs_key(sm, p.ego, *n0, *n1);
     PT_MARK(11);
   };
 
@@ -770,7 +777,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
           done = 0;
           okey = (uint64_t)ao;
 #else
-          tree_step(a, ao, j, &n0, &n1, &r, &done, &okey);
+          tree_step(a, ao, j, &n0, &n1, &r, &done, &okey, true);
 #endif
           bool match;
           const int ks = find_slot(sl, okey, &match);
@@ -922,9 +929,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         double r;
         int done;
         uint64_t okey;
-        tree_step(a, ao, j, &n0, &n1, &r, &done, &okey);
+        tree_step(a, ao, j, &n0, &n1, &r, &done, &okey, !skipc);
         bool match = false;
-        const int ks = skipc ? 0 : find_slot(sl, okey, &match);
+        int ks = 0;
+        if (!skipc) ks = find_slot(sl, okey, &match);
         PT_MARK(12);
         const uint32_t ani = (uint32_t)(blk * A + a);
         uint32_t cid = 0;

@@ -19,7 +19,7 @@ SOURCES = [os.path.join(CSRC, "pomcp_capi.hip")]
 SEARCH_SOURCE = os.path.join(CSRC, "pomcp_search_tu.hip")
 DEPS = SOURCES + [SEARCH_SOURCE] + [os.path.join(CSRC, f) for f in
                   ("pomcp_kernels.hip", "pomcp_search.hip", "pomcp_search_lds.hip", "pomcp_device.h", "driving.h",
-                   "driving_vec.h", "philox.h", "envs.h", "pursuit_evasion.h", "host_exp.h", "host_exp_table.h", "intmcp.hip", "intmcp_capi.hip")] + [
+                   "driving_vec.h", "philox.h", "envs.h", "pursuit_evasion.h", "host_exp.h", "host_exp_table.h", "host_api.cpp", "intmcp.hip", "intmcp_capi.hip")] + [
     os.path.join(INCLUDE, "pomcp.h"), os.path.join(INCLUDE, "pomcp_debug.h"),
     os.path.join(INCLUDE, "intmcp.h")]
 
