@@ -227,6 +227,7 @@ class OraclePOMCP:
         for _ in range(self.cfg.num_sims):
             parts = self.belief[root]
             st, t = parts[self.s.randint(S_BELIEF, len(parts))]   # belief.py:55
+            self.s.align_sim()                                     # (rng.py SIM_STREAMS)
             depth = self._simulate(st, t, root)
             self.on_visits[root] += 1                              # mcts.py:288
             max_depth = max(max_depth, depth)

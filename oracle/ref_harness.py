@@ -121,6 +121,7 @@ def make_reference_pomcp(model, agent_id, cfg_kwargs, num_sims, streams, planner
 
     def simulate(hps, obs_node, depth, search_policy):
         if depth == 0:
+            streams.align_sim()   # a simulation starts its step streams at a block (oracle/rng.py)
             count[0] += 1
             if count[0] >= num_sims:
                 clock.now += 1e9
@@ -421,6 +422,7 @@ def make_reference_potmmcp(model, agent_id, cfg_kwargs, num_sims, streams, spec)
 
     def simulate(hps, obs_node, depth, search_policy):
         if depth == 0:
+            streams.align_sim()   # a simulation starts its step streams at a block (oracle/rng.py)
             count[0] += 1
             if count[0] >= num_sims:
                 clock.now += 1e9
@@ -562,6 +564,7 @@ def make_reference_mcts(model, agent_id, cfg_kwargs, num_sims, streams, spec,
 
     def simulate(hps, obs_node, depth, search_policy):
         if depth == 0:
+            streams.align_sim()   # a simulation starts its step streams at a block (oracle/rng.py)
             count[0] += 1
             if count[0] >= num_sims:
                 clock.now += 1e9

@@ -26,6 +26,14 @@ S_MIXTURE = 4       # other_policy.py `random`: OtherAgentMixturePolicy.sample_i
 S_ACT_BASE = 8      # Discrete(n).sample() of agent i's action space: stream 8 + i
 S_ENV_MODEL = 32    # harness: the "real" environment's model RNG
 S_ENV_POLICY_BASE = 40  # harness: true (non-planning) agent i's random policy: 40 + i
+# The step streams of a simulation: the model's and both agents' action streams.
+# Each simulation of a search (a depth-0 ``_simulate`` call, mcts.py:286-288)
+# starts them at a Philox block boundary: their counters are rounded up to a
+# multiple of 4 (``Streams.align_sim``), so a simulation's first four draws of
+# each come from ONE block -- the HIP search computes one block per stream per
+# simulation instead of one per draw (DESIGN.md §4 "Simulation-aligned
+# streams").  Draws outside simulations (update, reinvigoration) are unaligned.
+SIM_STREAMS = (S_MODEL, S_ACT_BASE, S_ACT_BASE + 1)
 
 
 def philox4x32_10(c0, c1, c2, c3, k0, k1):
@@ -76,6 +84,14 @@ class Streams:
             cached = (b, words)
             self._blk[stream] = cached
         return cached[1][j & 3]
+
+    def align_sim(self):
+        """Start of a simulation: the step streams' counters to the next
+        multiple of 4 (``SIM_STREAMS``)."""
+        for s in SIM_STREAMS:
+            j = self.ctr.get(s, 0)
+            if j & 3:
+                self.ctr[s] = (j + 3) & ~3
 
     def randint(self, stream: int, n: int) -> int:
         """Uniform int in [0, n) (no rejection)."""

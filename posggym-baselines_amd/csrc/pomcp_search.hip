@@ -207,26 +207,93 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   // ---- RNG streams (philox.h): one stateless Philox block per draw
   auto d_belief = [&](uint32_t n) { return uniform_int(philox_word(seed, tkey, S_BELIEF, c_bel++), n); };
   auto d_select = [&](uint32_t n) { return uniform_int(philox_word(seed, tkey, S_SELECT, c_sel++), n); };
+  // (counters updated by selects: increments in the branches of a condition
+  // become a store through a selected pointer, i.e. scratch memory)
   auto d_act_word = [&](int agent) {
-    return agent == 0 ? philox_word(seed, tkey, S_ACT_BASE, c_a0++)
-                      : philox_word(seed, tkey, S_ACT_BASE + 1, c_a1++);
+    const bool a0 = agent == 0;
+    const uint32_t j = a0 ? c_a0 : c_a1;
+    c_a0 += a0 ? 1u : 0u;
+    c_a1 += a0 ? 0u : 1u;
+    return philox_word(seed, tkey, (uint32_t)S_ACT_BASE + (a0 ? 0u : 1u), j);
   };
-  // One-draw lookahead of the streams every tree step consumes (the other
-  // agent's action, the model's shuffle draw) and of the belief stream: the
-  // next word of each is computed right after the current one is consumed, at
-  // a point where the wave waits on memory anyway (after a level's loads are
-  // issued), so no Philox block is computed on the root level's critical
-  // path.  Each stream is still consumed in order, so results are unchanged;
-  // the stored counters exclude a computed-but-unconsumed word (pend_*).
-  uint32_t w_oth = 0u, w_mod = 0u, w_bel = 0u;
-  int pend_s = 0, pend_b = 0;   // a lookahead word is held (step streams / belief)
-  auto la_step = [&]() {
-    if (!pend_s) {
-      w_oth = p.other == 0 ? philox_word(seed, tkey, S_ACT_BASE, c_a0++)
-                           : philox_word(seed, tkey, S_ACT_BASE + 1, c_a1++);
-      if (Env::kStepDraws) w_mod = philox_word(seed, tkey, S_MODEL, c_mod++);
-      pend_s = 1;
+  // The step streams (the model's shuffle draw, the other agent's action) are
+  // simulation-aligned (oracle/rng.py SIM_STREAMS): every simulation starts
+  // them at a Philox block boundary, so the words of its first four steps come
+  // from ONE block per stream -- one block per stream and simulation instead of
+  // one per draw (DESIGN.md §4 "Simulation-aligned streams").  The next
+  // simulation's blocks are computed speculatively while the first level's
+  // node line is in flight (spec_blocks, after the root level: a simulation
+  // that draws 1..4 words of a stream starts the next one block further on);
+  // the simulation's words live in LDS (rw, [stream][word][lane]: registers
+  // spilled to AGPRs cost more, A/B DESIGN.md §6 r5e).  A simulation that drew 0
+  // or more than 4 words of a stream recomputes at the next start (divergent,
+  // rare), and a fifth step of a simulation draws its word on its own.  The
+  // belief stream keeps its one-draw lookahead, computed while a level's loads
+  // are in flight (la_bel); the stored counter excludes that word.
+  __shared__ uint32_t rw[2][4][TPB];   // this simulation's words: [model, other agent][k][lane]
+  uint32_t m_base = 0u, o_base = 0u;   // the aligned counters at this simulation's start
+  uint32_t w_bel = 0u;
+  int pend_b = 0;   // a belief lookahead word is held
+  uint32_t nm0 = 0u, nm1 = 0u, nm2 = 0u, nm3 = 0u, no0 = 0u, no1 = 0u, no2 = 0u, no3 = 0u;
+  uint32_t nm_base = 0xFFFFFFFFu, no_base = 0xFFFFFFFFu;   // the speculated blocks' counters
+  auto spec_blocks = [&]() {   // the next simulation's, assuming this one draws 1..4 words
+    const uint32_t cm = m_base + 4u, co = o_base + 4u;
+    uint32_t bo[4] = {co >> 2, 0u, (uint32_t)(S_ACT_BASE + p.other), (uint32_t)(seed >> 32)};
+    philox4x32_10(bo, (uint32_t)seed, tkey);
+    no0 = bo[0];
+    no1 = bo[1];
+    no2 = bo[2];
+    no3 = bo[3];
+    no_base = co;
+    if constexpr (Env::kStepDraws) {
+      uint32_t bm[4] = {cm >> 2, 0u, (uint32_t)S_MODEL, (uint32_t)(seed >> 32)};
+      philox4x32_10(bm, (uint32_t)seed, tkey);
+      nm0 = bm[0];
+      nm1 = bm[1];
+      nm2 = bm[2];
+      nm3 = bm[3];
+      nm_base = cm;
     }
+  };
+  auto sim_blocks = [&]() {   // a simulation starts: align, take (or compute) its blocks
+    c_mod = (c_mod + 3u) & ~3u;
+    c_a0 = (c_a0 + 3u) & ~3u;
+    c_a1 = (c_a1 + 3u) & ~3u;
+    const uint32_t co = p.other == 0 ? c_a0 : c_a1;
+    const bool hit = co == no_base && (!Env::kStepDraws || c_mod == nm_base);
+    if (!hit) {   // (divergent: the first simulation, or one that drew 0 or > 4 words)
+      uint32_t bo[4] = {co >> 2, 0u, (uint32_t)(S_ACT_BASE + p.other), (uint32_t)(seed >> 32)};
+      philox4x32_10(bo, (uint32_t)seed, tkey);
+      no0 = bo[0];
+      no1 = bo[1];
+      no2 = bo[2];
+      no3 = bo[3];
+      if constexpr (Env::kStepDraws) {
+        uint32_t bm[4] = {c_mod >> 2, 0u, (uint32_t)S_MODEL, (uint32_t)(seed >> 32)};
+        philox4x32_10(bm, (uint32_t)seed, tkey);
+        nm0 = bm[0];
+        nm1 = bm[1];
+        nm2 = bm[2];
+        nm3 = bm[3];
+      }
+    }
+    o_base = co;
+    m_base = c_mod;
+    rw[0][0][lid] = nm0;
+    rw[0][1][lid] = nm1;
+    rw[0][2][lid] = nm2;
+    rw[0][3][lid] = nm3;
+    rw[1][0][lid] = no0;
+    rw[1][1][lid] = no1;
+    rw[1][2][lid] = no2;
+    rw[1][3][lid] = no3;
+  };
+  // word k of this simulation's block of stream q (0 model, 1 the other
+  // agent's), else (k >= 4) a block of its own
+  auto blk_word = [&](int q, uint32_t k, uint32_t sid, uint32_t j) -> uint32_t {
+    uint32_t x = rw[q][k & 3u][lid];
+    if (k >= 4u) x = philox_word(seed, tkey, sid, j);
+    return x;
   };
   auto la_bel = [&]() {
     if (!pend_b) {
@@ -237,15 +304,27 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   // the other agent's action (mcts.py:602-615): uniform (RandomOtherAgentPolicy)
   // or, TM, by its particle's policy (OtherAgentMixturePolicy.sample_action)
   auto take_oth = [&]() -> uint32_t {
-    pend_s = 0;
+    const bool o0 = p.other == 0;
+    const uint32_t j = o0 ? c_a0 : c_a1;
+    const uint32_t w = blk_word(1, j - o_base, (uint32_t)S_ACT_BASE + (o0 ? 0u : 1u), j);
+    c_a0 += o0 ? 1u : 0u;
+    c_a1 += o0 ? 0u : 1u;
     if constexpr (TM != 0) {
-      if (tmt->other_uniform) return uniform_int(w_oth, (uint32_t)A);
-      return (uint32_t)tm_choice(tmt->oth_cum[pid], tmt->oth_tot[pid], A, w_oth);
+      if (tmt->other_uniform) return uniform_int(w, (uint32_t)A);
+      return (uint32_t)tm_choice(tmt->oth_cum[pid], tmt->oth_tot[pid], A, w);
     } else {
-      return uniform_int(w_oth, (uint32_t)A);
+      return uniform_int(w, (uint32_t)A);
     }
   };
-  auto take_mod = [&](uint32_t n) { return Env::kStepDraws ? uniform_int(w_mod, n) : 0u; };
+  auto take_mod = [&](uint32_t n) -> uint32_t {
+    if constexpr (Env::kStepDraws) {
+      const uint32_t w = blk_word(0, c_mod - m_base, (uint32_t)S_MODEL, c_mod);
+      ++c_mod;
+      return uniform_int(w, n);
+    } else {
+      return 0u;
+    }
+  };
   // ObsNode.add_child for every action (mcts.py:279-281, 318-321): zeroed block
   // (TM: its prior line = the action_probs of prior code `code`)
   auto alloc_block = [&](int code) -> int {
@@ -554,7 +633,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
     }
     pf = rbel[d_belief((uint32_t)bsize)];   // the first simulation's particle
     la_bel();
-    la_step();
   }
 
   // Overflow children (beyond the kSlots inline ones) of action node ani.
@@ -737,6 +815,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         depth = 0;
         plen = 0;
         r0_on = 0;
+        sim_blocks();   // the step streams of this simulation (oracle/rng.py SIM_STREAMS)
         if constexpr (TM != 0) {   // sample_policy (potmmcp.py:381-389), select stream
           pid = pr.w;
           if (!tmt->no_meta_draw) {   // (the base planner: one search policy, no draw)
@@ -858,9 +937,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
     }
     // refill the lookahead words the root level consumed while the first level's
     // statistics line (issued by descend) is in flight
-    if (phase != TP_DONE) {
-      la_step();
+    if (phase != TP_DONE) {   // while the first level's node line is in flight
       la_bel();
+      spec_blocks();
     }
     // ------------------------------------------------- the levels below the root
     while (__ballot(phase == TP_LEVEL) != 0ull) {
@@ -922,7 +1001,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   #pragma unroll
           for (int q = 0; q < kSlots; ++q) sl[q] = ap[part_slot(a, q)];
         }
-        la_step();   // the next step's draws, while the child line is in flight
         PT_MARK(3);
         append();   // the previous level's record, after this level's loads
         uint32_t n0, n1;
@@ -1019,7 +1097,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         else ae = uniform_int(aw, (uint32_t)A);
         const uint32_t j = take_mod(2);
         const uint32_t ao = take_oth();                       // other_policy.py:151
-        la_step();
         uint32_t n0, n1;
         double r;
         int dn;
@@ -1235,9 +1312,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   hw->mm_max = mm_max;
   hw->ctr[0] = c_bel - (uint32_t)pend_b;   // draws consumed, not looked ahead
   hw->ctr[1] = c_sel;
-  hw->ctr[2] = c_mod - (Env::kStepDraws ? (uint32_t)pend_s : 0u);
-  hw->ctr[3] = c_a0 - (p.other == 0 ? (uint32_t)pend_s : 0u);
-  hw->ctr[4] = c_a1 - (p.other == 1 ? (uint32_t)pend_s : 0u);
+  hw->ctr[2] = c_mod;
+  hw->ctr[3] = c_a0;
+  hw->ctr[4] = c_a1;
   pomcp_root_stats* const so = p.stats + tree;
   double* const xr = p.merge + (int64_t)tree * POMCP_XREC(A);   // exchange record (pomcp.h)
 #pragma unroll

@@ -248,11 +248,17 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
   const bool bel_lds = bsize <= kLdsBelief;
   if (bel_lds)
     for (int i = (int)threadIdx.x; i < bsize; i += (int)blockDim.x) bel[i] = rbel[i];
+  // the step streams are simulation-aligned (oracle/rng.py SIM_STREAMS): every
+  // simulation starts the model's and both agents' action streams at a Philox
+  // block boundary (counters rounded up to a multiple of 4)
+  auto al4 = [](uint32_t c) { return (c + 3u) & ~3u; };
   // the step tree's prediction: simulation k of this launch draws the model and
-  // the other agent's words from sync_m / sync_o + (k - sync_k) * (depth_limit + 1)
-  const int d1 = p.depth_limit + 1;
+  // the other agent's words from sync_m / sync_o + (k - sync_k) * stride, a
+  // simulation that does not terminate consuming depth_limit + 1 words from an
+  // aligned start (stride: that rounded up to a multiple of 4)
+  const int d1 = (int)al4((uint32_t)(p.depth_limit + 1));
   const int dm = Env::kStepDraws ? d1 : 0;
-  int syn_k = 0, syn_m = (int)sd.ctr, syn_o = (int)(p.other == 0 ? s0s.ctr : s1s.ctr);
+  int syn_k = 0, syn_m = (int)al4(sd.ctr), syn_o = (int)al4(p.other == 0 ? s0s.ctr : s1s.ctr);
   const uint32_t bctr0 = sb.ctr;
   if (NP > 0 && threadIdx.x == 0) {
     sp_ctl[SP_NEXT] = 0;
@@ -511,6 +517,9 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
   bool sp_off = false;   // the producers were stopped (a late hand-off): compute every step
   for (int it = 0; it < num_sims && run; ++it) {
     // ------------------------------------------------ start (mcts.py:286-287)
+    sd.ctr = al4(sd.ctr);   // the simulation's step streams start at a block
+    s0s.ctr = al4(s0s.ctr);
+    s1s.ctr = al4(s1s.ctr);
     uint4 pr = pf;                                         // belief.py:55
     if (sims + 1 < num_sims) {
       if (NP > 0) ++sb.ctr;
@@ -891,11 +900,12 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
       // the next simulation's counters off the prediction (this one terminated
       // early): re-base the producers -- before the slot is released, so the
       // producer it frees builds its slot from the new prediction
-      const uint32_t oc = p.other == 0 ? s0s.ctr : s1s.ctr;
-      if (sd.ctr != (uint32_t)(syn_m + (it + 1 - syn_k) * dm) ||
+      const uint32_t oc = al4(p.other == 0 ? s0s.ctr : s1s.ctr);   // the next one's aligned starts
+      const uint32_t mc = al4(sd.ctr);
+      if (mc != (uint32_t)(syn_m + (it + 1 - syn_k) * dm) ||
           oc != (uint32_t)(syn_o + (it + 1 - syn_k) * d1)) {
         syn_k = it + 1;
-        syn_m = (int)sd.ctr;
+        syn_m = (int)mc;
         syn_o = (int)oc;
         if (lane == 0) {
           sp_ctl[SP_SYNC_M] = syn_m;
