@@ -10,7 +10,10 @@
  * by the planner's own random choice, intmcp.py:750-753).  nesting_level = 2:
  * three trees per index -- tree 0 the planner's (level 2), tree 1 the other
  * agent's level-1 planner, tree 2 the level-0 planner of the planner's agent
- * (INTMCP.initialize's recursion, intmcp.py:950-994).  Paths relative to
+ * (INTMCP.initialize's recursion, intmcp.py:950-994); nesting_level = 3:
+ * four trees -- tree 0 the planner's (level 3), trees 1 and 2 the level-2 and
+ * level-1 planners of the other agent and the planner's agent, tree 3 the
+ * other agent's level-0 planner.  Paths relative to
  * posggym_baselines/planning/ in the reference.
  *
  * Same conventions as pomcp.h (plain pointers, POMCP_* status codes, a
@@ -30,7 +33,7 @@ extern "C" {
 typedef struct intmcp_config {
   pomcp_config base;              /* MCTSConfig + model + tables (num_trees = planner pairs) */
   int32_t state_belief_only;      /* MCTSConfig.state_belief_only (test config: 0) */
-  int32_t nesting_level;          /* 0, 1 or 2 (INTMCP.initialize's nesting_level) */
+  int32_t nesting_level;          /* 0 to 3 (INTMCP.initialize's nesting_level) */
   int64_t max_nodes;              /* obs nodes per tree */
   int64_t max_stats;              /* action-node statistics entries per tree (A per expanded node) */
   int64_t max_log;                /* particle log records per tree (16 B) */
@@ -94,8 +97,8 @@ int intmcp_get_root_belief(intmcp_ctx* ctx, int32_t pair, uint32_t* out, int32_t
  * visits i32, t i32, stats i32, -, obs key u64; info = parent action:3 |
  * absorbing:1 | path_ok:1 | registered:3 | registration order 6 x 3 bits) and
  * statistics entries (32 B: visits i32, -, value f64, total f64, agg f64 = 0: not kept);
- * tree 0 = the planner's (top) level, tree 1 the level below, tree 2 (nesting
- * level 2) level 0. */
+ * tree 0 = the planner's (top) level, tree k the level k below it (the last
+ * tree level 0). */
 int intmcp_get_nodes(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int32_t capacity,
                      int32_t* count);
 int intmcp_get_stats(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int32_t capacity,
@@ -105,10 +108,15 @@ int intmcp_get_stats(intmcp_ctx* ctx, int32_t pair, int32_t tree, void* out, int
 int intmcp_get_support(intmcp_ctx* ctx, int32_t pair, int32_t* entries, int32_t capacity_entries,
                        int32_t* n_entries, uint32_t* particles, int32_t capacity_particles,
                        int32_t* n_particles);
-/* Nesting level 2: the level-1 (middle, tree 1) planner's materialised beliefs
- * of the histories in the top root belief: entries (node, offset, size,
- * capacity) and their (v0, v1, level-0 node id) particles.  POMCP_E_INVALID at
- * other nesting levels.  (intmcp_get_support is always the level-0 tree's.) */
+/* Nesting levels 2, 3: middle tree `tree`'s (1 <= tree <= nesting level - 1)
+ * materialised beliefs of the histories in the belief distribution above it
+ * (tree 1: the top root belief's): entries (node, offset, size, capacity) and
+ * their (v0, v1, next tree's node id) particles.  POMCP_E_INVALID for any other
+ * tree.  (intmcp_get_support is always the level-0 tree's.) */
+int intmcp_get_middle_support(intmcp_ctx* ctx, int32_t pair, int32_t tree, int32_t* entries,
+                              int32_t capacity_entries, int32_t* n_entries, uint32_t* particles,
+                              int32_t capacity_particles, int32_t* n_particles);
+/* intmcp_get_middle_support of tree 1. */
 int intmcp_get_mid_support(intmcp_ctx* ctx, int32_t pair, int32_t* entries, int32_t capacity_entries,
                            int32_t* n_entries, uint32_t* particles, int32_t capacity_particles,
                            int32_t* n_particles);
@@ -119,7 +127,7 @@ int intmcp_get_mid_support(intmcp_ctx* ctx, int32_t pair, int32_t* entries, int3
 int intmcp_search_level(intmcp_ctx* ctx, int32_t level, int32_t sims, int32_t flags,
                         int32_t* actions_out);
 /* Arena counters of every pair: out[pair][tree][{nodes, log records, stats}]
- * for trees 0..2 (zeros for a tree the nesting level does not have), B x 9. */
+ * for trees 0..3 (zeros for a tree the nesting level does not have), B x 12. */
 int intmcp_get_tree_counts(intmcp_ctx* ctx, int32_t* out);
 /* INTMCP.initialize's search_policies (intmcp.py:956-971): the search policy of
  * agent `agent` at nesting level `level` -- NULL: RandomSearchPolicy

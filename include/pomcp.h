@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define POMCP_ABI_VERSION 5
+#define POMCP_ABI_VERSION 6
 #define POMCP_MAX_ACTIONS 8
 #define POMCP_MAX_TYPE_POLICIES 8
 

@@ -1,4 +1,4 @@
-"""I-NTMCP hot path (nesting levels 0-2, two agents) — CPU restatement (pure Python).
+"""I-NTMCP hot path (nesting levels 0-3, two agents) — CPU restatement (pure Python).
 
 TEST INFRASTRUCTURE (see ``oracle/__init__.py``).
 
@@ -31,7 +31,19 @@ from oracle.rng import S_ACT_BASE, S_BELIEF, S_SELECT, Streams, StreamRandom
 
 INF = float("inf")
 S_BELIEF_NESTED = 3   # the level-0 planner's random.Random(config.seed) (intmcp.py:66)
-S_BELIEF_MID = 5      # nesting level 2: the level-1 planner's random.Random(config.seed)
+S_BELIEF_MID = 5      # a middle planner's random.Random(config.seed): level l (1 <= l < the
+                      # nesting level) draws on S_BELIEF_MID + l - 1 (5, 6 at nesting level 3)
+MAX_NESTING = 3       # (streams 5..7 are free for middle levels; the engine builds 0-3)
+
+
+def belief_stream(level: int, nesting_level: int) -> int:
+    """The stream of the level-`level` planner's random.Random(seed) in a
+    nesting-`nesting_level` chain (construction order, intmcp.py:964-986)."""
+    if level == 0:
+        return S_BELIEF_NESTED
+    if level == nesting_level:
+        return S_BELIEF
+    return S_BELIEF_MID + level - 1
 
 
 class _Tree:
@@ -423,21 +435,21 @@ class OracleINTMCP:
         """search_probs: {level: {agent id: None or action probabilities}}
         (the search_policies of INTMCP.initialize; None: all random)."""
         assert cfg.num_sims is not None
-        if nesting_level not in (0, 1, 2):
-            raise NotImplementedError("nesting levels 0-2")
+        if not 0 <= nesting_level <= MAX_NESTING:
+            raise NotImplementedError(f"nesting levels 0-{MAX_NESTING}")
         sp = search_probs or {}
         ids = model.possible_agents
         ego = ids.index(agent_id)
         # construction order of INTMCP.initialize (intmcp.py:964-986): the
         # lowest level first; level 0 draws on S_BELIEF_NESTED, the top planner
-        # on S_BELIEF (nesting 0: the one planner is level 0), a middle level-1
-        # planner on S_BELIEF_MID.  Level k models agent ego if L - k is even.
+        # on S_BELIEF (nesting 0: the one planner is level 0), a middle level-l
+        # planner on S_BELIEF_MID + l - 1 (belief_stream).  Level k models agent
+        # ego if L - k is even.
         planners = []
         below = None
         for level in range(nesting_level + 1):
             who = ids[ego if (nesting_level - level) % 2 == 0 else 1 - ego]
-            stream = (S_BELIEF_NESTED if level == 0 else
-                      S_BELIEF if level == nesting_level else S_BELIEF_MID)
+            stream = belief_stream(level, nesting_level)
             below = _Planner(model, who, cfg, level, streams, stream, nested=below,
                              search_probs=sp.get(level))
             planners.append(below)

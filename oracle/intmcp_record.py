@@ -5,9 +5,9 @@ Hashes cover the level-1 root's particles (t, state words, the other agent's
 history as (action | -1, obs key) steps) and, for each distinct other-agent
 history in that belief (first-occurrence order), the level-0 node's visits,
 registered children (registration order) and particles.  Nesting level 2 adds
-``nested2``: the level-0 (third-tree) history of every particle of those
-second-tree nodes, in order, and each distinct such node's visits, children
-and particles."""
+``nested2``: the third tree's history of every particle of those second-tree
+nodes, in order, and each distinct such node's visits, children and
+particles; nesting level 3 adds ``nested3``, the same one tree further down."""
 import hashlib
 import json
 import struct
@@ -36,10 +36,12 @@ def _node_entry(h, node):
 
 
 def intmcp_record(rec, num_sims, search_depth, root_visits, kids, mn, mx, parts, nested_nodes,
-                  full=False, nested2=None):
-    """nested2 (nesting level 2): (per second-tree node of nested_nodes, the
+                  full=False, nested2=None, deeper=()):
+    """nested2 (nesting level >= 2): (per second-tree node of nested_nodes, the
     third-tree histories of its particles in order; [(history, node)] of the
-    distinct third-tree nodes, first-occurrence order)."""
+    distinct third-tree nodes, first-occurrence order).  deeper: the same for
+    the fourth tree (from the third tree's nodes) and on, recorded as
+    nested3_*, ..."""
     rec["num_sims"] = num_sims
     if num_sims > 0:
         rec["search_depth"] = search_depth
@@ -64,4 +66,9 @@ def intmcp_record(rec, num_sims, search_depth, root_visits, kids, mn, mx, parts,
               [_node_entry(h, node) for h, node in nodes2]]
         rec["nested2_count"] = len(nodes2)
         rec["nested2_digest"] = hashlib.sha1(json.dumps(o2, separators=(",", ":")).encode()).hexdigest()
+    for d, (seqs, nodes) in enumerate(deeper, start=3):
+        od = [[[hist_digest(h) for h in seq] for seq in seqs],
+              [_node_entry(h, node) for h, node in nodes]]
+        rec[f"nested{d}_count"] = len(nodes)
+        rec[f"nested{d}_digest"] = hashlib.sha1(json.dumps(od, separators=(",", ":")).encode()).hexdigest()
     return rec

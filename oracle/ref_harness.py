@@ -197,16 +197,13 @@ def make_reference_intmcp(model, agent_id, cfg_kwargs, num_sims, streams, nestin
     P = import_reference()
     import posggym_baselines.planning.intmcp as im
     import posggym_baselines.planning.belief as B
-    from oracle.intmcp import S_BELIEF_MID, S_BELIEF_NESTED
-    from oracle.rng import S_BELIEF, S_SELECT, StreamRandom
+    from oracle.intmcp import belief_stream
+    from oracle.rng import S_SELECT, StreamRandom
 
     select = StreamRandom(streams, S_SELECT)
-    # lowest level first: level 0, [level 1 of a nesting-2 planner], the top
-    order = [StreamRandom(streams, S_BELIEF_NESTED)]
-    if nesting_level == 2:
-        order.append(StreamRandom(streams, S_BELIEF_MID))
-    if nesting_level > 0:
-        order.append(StreamRandom(streams, S_BELIEF))
+    # lowest level first: level 0, the middle levels, the top (belief_stream)
+    order = [StreamRandom(streams, belief_stream(lv, nesting_level))
+             for lv in range(nesting_level + 1)]
     made = []
 
     def new_random(seed=None):
@@ -311,24 +308,31 @@ def reference_intmcp_record(planner, searched, action):
         n = _walk(nested.root, h)
         seen_nodes.append(n)
         nested_nodes.append((_hist_key(model, h), None if n is None else node(n)))
-    nested2 = None
-    if planner.nesting_level == 2:   # the third tree (the ego's level 0)
-        low = nested.other_agent_policies[planner.agent_id]
-        seqs, nodes2, seen2 = [], [], []
-        for n in seen_nodes:
+    # the third tree on (nesting level >= 2): the histories carried by the
+    # particles of the previous tree's recorded nodes, and those nodes
+    chain = []
+    upper, up_agent, up_nodes = nested, other, seen_nodes
+    for _ in range(planner.nesting_level - 1):
+        low_agent = planner.agent_id if up_agent == other else other
+        low = upper.other_agent_policies[low_agent]
+        seqs, nodes2, seen2, seen2_nodes = [], [], [], []
+        for n in up_nodes:
             seq = []
             for q in ([] if n is None else n.belief.particles):
-                h2 = q.history.get_agent_history(planner.agent_id)
+                h2 = q.history.get_agent_history(low_agent)
                 seq.append(_hist_key(model, h2))
                 if h2 not in seen2:
                     seen2.append(h2)
                     n2 = _walk(low.root, h2)
+                    seen2_nodes.append(n2)
                     nodes2.append((_hist_key(model, h2), None if n2 is None else node(n2)))
             seqs.append(seq)
-        nested2 = (seqs, nodes2)
+        chain.append((seqs, nodes2))
+        upper, up_agent, up_nodes = low, low_agent, seen2_nodes
     st = planner.step_statistics
     return intmcp_record(rec, int(st["num_sims"]), int(st["search_depth"]), root.visits, kids,
-                         st["min_value"], st["max_value"], parts, nested_nodes, nested2=nested2)
+                         st["min_value"], st["max_value"], parts, nested_nodes,
+                         nested2=chain[0] if chain else None, deeper=chain[1:])
 
 
 def reference_intmcp_episode(cfg_kwargs, num_sims, env_seed, ego="0", tree=0, max_steps=50,

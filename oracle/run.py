@@ -105,21 +105,26 @@ def oracle_intmcp_record(p, searched, action):
             continue
         seen.append(q[1])
         nested_nodes.append((p.history(nested.tree, q[1]), node(nested, q[1])))
-    nested2 = None
-    if p.nesting_level == 2:   # the third tree: histories carried by the second tree's particles
-        low = p.planners[0]
+    # the third tree on (nesting level >= 2): the histories carried by the
+    # particles of the previous tree's recorded nodes, and those nodes
+    chain = []
+    upper, seen_up = nested, seen
+    for lvl in range(p.nesting_level - 2, -1, -1):
+        low = p.planners[lvl]
         seqs, nodes2, seen2 = [], [], []
-        for m in seen:
+        for m in seen_up:
             seq = []
-            for r in nested.tree.belief[m]:
+            for r in upper.tree.belief[m]:
                 seq.append(p.history(low.tree, r[1]))
                 if r[1] not in seen2:
                     seen2.append(r[1])
                     nodes2.append((p.history(low.tree, r[1]), node(low, r[1])))
             seqs.append(seq)
-        nested2 = (seqs, nodes2)
+        chain.append((seqs, nodes2))
+        upper, seen_up = low, seen2
     return intmcp_record(rec, top.num_sims, top.search_depth, tr.visits[n], kids,
-                         top.mm_min, top.mm_max, parts, nested_nodes, nested2=nested2)
+                         top.mm_min, top.mm_max, parts, nested_nodes,
+                         nested2=chain[0] if chain else None, deeper=chain[1:])
 
 
 def oracle_intmcp_episode(cfg_kwargs, num_sims, env_seed, ego="0", tree=0, max_steps=50,

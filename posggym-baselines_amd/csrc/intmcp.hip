@@ -120,29 +120,35 @@ struct ISup {           // a materialised level-0 belief
   int32_t node, off, size, cap;
 };
 
-// Trees of a pair: nesting level 1 -- tree 0 (the planner's level-1 tree) and
-// tree 1 (the other agent's level-0 tree); nesting level 2 (ImParams::nt = 3)
-// -- tree 0 (level 2, the planner), tree 1 (level 1, the other agent), tree 2
-// (level 0, the planner's agent again).  Tree k models agent ego if k is even.
-// The bottom tree (nt - 1) is the level-0 one: its beliefs are the "support"
-// (sup / supp); at nesting level 2 the middle tree's beliefs are sup1 / supp1.
-constexpr int kImMaxT = 3;
+// Trees of a pair: nesting level L >= 1 keeps L + 1 trees, tree k the level-
+// (L - k) planner's -- tree 0 the planner's own, the last (nt - 1) the level-0
+// one; nesting level 1: tree 0 (the planner's level-1 tree) and tree 1 (the
+// other agent's level-0 tree); level 2 (ImParams::nt = 3) adds a middle tree
+// (tree 1, level 1, the other agent), level 3 two (trees 1 and 2, levels 2
+// and 1).  Tree k models agent ego if k is even.  The bottom tree's beliefs
+// are the "support" (sup / supp); middle tree k's are msup[k - 1] /
+// msupp[k - 1].
+constexpr int kImMaxT = 4;
+constexpr int kImMaxMid = kImMaxT - 2;   // middle trees (nesting level 3: trees 1 and 2)
 struct IHdr {
   int32_t n_nodes[kImMaxT], n_stats[kImMaxT], n_log[kImMaxT];
   int32_t cur, root_sel, root_size, sup_sel, n_sup, sup_used, err, last_action;
   int32_t num_sims, search_depth, sims_done, pad;
-  int32_t sup1_sel, n_sup1, sup1_used, pad1;   // nesting level 2: the middle tree's beliefs
+  // middle tree k = m + 1's beliefs: table select, entries, particles used, and
+  // the previous table's entry count during an update
+  int32_t msel[kImMaxMid], n_msup[kImMaxMid], msup_used[kImMaxMid], mpad[kImMaxMid];
   double mm_min[kImMaxT], mm_max[kImMaxT];
   uint64_t seed;
   uint32_t tree_key;
-  uint32_t ctr[7];      // belief (top), select, model, act0, act1, belief (level 0), belief (middle)
+  uint32_t ctr[8];      // belief (top), select, model, act0, act1, belief (level 0), belief
+                        // (middle trees 1, 2)
 };
 
 struct ImParams {
   int32_t B, A, ego, other, sel, depth_limit, step_limit, n_target, extra, has_kb,
       state_belief_only,
       nest0,            // nesting level 0: only tree 1, whose agent (p.other) is the planner
-      nt;               // trees per pair in the arenas: 2 (nesting levels 0, 1) or 3 (level 2)
+      nt;               // trees per pair in the arenas: 2 (nesting levels 0, 1), else level + 1
   double discount, c, limit_factor, kb_min, kb_max;
   int64_t Nn, Ns, Nl, H, Nr, Nsp;   // per tree: nodes, stat entries, log records, hash slots;
                                     // per pair: root belief, support particles
@@ -155,9 +161,9 @@ struct ImParams {
   uint4* root;          // [B][2][Nr] {v0, v1, nested, support slot}
   ISup* sup;            // [B][2][Nr] the bottom (level-0) tree's beliefs
   uint2* supp;          // [B][2][Nsp]
-  ISup* sup1;           // [B][2][Nr] nesting level 2: the middle tree's beliefs ...
-  uint4* supp1;         // [B][2][Nsp] ... {v0, v1, level-0 node, its support slot}
-  double* prob1;        // [B][Nr] nesting level 2: the middle tree's history distribution
+  ISup* msup[kImMaxMid];     // [B][2][Nr] middle tree m + 1's beliefs ...
+  uint4* msupp[kImMaxMid];   // [B][2][Nsp] ... {v0, v1, next tree's node, its table slot}
+  double* mprob[kImMaxMid];  // [B][Nr] middle tree m + 1's history distribution
   int4* path;           // [B][kImPath][3] path of the running simulation (deep levels)
   double* prob;         // [B][Nr] support probabilities (update scratch)
   const double* logtab;
@@ -226,7 +232,7 @@ __host__ __device__ __forceinline__ int im_order(uint32_t info, int k) { return 
 __device__ __forceinline__ bool im_has_stats(uint32_t info) { return (info & kImStatsBit) != 0u; }
 
 // One planner pair (lane): pointers, counters, RNG.  NT: trees per pair
-// (== ImParams::nt: 2, or 3 at nesting level 2).
+// (== ImParams::nt: 2, 3 at nesting level 2, 4 at level 3).
 template <class Env, int NT = 2>
 struct ImPair {
   using Model = typename Env::Model;
@@ -243,11 +249,11 @@ struct ImPair {
   uint4* rootb;   // [2][Nr]
   ISup* sup;      // [2][Nr] the level-0 tree's beliefs
   uint2* supp;    // [2][Nsp]
-  ISup* sup1;     // [2][Nr] nesting level 2: the middle tree's beliefs
-  uint4* supp1;   // [2][Nsp]
+  ISup* msup[kImMaxMid];     // [2][Nr] middle tree m + 1's beliefs
+  uint4* msupp[kImMaxMid];   // [2][Nsp]
+  double* mprob[kImMaxMid];  // [Nr]
   int4* path;
   double* prob;   // [Nr]
-  double* prob1;  // [Nr] nesting level 2
   IHdr h;
   // k_im_search only: math.log(N) for N < lt_n staged in LDS, and the level-1
   // root's view (this lane's column of an [kImRootWords][64] uint4 array),
@@ -265,7 +271,7 @@ struct ImPair {
   // wave waits on a load anyway; draw() consumes it.  Each stream is consumed
   // in order, so results are unchanged; stored counters exclude a computed but
   // unconsumed word (la_pend).
-  uint32_t la_w[7];
+  uint32_t la_w[8];
   uint32_t la_pend = 0u;
 #ifdef POMCP_PHASE_TIMING
   uint64_t pt[kImPhases] = {};
@@ -283,21 +289,19 @@ struct ImPair {
     rootb = p.root + (int64_t)b * 2 * p.Nr;
     sup = p.sup + (int64_t)b * 2 * p.Nr;
     supp = p.supp + (int64_t)b * 2 * p.Nsp;
-    if constexpr (NT == 3) {
-      sup1 = p.sup1 + (int64_t)b * 2 * p.Nr;
-      supp1 = p.supp1 + (int64_t)b * 2 * p.Nsp;
-      prob1 = p.prob1 + (int64_t)b * p.Nr;
-    } else {
-      sup1 = nullptr;
-      supp1 = nullptr;
-      prob1 = nullptr;
+#pragma unroll
+    for (int m = 0; m < kImMaxMid; ++m) {
+      const bool on = m < NT - 2;
+      msup[m] = on ? p.msup[m] + (int64_t)b * 2 * p.Nr : nullptr;
+      msupp[m] = on ? p.msupp[m] + (int64_t)b * 2 * p.Nsp : nullptr;
+      mprob[m] = on ? p.mprob[m] + (int64_t)b * p.Nr : nullptr;
     }
     path = p.path + (int64_t)b * kImPath * 3;
     prob = p.prob + (int64_t)b * p.Nr;
     h = p.hdr[b];
     dp = p.dpow;
   }
-  static constexpr int kCtrs = NT == 3 ? 7 : 6;   // RNG streams in use
+  static constexpr int kCtrs = NT > 2 ? 4 + NT : 6;   // RNG streams in use (slot 5 + k: middle tree k)
   __device__ __forceinline__ uint32_t ctr_stored(int q) const { return h.ctr[q] - ((la_pend >> q) & 1u); }
   // intmcp.py:326-330 (_prune_traverse's clear_belief at every update): the
   // particles of nodes more than two steps behind the current one are dropped
@@ -428,25 +432,32 @@ struct ImPair {
     }
     return philox_word(h.seed, h.tree_key, stream, h.ctr[slot]++);
   }
+  // the stream of counter slot q: slot 5 + k is middle tree k's planner's,
+  // whose level is NT - 1 - k: S_BELIEF_MID + level - 1 (oracle/intmcp.py
+  // belief_stream)
+  static __device__ __forceinline__ constexpr uint32_t slot_stream(int q) {
+    return q == 0 ? (uint32_t)S_BELIEF : q == 1 ? (uint32_t)S_SELECT : q == 2 ? (uint32_t)S_MODEL
+           : q == 3 ? (uint32_t)S_ACT_BASE : q == 4 ? (uint32_t)S_ACT_BASE + 1u
+           : q == 5 ? (uint32_t)S_BELIEF_NESTED : (uint32_t)(S_BELIEF_MID + NT + 3 - q);
+  }
   __device__ __forceinline__ void la_fill() {
-    constexpr uint32_t st[7] = {S_BELIEF, S_SELECT, S_MODEL, S_ACT_BASE, S_ACT_BASE + 1,
-                                S_BELIEF_NESTED, S_BELIEF_MID};
 #pragma unroll
     for (int q = 0; q < kCtrs; ++q) {
       if (q == 2 && !Env::kStepDraws) continue;
       if (!((la_pend >> q) & 1u)) {
-        la_w[q] = philox_word(h.seed, h.tree_key, st[q], h.ctr[q]++);
+        la_w[q] = philox_word(h.seed, h.tree_key, slot_stream(q), h.ctr[q]++);
         la_pend |= 1u << q;
       }
     }
   }
   // tree k's planner's random.Random(seed): the top planner's S_BELIEF, the
-  // level-0 planner's S_BELIEF_NESTED, a middle (level-1, nesting 2) planner's
-  // S_BELIEF_MID (the oracle's streams, oracle/intmcp.py OracleINTMCP)
+  // level-0 planner's S_BELIEF_NESTED, a middle tree's S_BELIEF_MID + its
+  // level - 1 (the oracle's streams, oracle/intmcp.py OracleINTMCP)
   __device__ __forceinline__ uint32_t d_bel(int k, uint32_t n) {
     if (k == kBot) return uniform_int(draw(5, S_BELIEF_NESTED), n);
     if (k == 0) return uniform_int(draw(0, S_BELIEF), n);
-    return uniform_int(draw(6, S_BELIEF_MID), n);
+    if (NT > 3 && k == 2) return uniform_int(draw(7, slot_stream(7)), n);
+    return uniform_int(draw(6, slot_stream(6)), n);
   }
   __device__ __forceinline__ uint32_t d_sel(uint32_t n) { return uniform_int(draw(1, S_SELECT), n); }
   __device__ __forceinline__ double d_sel_float() { return uniform_float(draw(1, S_SELECT)); }
@@ -1081,8 +1092,9 @@ struct ImPair {
   __device__ uint4* root_buf(int sel) { return rootb + (int64_t)sel * p.Nr; }
   __device__ ISup* sup_tab(int sel) { return sup + (int64_t)sel * p.Nr; }
   __device__ uint2* sup_parts(int sel) { return supp + (int64_t)sel * p.Nsp; }
-  __device__ ISup* sup1_tab(int sel) { return sup1 + (int64_t)sel * p.Nr; }
-  __device__ uint4* sup1_parts(int sel) { return supp1 + (int64_t)sel * p.Nsp; }
+  // middle tree m + 1's belief table `sel` and its particles
+  __device__ ISup* mtab(int m, int sel) { return msup[m] + (int64_t)sel * p.Nr; }
+  __device__ uint4* mparts(int m, int sel) { return msupp[m] + (int64_t)sel * p.Nsp; }
 
   // the slot of node n of tree k in the belief table tab (count entries): the
   // node's `support` field while the caller has that table's slots marked
@@ -1192,28 +1204,29 @@ struct ImPair {
     e.size = base + count + fill;
   }
 
-  // nesting level 2: the same for a node of the middle (level-1) tree, whose
-  // particles carry the level-0 history (intmcp.py:815-862 at level 1: the
-  // other agent acts by the level-0 planner's sample_action, the particle's
-  // history extends in the level-0 tree); parents in the previous middle table
-  // (h.pad1 entries), appends to entry `si` of table `sel`
-  __device__ void reinvig_mid(int n, int action, uint64_t okey, int target, int sel, int si) {
-    ISup& e = sup1_tab(sel)[si];
+  // the same for a node of middle tree k, whose particles carry the next
+  // tree's history (intmcp.py:815-862 at level >= 1: the other agent acts by
+  // the level below's sample_action, the particle's history extends in tree
+  // k + 1); parents in the previous table of tree k (h.mpad[k - 1] entries),
+  // appends to entry `si` of table `sel`
+  __device__ void reinvig_mid(int k, int n, int action, uint64_t okey, int target, int sel, int si) {
+    const int m = k - 1;
+    ISup& e = mtab(m, sel)[si];
     const int to_add = target - e.size;
     if (to_add <= 0) return;
-    const int par = N(1, n).parent;
-    const int pi = find_slot(1, sup1_tab(sel ^ 1), par, h.pad1);
+    const int par = N(k, n).parent;
+    const int pi = find_slot(k, mtab(m, sel ^ 1), par, h.mpad[m]);
     if (pi < 0) {
       fail(POMCP_E_UNSUPPORTED);   // parent belief not materialised
       return;
     }
-    const ISup pe = sup1_tab(sel ^ 1)[pi];
+    const ISup pe = mtab(m, sel ^ 1)[pi];
     if (pe.size <= 0) {
       fail(POMCP_E_STATE);
       return;
     }
-    const uint4* pp = sup1_parts(sel ^ 1) + pe.off;
-    uint4* cur = sup1_parts(sel) + e.off;
+    const uint4* pp = mparts(m, sel ^ 1) + pe.off;
+    uint4* cur = mparts(m, sel) + e.off;
     if (e.size + 2 * to_add > e.cap) {
       fail(POMCP_E_ARENA);
       return;
@@ -1223,13 +1236,13 @@ struct ImPair {
     const int base = e.size;
     while (count < to_add && (double)attempts < limit) {
       ++attempts;
-      const uint4 hp = pp[d_bel(1, (uint32_t)pe.size)];
-      const int ao = other_action(1, hp.z);
+      const uint4 hp = pp[d_bel(k, (uint32_t)pe.size)];
+      const int ao = other_action(k, hp.z);
       uint32_t n0, n1, nn;
       double r;
       int done;
       uint64_t k2;
-      step(1, hp.x, hp.y, hp.z, action, ao, &n0, &n1, &r, &done, &k2, &nn);
+      step(k, hp.x, hp.y, hp.z, action, ao, &n0, &n1, &r, &done, &k2, &nn);
       const uint4 rec = make_uint4(n0, n1, nn, 0u);
       if (k2 == okey) {
         cur[base + count++] = rec;
@@ -1307,17 +1320,16 @@ __device__ void im_support(ImPair<Env, NT>& P, int k, ISup* tab, double* prob, u
   *nsup = n;
 }
 
-// Nesting level 2: get_nested_history_dist (intmcp.py:334-362) of the middle
-// tree's distribution (n1 entries of table t1, probabilities p1, particles
-// parts1 with the level-0 node in .z): for each entry in order, each distinct
-// level-0 node of its particles (first occurrence) gains p1 x count / size;
-// the nodes in first-occurrence order over all entries.  Writes the bottom
-// table `tab` (sizes zeroed) and `prob`, and each particle's slot into .w.
+// Nesting level >= 2: get_nested_history_dist (intmcp.py:334-362) of middle
+// tree kt - 1's distribution (n1 entries of table t1, probabilities p1,
+// particles parts1 with the tree-kt node in .z): for each entry in order, each
+// distinct tree-kt node of its particles (first occurrence) gains p1 x count /
+// size; the nodes in first-occurrence order over all entries.  Writes tree
+// kt's table `tab` (sizes zeroed) and `prob`, and each particle's slot into .w.
 // (A lane per pair, or the wave's lanes in lockstep on the same pair.)
 template <class Env, int NT>
-__device__ void im_support_nested(ImPair<Env, NT>& P, const ISup* t1, const double* p1, int n1,
+__device__ void im_support_nested(ImPair<Env, NT>& P, int kB, const ISup* t1, const double* p1, int n1,
                                   uint4* parts1, ISup* tab, double* prob, int* nsup) {
-  constexpr int kB = NT - 1;
   int n = 0;
   for (int q = 0; q < n1; ++q) {
     const ISup e = t1[q];
@@ -1479,10 +1491,12 @@ __global__ __launch_bounds__(64) void k_im_reset(ImParams p) {
   h.search_depth = 0;
   h.sims_done = 0;
   h.pad = 0;
-  h.sup1_sel = 0;
-  h.n_sup1 = 0;
-  h.sup1_used = 0;
-  h.pad1 = 0;
+  for (int m = 0; m < kImMaxMid; ++m) {
+    h.msel[m] = 0;
+    h.n_msup[m] = 0;
+    h.msup_used[m] = 0;
+    h.mpad[m] = 0;
+  }
   p.hdr[b] = h;
 }
 
@@ -1651,21 +1665,24 @@ __device__ int im_extract_root(ImPair<Env, NT>& P, int node, uint4* rb) {
   return n;
 }
 
-// INTMCP.update (intmcp.py:198-300) of a nesting-level-2 planner: tree 0's
-// re-root (or initial belief) and reinvigoration, then the middle planner's
-// (tree 1) _initial_nested_update / _nested_update over the history
-// distribution of the new root belief, then the level-0 planner's (tree 2)
-// over the middle beliefs' nested distribution (get_nested_history_dist,
-// intmcp.py:334-362, summed over every node of the distribution) -- the
-// oracle's order (oracle/intmcp.py _Planner.update / _nested_update).
-template <class Env, bool kWave>
-__device__ void im_update_nest2(ImPair<Env, 3>& P, const typename Env::Model& sm, uint64_t obs,
+// INTMCP.update (intmcp.py:198-300) of a nesting-level-2 or -3 planner: tree
+// 0's re-root (or initial belief) and reinvigoration, then each middle
+// planner's (tree k = 1 .. NT - 2) _initial_nested_update / _nested_update over
+// the history distribution of the belief above (the new root belief for tree
+// 1, the nested distribution of tree k - 1's beliefs below that,
+// get_nested_history_dist, intmcp.py:334-362, summed over every node of the
+// distribution), then the level-0 planner's (tree NT - 1) -- the oracle's
+// order (oracle/intmcp.py _Planner.update / _nested_update).
+template <class Env, int NT, bool kWave>
+__device__ void im_update_nestN(ImPair<Env, NT>& P, const typename Env::Model& sm, uint64_t obs,
                                 int action) {
+  static_assert(NT >= 3 && NT <= kImMaxT, "a middle tree");
+  constexpr int kB = NT - 1;
   const ImParams& p = P.p;
   auto draw_model = [&](uint32_t n) { return P.d_model(n); };
   const bool initial = P.N(0, P.h.cur).t == 0;
   int node, n = 0;
-  if (initial) {   // _initial_nested_update, level 2
+  if (initial) {   // _initial_nested_update, the top level
     node = P.child(0, 0, p.A, obs);
     if (node < 0) return;
     P.traverse(0, node);
@@ -1683,7 +1700,7 @@ __device__ void im_update_nest2(ImPair<Env, 3>& P, const typename Env::Model& sm
       const int c = P.child(1, 0, p.A, ok);
       rb[n++] = make_uint4(s0, s1, (uint32_t)(c < 0 ? 0 : c), 0u);
     }
-  } else {         // _nested_update, level 2: re-root to (action, obs)
+  } else {         // _nested_update, the top level: re-root to (action, obs)
     node = (action >= 0 && action < p.A) ? P.child(0, P.h.cur, action, obs) : -1;
     if (node < 0) {
       P.fail(POMCP_E_NOT_FOUND);
@@ -1692,7 +1709,7 @@ __device__ void im_update_nest2(ImPair<Env, 3>& P, const typename Env::Model& sm
     P.traverse(0, node);
     const int prev_size = P.h.root_size;
     P.h.root_sel ^= 1;
-    n = im_extract_root<Env, 3, kWave>(P, node, P.root_buf(P.h.root_sel));
+    n = im_extract_root<Env, NT, kWave>(P, node, P.root_buf(P.h.root_sel));
     P.h.pad = prev_size;
     if (!im_absorbing(P.N(0, node).info) && P.h.err == 0)
       P.reinvig_top(node, action, obs, p.n_target, &n);   // ceil(1.0 * target)
@@ -1700,78 +1717,96 @@ __device__ void im_update_nest2(ImPair<Env, 3>& P, const typename Env::Model& sm
   P.h.cur = node;
   P.h.root_size = n;
   if (P.h.err != 0 || n == 0) return;
-  // ---- the middle (level-1) planner: the root belief's history distribution
-  const int sel1 = P.h.sup1_sel ^ 1;
-  ISup* t1 = P.sup1_tab(sel1);
-  uint4* q1 = P.sup1_parts(sel1);
-  int n1 = 0;
-  im_support<Env, 3, kWave>(P, 1, t1, P.prob1, P.root_buf(P.h.root_sel), n, &n1);
-  if (initial) {   // _initial_nested_update, level 1
-    uint32_t s0, s1;
-    Env::sample_agent_initial(sm, p.other, P.C(1, t1[0].node).okey, draw_model, &s0, &s1);   // probe
-    int off = 0;
-    for (int q = 0; q < n1 && P.h.err == 0; ++q) {
-      P.traverse(1, t1[q].node);
-      const uint64_t oq = P.C(1, t1[q].node).okey;
-      t1[q].off = off;
-      int m = 0;
-      while ((double)m < P.prob1[q] * (double)p.n_target) {
-        if (off + m >= p.Nsp) {
-          P.fail(POMCP_E_ARENA);
-          break;
+  // ---- the middle planners, top down: tree k's beliefs from the distribution above
+  ISup* up_t = nullptr;
+  const double* up_p = nullptr;
+  uint4* up_q = nullptr;
+  int up_n = 0;
+  for (int k = 1; k < kB; ++k) {
+    const int m = k - 1;
+    const int sel1 = P.h.msel[m] ^ 1;
+    ISup* t1 = P.mtab(m, sel1);
+    uint4* q1 = P.mparts(m, sel1);
+    double* pr = P.mprob[m];
+    int n1 = 0;
+    if (k == 1) im_support<Env, NT, kWave>(P, 1, t1, pr, P.root_buf(P.h.root_sel), n, &n1);
+    else im_support_nested<Env, NT>(P, k, up_t, up_p, up_n, up_q, t1, pr, &n1);
+    if (n1 == 0) {
+      P.fail(POMCP_E_STATE);
+      return;
+    }
+    if (initial) {   // _initial_nested_update, tree k's level
+      const int who = P.agent(k);
+      uint32_t s0, s1;
+      Env::sample_agent_initial(sm, who, P.C(k, t1[0].node).okey, draw_model, &s0, &s1);   // probe
+      int off = 0;
+      for (int q = 0; q < n1 && P.h.err == 0; ++q) {
+        P.traverse(k, t1[q].node);
+        const uint64_t oq = P.C(k, t1[q].node).okey;
+        t1[q].off = off;
+        int c0 = 0;
+        while ((double)c0 < pr[q] * (double)p.n_target) {
+          if (off + c0 >= p.Nsp) {
+            P.fail(POMCP_E_ARENA);
+            break;
+          }
+          Env::sample_agent_initial(sm, who, oq, draw_model, &s0, &s1);
+          const uint64_t ok = Env::obs_key(sm, P.agent(k + 1), s0, s1);
+          const int c = P.child(k + 1, 0, p.A, ok);
+          q1[off + c0++] = make_uint4(s0, s1, (uint32_t)(c < 0 ? 0 : c), 0u);
         }
-        Env::sample_agent_initial(sm, p.other, oq, draw_model, &s0, &s1);
-        const uint64_t ok = Env::obs_key(sm, p.ego, s0, s1);
-        const int c = P.child(2, 0, p.A, ok);
-        q1[off + m++] = make_uint4(s0, s1, (uint32_t)(c < 0 ? 0 : c), 0u);
+        t1[q].size = c0;
+        t1[q].cap = c0;
+        off += c0;
       }
-      t1[q].size = m;
-      t1[q].cap = m;
-      off += m;
+      P.h.msup_used[m] = off;
+    } else {         // _nested_update, tree k's level
+      im_extract_support<Env, NT, kWave>(P, k, t1, q1, pr, n1);
+      if (P.h.err != 0) return;
+      P.h.mpad[m] = P.h.n_msup[m];   // the previous table of tree k (parents)
+      P.mark_slots(k, P.mtab(m, sel1 ^ 1), P.h.mpad[m], true);
+      for (int q = 0; q < n1 && P.h.err == 0; ++q) {
+        const int nd = t1[q].node;
+        P.traverse(k, nd);
+        if (im_absorbing(P.N(k, nd).info)) continue;
+        const int tq = (int)ceil(pr[q] * (double)p.n_target);
+        P.reinvig_mid(k, nd, (int)im_paction(P.N(k, nd).info), P.C(k, nd).okey, tq, sel1, q);
+      }
+      P.mark_slots(k, P.mtab(m, sel1 ^ 1), P.h.mpad[m], false);
+      int used = 0;
+      for (int q = 0; q < n1; ++q) used = max(used, t1[q].off + t1[q].cap);
+      P.h.msup_used[m] = used;
     }
-    P.h.sup1_used = off;
-  } else {         // _nested_update, level 1
-    im_extract_support<Env, 3, kWave>(P, 1, t1, q1, P.prob1, n1);
+    P.h.msel[m] = sel1;
+    P.h.n_msup[m] = n1;
     if (P.h.err != 0) return;
-    P.h.pad1 = P.h.n_sup1;   // the previous middle table (parents)
-    P.mark_slots(1, P.sup1_tab(sel1 ^ 1), P.h.pad1, true);
-    for (int q = 0; q < n1 && P.h.err == 0; ++q) {
-      const int m = t1[q].node;
-      P.traverse(1, m);
-      if (im_absorbing(P.N(1, m).info)) continue;
-      const int tq = (int)ceil(P.prob1[q] * (double)p.n_target);
-      P.reinvig_mid(m, (int)im_paction(P.N(1, m).info), P.C(1, m).okey, tq, sel1, q);
-    }
-    P.mark_slots(1, P.sup1_tab(sel1 ^ 1), P.h.pad1, false);
-    int used = 0;
-    for (int q = 0; q < n1; ++q) used = max(used, t1[q].off + t1[q].cap);
-    P.h.sup1_used = used;
+    up_t = t1;
+    up_p = pr;
+    up_q = q1;
+    up_n = n1;
   }
-  P.h.sup1_sel = sel1;
-  P.h.n_sup1 = n1;
-  if (P.h.err != 0) return;
-  // ---- the level-0 planner: the middle beliefs' nested history distribution
+  // ---- the level-0 planner: the last middle beliefs' nested history distribution
   const int sel = P.h.sup_sel ^ 1;
   ISup* tab = P.sup_tab(sel);
   int n2 = 0;
-  im_support_nested<Env, 3>(P, t1, P.prob1, n1, q1, tab, P.prob, &n2);
+  im_support_nested<Env, NT>(P, kB, up_t, up_p, up_n, up_q, tab, P.prob, &n2);
   if (n2 == 0) {
     P.fail(POMCP_E_STATE);
     return;
   }
   if (initial) {
-    P.h.sup_used = im_initial_bottom<Env, 3>(P, sm, sel, n2, P.prob);
+    P.h.sup_used = im_initial_bottom<Env, NT>(P, sm, sel, n2, P.prob);
   } else {
-    im_extract_support<Env, 3, kWave>(P, 2, tab, P.sup_parts(sel), P.prob, n2);
+    im_extract_support<Env, NT, kWave>(P, kB, tab, P.sup_parts(sel), P.prob, n2);
     if (P.h.err != 0) return;
     P.h.pad = P.h.n_sup;   // previous support count (parents)
     P.mark_support(sel ^ 1, P.h.pad, true);
     for (int q = 0; q < n2 && P.h.err == 0; ++q) {
-      const int m = tab[q].node;
-      P.traverse(2, m);
-      if (im_absorbing(P.N(2, m).info)) continue;
+      const int nd = tab[q].node;
+      P.traverse(kB, nd);
+      if (im_absorbing(P.N(kB, nd).info)) continue;
       const int tq = (int)ceil(P.prob[q] * (double)p.n_target);
-      P.reinvig_nested(m, (int)im_paction(P.N(2, m).info), P.C(2, m).okey, tq, sel, q);
+      P.reinvig_nested(nd, (int)im_paction(P.N(kB, nd).info), P.C(kB, nd).okey, tq, sel, q);
     }
     P.mark_support(sel ^ 1, P.h.pad, false);
     int used = 0;
@@ -1783,14 +1818,14 @@ __device__ void im_update_nest2(ImPair<Env, 3>& P, const typename Env::Model& sm
   if (P.h.err == 0) P.template clear_old_beliefs<kWave>(P.N(0, node).t);
 }
 
-// k_im_update at nesting level 2 (three trees per pair; as k_im_update)
-template <class Env, bool kWave>
-__global__ __launch_bounds__(64) void k_im_update3(ImParams p) {
+// k_im_update at nesting level 2 or 3 (NT = 3 or 4 trees per pair; as k_im_update)
+template <class Env, int NT, bool kWave>
+__global__ __launch_bounds__(64) void k_im_updateN(ImParams p) {
   __shared__ typename Env::Model sm;
   stage_model(p.model, sm);
   const int b = kWave ? (int)blockIdx.x : (int)(blockIdx.x * blockDim.x + threadIdx.x);
   if (b >= p.B) return;
-  ImPair<Env, 3> P(p, sm, b);
+  ImPair<Env, NT> P(p, sm, b);
   const uint64_t obs = p.in_obs[b];
   if (p.in_actions[b] == kImSkip) {
     p.out[2 * b] = im_absorbing(P.N(0, P.h.cur).info) ? 1 : 0;
@@ -1800,9 +1835,9 @@ __global__ __launch_bounds__(64) void k_im_update3(ImParams p) {
   P.h.num_sims = 0;
   P.h.search_depth = 0;
   if (P.h.err == 0 && !im_absorbing(P.N(0, P.h.cur).info))
-    im_update_nest2<Env, kWave>(P, sm, obs, p.in_actions[b]);
+    im_update_nestN<Env, NT, kWave>(P, sm, obs, p.in_actions[b]);
   P.h.pad = 0;
-  P.h.pad1 = 0;
+  for (int m = 0; m < kImMaxMid; ++m) P.h.mpad[m] = 0;
   P.store();
   p.out[2 * b] = im_absorbing(P.N(0, P.h.cur).info) ? 1 : 0;
   p.out[2 * b + 1] = P.h.err;
@@ -2117,17 +2152,19 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
   P.store_search();
 }
 
-// INTMCP.get_action (intmcp.py:368-408) at nesting level 2: sims[l]
-// simulations at level l = 0, 1, 2 in turn.  Every simulation samples a root
-// particle of the top planner (its stream); below level 2 it dispatches down
-// the levels (_nested_sim, intmcp.py:410-442): the middle planner's
-// traverse + expand of the particle's history node, a particle of its belief
-// (the middle stream), and at level 0 the same again in the level-0 tree; the
-// planner whose level is the search level runs _simulate.  (Correctness
-// first: a plain serial lane per pair, no lookahead of the next particle.)
-template <class Env>
-__global__ __launch_bounds__(64) void k_im_search3(ImParams p, int sims0, int sims1, int sims2,
-                                                   int flags) {
+// INTMCP.get_action (intmcp.py:368-408) at nesting level NT - 1 = 2 or 3:
+// sims[l] simulations at level l = 0 .. NT - 1 in turn.  Every simulation
+// samples a root particle of the top planner (its stream); below the top it
+// dispatches down the levels (_nested_sim, intmcp.py:410-442): each middle
+// planner's traverse + expand of the particle's history node and a particle
+// of its belief (its stream), down to the planner whose level is the search
+// level, which runs _simulate.  (Correctness first: a plain serial lane per
+// pair, no lookahead of the next particle.)
+template <class Env, int NT>
+__global__ __launch_bounds__(64) void k_im_searchN(ImParams p, int sims0, int sims1, int sims2,
+                                                   int sims3, int flags) {
+  static_assert(NT >= 3 && NT <= kImMaxT, "a middle tree");
+  constexpr int kB = NT - 1;
   __shared__ typename Env::Model sm;
   __shared__ double slog[kImLogLds];
   __shared__ uint4 srv[kImRootWords * kWave];
@@ -2142,7 +2179,7 @@ __global__ __launch_bounds__(64) void k_im_search3(ImParams p, int sims0, int si
   stage_model(p.model, sm);   // (synchronises)
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= p.B) return;
-  ImPair<Env, 3> P(p, sm, b);
+  ImPair<Env, NT> P(p, sm, b);
   P.lt_lds = slog;
   P.lt_n = ltn;
   P.rv = srv + threadIdx.x;
@@ -2156,58 +2193,57 @@ __global__ __launch_bounds__(64) void k_im_search3(ImParams p, int sims0, int si
   int action = 0;
   if (P.h.err == 0 && !im_absorbing(P.N(0, root).info) && P.N(0, root).t > 0) {
     const uint4* const rb = P.root_buf(P.h.root_sel);
-    if (sims0 + sims1 + sims2 > 0) {   // the top planner's _nested_sim head (no draws)
+    if (sims0 + sims1 + sims2 + sims3 > 0) {   // the top planner's _nested_sim head (no draws)
       P.traverse(0, root);
       if (im_nreg(P.N(0, root).info) == 0) P.expand(0, root);
       if (P.h.root_size == 0 || P.h.root_size < p.extra) P.fail(POMCP_E_UNSUPPORTED);
     }
-    const ISup* const t1 = P.sup1_tab(P.h.sup1_sel);
-    const uint4* const q1s = P.sup1_parts(P.h.sup1_sel);
     const ISup* const t2 = P.sup_tab(P.h.sup_sel);
     const uint2* const q2s = P.sup_parts(P.h.sup_sel);
-    for (int level = 0; level < 3 && P.h.err == 0; ++level) {
-      const int num_sims = level == 0 ? sims0 : level == 1 ? sims1 : sims2;
-      if (level == 2 && num_sims > 0) {   // the root's view, kept current by the backups
+    for (int level = 0; level < NT && P.h.err == 0; ++level) {
+      const int num_sims = level == 0 ? sims0 : level == 1 ? sims1 : level == 2 ? sims2 : sims3;
+      if (level == kB && num_sims > 0) {   // the root's view, kept current by the backups
         P.rv_put(P.view(0, root));
         P.rv_root = root;
       }
+      const int kt = kB - level;   // the tree that simulates
       for (int s = 0; s < num_sims && P.h.err == 0; ++s) {
         const uint4 hp = rb[P.d_bel(0, (uint32_t)P.h.root_size)];
-        if (level == 2) {
+        if (kt == 0) {
           const auto v = P.rv_get();
           const int d = P.simulate(0, hp.x, hp.y, hp.z, root, v);
           P.N(0, root).visits = v.x.visits + 1;
           P.rv[0].z = (uint32_t)(v.x.visits + 1);
           if (d > P.h.search_depth) P.h.search_depth = d;
         } else {
-          // the middle planner's _nested_sim at the particle's history
-          const int n1 = (int)hp.z;
-          const ISup e1 = t1[hp.w];
-          P.traverse(1, n1);
-          if (im_nreg(P.N(1, n1).info) == 0) P.expand(1, n1);
-          if (e1.size == 0) {
-            P.fail(POMCP_E_UNSUPPORTED);   // depleted node (not reached by the goldens)
-            break;
-          }
-          const uint4 q1 = q1s[e1.off + P.d_bel(1, (uint32_t)e1.size)];
-          if (level == 1) {
-            auto v = P.view(1, n1);
-            P.simulate(1, q1.x, q1.y, q1.z, n1, v);
-            P.N(1, n1).visits = v.x.visits + 1;
-          } else {   // ... and the level-0 planner's at the middle particle's history
-            const int n2 = (int)q1.z;
-            const ISup e2 = t2[q1.w];
-            P.traverse(2, n2);
-            if (im_nreg(P.N(2, n2).info) == 0) P.expand(2, n2);
-            if (e2.size == 0) {
-              P.fail(POMCP_E_UNSUPPORTED);
+          // each middle planner's _nested_sim at the particle's history, down to tree kt
+          uint32_t nx = hp.z, slot = hp.w;
+          for (int k = 1; k <= kt; ++k) {
+            const int nk = (int)nx;
+            const ISup e = k < kB ? P.mtab(k - 1, P.h.msel[k - 1])[slot] : t2[slot];
+            P.traverse(k, nk);
+            if (im_nreg(P.N(k, nk).info) == 0) P.expand(k, nk);
+            if (e.size == 0) {
+              P.fail(POMCP_E_UNSUPPORTED);   // depleted node (not reached by the goldens)
               break;
             }
-            const uint2 q2 = q2s[e2.off + P.d_bel(2, (uint32_t)e2.size)];
-            auto v = P.view(2, n2);
-            P.simulate(2, q2.x, q2.y, 0u, n2, v);
-            P.N(2, n2).visits = v.x.visits + 1;
+            if (k < kB) {
+              const uint4 q = P.mparts(k - 1, P.h.msel[k - 1])[e.off + P.d_bel(k, (uint32_t)e.size)];
+              if (k == kt) {
+                auto v = P.view(k, nk);
+                P.simulate(k, q.x, q.y, q.z, nk, v);
+                P.N(k, nk).visits = v.x.visits + 1;
+              }
+              nx = q.z;
+              slot = q.w;
+            } else {
+              const uint2 q = q2s[e.off + P.d_bel(kB, (uint32_t)e.size)];
+              auto v = P.view(kB, nk);
+              P.simulate(kB, q.x, q.y, 0u, nk, v);
+              P.N(kB, nk).visits = v.x.visits + 1;
+            }
           }
+          if (P.h.err != 0) break;
         }
         P.h.num_sims += 1;
       }

@@ -1,5 +1,7 @@
 // C-ABI host side of the I-NTMCP engine (include/intmcp.h).  Part of the
 // single translation unit of pomcp_capi.hip.
+#include <type_traits>
+
 #include "../../include/intmcp.h"
 
 struct intmcp_ctx {
@@ -56,7 +58,7 @@ __global__ __launch_bounds__(64) void k_im_root_stats(ImParams d, intmcp_root_st
   }
   o.min_value = h.mm_min[T];
   o.max_value = h.mm_max[T];
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < 2; ++k) {   // (the first two trees; intmcp_get_tree_counts has them all)
     o.n_nodes[k] = h.n_nodes[k];
     o.n_log[k] = h.n_log[k];
     o.n_stats[k] = h.n_stats[k];
@@ -156,8 +158,8 @@ int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, in
   if (c.action_selection != POMCP_SEL_UCB && c.action_selection != POMCP_SEL_UNIFORM)
     return bad(POMCP_E_UNSUPPORTED, "I-NTMCP pucb reads self.action_space (intmcp.py:645): ucb / uniform only");
   if (c.ego_agent < 0 || c.ego_agent > 1 || c.num_trees < 1) return bad(POMCP_E_INVALID, "ego / pairs");
-  if (cfg->nesting_level < 0 || cfg->nesting_level > 2)
-    return bad(POMCP_E_UNSUPPORTED, "nesting levels 0, 1 and 2");
+  if (cfg->nesting_level < 0 || cfg->nesting_level > kImMaxT - 1)
+    return bad(POMCP_E_UNSUPPORTED, "nesting levels 0 to 3");
   if (c.depth_limit < 0 || c.step_limit < 0 || c.num_particles < 1) return bad(POMCP_E_INVALID, "limits");
   if (cfg->max_nodes < 2 || cfg->max_nodes >= (1ll << 28) || cfg->max_stats < c.num_actions ||
       cfg->max_log < 1 || cfg->hash_slots < 16 || (cfg->hash_slots & (cfg->hash_slots - 1)) ||
@@ -201,7 +203,7 @@ int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, in
   d.A = c.num_actions;
   // nesting level 0: the planner's tree is tree 1, whose agent is p.other
   d.nest0 = cfg->nesting_level == 0 ? 1 : 0;
-  d.nt = cfg->nesting_level == 2 ? 3 : 2;   // nesting level 2: a third (level-0) tree
+  d.nt = cfg->nesting_level >= 2 ? cfg->nesting_level + 1 : 2;   // a tree per level (nesting 0: 2)
   d.ego = d.nest0 ? 1 - c.ego_agent : c.ego_agent;
   d.other = 1 - d.ego;
   d.sel = c.action_selection;
@@ -232,7 +234,7 @@ int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, in
       intmcp_destroy(ctx);                                                      \
       return rc;                                                                \
     }                                                                           \
-    d.field = reinterpret_cast<decltype(d.field)>(p);                           \
+    d.field = reinterpret_cast<std::remove_reference_t<decltype(d.field)>>(p);  \
   } while (0)
   IM_ALLOC(hdr, IHdr, B);
   d.nstride = kImBlock;   // node blocks (intmcp.hip), interleaved by wave: im_node_off
@@ -242,10 +244,12 @@ int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, in
   IM_ALLOC(root, uint4, B * 2 * d.Nr);
   IM_ALLOC(sup, ISup, B * 2 * d.Nr);
   IM_ALLOC(supp, uint2, B * 2 * d.Nsp);
-  const bool mid = d.nt == 3;   // the middle planner's beliefs and distribution
-  IM_ALLOC(sup1, ISup, mid ? B * 2 * d.Nr : 1);
-  IM_ALLOC(supp1, uint4, mid ? B * 2 * d.Nsp : 1);
-  IM_ALLOC(prob1, double, mid ? B * d.Nr : 1);
+  for (int m = 0; m < kImMaxMid; ++m) {   // the middle planners' beliefs and distributions
+    const bool mid = m < d.nt - 2;
+    IM_ALLOC(msup[m], ISup, mid ? B * 2 * d.Nr : 1);
+    IM_ALLOC(msupp[m], uint4, mid ? B * 2 * d.Nsp : 1);
+    IM_ALLOC(mprob[m], double, mid ? B * d.Nr : 1);
+  }
   IM_ALLOC(path, int4, B * kImPath * 3);
   IM_ALLOC(prob, double, B * d.Nr);
   IM_ALLOC(logtab, double, c.log_table_size);
@@ -333,14 +337,20 @@ int intmcp_update(intmcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_k
   // shared by the wave's lanes (k_im_update kWave); a lane per pair otherwise
   const bool wave = B <= 1024;
   const dim3 ugrid(wave ? (unsigned)B : (unsigned)im_blocks(B));
-  if (ctx->ip.nt == 3) {   // nesting level 2
-    if (ctx->cfg.base.env_id == POMCP_ENV_PURSUIT_EVASION) {
-      if (wave) hipLaunchKernelGGL((k_im_update3<EnvPursuitEvasion, true>), ugrid, dim3(64), 0, ctx->stream, ctx->ip);
-      else hipLaunchKernelGGL((k_im_update3<EnvPursuitEvasion, false>), ugrid, dim3(64), 0, ctx->stream, ctx->ip);
-    } else {
-      if (wave) hipLaunchKernelGGL((k_im_update3<EnvDriving, true>), ugrid, dim3(64), 0, ctx->stream, ctx->ip);
-      else hipLaunchKernelGGL((k_im_update3<EnvDriving, false>), ugrid, dim3(64), 0, ctx->stream, ctx->ip);
-    }
+#define IM_UPDATE_N(NT)                                                                                     \
+  do {                                                                                                      \
+    if (ctx->cfg.base.env_id == POMCP_ENV_PURSUIT_EVASION) {                                                \
+      if (wave) hipLaunchKernelGGL((k_im_updateN<EnvPursuitEvasion, NT, true>), ugrid, dim3(64), 0, ctx->stream, ctx->ip); \
+      else hipLaunchKernelGGL((k_im_updateN<EnvPursuitEvasion, NT, false>), ugrid, dim3(64), 0, ctx->stream, ctx->ip); \
+    } else {                                                                                                \
+      if (wave) hipLaunchKernelGGL((k_im_updateN<EnvDriving, NT, true>), ugrid, dim3(64), 0, ctx->stream, ctx->ip); \
+      else hipLaunchKernelGGL((k_im_updateN<EnvDriving, NT, false>), ugrid, dim3(64), 0, ctx->stream, ctx->ip); \
+    }                                                                                                       \
+  } while (0)
+  if (ctx->ip.nt == 4) {   // nesting level 3
+    IM_UPDATE_N(4);
+  } else if (ctx->ip.nt == 3) {   // nesting level 2
+    IM_UPDATE_N(3);
   } else if (ctx->cfg.base.env_id == POMCP_ENV_PURSUIT_EVASION) {
     if (wave) hipLaunchKernelGGL((k_im_update<EnvPursuitEvasion, true>), ugrid, dim3(64), 0, ctx->stream, ctx->ip);
     else hipLaunchKernelGGL((k_im_update<EnvPursuitEvasion, false>), ugrid, dim3(64), 0, ctx->stream, ctx->ip);
@@ -364,8 +374,8 @@ static int im_fetch_hdr(intmcp_ctx* ctx) {
   return POMCP_OK;
 }
 
-// one launch of sims[l] simulations at level l (l = 0, 1, 2 in turn)
-static int im_search3(intmcp_ctx* ctx, const int32_t sims[3], int32_t flags, int32_t* actions_out);
+// one launch of sims[l] simulations at level l (l = 0 .. nt - 1 in turn; nt >= 3)
+static int im_searchN(intmcp_ctx* ctx, const int32_t sims[kImMaxT], int32_t flags, int32_t* actions_out);
 
 int intmcp_search_levels(intmcp_ctx* ctx, int32_t level0_sims, int32_t level1_sims,
                          int32_t flags, int32_t* actions_out) {
@@ -375,9 +385,9 @@ int intmcp_search_levels(intmcp_ctx* ctx, int32_t level0_sims, int32_t level1_si
     ctx->err = "search_levels: nesting level 0 has no level-1 simulations";
     return POMCP_E_INVALID;
   }
-  if (ctx->ip.nt == 3) {
-    const int32_t sims[3] = {level0_sims, level1_sims, 0};
-    return im_search3(ctx, sims, flags, actions_out);
+  if (ctx->ip.nt >= 3) {
+    const int32_t sims[kImMaxT] = {level0_sims, level1_sims, 0, 0};
+    return im_searchN(ctx, sims, flags, actions_out);
   }
   IM_TRY(ctx, hipSetDevice(ctx->device));
   IM_LAUNCH(ctx, k_im_search, dim3(im_blocks(ctx->ip.B)), dim3(64), ctx->ip, (int)level0_sims,
@@ -396,10 +406,18 @@ int intmcp_search_levels(intmcp_ctx* ctx, int32_t level0_sims, int32_t level1_si
   return POMCP_OK;
 }
 
-static int im_search3(intmcp_ctx* ctx, const int32_t sims[3], int32_t flags, int32_t* actions_out) {
+static int im_searchN(intmcp_ctx* ctx, const int32_t sims[kImMaxT], int32_t flags, int32_t* actions_out) {
   IM_TRY(ctx, hipSetDevice(ctx->device));
-  IM_LAUNCH(ctx, k_im_search3, dim3(im_blocks(ctx->ip.B)), dim3(64), ctx->ip, (int)sims[0],
-            (int)sims[1], (int)sims[2], (int)flags);
+  const dim3 grid(im_blocks(ctx->ip.B));
+  const bool pe = ctx->cfg.base.env_id == POMCP_ENV_PURSUIT_EVASION;
+  const int s0 = sims[0], s1 = sims[1], s2 = sims[2], s3 = sims[3];
+  if (ctx->ip.nt == 4) {
+    if (pe) hipLaunchKernelGGL((k_im_searchN<EnvPursuitEvasion, 4>), grid, dim3(64), 0, ctx->stream, ctx->ip, s0, s1, s2, s3, (int)flags);
+    else hipLaunchKernelGGL((k_im_searchN<EnvDriving, 4>), grid, dim3(64), 0, ctx->stream, ctx->ip, s0, s1, s2, s3, (int)flags);
+  } else {
+    if (pe) hipLaunchKernelGGL((k_im_searchN<EnvPursuitEvasion, 3>), grid, dim3(64), 0, ctx->stream, ctx->ip, s0, s1, s2, 0, (int)flags);
+    else hipLaunchKernelGGL((k_im_searchN<EnvDriving, 3>), grid, dim3(64), 0, ctx->stream, ctx->ip, s0, s1, s2, 0, (int)flags);
+  }
   IM_TRY(ctx, hipGetLastError());
   if (!actions_out) return POMCP_OK;
   int rc = im_fetch_hdr(ctx);
@@ -416,9 +434,10 @@ static int im_search3(intmcp_ctx* ctx, const int32_t sims[3], int32_t flags, int
 
 int intmcp_search(intmcp_ctx* ctx, int32_t num_sims, int32_t* actions_out) {
   if (!ctx || num_sims < 0) return POMCP_E_INVALID;
-  if (ctx->ip.nt == 3) {
-    const int32_t sims[3] = {num_sims, num_sims, num_sims};
-    return im_search3(ctx, sims, kImBegin | kImFinal, actions_out);
+  if (ctx->ip.nt >= 3) {
+    int32_t sims[kImMaxT] = {0, 0, 0, 0};
+    for (int l = 0; l < ctx->ip.nt; ++l) sims[l] = num_sims;
+    return im_searchN(ctx, sims, kImBegin | kImFinal, actions_out);
   }
   return intmcp_search_levels(ctx, num_sims, ctx->ip.nest0 ? 0 : num_sims, kImBegin | kImFinal,
                               actions_out);
@@ -432,10 +451,10 @@ int intmcp_search_level(intmcp_ctx* ctx, int32_t level, int32_t sims, int32_t fl
     ctx->err = "search_level: no level " + std::to_string(level);
     return POMCP_E_INVALID;
   }
-  if (ctx->ip.nt == 3) {
-    int32_t s[3] = {0, 0, 0};
+  if (ctx->ip.nt >= 3) {
+    int32_t s[kImMaxT] = {0, 0, 0, 0};
     s[level] = sims;
-    return im_search3(ctx, s, flags, actions_out);
+    return im_searchN(ctx, s, flags, actions_out);
   }
   return intmcp_search_levels(ctx, level == 0 ? sims : 0, level == 1 ? sims : 0, flags, actions_out);
 }
@@ -668,30 +687,31 @@ int intmcp_get_support(intmcp_ctx* ctx, int32_t pair, int32_t* entries, int32_t 
   return POMCP_OK;
 }
 
-int intmcp_get_mid_support(intmcp_ctx* ctx, int32_t pair, int32_t* entries, int32_t capacity_entries,
-                           int32_t* n_entries, uint32_t* particles, int32_t capacity_particles,
-                           int32_t* n_particles) {
+int intmcp_get_middle_support(intmcp_ctx* ctx, int32_t pair, int32_t tree, int32_t* entries,
+                              int32_t capacity_entries, int32_t* n_entries, uint32_t* particles,
+                              int32_t capacity_particles, int32_t* n_particles) {
   if (!ctx || !n_entries || !n_particles || pair < 0 || pair >= ctx->ip.B) return POMCP_E_INVALID;
-  if (ctx->ip.nt != 3) {
-    ctx->err = "get_mid_support: nesting level 2 only";
+  if (tree < 1 || tree > ctx->ip.nt - 2) {
+    ctx->err = "get_middle_support: no middle tree " + std::to_string(tree) + " (nesting levels 2, 3)";
     return POMCP_E_INVALID;
   }
   int rc = im_fetch_hdr(ctx);
   if (rc != POMCP_OK) return rc;
   const IHdr& h = ctx->host_hdr[pair];
-  *n_entries = h.n_sup1;
-  *n_particles = h.sup1_used;
-  if (entries && capacity_entries >= h.n_sup1) {
+  const int m = tree - 1;
+  *n_entries = h.n_msup[m];
+  *n_particles = h.msup_used[m];
+  if (entries && capacity_entries >= h.n_msup[m]) {
     rc = im_copy(ctx, reinterpret_cast<ISup*>(entries),
-                 ctx->ip.sup1 + ((int64_t)pair * 2 + h.sup1_sel) * ctx->ip.Nr, (size_t)h.n_sup1);
+                 ctx->ip.msup[m] + ((int64_t)pair * 2 + h.msel[m]) * ctx->ip.Nr, (size_t)h.n_msup[m]);
     if (rc != POMCP_OK) return rc;
   }
-  if (particles && capacity_particles >= h.sup1_used) {
-    std::vector<uint4> buf((size_t)h.sup1_used);
-    rc = im_copy(ctx, buf.data(), ctx->ip.supp1 + ((int64_t)pair * 2 + h.sup1_sel) * ctx->ip.Nsp,
-                 (size_t)h.sup1_used);
+  if (particles && capacity_particles >= h.msup_used[m]) {
+    std::vector<uint4> buf((size_t)h.msup_used[m]);
+    rc = im_copy(ctx, buf.data(), ctx->ip.msupp[m] + ((int64_t)pair * 2 + h.msel[m]) * ctx->ip.Nsp,
+                 (size_t)h.msup_used[m]);
     if (rc != POMCP_OK) return rc;
-    for (int i = 0; i < h.sup1_used; ++i) {
+    for (int i = 0; i < h.msup_used[m]; ++i) {
       particles[3 * i] = buf[i].x;
       particles[3 * i + 1] = buf[i].y;
       particles[3 * i + 2] = buf[i].z;
@@ -700,17 +720,24 @@ int intmcp_get_mid_support(intmcp_ctx* ctx, int32_t pair, int32_t* entries, int3
   return POMCP_OK;
 }
 
+int intmcp_get_mid_support(intmcp_ctx* ctx, int32_t pair, int32_t* entries, int32_t capacity_entries,
+                           int32_t* n_entries, uint32_t* particles, int32_t capacity_particles,
+                           int32_t* n_particles) {
+  return intmcp_get_middle_support(ctx, pair, 1, entries, capacity_entries, n_entries, particles,
+                                   capacity_particles, n_particles);
+}
+
 int intmcp_get_tree_counts(intmcp_ctx* ctx, int32_t* out) {
   if (!ctx || !out) return POMCP_E_INVALID;
   int rc = im_fetch_hdr(ctx);
   if (rc != POMCP_OK) return rc;
   for (int t = 0; t < ctx->ip.B; ++t) {
     const IHdr& h = ctx->host_hdr[t];
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < kImMaxT; ++k) {
       const bool on = k < ctx->ip.nt;
-      out[9 * t + 3 * k] = on ? h.n_nodes[k] : 0;
-      out[9 * t + 3 * k + 1] = on ? h.n_log[k] : 0;
-      out[9 * t + 3 * k + 2] = on ? h.n_stats[k] : 0;
+      out[3 * kImMaxT * t + 3 * k] = on ? h.n_nodes[k] : 0;
+      out[3 * kImMaxT * t + 3 * k + 1] = on ? h.n_log[k] : 0;
+      out[3 * kImMaxT * t + 3 * k + 2] = on ? h.n_stats[k] : 0;
     }
   }
   return POMCP_OK;

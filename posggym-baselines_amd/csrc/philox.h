@@ -24,7 +24,8 @@ enum Stream : uint32_t {
   S_MODEL = 2,    // model RNG: initial state sampling, execution-order shuffle
   S_BELIEF_NESTED = 3,  // I-NTMCP level-0 planner's random.Random(seed) (intmcp.py:66)
   S_MIXTURE = 4,  // other_policy.py `random`: OtherAgentMixturePolicy's policy draw (POTMMCP)
-  S_BELIEF_MID = 5,  // I-NTMCP nesting level 2: the level-1 planner's random.Random(seed)
+  S_BELIEF_MID = 5,  // I-NTMCP middle planners' random.Random(seed): level l on 5 + l - 1
+                     // (5 at nesting level 2; 5, 6 at level 3)
   S_ACT_BASE = 8, // Discrete.sample() of agent i: 8 + i
   S_ENV_MODEL = 32,
   S_ENV_POLICY_BASE = 40,

@@ -11,7 +11,7 @@ import os
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.environ.get("POMCP_LIB_PATH") or os.path.join(LIB_DIR, "libpomcp_hip.so")
 
-POMCP_ABI_VERSION = 5
+POMCP_ABI_VERSION = 6
 POMCP_MAX_TYPE_POLICIES = 8
 POMCP_MAX_ACTIONS = 8
 POMCP_XREC_STATS = 6
@@ -311,6 +311,8 @@ INTMCP_SIGNATURES = [
      [_CTX, C.c_int32, _P32, C.c_int32, _P32, _PU32, C.c_int32, _P32]),
     ("intmcp_get_mid_support", C.c_int,
      [_CTX, C.c_int32, _P32, C.c_int32, _P32, _PU32, C.c_int32, _P32]),
+    ("intmcp_get_middle_support", C.c_int,
+     [_CTX, C.c_int32, C.c_int32, _P32, C.c_int32, _P32, _PU32, C.c_int32, _P32]),
     ("intmcp_search_level", C.c_int, [_CTX, C.c_int32, C.c_int32, C.c_int32, _P32]),
     ("intmcp_get_tree_counts", C.c_int, [_CTX, _P32]),
     ("intmcp_synthetic_obs", C.c_int, [_CTX, C.c_uint64, _PU64]),

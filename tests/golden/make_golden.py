@@ -115,6 +115,16 @@ INTMCP2_CASES = {
 }
 
 
+# I-NTMCP nesting_level=3: a chain of four planners, the ego's level-3 tree over
+# the other agent's level-2, the ego's level-1 and the other agent's level-0
+# (the same recursion); search_time_limit = 0.1 * 4
+INTMCP3_CFG = dict(TEST_CFG, search_time_limit=0.4, state_belief_only=False)
+INTMCP3_CASES = {
+    "intmcp3_ucb": ({}, 16, [(70, 70)], "0", 12, "Driving-v1"),
+    "intmcp3_pe": ({}, 12, [(71, 71)], "1", 15, "PursuitEvasion-v1"),
+}
+
+
 # I-NTMCP with caller-supplied search policies (intmcp.py:956-971):
 # {level: {agent: probs}} -> SearchPolicyWrapper(FixedDistributionPolicy) on
 # the agent's action stream, RandomSearchPolicy for the agents left out.
@@ -139,7 +149,10 @@ def run_intmcp_case(name):
     sp = None
     if name in INTMCP_SP_CASES:
         level, sp, num_sims, pairs, ego, max_steps, env = INTMCP_SP_CASES[name]
-        over, base = {}, (INTMCP0_CFG, INTMCP_CFG, INTMCP2_CFG)[level]
+        over, base = {}, (INTMCP0_CFG, INTMCP_CFG, INTMCP2_CFG, INTMCP3_CFG)[level]
+    elif name in INTMCP3_CASES:
+        over, num_sims, pairs, ego, max_steps, env = INTMCP3_CASES[name]
+        base, level = INTMCP3_CFG, 3
     elif name in INTMCP2_CASES:
         over, num_sims, pairs, ego, max_steps, env = INTMCP2_CASES[name]
         base, level = INTMCP2_CFG, 2
@@ -429,7 +442,7 @@ def main(only=None, out_dir=HERE):
         n = sum(len(e["records"]) for e in data["episodes"])
         print(f"{name}: {len(data['episodes'])} episodes, {n} records")
     for name in (list(INTMCP_CASES) + list(INTMCP0_CASES) + list(INTMCP2_CASES)
-                 + list(INTMCP_SP_CASES) if only is None
+                 + list(INTMCP3_CASES) + list(INTMCP_SP_CASES) if only is None
                  else (only if isinstance(only, list) else ())):
         data = run_intmcp_case(name)
         _write(out_dir, name, data)

@@ -45,6 +45,9 @@ INTMCP_SP_CASES = ["intmcp_sp_ucb", "intmcp0_sp_ego1", "intmcp_sp_pe", "intmcp2_
 # I-NTMCP nesting_level=2 (make_golden.py INTMCP2_CASES): three trees
 INTMCP2_CASES = ["intmcp2_ucb", "intmcp2_ego1_uniform", "intmcp2_pe"]
 
+# I-NTMCP nesting_level=3 (make_golden.py INTMCP3_CASES): four trees
+INTMCP3_CASES = ["intmcp3_ucb", "intmcp3_pe"]
+
 
 def search_probs(data):
     """A golden's {level: {agent: probs}} with integer levels (None if absent)."""

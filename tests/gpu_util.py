@@ -206,9 +206,12 @@ def intmcp_state_record(eng, pair, searched, action):
             rows_ = parts_[int(e["off"]):int(e["off"]) + int(e["size"])]
         return (int(nd["visits"]), nk, [(int(nd["t"]), (int(q[0]), int(q[1]))) for q in rows_]), rows_
 
-    # the middle tree's beliefs at nesting level 2 (tree 1), else the level-0 support
-    mid = eng.nesting_level == 2
-    ent1, parts1 = eng.mid_support(pair) if mid else (ent, sparts)
+    L = eng.nesting_level
+
+    def table(k):   # tree k's materialised beliefs: a middle tree's, else the level-0 support
+        return eng.mid_support(pair, k) if 1 <= k <= L - 1 else (ent, sparts)
+
+    ent1, parts1 = table(1)
     # the root's t: every root particle's other-agent history has that length
     t_root = int(n1[int(rows[0][2])]["t"]) if len(rows) else 0
     parts = [(t_root, (int(r[0]), int(r[1])), history(n1, int(r[2]))) for r in rows]
@@ -221,23 +224,29 @@ def intmcp_state_record(eng, pair, searched, action):
         nd, rows_ = node(n1, s1, m, ent1, parts1)
         nested.append((history(n1, m), nd))
         mrows.append(rows_)
-    nested2 = None
-    if mid:   # the third tree: histories carried by the middle beliefs' particles
-        n2 = eng.nodes(pair, 2)
-        s2 = eng.stats(pair, 2)
-        seqs, nodes2, seen2 = [], [], []
-        for rows_ in mrows:
+    # the third tree on (nesting level >= 2): the histories carried by the
+    # particles of the previous tree's recorded nodes, and those nodes
+    chain, up_rows = [], mrows
+    for k in range(2, L + 1):
+        nk_, sk_ = eng.nodes(pair, k), eng.stats(pair, k)
+        ek, pk = table(k)
+        seqs, nodes2, seen2, rows2 = [], [], [], []
+        for rows_ in up_rows:
             seq = []
             for q in rows_:
                 h2 = int(q[2])
-                seq.append(history(n2, h2))
+                seq.append(history(nk_, h2))
                 if h2 not in seen2:
                     seen2.append(h2)
-                    nodes2.append((history(n2, h2), node(n2, s2, h2, ent, sparts)[0]))
+                    nd, r2 = node(nk_, sk_, h2, ek, pk)
+                    nodes2.append((history(nk_, h2), nd))
+                    rows2.append(r2)
             seqs.append(seq)
-        nested2 = (seqs, nodes2)
+        chain.append((seqs, nodes2))
+        up_rows = rows2
     return intmcp_record(rec, int(st.num_sims), int(st.search_depth), int(st.root_visits), kids,
-                         st.min_value, st.max_value, parts, nested, nested2=nested2)
+                         st.min_value, st.max_value, parts, nested,
+                         nested2=chain[0] if chain else None, deeper=chain[1:])
 
 
 def _softmax_debug(ctx, slack):

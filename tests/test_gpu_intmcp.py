@@ -9,18 +9,20 @@ import pytest
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
 
-from golden_util import (INTMCP0_CASES, INTMCP2_CASES, INTMCP_CASES, INTMCP_SP_CASES, cfg_kwargs,
-                         load, search_probs)
+from golden_util import (INTMCP0_CASES, INTMCP2_CASES, INTMCP3_CASES, INTMCP_CASES,
+                         INTMCP_SP_CASES, cfg_kwargs, load, search_probs)
 from gpu_util import gpu_intmcp_episode
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("case", INTMCP_CASES + INTMCP0_CASES + INTMCP2_CASES + INTMCP_SP_CASES)
+@pytest.mark.parametrize("case", INTMCP_CASES + INTMCP0_CASES + INTMCP2_CASES + INTMCP3_CASES
+                         + INTMCP_SP_CASES)
 def test_gpu_intmcp_matches_reference_goldens(case):
     """Nesting level 1 (intmcp_*) and 0 (intmcp0_*: the planner's own tree,
-    the other agent acting by the planner's random choice); *_sp_*: fixed-
-    distribution search policies per level and agent."""
+    the other agent acting by the planner's random choice), 2 and 3
+    (intmcp2_*, intmcp3_*: three and four trees); *_sp_*: fixed-distribution
+    search policies per level and agent."""
     data = load(case)
     for ep in data["episodes"]:
         kw = cfg_kwargs(ep["config"])

@@ -104,7 +104,37 @@ def test_intmcp_nesting2_capacities_and_headroom():
     target = cfg.num_particles + cfg.extra_particles
     reserve = 2 * (int(-(-cfg.reinvigoration_sample_limit_factor * target // 1)) + target) \
         + 2 * target + 8
-    counts = np.zeros((1, 3, 3), dtype=np.int32)
+    counts = np.zeros((1, 4, 3), dtype=np.int32)
     counts[0, 2, 0] = 1000     # the level-0 tree holds the most nodes
     eng.tree_counts = lambda: counts
     assert eng.headroom() == (caps.max_nodes - 1000 - reserve) // L
+
+
+def test_intmcp_nesting3_capacities_and_headroom():
+    """Nesting level 3 (four trees per pair): a fourth tree and a second middle
+    belief table in the arenas and the bytes per pair; the wall-clock split
+    over four levels; the headroom takes the fullest of the four trees."""
+    import numpy as np
+    from posggym_baselines_amd.planning import MCTSConfig
+    from posggym_baselines_amd.planning import intmcp as M
+    cfg = MCTSConfig(discount=0.95, c=1.4, truncated=False, search_time_limit=1.0)
+    c2 = M.plan_intmcp_capacities(cfg, 50, 256, 4, 5, nesting_level=2)
+    c3 = M.plan_intmcp_capacities(cfg, 50, 256, 4, 5, nesting_level=3)
+    assert c3.trees == 4
+    assert c3.max_nodes > c2.max_nodes and c3.max_root_belief > c2.max_root_belief
+    assert c3.bytes_per_pair(5) > 1.25 * c2.bytes_per_pair(5)
+    assert c3.log_table_size >= 4 * 256 * 4
+    caps, sims = M.plan_intmcp_wallclock_capacities(cfg, 50, 5, nesting_level=3)
+    assert caps.trees == 4 and sims == int(1.0 / 4 * M.INTMCP_WALL_CLOCK_SIMS_PER_S + 0.999)
+    assert caps.bytes_per_pair(5) <= M.INTMCP_WALL_CLOCK_HBM_BUDGET * 1.1
+    eng = object.__new__(M.IntmcpEngine)
+    eng.config, eng.capacities, eng.step_limit, eng.A, eng.num_pairs = cfg, caps, 50, 5, 1
+    eng.nesting_level = 3
+    L = min(cfg.depth_limit, 50) + 1
+    target = cfg.num_particles + cfg.extra_particles
+    reserve = 2 * (int(-(-cfg.reinvigoration_sample_limit_factor * target // 1)) + target) \
+        + 2 * target + 8
+    counts = np.zeros((1, 4, 3), dtype=np.int32)
+    counts[0, 3, 1] = 2000     # the level-0 tree's log is the fullest
+    eng.tree_counts = lambda: counts
+    assert eng.headroom() == (caps.max_log - 2000 - reserve) // L

@@ -77,7 +77,8 @@ def test_oracle_matches_reference_goldens(case):
                                   "intmcp_pe", "intmcp0_ucb", "intmcp0_ego1_uniform",
                                   "intmcp0_deep", "intmcp0_pe", "intmcp_sp_ucb",
                                   "intmcp0_sp_ego1", "intmcp_sp_pe", "intmcp2_ucb",
-                                  "intmcp2_ego1_uniform", "intmcp2_pe", "intmcp2_sp_ucb"])
+                                  "intmcp2_ego1_uniform", "intmcp2_pe", "intmcp2_sp_ucb",
+                                  "intmcp3_ucb", "intmcp3_pe"])
 def test_intmcp_oracle_matches_reference_goldens(case):
     """I-NTMCP nesting 1 (BASELINE config 5) and nesting 0: the oracle
     restatement against the real reference planner's records (root children,
