@@ -220,6 +220,10 @@ def parse():
                     help="each timed step = search + the environment's answer + update() "
                          "(re-root, extraction, reinvigoration, subtree compaction) instead of a "
                          "restore() + search (single GPU)")
+    ap.add_argument("--defer", default="auto", choices=["auto", "on", "off"],
+                    help="cut-off children deferred to the re-root (pomcp_set_defer_cutoff): "
+                         "auto = the planners' own choice (search-only step: on; "
+                         "--update-step: the POMCP drop-in's)")
     ap.add_argument("--no-sub", action="store_true",
                     help="skip the secondary-configuration records (`sub`) the default run "
                          "appends after the headline (profiling runs)")
@@ -900,7 +904,8 @@ def main():
     r = run_pomcp(dev, env=args.env, B=B, S=S, K=K, base_cfg=base_cfg, tm=tm, steps=args.steps,
                   warmup=args.warmup, seed=args.seed, max_blocks=args.max_blocks, world=world,
                   rank=rank, dist=dist if world > 1 else None, clocks=True,
-                  update_step=args.update_step)
+                  update_step=args.update_step,
+                  defer=None if args.defer == "auto" else args.defer == "on")
     caps = r["caps"]
     out = {
         "metric": (f"MCTS simulations/sec on {args.env} (POTMMCP exact search, fixed-distribution "

@@ -216,6 +216,19 @@ def test_wall_clock_nesting2_episode():
     print("I-NTMCP nesting-2 wall-clock sims per step:", [st["num_sims"] for st in steps])
 
 
+def test_wall_clock_nesting3_episode():
+    """Nesting level 3 in the reference's default mode: the time limit split
+    over four levels, within the headroom of all four trees, no arena failure."""
+    trace, steps, ceiling = _wall_clock_episode(0.8, 47, 6, nesting_level=3)
+    assert len(steps) >= 2
+    for st in steps:
+        assert not st.get("arena_full")
+        assert 0.7 <= st["search_time"] < 3.0
+        assert 4 <= st["num_sims"] <= 4 * ceiling
+        assert 0 < st["child_visits"] <= st["visits"]
+    print("I-NTMCP nesting-3 wall-clock sims per step:", [st["num_sims"] for st in steps])
+
+
 def test_wall_clock_small_arena_stops_early(monkeypatch):
     """A 64 K-node arena (the floor) cannot hold a 1 s episode: the chunk loop
     stops at the headroom (step_statistics["arena_full"]) instead of failing,
@@ -333,6 +346,62 @@ def test_gpu_intmcp_nesting2_batched_pairs_match_oracle(env, ego):
         assert len(got[b]) == len(exp), b
         for t, (g, e) in enumerate(zip(got[b], exp)):
             assert g == e, f"{env} pair {b} step {t}"
+
+
+@pytest.mark.parametrize("env,ego", [("Driving-v1", "1"), ("PursuitEvasion-v1", "0")])
+def test_gpu_intmcp_nesting3_batched_pairs_match_oracle(env, ego):
+    """Nesting level 3 (four trees per pair, two middle belief tables), many
+    planners in one launch: every planner's records against the oracle
+    (pinned at nesting 3 by the intmcp3_* goldens) with that planner's tree key."""
+    from gpu_util import batched_intmcp_episodes
+    from oracle.run import oracle_intmcp_episode
+    B, sims, steps = 4, 20, 5
+    seeds = [450 + b for b in range(B)]
+    got = batched_intmcp_episodes(TEST_CFG, sims, seeds, steps, env=env, ego=ego,
+                                  nesting_level=3)
+    for b in range(B):
+        _, exp = oracle_intmcp_episode(TEST_CFG, sims, seeds[b], ego=ego, tree=b,
+                                       max_steps=steps, env=env, nesting_level=3)
+        assert len(got[b]) == len(exp), b
+        for t, (g, e) in enumerate(zip(got[b], exp)):
+            assert g == e, f"{env} pair {b} step {t}"
+
+
+def test_intmcp_nesting3_search_level_chunks_equal_one_search():
+    """Nesting level 3: chunks per level (intmcp_search_level) equal one launch
+    of all four levels, record for record (every tree, both middle tables)."""
+    import numpy as np
+    from gpu_util import intmcp_state_record, product_config, product_model
+    from posggym_baselines_amd import _native as N
+    from posggym_baselines_amd.planning.intmcp import BatchedINTMCP
+    model = product_model("Driving-v1")
+    cfg = product_config(TEST_CFG, 20)
+    one = BatchedINTMCP(model, "0", cfg, 3, 20, searches=3, nesting_level=3)
+    split = BatchedINTMCP(model, "0", cfg, 3, 20, searches=3, nesting_level=3)
+    keys = one.init_synthetic(600)
+    split.init_synthetic(600)
+    for step in range(2):
+        a1 = one.search()
+        e = split.engine
+        e.search_level(0, 9, N.INTMCP_BEGIN)
+        e.search_level(0, 11, 0)
+        e.search_level(1, 20, 0)
+        e.search_level(2, 20, 0)
+        e.search_level(3, 5, 0)
+        a2 = e.search_level(3, 15, N.INTMCP_FINAL, fetch=True)
+        assert np.array_equal(a1, a2), step
+        for b in range(3):
+            assert e.root_stats()[b].num_sims == 80
+            r1 = intmcp_state_record(one.engine, b, True, int(a1[b]))
+            r2 = intmcp_state_record(e, b, True, int(a2[b]))
+            assert r1 == r2 and "nested3_digest" in r1, (step, b)
+        acts = np.asarray(a1, dtype=np.int32)
+        one.engine.update(acts, keys)
+        e.update(acts, keys)
+    with pytest.raises(Exception):
+        e.mid_support(0, 3)   # the level-0 tree is not a middle tree
+    one.close()
+    split.close()
 
 
 def test_intmcp_nesting2_search_level_chunks_equal_one_search():
