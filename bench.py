@@ -222,8 +222,7 @@ def parse():
                          "restore() + search (single GPU)")
     ap.add_argument("--defer", default="auto", choices=["auto", "on", "off"],
                     help="cut-off children deferred to the re-root (pomcp_set_defer_cutoff): "
-                         "auto = the planners' own choice (search-only step: on; "
-                         "--update-step: the POMCP drop-in's)")
+                         "auto = the planners' default (on)")
     ap.add_argument("--no-sub", action="store_true",
                     help="skip the secondary-configuration records (`sub`) the default run "
                          "appends after the headline (profiling runs)")
@@ -566,10 +565,10 @@ def run_pomcp(dev, *, env, B, S, K, base_cfg, tm, steps, warmup, seed=0, max_blo
         caps = plan_capacities(cfg, step_limit, S, 1, reroot=False, max_blocks=mb,
                                overflow_slots=1024)
     stream = torch.cuda.Stream(device=dev)
-    # an update()-inclusive step re-roots after every search: the episode
-    # planners' eager cut-off lookup (POMCP drop-in; pomcp_set_defer_cutoff);
-    # a search-only step (restore) re-searches the same roots: deferred records
-    defer = (not update_step) if defer is None else bool(defer)
+    # cut-off children deferred to the re-root (the planners' default, the
+    # POMCP drop-in's included: pomcp_set_defer_cutoff); defer=False: the eager
+    # lookup (a sub record)
+    defer = True if defer is None else bool(defer)
     bp = BatchedPOMCP(model, "0", cfg, B, S, capacities=caps, stream=stream.cuda_stream,
                       defer_cutoff=defer,
                       device=dev, type_policies=type_policies(model) if tm else None)
@@ -730,7 +729,7 @@ def sub_records(dev, seed):
     region) and 5, each with a few timed steps; a failure is recorded, never
     fatal to the headline line."""
     jobs = [
-        ("C2 headline workload, eager cut-off lookup (the POMCP drop-in's mode)",
+        ("C2 headline workload, eager cut-off lookup (pomcp_set_defer_cutoff(0))",
          lambda: run_pomcp(dev, env="Driving-v1", B=65536, S=65536, K=1, base_cfg=TEST_CFG,
                            tm=False, steps=3, warmup=1, seed=seed, defer=False)),
         ("C2 exact single tree (1 x 65536 sims)",

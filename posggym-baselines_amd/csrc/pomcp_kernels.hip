@@ -887,13 +887,19 @@ __device__ __forceinline__ uint64_t ld_agent_u64(const uint64_t* p) {
 // absorbing flag follow from the record's state (Env::obs_key, Env::done_of);
 // it is found among the action node's inline slots or inserted there
 // (compare-and-swap: the threads insert concurrently), else in the overflow
-// map (the pass's such records one at a time, by wave 0), and its absorbing
+// map (a chunk's such records one at a time, by wave 0), and its absorbing
 // flag is that of its LAST arrival (mcts.py:370; records in log order).  Which
 // slot a child takes is a label (ActionNode.children is only ever looked up by
 // observation in the reference), so results are unchanged.  A pass reads
-// 64 kLogWaves consecutive records, one per thread; all of them are loaded
-// before any is stored, and a kept record goes to a place at or before its
-// own, so the log is filtered in place.
+// kLogRecs x 64 kLogWaves consecutive records; all of them are loaded before
+// any is stored, and a kept record goes to a place at or before its own, so
+// the log is filtered in place.  Deferred records are kept and stored like
+// the others but materialised in bulk: each pass appends them (log order) to
+// a workgroup queue in LDS, and when the queue is full (and at the end) its
+// records are materialised T at a time -- full chunks instead of a barrier-
+// heavy block per sub-pass with ~1 in 8 threads active -- and only their id
+// words are rewritten in place (the place stays reserved: nothing reads
+// below the pass's read frontier).
 // Section timing of k_compact_log (diagnostics builds, -DPB_CLOG_TIMING): thread
 // 0's s_memtime deltas per section and per-workgroup counters into
 // p.timing[search wave][16] (tools/clog_timing.py).
@@ -937,7 +943,14 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
   __shared__ int32_t ovq[T];        // threads whose child goes to the overflow map, in order
   __shared__ int32_t ovres[T];      // per thread: its overflow entry (-1: map full)
   __shared__ uint32_t ovd[5][T];    // per thread: tree lane, action node, key lo / hi, done
-  __shared__ uint64_t fpl[T];       // the pass's children (flag word addresses), thread order
+  // a chunk's children (flag word addresses), hashed: the last thread naming
+  // each and its number of arrivals
+  constexpr int kH = 2 * T;
+  __shared__ unsigned long long hk[kH];
+  __shared__ int32_t hl[kH], hc[kH];
+  constexpr int kQ = kLogRecs * T;  // deferred-record queue: a pass's records always fit
+  __shared__ uint32_t q_at[kQ], q_nani[kQ], q_klo[kQ], q_khi[kQ], q_ld[kQ];   // place, action
+                                    // node, obs key, tree lane | done << 8
 #ifdef PB_CLOG_TIMING
   uint64_t clt[6] = {0, 0, 0, 0, 0, 0};
   uint64_t cl_last = __builtin_amdgcn_s_memtime();
@@ -975,12 +988,21 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
   constexpr int R = kLogRecs;
   const uint64_t below = (1ull << lane) - 1ull;
   __shared__ int32_t ksum[R][kLogWaves];   // kept records per sub-pass and wave
+  __shared__ int32_t msum[R][kLogWaves];   // deferred records to materialise, likewise
   // A deferred record's child, found or inserted (inline slots by CAS, else the
-  // overflow map in log order) and its absorbing flag set by the last arrival
-  // of the sub-pass; every thread calls it (workgroup barriers inside)
+  // overflow map in log order), its absorbing flag set by the last arrival of
+  // the chunk and its visits raised by the chunk's arrivals (one atomic per
+  // child); every thread calls it (workgroup barriers inside)
   auto mat_block = [&](bool mat, int tree, uint32_t l, uint32_t nani, uint64_t okey, int done,
-                       int32_t& nid, int32_t*& vis, bool& keep) {
+                       int32_t& nid, bool& keep) {
+    hk[t] = 0ull;
+    hk[t + T] = 0ull;
+    hl[t] = -1;
+    hl[t + T] = -1;
+    hc[t] = 0;
+    hc[t + T] = 0;
     if (__syncthreads_or(mat ? 1 : 0)) {
+      int32_t* vis = nullptr;
       uint32_t* flagw = nullptr;   // the word holding the child's absorbing flag ...
       uint32_t fbit = 0u;          // ... and its bit
       bool need_ovf = false;
@@ -1124,26 +1146,58 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
         }
       }
       CL_MARK(2);
-      // the absorbing flag of each child = that of its last arrival: the pass's
-      // children in thread order; the last thread naming a child sets it
-      int nf = 0;
-      const uint64_t fp = reinterpret_cast<uint64_t>(flagw);
-      const int fpos = wg_rank(flagw != nullptr, &nf);
-      if (flagw != nullptr) fpl[fpos] = fp;
-      __syncthreads();
+      // the absorbing flag of each child = that of its last arrival (thread
+      // order = log order): the chunk's children in an LDS hash (open
+      // addressing on the flag word's address) holding the highest thread and
+      // the arrival count; that thread sets the flag and adds the visits
+      const unsigned long long fp = (unsigned long long)reinterpret_cast<uintptr_t>(flagw);
+      int h = 0;
       if (flagw != nullptr) {
-        bool last = true;
-        for (int x = fpos + 1; x < nf; ++x) last &= fpl[x] != fp;
-        if (last) {
-          if (done) atomicOr(flagw, fbit);
-          else atomicAnd(flagw, ~fbit);
+        uint32_t x = (uint32_t)(fp >> 2) ^ (uint32_t)(fp >> 34);
+        x *= 0x9E3779B1u;
+        h = (int)(x >> 23) & (kH - 1);   // (kH = 512: 9 bits)
+        for (;;) {
+          const unsigned long long old = atomicCAS(&hk[h], 0ull, fp);
+          if (old == 0ull || old == fp) break;
+          h = (h + 1) & (kH - 1);
         }
+        atomicMax(&hl[h], t);
+        atomicAdd(&hc[h], 1);
       }
-      wg_fence();   // the pass's inserts and flags land before the next pass's
+      __syncthreads();
+      if (flagw != nullptr && hl[h] == t) {
+        if (done) atomicOr(flagw, fbit);
+        else atomicAnd(flagw, ~fbit);
+        atomicAdd(vis, hc[h]);
+      }
+      wg_fence();   // the chunk's inserts, flags and visits land before the next chunk's
       CL_MARK(3);
       CL_CNT(3, flagw != nullptr);
     }
+    __syncthreads();   // (the hash is cleared by the next chunk)
   };
+  // materialise the queue's qn records (log order), T per chunk; each record's
+  // id word gets its child's id.  Every thread calls it.
+  auto flush = [&](int qn) {
+    for (int c = 0; c < qn; c += T) {
+      const int e = c + t;
+      const bool m = e < qn;
+      uint32_t at = 0u, nani = 0u, ld = 0u;
+      uint64_t ok = 0ull;
+      if (m) {
+        at = q_at[e];
+        nani = q_nani[e];
+        ok = ((uint64_t)q_khi[e] << 32) | q_klo[e];
+        ld = q_ld[e];
+      }
+      const uint32_t ll = ld & 0xFFu;
+      int32_t nid = -1;
+      bool keep = true;
+      mat_block(m, sw * kWave + (int)ll, ll, nani, ok, (int)(ld >> 8), nid, keep);
+      if (m && keep) wl.id[at] = (uint32_t)nid | (ll << kIdBits);   // (else the tree has failed: E_ARENA)
+    }
+  };
+  int qn = 0;   // queued deferred records (uniform over the workgroup)
   uint32_t out = 0;
   // a pass = kLogRecs sub-passes of T records (sub-pass j: record base + j T +
   // t), all loaded before any is stored, the next pass's loaded while this one
@@ -1179,7 +1233,6 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
     int done[R], tree[R];
     int32_t nid[R];
     int32_t* vis[R];   // the node's visits (zeroed by k_compact): + 1 per record
-    bool any_mat = false;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       const uint32_t i = base + (uint32_t)(j * T + t);
@@ -1222,53 +1275,71 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
           keep[j] = nid[j] >= 0 || mat[j];
         }
       }
-      any_mat |= mat[j];
       CL_CNT(0, i < n);
       CL_CNT(1, mat[j]);
     }
     CL_MARK(0);
-    // deferred records: the sub-passes in log order (cmap / ovf_new are
-    // k_compact's output: plain loads; slots and the overflow map change
-    // here: ld_agent)
-    if (__syncthreads_or(any_mat ? 1 : 0)) {
-#pragma unroll
-      for (int j = 0; j < R; ++j)
-        mat_block(mat[j], tree[j], l[j], nani[j], okey[j], done[j], nid[j], vis[j], keep[j]);
-    }
-    // visits, relabelling, per-tree counts, the pass's places
+    // visits, relabelling (a deferred record keeps its id until its child is
+    // materialised), per-tree counts, the pass's places
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       const uint32_t i = base + (uint32_t)(j * T + t);
       if (i < n && act[l[j]]) {
         if (vis[j] != nullptr) atomicAdd(vis[j], 1);
-        if (keep[j]) r[j].id = (uint32_t)nid[j] | (l[j] << kIdBits);
+        if (keep[j] && !mat[j]) r[j].id = (uint32_t)nid[j] | (l[j] << kIdBits);
       }
       const uint64_t same = same_lane_mask(l[j], keep[j]);
       if (keep[j] && (same >> lane) == 1ull) atomicAdd(&kept[l[j]], __popcll(same));
     }
-    uint64_t mk[R];
+    uint64_t mk[R], mm[R];
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       mk[j] = __ballot(keep[j]);
-      if (lane == 0) ksum[j][w] = __popcll(mk[j]);
+      mm[j] = __ballot(mat[j]);
+      if (lane == 0) {
+        ksum[j][w] = __popcll(mk[j]);
+        msum[j][w] = __popcll(mm[j]);
+      }
     }
     __syncthreads();
-    int tot = 0;
+    int mtot = 0;
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+#pragma unroll
+      for (int v = 0; v < kLogWaves; ++v) mtot += msum[j][v];
+    CL_MARK(4);
+    if (qn + mtot > kQ) {   // (uniform) materialise the queue first
+      flush(qn);
+      qn = 0;
+    }
+    int tot = 0, mt = qn;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-      int pre = 0, tj = 0;
+      int pre = 0, tj = 0, mpre = 0, mj = 0;
 #pragma unroll
       for (int v = 0; v < kLogWaves; ++v) {
         pre += v < w ? ksum[j][v] : 0;
         tj += ksum[j][v];
+        mpre += v < w ? msum[j][v] : 0;
+        mj += msum[j][v];
       }
       if (keep[j]) {
         const uint32_t at = out + (uint32_t)(tot + pre + __popcll(mk[j] & below));
         wl.store(at, r[j]);
         if (p.tm) wl.aux[at] = aux[j];
+        if (mat[j]) {
+          const int e = mt + mpre + __popcll(mm[j] & below);
+          q_at[e] = at;
+          q_nani[e] = nani[j];
+          q_klo[e] = (uint32_t)okey[j];
+          q_khi[e] = (uint32_t)(okey[j] >> 32);
+          q_ld[e] = l[j] | ((uint32_t)done[j] << 8);
+        }
       }
       tot += tj;
+      mt += mj;
     }
+    qn += mtot;
     out += (uint32_t)tot;
     __syncthreads();   // (ksum is rewritten by the next pass)
 #pragma unroll
@@ -1276,6 +1347,7 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
     CL_MARK(4);
   }
   __syncthreads();
+  if (qn > 0) flush(qn);
 #ifdef PB_CLOG_TIMING
   if (t == 0 && p.timing != nullptr) {
     for (int q = 0; q < 5; ++q) p.timing[sw * 16 + q] = clt[q];

@@ -325,9 +325,10 @@ class PomcpEngine:
         self._check(self._lib.pomcp_set_search_kernel(self._ctx, k), "set_search_kernel")
 
     def set_defer_cutoff(self, on):
-        """Defer cut-off children to the re-root (True, the default: batched search
-        throughput) or look them up during the search (False: one search per
-        re-root, the episode planners); same results (``pomcp_set_defer_cutoff``).
+        """Defer cut-off children to the re-root (True, the default: the search
+        skips their slot lines and the re-root materialises the survivors in
+        bulk) or look them up during the search (False); same results
+        (``pomcp_set_defer_cutoff``).
         A process-wide POMCP_DEFER_CUTOFF override (tests) wins."""
         if getattr(self, "_defer_forced", False):
             return

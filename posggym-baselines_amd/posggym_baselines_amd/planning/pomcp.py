@@ -111,10 +111,10 @@ class POMCP:
         self._engine = PomcpEngine(model, agent_id, config, num_trees=self._K,
                                    num_sims=per, tree_key_base=self._rank * self._K,
                                    wall_clock=per is None, type_policies=type_policies)
-        # an episode planner re-roots after every search: look cut-off children
-        # up during the search rather than materialising them at every re-root
-        # (pomcp_set_defer_cutoff; same results, DESIGN.md §4 "Deferred records")
-        self._engine.set_defer_cutoff(False)
+        # cut-off children are deferred to the re-root (the engine's default):
+        # with their bulk materialisation in k_compact_log that is the faster
+        # mode for an episode planner too (pomcp_set_defer_cutoff; same results,
+        # DESIGN.md §4 "Deferred records")
         self.step_limit = self._engine.step_limit
         self._logger = logging.getLogger()
         self._last_action = None
@@ -324,9 +324,9 @@ class BatchedPOMCP:
                  *, searches: int = 1, reroot: bool = False, capacities=None, stream=None,
                  tree_key_base: int = 0, device: Optional[int] = None, type_policies=None,
                  defer_cutoff: bool = True):
-        """defer_cutoff: defer cut-off children to the re-root (the default: the
-        trees are searched several times per re-root, e.g. restore()); False
-        when every search is followed by an update (``pomcp_set_defer_cutoff``)."""
+        """defer_cutoff: defer cut-off children to the re-root (the default, the
+        faster mode with or without an update after every search) or look them
+        up during the search (False); same results (``pomcp_set_defer_cutoff``)."""
         from posggym_baselines_amd.planning.engine import plan_capacities
         if capacities is None:
             step_limit = config.step_limit or model.spec.max_episode_steps

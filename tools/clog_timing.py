@@ -62,7 +62,7 @@ def main():
         print(f"  {n:28s} {per[:, i].mean() / 1e5:9.2f} ms  {100 * per[:, i].sum() / tot.sum():5.1f}%")
     for i, n in enumerate(COUNTERS):
         print(f"  {n:28s} {per[:, 8 + i].mean():14.0f}")
-    passes = per[:, 8].mean() / 256
+    passes = per[:, 8].mean() / 1024   # kLogRecs x 256 records per pass
     print(f"  passes {passes:.0f}, ticks per pass {tot.mean() / passes:.0f}")
     bp.close()
     torch.cuda.synchronize()
