@@ -396,6 +396,19 @@ struct ImPair {
     for (int q = 0; q < kNA; ++q) v.sh[q] = make_uint4(w[4 + 3 * q], 0u, w[5 + 3 * q], w[6 + 3 * q]);
     return v;
   }
+  // the node alone (one load): a child at which the descent stops -- its
+  // statistics heads would only serve a next level's selection
+  __device__ __forceinline__ View view_node(int k, int n) const {
+    const uint4 u = *reinterpret_cast<const uint4*>(nb[k] + (int64_t)n * ns);
+    View v;
+    v.x.parent = (int32_t)u.x;
+    v.x.info = u.y;
+    v.x.visits = (int32_t)u.z;
+    v.x.t = (int32_t)u.w;
+#pragma unroll
+    for (int q = 0; q < kNA; ++q) v.sh[q] = make_uint4(0, 0, 0, 0);
+    return v;
+  }
   // a node just created (INode x, zero statistics): its view without a load
   __device__ __forceinline__ static View fresh_view(const INode& x) {
     View v;
@@ -1002,18 +1015,23 @@ struct ImPair {
       // level 1, the other agent's history extension likewise.  (Loads are
       // issued before the stores of a creation: a wait for a load also waits
       // for every store issued before it.)
+      // whether the descent goes on below the child (the loop's own test at
+      // the next level: the child's t is x.t + 1): if not, the child's heads
+      // and the other agent's next history view are never read -- load only
+      // the child's INode (its visits / flags are updated below)
+      const bool more = !done && depth + 1 <= p.depth_limit && x.t + depth + 2 <= p.step_limit;
       bool created;
       INode cx;
       const int c = child_rec(k, n, a, okey, ra, &created, x.t, &cx, false);
       if (c < 0) return depth;
       View cv;
-      if (!created) cv = view(k, c);
+      if (!created) cv = more ? view(k, c) : view_node(k, c);
       if (k < kBot) {
         bool ncr;
         INode nx;
         const int cn = child_rec(k + 1, (int)nested, ao, ok, rn, &ncr, nested_k ? nv.x.t : -1, &nx);
         nn = cn < 0 ? 0u : (uint32_t)cn;
-        if (nested_k) {   // the next level's other-agent view (no wait)
+        if (nested_k && more) {   // the next level's other-agent view (no wait)
           nv = ncr ? fresh_view(nx) : view(k + 1, (int)nn);
           have_nv = true;
         }
