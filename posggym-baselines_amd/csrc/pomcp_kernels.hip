@@ -949,8 +949,8 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
   __shared__ unsigned long long hk[kH];
   __shared__ int32_t hl[kH], hc[kH];
   constexpr int kQ = kLogRecs * T;  // deferred-record queue: a pass's records always fit
-  __shared__ uint32_t q_at[kQ], q_nani[kQ], q_klo[kQ], q_khi[kQ], q_ld[kQ];   // place, action
-                                    // node, obs key, tree lane | done << 8
+  __shared__ uint32_t q_at[kQ], q_nani[kQ], q_v0[kQ], q_v1[kQ], q_l[kQ];   // place, action
+                                    // node, state (the key and done follow), tree lane
 #ifdef PB_CLOG_TIMING
   uint64_t clt[6] = {0, 0, 0, 0, 0, 0};
   uint64_t cl_last = __builtin_amdgcn_s_memtime();
@@ -1182,18 +1182,20 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
     for (int c = 0; c < qn; c += T) {
       const int e = c + t;
       const bool m = e < qn;
-      uint32_t at = 0u, nani = 0u, ld = 0u;
+      uint32_t at = 0u, nani = 0u, ll = 0u;
       uint64_t ok = 0ull;
-      if (m) {
+      int dn = 0;
+      if (m) {   // the child's observation key and absorbing flag from the record's state
         at = q_at[e];
         nani = q_nani[e];
-        ok = ((uint64_t)q_khi[e] << 32) | q_klo[e];
-        ld = q_ld[e];
+        ll = q_l[e];
+        const uint32_t v0 = q_v0[e], v1 = q_v1[e];
+        ok = Env::obs_key(sm, p.ego, v0, v1);
+        dn = Env::done_of(p.ego, v0, v1);
       }
-      const uint32_t ll = ld & 0xFFu;
       int32_t nid = -1;
       bool keep = true;
-      mat_block(m, sw * kWave + (int)ll, ll, nani, ok, (int)(ld >> 8), nid, keep);
+      mat_block(m, sw * kWave + (int)ll, ll, nani, ok, dn, nid, keep);
       if (m && keep) wl.id[at] = (uint32_t)nid | (ll << kIdBits);   // (else the tree has failed: E_ARENA)
     }
   };
@@ -1229,8 +1231,7 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
     }
     bool keep[R], mat[R];
     uint32_t l[R], nani[R];
-    uint64_t okey[R];
-    int done[R], tree[R];
+    int tree[R];
     int32_t nid[R];
     int32_t* vis[R];   // the node's visits (zeroed by k_compact): + 1 per record
 #pragma unroll
@@ -1240,8 +1241,6 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
       mat[j] = false;
       l[j] = 0u;
       nani[j] = 0u;
-      okey[j] = 0ull;
-      done[j] = 0;
       nid[j] = -1;
       vis[j] = nullptr;
       tree[j] = sw * kWave + (int)((i < n ? r[j].id : 0u) >> kIdBits);
@@ -1255,9 +1254,7 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
             const int nb = p.cmap[(int64_t)tree[j] * p.Nb + (int)(ani / A)];
             if (nb >= 0) {
               mat[j] = true;
-              nani[j] = (uint32_t)nb * A + ani % A;
-              okey[j] = Env::obs_key(sm, p.ego, r[j].v0, r[j].v1);
-              done[j] = Env::done_of(p.ego, r[j].v0, r[j].v1);
+              nani[j] = (uint32_t)nb * A + ani % A;   // (key and done: at the flush, dense)
             }
           } else if (id >= p.ovf_base) {
             nid[j] = p.ovf_new[(int64_t)tree[j] * p.H + (id - p.ovf_base)];
@@ -1331,9 +1328,9 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
           const int e = mt + mpre + __popcll(mm[j] & below);
           q_at[e] = at;
           q_nani[e] = nani[j];
-          q_klo[e] = (uint32_t)okey[j];
-          q_khi[e] = (uint32_t)(okey[j] >> 32);
-          q_ld[e] = l[j] | ((uint32_t)done[j] << 8);
+          q_v0[e] = r[j].v0;
+          q_v1[e] = r[j].v1;
+          q_l[e] = l[j];
         }
       }
       tot += tj;
