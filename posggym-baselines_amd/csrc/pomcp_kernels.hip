@@ -401,7 +401,10 @@ __global__ __launch_bounds__(256) void k_reroot_child(DevParams p) {
 // at 65,536 trees x 65,536 simulations: one dependent round trip per 64
 // records.)
 constexpr int kLogWaves = 4;
-constexpr int kLogRecs = 4;   // records per thread per pass
+#ifndef PB_LOG_RECS   // A/B builds only
+#define PB_LOG_RECS 4
+#endif
+constexpr int kLogRecs = PB_LOG_RECS;   // records per thread per pass
 
 // The lanes whose 6-bit key equals this lane's, among the active ones (a
 // match-any on the tree lane of a log record: 6 ballots).
