@@ -56,10 +56,10 @@ def main():
     assert fn(bp.engine._ctx, buf.ctypes.data_as(C.POINTER(C.c_uint64)), cnt.value, C.byref(cnt)) == 0
     per = buf.reshape(-1, 16).astype(np.float64)
     per = per[per[:, 8] > 0]
-    print(f"workgroups {len(per)}; per workgroup (mean, s_memtime ticks = 100 MHz):")
+    print(f"workgroups {len(per)}; per workgroup (mean, s_memtime = shader clock cycles on gfx950):")
     tot = per[:, :5].sum(1)
     for i, n in enumerate(SECTIONS):
-        print(f"  {n:28s} {per[:, i].mean() / 1e5:9.2f} ms  {100 * per[:, i].sum() / tot.sum():5.1f}%")
+        print(f"  {n:28s} {per[:, i].mean() / 1e6:9.2f} Mcycles  {100 * per[:, i].sum() / tot.sum():5.1f}%")
     for i, n in enumerate(COUNTERS):
         print(f"  {n:28s} {per[:, 8 + i].mean():14.0f}")
     passes = per[:, 8].mean() / 1024   # kLogRecs x 256 records per pass
