@@ -705,7 +705,7 @@ struct ImPair {
         const double lo = h.mm_min[k], hi = h.mm_max[k];
         const bool nz = hi > lo;
         const double rr = nz ? rcp_nr(hi - lo) : 1.0;
-        const double csl = p.c * sqrt(log_n);
+        const double csl = p.c * sqrt_fast(log_n);
         double sf[kImMaxA], mg[kImMaxA];
         int bi = 0;
         double bf = -__builtin_inf(), bm = 0.0;

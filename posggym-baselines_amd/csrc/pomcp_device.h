@@ -290,21 +290,38 @@ __device__ __forceinline__ double uni_d(double v) {
 }
 
 // 1 / x and 1 / sqrt(x) in FP64: the hardware estimates (v_rcp_f64 /
-// v_rsq_f64, relative error ~2^-23) refined by two Newton steps each, to a few
-// ulp (the fast UCB scores of k_search, select_action: their error bound
-// decides when the exact scores are needed).
+// v_rsq_f64, relative error ~2^-24) refined by one Newton step each: relative
+// error <= 5e-15 measured on every visit count below 2^20 and random doubles
+// (tools/recip_err.py, test_fast_ucb_reciprocals_error_bound), far inside the
+// fast UCB scores' 1e-12 fallback margin (select_action: the exact scores
+// decide near-ties).  A second step (round 4) measured -0.3% (r5n).
+#ifndef PB_NR_STEPS   // A/B builds: Newton steps of the fast reciprocals
+#define PB_NR_STEPS 1
+#endif
 __device__ __forceinline__ double rcp_nr(double x) {
   double y = __builtin_amdgcn_rcp(x);
-  double e = __builtin_fma(-x, y, 1.0);
-  y = __builtin_fma(y, e, y);
-  e = __builtin_fma(-x, y, 1.0);
-  return __builtin_fma(y, e, y);
+#pragma unroll
+  for (int i = 0; i < PB_NR_STEPS; ++i) {
+    const double e = __builtin_fma(-x, y, 1.0);
+    y = __builtin_fma(y, e, y);
+  }
+  return y;
 }
 __device__ __forceinline__ double rsq_nr(double x) {
   double y = __builtin_amdgcn_rsq(x);
   const double hx = 0.5 * x;
-  y = y * __builtin_fma(-hx, y * y, 1.5);
-  return y * __builtin_fma(-hx, y * y, 1.5);
+#pragma unroll
+  for (int i = 0; i < PB_NR_STEPS; ++i) y = y * __builtin_fma(-hx, y * y, 1.5);
+  return y;
+}
+// sqrt(x) for a fast score (x >= 0): the IEEE square root (PB_FAST_SQRT A/B
+// builds: x rsq_nr(x), measured +-0%)
+__device__ __forceinline__ double sqrt_fast(double x) {
+#ifdef PB_FAST_SQRT
+  return x > 0.0 ? x * rsq_nr(x) : 0.0;
+#else
+  return __builtin_sqrt(x);
+#endif
 }
 
 __device__ __forceinline__ uint32_t spread16(uint32_t x) {

@@ -391,7 +391,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
 #else
         // Fast scores: (v - min) * rcp(range) + c sqrt(log N) rsq(n), each
         // within a few ulp of the reference's (v - min) / range + c
-        // sqrt(log N / n) (rcp_nr / rsq_nr: |fast - exact| < 4e-15 (|q| + e)).
+        // sqrt(log N / n) (rcp_nr / rsq_nr: |fast - exact| < ~1e-14 (|q| + e)).
         // When the leader beats every action with different statistics by
         // more than 1e-12 of their magnitudes, the reference's strict '>'
         // scan picks the same action; otherwise (~6e-4 of selections, mostly
@@ -400,7 +400,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         // first of them wins in both).
         {
           const double rr = nz ? rcp_nr(range) : 1.0;
-          const double csl = p.c * sqrt(log_n);
+          const double csl = p.c * sqrt_fast(log_n);
           double sf[A], mg[A];
 #pragma unroll
           for (int q = 0; q < A; ++q) {
