@@ -949,6 +949,7 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
   // a chunk's children (flag word addresses), hashed: the last thread naming
   // each and its number of arrivals
   constexpr int kH = 2 * T;
+  static_assert(kH == 512, "the hash takes 9 bits (mat_block)");
   __shared__ unsigned long long hk[kH];
   __shared__ int32_t hl[kH], hc[kH];
   constexpr int kQ = kLogRecs * T;  // deferred-record queue: a pass's records always fit
