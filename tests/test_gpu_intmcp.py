@@ -316,6 +316,28 @@ def test_gpu_intmcp_nesting0_batched_pairs_match_oracle(env, ego):
             assert g == e, f"{env} pair {b} step {t}"
 
 
+@pytest.mark.parametrize("nesting", [1, 2])
+def test_gpu_intmcp_step_limit_cutoffs_match_oracle(nesting):
+    """A planner step limit well below the depth limit (step_limit=6, epsilon
+    0.05: depth_limit 59): the descent stops at obs_node.t + depth >
+    step_limit (intmcp.py:450-453), at a depth that shrinks every step -- the
+    level at which k_im_search loads only the child's node (no statistics
+    heads, no next history view) is then decided by the step limit.  5 pairs
+    x 6 steps against the oracle."""
+    from gpu_util import batched_intmcp_episodes
+    from oracle.run import oracle_intmcp_episode
+    cfg = dict(TEST_CFG, step_limit=6, epsilon=0.05)
+    B, sims, steps = 5, 24, 6
+    seeds = [700 + b for b in range(B)]
+    got = batched_intmcp_episodes(cfg, sims, seeds, steps, nesting_level=nesting)
+    for b in range(B):
+        _, exp = oracle_intmcp_episode(cfg, sims, seeds[b], tree=b, max_steps=steps,
+                                       nesting_level=nesting)
+        assert len(got[b]) == len(exp), b
+        for t, (g, e) in enumerate(zip(got[b], exp)):
+            assert g == e, f"nesting {nesting} pair {b} step {t}"
+
+
 def test_intmcp_nesting0_rejects_level1_simulations():
     import ctypes as C
     from gpu_util import product_config, product_model

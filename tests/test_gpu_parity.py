@@ -18,15 +18,15 @@ def search_kernel(request, monkeypatch):
     """Every parity test runs on every search kernel: k_search (a tree per lane,
     tree in HBM) with cut-off children deferred to the re-root ("lane") and
     looked up during the search ("lane_eager", pomcp_set_defer_cutoff) -- both
-    forced through POMCP_DEFER_CUTOFF, so they also hold for the POMCP episode
-    planners, which otherwise pick the eager lookup -- and
+    forced through POMCP_DEFER_CUTOFF, so they hold for every planner whatever
+    its own choice (the default: deferred) -- and
     k_search_lds (a wave per tree, tree in LDS) -- with its step-tree producer
     waves as the engine picks them ("wave"), forced on for any depth limit
     ("wave_tree") and off ("wave_plain"); they must give the same bits as the
     reference / oracle."""
     kind, _, mode = request.param.partition("_")
     monkeypatch.setenv("POMCP_SEARCH_KERNEL", kind)
-    if kind == "lane":   # the override wins over the episode planners' eager choice
+    if kind == "lane":   # the override wins over the planners' own choice
         monkeypatch.setenv("POMCP_DEFER_CUTOFF", "0" if mode == "eager" else "1")
     elif mode:
         monkeypatch.setenv("POMCP_STEP_TREE", "1" if mode == "tree" else "0")
@@ -270,6 +270,29 @@ def test_batched_episodes_reroot_across_waves():
             exp.append(recs)
         s += 1
     got = batched_episodes(TEST_CFG, S, seeds, K)
+    for b in range(len(seeds)):
+        assert got[b] == exp[b], f"tree {b} (env seed {seeds[b]})"
+
+
+def test_step_limit_cutoffs_in_batched_episodes():
+    """A planner step limit below the depth limit (MCTSConfig.step_limit=5,
+    depth_limit 90): the cut-offs come from t + 1 > step_limit (mcts.py:315),
+    deferred or looked up, at a depth that shrinks every step; 12 planners x 5
+    real steps (the reference asserts root.t <= step_limit, mcts.py:114) equal
+    the oracle, re-roots included."""
+    from gpu_util import batched_episodes
+    from oracle.run import oracle_episode
+    cfg = dict(TEST_CFG, step_limit=5, epsilon=0.01)
+    S, K = 128, 5
+    seeds, exp = [], []
+    s = 5200
+    while len(seeds) < 12:
+        trace, recs = oracle_episode(cfg, S, s, tree=len(seeds), max_steps=K)
+        if trace["len"] >= K and all(r["searched"] for r in recs):
+            seeds.append(s)
+            exp.append(recs)
+        s += 1
+    got = batched_episodes(cfg, S, seeds, K)
     for b in range(len(seeds)):
         assert got[b] == exp[b], f"tree {b} (env seed {seeds[b]})"
 
