@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round 5: the Driving step with the three candidate cells' distances loaded
+# with the plan (dpf) vs the in-tree library; parity of dpf.
+set -o pipefail
+O=gpurun_out/r5v; mkdir -p $O
+for v in cur dpf cur dpf cur dpf; do
+  lib=""; [ $v != cur ] && lib=$PWD/variants/lib_$v.so
+  echo "== $v" >> $O/ab.log
+  POMCP_LIB_PATH=$lib timeout -k 10 300 python bench.py --no-cpu-baseline --no-sub --steps 3 --warmup 1 >> $O/ab.log 2>&1 || { tail -20 $O/ab.log; exit 1; }
+done
+grep -E "^==|^\{" $O/ab.log | python3 -c "
+import sys,json
+for l in sys.stdin:
+    if l.startswith('=='): n=l.strip()
+    else:
+        d=json.loads(l); r=d['roofline']; print(n, round(d['value']/1e9,4), 'G', round(r['kernel_ms'],2), 'ms', round(r['frac'],4))"
+POMCP_LIB_PATH=$PWD/variants/lib_dpf.so timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_env_model.py -x -q -k "lane or golden or env" --timeout 300 --timeout-method thread > $O/parity.log 2>&1 || { echo "parity FAILED"; grep -E "FAILED|Error|assert" $O/parity.log | head -20; tail -30 $O/parity.log; exit 1; }
+echo "parity: $(tail -1 $O/parity.log)"
+echo done
