@@ -400,7 +400,14 @@ __global__ __launch_bounds__(256) void k_reroot_child(DevParams p) {
 // together and the next pass's while it runs.  (One wave per log took ~0.3 s
 // at 65,536 trees x 65,536 simulations: one dependent round trip per 64
 // records.)
-constexpr int kLogWaves = 4;
+// 16 waves (1,024 threads, one workgroup per CU: 150 KB of LDS in
+// k_compact_log): 4,096 records per pass; the update()-inclusive PursuitEvasion
+// step's update 142 -> 130 ms vs 4 waves, 237 ms with 2
+// (profiles/r5w_log_waves_ab.txt)
+#ifndef PB_LOG_WAVES   // A/B builds only
+#define PB_LOG_WAVES 16
+#endif
+constexpr int kLogWaves = PB_LOG_WAVES;
 #ifndef PB_LOG_RECS   // A/B builds only
 #define PB_LOG_RECS 4
 #endif
@@ -949,7 +956,8 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
   // a chunk's children (flag word addresses), hashed: the last thread naming
   // each and its number of arrivals
   constexpr int kH = 2 * T;
-  static_assert(kH == 512, "the hash takes 9 bits (mat_block)");
+  constexpr int kHBits = kH == 256 ? 8 : kH == 512 ? 9 : kH == 1024 ? 10 : kH == 2048 ? 11 : -1;
+  static_assert(kHBits > 0, "the hash takes log2(kH) bits (mat_block)");
   __shared__ unsigned long long hk[kH];
   __shared__ int32_t hl[kH], hc[kH];
   constexpr int kQ = kLogRecs * T;  // deferred-record queue: a pass's records always fit
@@ -1159,7 +1167,7 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
       if (flagw != nullptr) {
         uint32_t x = (uint32_t)(fp >> 2) ^ (uint32_t)(fp >> 34);
         x *= 0x9E3779B1u;
-        h = (int)(x >> 23) & (kH - 1);   // (kH = 512: 9 bits)
+        h = (int)(x >> (32 - kHBits)) & (kH - 1);
         for (;;) {
           const unsigned long long old = atomicCAS(&hk[h], 0ull, fp);
           if (old == 0ull || old == fp) break;
