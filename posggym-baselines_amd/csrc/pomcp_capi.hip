@@ -281,6 +281,7 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
   if (d.tm) ALLOC(tmt, TmTables, 1);
   ALLOC(wlog, uint32_t, search_waves((int)B));
   ALLOC(want, uint32_t, B);
+  ALLOC(want_info, int4, B);
   ALLOC(cnt, int32_t, B);
   ALLOC(belief, uint4, B * 2 * d.Nr);
   ALLOC(path, uint4, B * 3 * kMaxPath);
@@ -416,16 +417,12 @@ int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_key
                               hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(ctx, hipMemcpyAsync((void*)ctx->dp.in_obs, obs_keys, sizeof(uint64_t) * B,
                               hipMemcpyHostToDevice, ctx->stream));
-  // re-root: child lookup per tree, one ordered scan of each search wave's log,
-  // then the per-tree update (initial belief / re-root + reinvigoration)
+  // re-root: child lookup per tree; subtree compaction to the child's subtree
+  // (re-roots only: an initial update leaves an empty arena) with one ordered
+  // scan of each search wave's log that also extracts the child's particles;
+  // then the per-tree update (initial belief / new root + reinvigoration)
   PB_ENV_LAUNCH(ctx, k_reroot_child, dim3(grid_blocks(B)), dim3(256), ctx->dp);
   HIP_TRY(ctx, hipGetLastError());
-  hipLaunchKernelGGL(k_extract, dim3((unsigned)search_waves(B)), dim3(64 * kLogWaves), 0,
-                     ctx->stream, ctx->dp);
-  HIP_TRY(ctx, hipGetLastError());
-  PB_ENV_LAUNCH(ctx, k_update, dim3(grid_blocks(B)), dim3(256), ctx->dp);
-  HIP_TRY(ctx, hipGetLastError());
-  // subtree compaction (re-roots only: an initial update leaves an empty arena)
   bool reroot = false;
   for (int t = 0; t < B && !reroot; ++t) reroot = acts[t] >= 0;
   if (reroot) {
@@ -437,6 +434,8 @@ int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_key
                   ctx->dp);
     HIP_TRY(ctx, hipGetLastError());
   }
+  PB_ENV_LAUNCH(ctx, k_update, dim3(grid_blocks(B)), dim3(256), ctx->dp);
+  HIP_TRY(ctx, hipGetLastError());
   HIP_TRY(ctx, hipMemcpyAsync(ctx->host_upd.data(), ctx->dp.upd_out, sizeof(int32_t) * 2 * B,
                               hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));

@@ -67,7 +67,8 @@ __host__ __device__ constexpr int part_vt(int a) { return 2 + a; }   // {value, 
 // The log is shared by the 64 trees of a search wavefront (one tree per lane):
 // the lanes appending in one step write consecutive records, so one store
 // instruction writes whole lines instead of 64 scattered 12 B pieces.  A
-// tree's records keep their insertion order; k_extract separates them again.
+// tree's records keep their insertion order; the re-root (k_compact_log)
+// separates them again.
 constexpr int kIdBits = 26;                       // obs node ids < 2^26 (pomcp_create checks)
 constexpr uint32_t kIdMask = (1u << kIdBits) - 1u;
 // Deferred records (k_search): a simulation that reaches an obs node whose
@@ -227,6 +228,7 @@ struct DevParams {
                         // first use), appended to plog by k_log_merge
   uint32_t* wlog;       // [waves] records in each wave's log
   uint32_t* want;       // [B] re-root: log id of the child to extract (0xFFFFFFFF: none)
+  int4* want_info;      // [B] re-root: that child's {block, absorbing, code, found} (k_update)
   int32_t* cnt;         // [B] re-root: particles extracted into the new root belief
   uint4* belief;        // [B][2][Nr] {t, v0, v1, 0}
   uint4* path;          // [B][3 * kMaxPath] search path of the running simulation

@@ -367,7 +367,9 @@ __global__ __launch_bounds__(256) void k_reset(DevParams p) {
 }
 
 // Re-root, step 1 (MCTS._update, mcts.py:236-247): find or create the root's
-// child (action, obs) and publish its log id for k_extract.
+// child (action, obs) and publish its log id (the records k_compact_log
+// extracts into the new root belief) and its block / flags (k_compact's new
+// root, k_update's new root fields).
 template <class Env>
 __global__ __launch_bounds__(256) void k_reroot_child(DevParams p) {
   __shared__ typename Env::Model sm;
@@ -376,30 +378,31 @@ __global__ __launch_bounds__(256) void k_reroot_child(DevParams p) {
   if (tree >= p.B) return;
   Tree<Env> T(p, sm, tree);
   uint32_t want = 0xFFFFFFFFu;
+  int4 info = make_int4(-1, 0, 0, 0);
   if (T.err == 0 && !T.root_abs && T.root_t > 0) {
     const int action = uni(p.in_actions[tree]);
     if (T.root_blk >= 0 && action >= 0 && action < p.A) {
       uint4 q = T.load_block(T.root_blk);
       ChildRef c;
-      if (T.child_ref(q, T.root_blk, action, uni64(p.in_obs[tree]), false, T.root_abs, &c))
+      if (T.child_ref(q, T.root_blk, action, uni64(p.in_obs[tree]), false, T.root_abs, &c)) {
         want = c.id | ((uint32_t)(tree & (kWave - 1)) << kIdBits);
+        info = make_int4(c.blk, c.absorbing, c.code, 1);
+      }
     }
   }
   T.store_header();   // child_ref may have created the child (n_nodes)
-  if (T.lane == 0) p.want[tree] = want;
+  if (T.lane == 0) {
+    p.want[tree] = want;
+    p.want_info[tree] = info;
+  }
 }
 
-// Re-root, step 2: one WORKGROUP (kLogWaves waves) per SEARCH wave scans that
-// wave's shared log once, in order, and appends each record of a wanted child
-// to its tree's new root belief ({root_t + 1, v0, v1}), preserving insertion
-// order per tree.  A pass reads kLogRecs x 64 kLogWaves consecutive records
-// (sub-pass j: record base + j T + thread); a record's place is its tree's
-// count before the pass + the same tree's matches earlier in the pass
-// (earlier sub-passes, then earlier waves of its sub-pass) + its rank in its
-// wave (same_lane_mask: 6 ballots, no loop).  All of a pass's loads are issued
-// together and the next pass's while it runs.  (One wave per log took ~0.3 s
-// at 65,536 trees x 65,536 simulations: one dependent round trip per 64
-// records.)
+// Re-root, step 3 (k_compact_log below): one WORKGROUP (kLogWaves waves) per
+// SEARCH wave scans that wave's shared log once, in order.  A pass reads
+// kLogRecs x 64 kLogWaves consecutive records (sub-pass j: record base + j T +
+// thread); all of a pass's loads are issued together and the next pass's while
+// it runs.  (One wave per log took ~0.3 s at 65,536 trees x 65,536
+// simulations: one dependent round trip per 64 records.)
 // 16 waves (1,024 threads, one workgroup per CU: 150 KB of LDS in
 // k_compact_log): 4,096 records per pass; the update()-inclusive PursuitEvasion
 // step's update 142 -> 130 ms vs 4 waves, 237 ms with 2
@@ -424,98 +427,6 @@ __device__ __forceinline__ uint64_t same_lane_mask(uint32_t key, bool active) {
     m &= bit ? bb : ~bb;
   }
   return m;
-}
-
-__global__ __launch_bounds__(64 * kLogWaves) void k_extract(DevParams p) {
-  constexpr uint32_t T = kWave * kLogWaves;
-  constexpr int R = kLogRecs;
-  const int sw = blockIdx.x;   // search wave
-  const int lane = lane_id();
-  const int w = (int)(threadIdx.x >> 6);
-  const uint64_t below = (1ull << lane) - 1ull;
-  __shared__ uint32_t want[kWave];
-  __shared__ int32_t cnt[kWave];
-  __shared__ uint32_t tval[kWave];
-  __shared__ int64_t dst[kWave];
-  __shared__ int32_t wc[R][kLogWaves][kWave];   // this pass's matches per sub-pass, wave and tree
-  if (w == 0) {
-    const int tree = sw * kWave + lane;
-    const bool valid = tree < p.B;
-    const TreeHdr h = p.hdr[valid ? tree : 0];
-    want[lane] = valid ? p.want[tree] : 0xFFFFFFFFu;
-    cnt[lane] = 0;
-    tval[lane] = (uint32_t)h.root_t + 1u;
-    dst[lane] = ((int64_t)tree * 2 + (h.belief_sel ^ 1)) * p.Nr;
-  }
-  for (int q = (int)threadIdx.x; q < R * kLogWaves * kWave; q += (int)T) (&wc[0][0][0])[q] = 0;
-  __syncthreads();
-  const WaveLog wl(p.plog, p.Np, sw, p.tm);
-  const uint32_t n = p.wlog[sw];
-  LogRec rn[R];
-  uint32_t auxn[R];
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-    const uint32_t i = (uint32_t)j * T + threadIdx.x;
-    rn[j] = LogRec{0xFFFFFFFFu, 0u, 0u};
-    auxn[j] = 0u;   // type-based: the particle's other-agent policy
-    if (i < n) {
-      rn[j] = wl.load(i);
-      if (p.tm) auxn[j] = wl.aux[i];
-    }
-  }
-  for (uint32_t base = 0; base < n; base += (uint32_t)R * T) {
-    LogRec r[R];
-    uint32_t aux[R];
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      r[j] = rn[j];
-      aux[j] = auxn[j];
-      const uint32_t i2 = base + (uint32_t)(R + j) * T + threadIdx.x;   // the next pass
-      if (i2 < n) {
-        rn[j] = wl.load(i2);
-        if (p.tm) auxn[j] = wl.aux[i2];
-      }
-    }
-    bool m[R];
-    uint32_t l[R];
-    int rank[R];
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      const uint32_t i = base + (uint32_t)j * T + threadIdx.x;
-      l[j] = r[j].id >> kIdBits;
-      m[j] = i < n && want[l[j]] == r[j].id;
-      const uint64_t same = same_lane_mask(l[j], m[j]);
-      rank[j] = __popcll(same & below);
-      if (m[j] && (same >> lane) == 1ull) wc[j][w][l[j]] = __popcll(same);   // the tree's last lane
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      if (m[j]) {
-        const int lj = (int)l[j];
-        int pos = cnt[lj] + rank[j];
-        for (int jj = 0; jj < j; ++jj)
-          for (int v = 0; v < kLogWaves; ++v) pos += wc[jj][v][lj];
-        for (int v = 0; v < w; ++v) pos += wc[j][v][lj];
-        if (pos < p.Nr) p.belief[dst[lj] + pos] = make_uint4(tval[lj], r[j].v0, r[j].v1, aux[j]);
-      }
-    }
-    __syncthreads();
-    if (w == 0) {
-      int add = 0;
-#pragma unroll
-      for (int j = 0; j < R; ++j)
-#pragma unroll
-        for (int v = 0; v < kLogWaves; ++v) {
-          add += wc[j][v][lane];
-          wc[j][v][lane] = 0;
-        }
-      cnt[lane] += add;
-    }
-    __syncthreads();
-  }
-  const int tree = sw * kWave + lane;
-  if (w == 0 && tree < p.B) p.cnt[tree] = cnt[lane];
 }
 
 template <class Env>
@@ -565,14 +476,20 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
     } else {
       // _update (mcts.py:229-263)
       const int action = uni(p.in_actions[tree]);
-      if (T.root_blk < 0 || action < 0 || action >= p.A) {
+      // the child k_reroot_child found or created; the tree has been compacted
+      // to its subtree since (k_compact: its block is block 0)
+      const int4 wi = p.want_info[tree];
+      if (uni(wi.w) == 0) {
         T.err = POMCP_E_NOT_FOUND;
       } else {
-        uint4 q = T.load_block(T.root_blk);
         ChildRef c;
-        if (T.child_ref(q, T.root_blk, action, obs, false, T.root_abs, &c)) {
+        c.id = uniu(p.want[tree]) & kIdMask;
+        c.blk = uni(wi.x) >= 0 ? 0 : -1;
+        c.absorbing = uni(wi.y);
+        c.code = uni(wi.z);
+        {
           // the child's belief: its particles from the log in insertion order,
-          // already gathered into the other belief buffer by k_extract
+          // already gathered into the other belief buffer by k_compact_log
           uint4* nb = T.other_belief();
           int n = uni(p.cnt[tree]);
           // ObsNode.visits of the new root = its particle records (one per
@@ -708,19 +625,21 @@ __device__ __forceinline__ uint32_t ld_agent_u32(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One wave per tree: reachability from the new root, block move, overflow map
-// rebuild.  Runs after k_update for trees re-rooted without error.
+// One wave per tree: reachability from the new root (the child k_reroot_child
+// found), block move, overflow map rebuild.  Runs before k_update (which takes
+// its new root from the compacted tree) for trees re-rooted without error.
 __global__ __launch_bounds__(256) void k_compact(DevParams p) {
   const int tree = blockIdx.x * kTreesPerBlock + (threadIdx.x >> 6);
   if (tree >= p.B) return;
   const int lane = lane_id();
   TreeHdr h = p.hdr[tree];
-  const bool on = uni(h.error) == 0 && uni(h.root_t) >= 2;
+  const int4 wi = p.want_info[tree];
+  const bool on = uni(h.error) == 0 && uni(wi.w) != 0;
   if (lane == 0) p.cnt[tree] = on ? 1 : 0;   // read by k_compact_log
   if (!on) return;
   const int A = p.A;
   const int nb = uni(h.n_blocks);
-  const int R = uni(h.root_blk);
+  const int R = uni(wi.x);   // the new root's block (-1: a leaf)
   Line* const an = p.an + tree_base_lines(tree, p.Nb, p.lines);
   const int64_t bstride = blk_stride_lines(p.lines);
   int32_t* const cmap = p.cmap + (int64_t)tree * p.Nb;
@@ -888,10 +807,17 @@ __device__ __forceinline__ uint64_t ld_agent_u64(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One WORKGROUP (kLogWaves waves, as k_extract) per SEARCH wave: filter that
+// One WORKGROUP (kLogWaves waves) per SEARCH wave: filter that
 // wave's shared particle log to the records of obs nodes that survived
 // k_compact (insertion order kept) and relabel them; every tree's record count
-// is recounted.  A deferred record (pomcp_device.h: an arrival at a child
+// is recounted.  The same scan extracts the new root's records (the child
+// k_reroot_child found, by its old id) into the tree's other belief buffer as
+// {root_t + 1, v0, v1, aux}, in insertion order (mcts.py:248-252): a record's
+// place is its tree's count before the pass + the same tree's records in the
+// earlier sub-passes, then earlier waves of its sub-pass + its rank in its wave
+// (same_lane_mask); k_update takes the count as the new root's belief size and
+// visits.  (A separate extraction scan before k_update read the whole log once
+// more: 31 ms of the PursuitEvasion step's 130 ms update.)  A deferred record (pomcp_device.h: an arrival at a child
 // beyond the depth / step limits, never looked up by k_search) whose action
 // node survived gets its child here: the child's observation key and
 // absorbing flag follow from the record's state (Env::obs_key, Env::done_of);
@@ -947,6 +873,12 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
   const int t = (int)threadIdx.x;
   __shared__ int32_t kept[kWave];
   __shared__ int32_t act[kWave];
+  __shared__ uint32_t want[kWave];  // the new root's log id per tree (k_reroot_child) ...
+  __shared__ int32_t xcnt[kWave];   // ... its records extracted so far
+  __shared__ uint32_t tval[kWave];
+  __shared__ int64_t xdst[kWave];
+  __shared__ uint8_t xw[kLogRecs][kLogWaves][kWave];   // this pass's extracted records per
+                                                      // sub-pass, wave and tree (<= 64)
   __shared__ int32_t made[kWave];   // children materialised per tree
   __shared__ int32_t bad[kWave];    // overflow map full
   __shared__ int32_t wsum[kLogWaves];
@@ -975,6 +907,12 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
     made[lane] = 0;
     bad[lane] = 0;
     act[lane] = mytree < p.B ? p.cnt[mytree] : 0;
+    const bool valid = mytree < p.B;
+    const TreeHdr h = p.hdr[valid ? mytree : 0];
+    want[lane] = valid ? p.want[mytree] : 0xFFFFFFFFu;
+    xcnt[lane] = 0;
+    tval[lane] = (uint32_t)h.root_t + 1u;
+    xdst[lane] = ((int64_t)mytree * 2 + (h.belief_sel ^ 1)) * p.Nr;
   }
   __syncthreads();
   // a thread's place among the workgroup's threads with f set (thread order);
@@ -1241,16 +1179,18 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
         if (p.tm) auxn[j] = wl.aux[i2];
       }
     }
-    bool keep[R], mat[R];
+    bool keep[R], mat[R], ex[R];
     uint32_t l[R], nani[R];
     int tree[R];
     int32_t nid[R];
     int32_t* vis[R];   // the node's visits (zeroed by k_compact): + 1 per record
+    int xr[R];         // an extracted record's rank among its wave's of the same tree
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       const uint32_t i = base + (uint32_t)(j * T + t);
       keep[j] = false;
       mat[j] = false;
+      ex[j] = false;
       l[j] = 0u;
       nani[j] = 0u;
       nid[j] = -1;
@@ -1259,6 +1199,7 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
       if (i < n) {
         l[j] = r[j].id >> kIdBits;
         const uint32_t id = r[j].id & kIdMask;
+        ex[j] = want[l[j]] == r[j].id;   // a record of the new root (never kept below)
         keep[j] = true;
         if (act[l[j]]) {
           if (id >= p.cut_base) {   // deferred record: its child is materialised below
@@ -1294,11 +1235,21 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
     for (int j = 0; j < R; ++j) {
       const uint32_t i = base + (uint32_t)(j * T + t);
       if (i < n && act[l[j]]) {
+#ifndef PB_ABLATE_VIS   // ablation builds only (wrong visits)
         if (vis[j] != nullptr) atomicAdd(vis[j], 1);
+#endif
         if (keep[j] && !mat[j]) r[j].id = (uint32_t)nid[j] | (l[j] << kIdBits);
       }
       const uint64_t same = same_lane_mask(l[j], keep[j]);
       if (keep[j] && (same >> lane) == 1ull) atomicAdd(&kept[l[j]], __popcll(same));
+      xw[j][w][lane] = 0;
+      xr[j] = 0;
+      if (__ballot(ex[j]) != 0ull) {
+        const uint64_t xs = same_lane_mask(l[j], ex[j]);
+        xr[j] = __popcll(xs & below);
+        asm volatile("" ::: "memory");   // (the zero lands first: one wave's LDS ops run in order)
+        if (ex[j] && (xs >> lane) == 1ull) xw[j][w][l[j]] = (uint8_t)__popcll(xs);   // the tree's last lane
+      }
     }
     uint64_t mk[R], mm[R];
 #pragma unroll
@@ -1311,6 +1262,27 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
       }
     }
     __syncthreads();
+    // the new root belief ({root_t + 1, v0, v1, aux}, mcts.py:248-252): a record's
+    // place = its tree's count before the pass + the same tree's records in
+    // earlier sub-passes, then earlier waves of its sub-pass + its rank in its wave
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      if (ex[j]) {
+        const int lj = (int)l[j];
+        int pos = xcnt[lj] + xr[j];
+        for (int jj = 0; jj < j; ++jj)
+          for (int v = 0; v < kLogWaves; ++v) pos += xw[jj][v][lj];
+        for (int v = 0; v < w; ++v) pos += xw[j][v][lj];
+        if (pos < p.Nr) p.belief[xdst[lj] + pos] = make_uint4(tval[lj], r[j].v0, r[j].v1, aux[j]);
+      }
+    }
+    int xadd = 0;   // wave 0: this pass's extracted records of tree `lane`
+    if (w == 0) {
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+#pragma unroll
+        for (int v = 0; v < kLogWaves; ++v) xadd += xw[j][v][lane];
+    }
     int mtot = 0;
 #pragma unroll
     for (int j = 0; j < R; ++j)
@@ -1350,7 +1322,8 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
     }
     qn += mtot;
     out += (uint32_t)tot;
-    __syncthreads();   // (ksum is rewritten by the next pass)
+    __syncthreads();   // (ksum and xw are rewritten by the next pass)
+    if (w == 0) xcnt[lane] += xadd;   // (read again after the next pass's first barrier)
 #pragma unroll
     for (int j = 0; j < R; ++j) CL_CNT(4, keep[j]);
     CL_MARK(4);
@@ -1366,6 +1339,7 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
   if (w == 0) {
     const int mytree = sw * kWave + lane;
     if (mytree < p.B) {
+      p.cnt[mytree] = xcnt[lane];   // the new root's particles (k_update)
       p.hdr[mytree].n_log = kept[lane];
       if (made[lane] != 0) p.hdr[mytree].n_nodes += made[lane];
       if (bad[lane] != 0) {

@@ -1045,8 +1045,8 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
 
 // After k_search_lds: append every tree's scratch records of the launch
 // (stats.n_levels of them, in insertion order) to its search wave's shared
-// log, trees in lane order.  A tree's records keep their order; k_extract /
-// k_compact_log separate the trees by lane tag.  One workgroup per (tree lane,
+// log, trees in lane order.  A tree's records keep their order; the re-root
+// (k_compact_log) separates the trees by lane tag.  One workgroup per (tree lane,
 // search wave) -- grid (min(B, 64), search waves) -- copies one tree's records
 // to its range (the prefix of the lower lanes' counts), so the trees of a
 // batch are copied in parallel (one wave copied them in turn: 64 trees x 65,536
