@@ -892,6 +892,21 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
   static_assert(kHBits > 0, "the hash takes log2(kH) bits (mat_block)");
   __shared__ unsigned long long hk[kH];
   __shared__ int32_t hl[kH], hc[kH];
+  // between flushes the same LDS holds a pass's visits table: 2 kH keys (the
+  // relabelled record id: node id | tree lane, unique in the workgroup) in hk,
+  // their arrival counts in hl then hc -- one visits atomic per node and pass
+  constexpr int kV = 2 * kH;
+  constexpr int kVBits = kHBits + 1;
+  static_assert(kLogRecs * T <= kV, "a pass's records fit the visits table");
+  uint32_t* const vkey = reinterpret_cast<uint32_t*>(hk);
+  auto vcnt = [&](int h) -> int32_t* { return h < kH ? &hl[h] : &hc[h - kH]; };
+  auto vclear = [&]() {
+#pragma unroll
+    for (int q = 0; q < kV / T; ++q) {
+      vkey[q * T + t] = 0xFFFFFFFFu;   // (ids < kIdMask: pomcp_create)
+      *vcnt(q * T + t) = 0;
+    }
+  };
   constexpr int kQ = kLogRecs * T;  // deferred-record queue: a pass's records always fit
   __shared__ uint32_t q_at[kQ], q_nani[kQ], q_v0[kQ], q_v1[kQ], q_l[kQ];   // place, action
                                     // node, state (the key and done follow), tree lane
@@ -914,6 +929,7 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
     tval[lane] = (uint32_t)h.root_t + 1u;
     xdst[lane] = ((int64_t)mytree * 2 + (h.belief_sel ^ 1)) * p.Nr;
   }
+  vclear();
   __syncthreads();
   // a thread's place among the workgroup's threads with f set (thread order);
   // every thread calls it
@@ -1229,15 +1245,29 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
       CL_CNT(1, mat[j]);
     }
     CL_MARK(0);
-    // visits, relabelling (a deferred record keeps its id until its child is
-    // materialised), per-tree counts, the pass's places
+    __syncthreads();   // (the visits table is clear)
+    // visits (each record's node counted in the table; the thread that entered
+    // the node adds its count below), relabelling (a deferred record keeps its
+    // id until its child is materialised), per-tree counts, the pass's places
+    int vh[R];   // the table entry this thread adds to its node's visits (-1: none)
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       const uint32_t i = base + (uint32_t)(j * T + t);
+      vh[j] = -1;
       if (i < n && act[l[j]]) {
-#ifndef PB_ABLATE_VIS   // ablation builds only (wrong visits)
-        if (vis[j] != nullptr) atomicAdd(vis[j], 1);
-#endif
+        if (vis[j] != nullptr) {
+          const uint32_t key = (uint32_t)nid[j] | (l[j] << kIdBits);
+          int h = (int)((key * 0x9E3779B1u) >> (32 - kVBits));
+          bool first = false;
+          for (;;) {   // (a pass holds at most kV records: a free entry remains)
+            const uint32_t old = atomicCAS(&vkey[h], 0xFFFFFFFFu, key);
+            if (old == 0xFFFFFFFFu) first = true;
+            if (old == 0xFFFFFFFFu || old == key) break;
+            h = (h + 1) & (kV - 1);
+          }
+          atomicAdd(vcnt(h), 1);
+          vh[j] = first ? h : -1;
+        }
         if (keep[j] && !mat[j]) r[j].id = (uint32_t)nid[j] | (l[j] << kIdBits);
       }
       const uint64_t same = same_lane_mask(l[j], keep[j]);
@@ -1276,6 +1306,9 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
         if (pos < p.Nr) p.belief[xdst[lj] + pos] = make_uint4(tval[lj], r[j].v0, r[j].v1, aux[j]);
       }
     }
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+      if (vh[j] >= 0) atomicAdd(vis[j], *vcnt(vh[j]));   // the node's arrivals in this pass
     int xadd = 0;   // wave 0: this pass's extracted records of tree `lane`
     if (w == 0) {
 #pragma unroll
@@ -1290,6 +1323,7 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
       for (int v = 0; v < kLogWaves; ++v) mtot += msum[j][v];
     CL_MARK(4);
     if (qn + mtot > kQ) {   // (uniform) materialise the queue first
+      __syncthreads();   // (the visits table's counts are read: mat_block reuses its LDS)
       flush(qn);
       qn = 0;
     }
@@ -1324,6 +1358,7 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
     out += (uint32_t)tot;
     __syncthreads();   // (ksum and xw are rewritten by the next pass)
     if (w == 0) xcnt[lane] += xadd;   // (read again after the next pass's first barrier)
+    vclear();
 #pragma unroll
     for (int j = 0; j < R; ++j) CL_CNT(4, keep[j]);
     CL_MARK(4);
