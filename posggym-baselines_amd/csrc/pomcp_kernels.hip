@@ -403,16 +403,17 @@ __global__ __launch_bounds__(256) void k_reroot_child(DevParams p) {
 // thread); all of a pass's loads are issued together and the next pass's while
 // it runs.  (One wave per log took ~0.3 s at 65,536 trees x 65,536
 // simulations: one dependent round trip per 64 records.)
-// 16 waves (1,024 threads, one workgroup per CU: 150 KB of LDS in
-// k_compact_log): 4,096 records per pass; the update()-inclusive PursuitEvasion
-// step's update 142 -> 130 ms vs 4 waves, 237 ms with 2
-// (profiles/r5w_log_waves_ab.txt)
+// 16 waves (1,024 threads, one workgroup per CU), 3 records per thread: 3,072
+// records per pass.  The update()-inclusive PursuitEvasion step's update:
+// 4 -> 16 waves 142 -> 130 ms (2 waves 237 ms, profiles/r5w_log_waves_ab.txt);
+// at 16 waves 4 -> 3 records 115 -> 107.6 ms with 128 VGPRs (the most 1,024
+// threads allow; 2 records 111 ms, profiles/r5zc_compact_log_ab.txt)
 #ifndef PB_LOG_WAVES   // A/B builds only
 #define PB_LOG_WAVES 16
 #endif
 constexpr int kLogWaves = PB_LOG_WAVES;
 #ifndef PB_LOG_RECS   // A/B builds only
-#define PB_LOG_RECS 4
+#define PB_LOG_RECS 3
 #endif
 constexpr int kLogRecs = PB_LOG_RECS;   // records per thread per pass
 
@@ -950,6 +951,10 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
   const WaveLog wl(p.plog, p.Np, sw, p.tm);
   const uint32_t n = p.wlog[sw];
   const uint32_t A = (uint32_t)p.A;
+  // x / A by a multiply: amag = ceil(2^32 / A) is exact for x < 2^32 / A
+  // (x < 2^26: node ids, pomcp_create; A <= 5)
+  const uint64_t amag = (0x100000000ull + A - 1u) / A;
+  auto divA = [&](uint32_t x) -> uint32_t { return (uint32_t)(((uint64_t)x * amag) >> 32); };
   const int64_t bstride = blk_stride_lines(p.lines);
   constexpr int R = kLogRecs;
   const uint64_t below = (1ull << lane) - 1ull;
@@ -973,9 +978,10 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
       uint32_t fbit = 0u;          // ... and its bit
       bool need_ovf = false;
       if (mat) {   // inline slots, filled in order; concurrent inserts by CAS on the key
+        const uint32_t nq = divA(nani);
         uint4* const sl0 = reinterpret_cast<uint4*>(p.an + tree_base_lines(tree, p.Nb, p.lines) +
-                                                    (int64_t)(nani / A) * bstride) +
-                           part_slot((int)(nani % A), 0);
+                                                    (int64_t)nq * bstride) +
+                           part_slot((int)(nani - nq * A), 0);
         const uint64_t nk = okey | kValidBit | ((uint64_t)done << 63);
         uint64_t kk[kSlots];
 #pragma unroll
@@ -1220,22 +1226,24 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
         if (act[l[j]]) {
           if (id >= p.cut_base) {   // deferred record: its child is materialised below
             const uint32_t ani = id - p.cut_base;
-            const int nb = p.cmap[(int64_t)tree[j] * p.Nb + (int)(ani / A)];
+            const uint32_t aq = divA(ani);
+            const int nb = p.cmap[(int64_t)tree[j] * p.Nb + (int)aq];
             if (nb >= 0) {
               mat[j] = true;
-              nani[j] = (uint32_t)nb * A + ani % A;   // (key and done: at the flush, dense)
+              nani[j] = (uint32_t)nb * A + (ani - aq * A);   // (key and done: at the flush, dense)
             }
           } else if (id >= p.ovf_base) {
             nid[j] = p.ovf_new[(int64_t)tree[j] * p.H + (id - p.ovf_base)];
             if (nid[j] >= 0) vis[j] = &p.ovf[(int64_t)tree[j] * p.H + ((uint32_t)nid[j] - p.ovf_base)].visits;
           } else if (id >= 1u) {
             const uint32_t ani = (id - 1u) / kSlots, k = (id - 1u) % kSlots;
-            const int nb = p.cmap[(int64_t)tree[j] * p.Nb + (int)(ani / A)];
+            const uint32_t aq = divA(ani), ar = ani - aq * A;
+            const int nb = p.cmap[(int64_t)tree[j] * p.Nb + (int)aq];
             if (nb >= 0) {
-              nid[j] = (int32_t)(((uint32_t)nb * A + ani % A) * kSlots + k + 1u);
+              nid[j] = (int32_t)(((uint32_t)nb * A + ar) * kSlots + k + 1u);
               uint4* const bp = reinterpret_cast<uint4*>(p.an + tree_base_lines(tree[j], p.Nb, p.lines) +
                                                          (int64_t)nb * bstride);
-              vis[j] = reinterpret_cast<int32_t*>(bp + part_slot((int)(ani % A), (int)k)) + 3;
+              vis[j] = reinterpret_cast<int32_t*>(bp + part_slot((int)ar, (int)k)) + 3;
             }
           }
           keep[j] = nid[j] >= 0 || mat[j];
@@ -1270,8 +1278,9 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
         }
         if (keep[j] && !mat[j]) r[j].id = (uint32_t)nid[j] | (l[j] << kIdBits);
       }
-      const uint64_t same = same_lane_mask(l[j], keep[j]);
-      if (keep[j] && (same >> lane) == 1ull) atomicAdd(&kept[l[j]], __popcll(same));
+      // (a count only: one LDS atomic per kept record -- a wave's records mostly
+      // belong to distinct trees, lane = tree lane, so they seldom collide)
+      if (keep[j]) atomicAdd(&kept[l[j]], 1);
       xw[j][w][lane] = 0;
       xr[j] = 0;
       if (__ballot(ex[j]) != 0ull) {
