@@ -98,7 +98,7 @@ def _arena_usage(engine):
 
 def batched_episodes(cfg_kwargs, num_sims, env_seeds, steps, capacities=None, usage=None,
                      inline_slots=None, probes=None, spin_limit=None, env="Driving-v1",
-                     select_margin=None, counters=None):
+                     select_margin=None, counters=None, ego="0"):
     """Lockstep episodes of len(env_seeds) independent planners in ONE engine
     (tree b = planner b, env seed env_seeds[b]), `steps` real steps each.
     Returns per-tree record lists in the oracle format.  inline_slots: use only
@@ -107,16 +107,17 @@ def batched_episodes(cfg_kwargs, num_sims, env_seeds, steps, capacities=None, us
     k_search_lds's polls of a late step-tree hand-off (pomcp_debug_set_spin_limit);
     select_margin: k_search's fast-selection margin (pomcp_debug_set_select_margin);
     counters: a list that receives each search's summed (n_exact_selects,
-    n_deferred, n_cutoff)."""
+    n_deferred, n_cutoff); ego: the planning agent (the other acts uniformly
+    at random on the env's own stream, oracle/episode.py run_episode)."""
     import numpy as np
     from oracle.envs import make_model
     from oracle.episode import ENV_TREE_BASE
     from oracle.rng import S_ENV_POLICY_BASE, Streams
     from posggym_baselines_amd.planning import BatchedPOMCP
     model = product_model(env)
-    A = model.action_spaces["0"].n
+    A = model.action_spaces[ego].n
     B = len(env_seeds)
-    bp = BatchedPOMCP(model, "0", product_config(cfg_kwargs, num_sims), B, num_sims,
+    bp = BatchedPOMCP(model, ego, product_config(cfg_kwargs, num_sims), B, num_sims,
                       searches=steps, reroot=True, capacities=capacities)
     if inline_slots is not None:
         from posggym_baselines_amd import _native as N
@@ -136,7 +137,7 @@ def batched_episodes(cfg_kwargs, num_sims, env_seeds, steps, capacities=None, us
     records = [[] for _ in range(B)]
     last = np.full(B, -1, dtype=np.int32)
     for t in range(steps):
-        keys = np.array([e[1].pack_obs(e[3]["0"]) for e in envs], dtype=np.uint64)
+        keys = np.array([e[1].pack_obs(e[3][ego]) for e in envs], dtype=np.uint64)
         if usage is not None:
             usage.append(("before_update", _arena_usage(bp.engine)))
         bp.engine.update(last, keys)
@@ -153,8 +154,9 @@ def batched_episodes(cfg_kwargs, num_sims, env_seeds, steps, capacities=None, us
         for b in range(B):
             records[b].append(stats_record(stats[b], A, True, actions[b], bp.engine.root_belief(b)))
             es, e, st, obs = envs[b]
-            acts = {"0": int(actions[b]), "1": es.randint(S_ENV_POLICY_BASE + 1,
-                                                          e.action_spaces["1"].n)}
+            acts = {i: int(actions[b]) if i == ego else
+                    es.randint(S_ENV_POLICY_BASE + int(i), e.action_spaces[i].n)
+                    for i in e.possible_agents}
             ts = e.step(st, acts)
             envs[b][2], envs[b][3] = ts.state, ts.observations
         last = actions.astype(np.int32)

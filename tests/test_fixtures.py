@@ -39,13 +39,28 @@ def test_make_golden_regenerates_committed_fixtures(tmp_path):
                        text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     # (oracle_digests.json comes from the oracle, not the reference:
-    # make_oracle_digests.py, pinned by tests/test_oracle.py)
+    # make_oracle_digests.py, pinned by tests/test_oracle.py; fullsize_reroot.json
+    # from make_fullsize_reroot.py, below)
     committed = sorted(f for f in os.listdir(GOLDEN) if f.endswith(".json")
-                       and f != "oracle_digests.json")
+                       and f not in ("oracle_digests.json", "fullsize_reroot.json"))
     made = sorted(f for f in os.listdir(out) if f.endswith(".json"))
     assert made == committed
     _, mismatch, errors = filecmp.cmpfiles(GOLDEN, str(out), committed, shallow=False)
     assert mismatch == [] and errors == []
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/posggym_baselines"),
+                    reason="the reference exists only in the build container")
+def test_make_fullsize_reroot_regenerates_committed_fixture(tmp_path):
+    """The 65,536-simulation re-root episodes (test_gpu_parity.py
+    test_full_size_reroot_episodes): the real reference and the oracle agree
+    at the benchmarked size and reproduce the committed fixture byte for byte
+    (about a minute on 8 cores)."""
+    out = tmp_path / "fullsize_reroot.json"
+    r = subprocess.run([sys.executable, os.path.join(GOLDEN, "make_fullsize_reroot.py"), str(out)],
+                       cwd=ROOT, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert filecmp.cmp(os.path.join(GOLDEN, "fullsize_reroot.json"), str(out), shallow=False)
 
 
 def _dec(v):

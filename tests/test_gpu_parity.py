@@ -313,6 +313,41 @@ def test_pursuit_evasion_full_size_65536_sims():
     assert sum(st.child_visits[:4]) == 65536
 
 
+@pytest.mark.parametrize("env", ["Driving-v1", "PursuitEvasion-v1"])
+def test_full_size_reroot_episodes(search_kernel, env):
+    """The re-root at the benchmarked size (BASELINE configs 2 / 3, bench.py's
+    update()-inclusive step): 3-step episodes at 65,536 simulations per search
+    -- the initial update, then two re-roots of a 65,536-simulation tree --
+    for two planners in one engine, against the REAL reference planner's
+    records at that size (tests/golden/make_fullsize_reroot.py runs the
+    reference and the oracle and checks they agree): actions, root statistics
+    (FP64 bits) and the re-rooted belief (size and insertion-order digest)
+    every step.  A re-root here keeps ~10^4 particles, thousands of deferred
+    cut-off records per tree (several k_compact_log materialisation chunks of
+    1,024) and overflow-free inline slots; Driving plans as agent "0",
+    PursuitEvasion as agent "1" (the pursuer)."""
+    import os
+    from gpu_util import batched_episodes
+    data = load("fullsize_reroot")
+    cases = [c for c in data["cases"] if c["env"] == env]
+    S, K = data["num_sims"], data["steps"]
+    assert S == 65536 and K >= 3 and [c["tree"] for c in cases] == list(range(len(cases)))
+    # the kept subtree of every re-root holds more cut-off records than one
+    # materialisation chunk of k_compact_log (T = 1,024 threads)
+    assert all(min(c["kept_cutoff_records"]) > 1024 for c in cases), \
+        [c["kept_cutoff_records"] for c in cases]
+    assert all(min(r["belief_size"] for r in c["records"][1:]) > 1000 for c in cases)
+    counters = []
+    got = batched_episodes(cfg_kwargs(data["config"]), S, [c["env_seed"] for c in cases], K,
+                           env=env, ego=cases[0]["ego"], counters=counters)
+    for b, c in enumerate(cases):
+        for t in range(K):
+            assert got[b][t] == c["records"][t], f"{env} tree {b} step {t}"
+    if search_kernel == "lane" and os.environ.get("POMCP_DEFER_CUTOFF") == "1":
+        # every search deferred > 1,000 cut-off records per tree
+        assert all(d > 1000 * len(cases) for _, d, _ in counters), counters
+
+
 @pytest.mark.parametrize("case", ["c1_ucb", "pe_evader_ucb"])
 def test_episode_harness_replays_reference_episodes(case):
     """run_planning_episodes (exp_utils.py:468-552 / test_pomcp.py:16-33) with the
