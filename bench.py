@@ -537,26 +537,14 @@ def run_pomcp(dev, *, env, B, S, K, base_cfg, tm, steps, warmup, seed=0, max_blo
     mb = min(max_blocks, S + 64)
     note = ""
     if update_step:
-        # the re-root keeps the chosen child's particles (its visits: thousands)
-        # in the root belief: size that buffer from a 1,024-root probe of the same
-        # workload (x1.5; an overflow still fails loudly, POMCP_E_ARENA)
+        # the root belief region (pomcp_device.h bel_at) holds the restored root's
+        # n_target particles and the re-rooted belief: at most one particle per
+        # simulation (a node's records), or 2 n_target while reinvigorating --
+        # the worst case, so no probe of the workload is needed
         n_target = cfg.num_particles + cfg.extra_particles
-        pc = plan_capacities(cfg, step_limit, S, 1, reroot=True, max_blocks=mb,
-                             overflow_slots=1024)
-        nprobe = min(B, 1024)
-        probe = BatchedPOMCP(model, "0", cfg, nprobe, S, capacities=pc, device=dev,
-                             defer_cutoff=False)
-        try:
-            probe.init_synthetic(1000)
-            acts = probe.search()
-            probe.engine.update(acts, probe.engine.synthetic_step(1000, acts))
-            probe.engine.search(1, fetch=False)
-            bmax = max(s.belief_size for s in probe.engine.root_stats())
-        finally:
-            probe.close()
         caps = plan_capacities(cfg, step_limit, S, 1, reroot=True, max_blocks=mb,
                                overflow_slots=1024)
-        caps.max_belief = min(caps.max_belief, int(1.5 * bmax) + 2 * n_target + 64)
+        caps.max_belief = min(caps.max_belief, max(S, 2 * n_target) + n_target + 64)
         free = torch.cuda.mem_get_info(dev)[0]
         while B > 1024 and caps.bytes_per_tree(A) * B > 0.92 * free:
             B //= 2

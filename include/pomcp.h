@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define POMCP_ABI_VERSION 6
+#define POMCP_ABI_VERSION 7
 #define POMCP_MAX_ACTIONS 8
 #define POMCP_MAX_TYPE_POLICIES 8
 
@@ -90,7 +90,9 @@ typedef struct pomcp_config {
   /* per-tree arena capacities */
   int64_t max_blocks;           /* expanded obs nodes: A x 128 B action nodes each */
   int64_t max_particles;        /* particle log records (16 B) */
-  int64_t max_belief;           /* root belief records (16 B), x2 ping-pong */
+  int64_t max_belief;           /* root belief region (16 B records): the root belief and
+                                   the one a re-root builds, one from each end (ABI 7;
+                                   was one of two ping-pong buffers); < 2^31 */
   int64_t overflow_slots;       /* children beyond 6 per action node; power of two >= 16 */
   /* host-computed FP64 tables (Python's own math.log / float.__pow__) */
   const double* log_table;      /* log_table[n] = math.log(n), n >= 1 */

@@ -1,7 +1,7 @@
 // Philox4x32-10 counter-based RNG streams (host + device).
 //
 // Draw j of stream s under key (seed, tree) is word (j & 3) of
-// philox4x32_10(ctr = {j >> 2, 0, s, seed >> 32}, key = {seed & 0xffffffff, tree}).
+// philox4x32(ctr = {j >> 2, 0, s, seed >> 32}, key = {seed & 0xffffffff, tree}).
 // uniform int in [0, n) = (u32 * n) >> 32; uniform float = u32 * 2^-32.
 // This is the build's definition of "the reference's RNG" (SURVEY Appendix B):
 // every random draw on the hot path (planner Random(seed), global `random`,
@@ -36,7 +36,7 @@ enum Stream : uint32_t {
 #ifndef PB_PHILOX_ROUNDS
 #define PB_PHILOX_ROUNDS 10
 #endif
-PB_HD void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+PB_HD void philox4x32(uint32_t c[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < PB_PHILOX_ROUNDS; ++r) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
@@ -55,7 +55,7 @@ PB_HD void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
 // Word j of stream s (stateless form).
 PB_HD uint32_t philox_word(uint64_t seed, uint32_t tree, uint32_t s, uint32_t j) {
   uint32_t c[4] = {j >> 2, 0u, s, (uint32_t)(seed >> 32)};
-  philox4x32_10(c, (uint32_t)seed, tree);
+  philox4x32(c, (uint32_t)seed, tree);
   return c[j & 3];
 }
 

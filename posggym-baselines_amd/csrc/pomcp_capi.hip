@@ -176,7 +176,10 @@ static int validate(const pomcp_config* c, std::string* why) {
   // (max_blocks * A, pomcp_device.h)
   if (c->max_blocks * c->num_actions * (kSlots + 1) + 1 + c->overflow_slots >= (int64_t)kIdMask)
     return bad("obs node ids exceed 2^26 (max_blocks * A * 7 + overflow_slots)");
+  // max_belief: the root belief region (the root belief and the next, one from
+  // each end: pomcp_device.h bel_at)
   if (c->max_belief < 2 * (c->num_particles + c->extra_particles)) return bad("max_belief too small");
+  if (c->max_belief > INT32_MAX) return bad("max_belief < 2^31");
   if (c->overflow_slots < kBucket || (c->overflow_slots & (c->overflow_slots - 1)) != 0 ||
       c->overflow_slots > (1ll << 28))
     return bad("overflow_slots must be a power of two in [16, 2^28]");
@@ -283,7 +286,7 @@ int pomcp_create(const pomcp_config* cfg, int32_t device, void* hip_stream, pomc
   ALLOC(want, uint32_t, B);
   ALLOC(want_info, int4, B);
   ALLOC(cnt, int32_t, B);
-  ALLOC(belief, uint4, B * 2 * d.Nr);
+  ALLOC(belief, uint4, B * d.Nr);
   ALLOC(path, uint4, B * 3 * kMaxPath);
   ALLOC(logtab, double, c.log_table_size);
   ALLOC(dpow, double, c.discount_pow_size);
@@ -581,7 +584,8 @@ int pomcp_set_root_belief(pomcp_ctx* ctx, int32_t tree, const uint32_t* particle
     return fail(ctx, POMCP_E_INVALID, "set_root_belief: bad arguments");
   if (ctx->dp.tm)
     return fail(ctx, POMCP_E_UNSUPPORTED, "set_root_belief: type-based particles carry a policy");
-  if (count > ctx->dp.Nr) return fail(ctx, POMCP_E_ARENA, "set_root_belief: more particles than max_belief");
+  if (count > ctx->dp.Nr / 2)   // (the next belief needs room too: half the region)
+    return fail(ctx, POMCP_E_ARENA, "set_root_belief: more particles than max_belief / 2");
   const uint32_t t = particles[0];
   for (int32_t i = 0; i < count; ++i)
     if (particles[3 * i] != t || t < 1u)
@@ -593,11 +597,15 @@ int pomcp_set_root_belief(pomcp_ctx* ctx, int32_t tree, const uint32_t* particle
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   if (h.root_t != 0 || h.n_blocks != 0 || h.error != 0)
     return fail(ctx, POMCP_E_STATE, "set_root_belief: the tree must be fresh (pomcp_reset)");
+  // the region's records [at, at + count) in memory order (bel_at: the end of
+  // the region, reversed, when the belief grows from there)
+  const int sel = h.belief_sel ^ 1;
+  const int64_t at = sel ? ctx->dp.Nr - count : 0;
   std::vector<uint4> b((size_t)count);
   for (int32_t i = 0; i < count; ++i)
-    b[i] = make_uint4(particles[3 * i], particles[3 * i + 1], particles[3 * i + 2], 0u);
-  const int sel = h.belief_sel ^ 1;
-  uint4* dst = ctx->dp.belief + (int64_t)tree * 2 * ctx->dp.Nr + (int64_t)sel * ctx->dp.Nr;
+    b[bel_at(sel, ctx->dp.Nr, i) - at] =
+        make_uint4(particles[3 * i], particles[3 * i + 1], particles[3 * i + 2], 0u);
+  uint4* dst = ctx->dp.belief + (int64_t)tree * ctx->dp.Nr + at;
   HIP_TRY(ctx, hipMemcpyAsync(dst, b.data(), sizeof(uint4) * (size_t)count, hipMemcpyHostToDevice,
                               ctx->stream));
   h.belief_sel = sel;
@@ -614,6 +622,19 @@ int pomcp_set_root_belief(pomcp_ctx* ctx, int32_t tree, const uint32_t* particle
   return POMCP_OK;
 }
 
+// The first n particles of a tree's root belief, in order (pomcp_device.h
+// bel_at: a belief grown from the region's end is stored reversed)
+static int read_root_belief(pomcp_ctx* ctx, int32_t tree, const TreeHdr& h, int n, uint4* out) {
+  const int sel = h.belief_sel;
+  const int64_t at = sel ? ctx->dp.Nr - n : 0;
+  std::vector<uint4> raw((size_t)n);
+  HIP_TRY(ctx, hipMemcpyAsync(raw.data(), ctx->dp.belief + (int64_t)tree * ctx->dp.Nr + at,
+                              sizeof(uint4) * n, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  for (int i = 0; i < n; ++i) out[i] = raw[bel_at(sel, ctx->dp.Nr, i) - at];
+  return POMCP_OK;
+}
+
 int pomcp_get_root_belief(pomcp_ctx* ctx, int32_t tree, uint32_t* out, int32_t capacity,
                           int32_t* count) {
   if (!ctx || !count || tree < 0 || tree >= ctx->dp.B) return POMCP_E_INVALID;
@@ -626,11 +647,9 @@ int pomcp_get_root_belief(pomcp_ctx* ctx, int32_t tree, uint32_t* out, int32_t c
   if (!out || capacity <= 0) return POMCP_OK;
   const int n = h.belief_size < capacity ? h.belief_size : capacity;
   std::vector<uint4> tmp((size_t)n);
-  const uint4* src = ctx->dp.belief + (int64_t)tree * 2 * ctx->dp.Nr + (int64_t)h.belief_sel * ctx->dp.Nr;
   if (n > 0) {
-    HIP_TRY(ctx, hipMemcpyAsync(tmp.data(), src, sizeof(uint4) * n, hipMemcpyDeviceToHost,
-                                ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    int rc = read_root_belief(ctx, tree, h, n, tmp.data());
+    if (rc != POMCP_OK) return rc;
   }
   for (int i = 0; i < n; ++i) {
     out[3 * i + 0] = tmp[i].x;
@@ -732,11 +751,9 @@ int pomcp_get_root_policies(pomcp_ctx* ctx, int32_t tree, int32_t* out, int32_t 
   if (!out || capacity <= 0) return POMCP_OK;
   const int n = h.belief_size < capacity ? h.belief_size : capacity;
   std::vector<uint4> tmp((size_t)n);
-  const uint4* src = ctx->dp.belief + (int64_t)tree * 2 * ctx->dp.Nr + (int64_t)h.belief_sel * ctx->dp.Nr;
   if (n > 0) {
-    HIP_TRY(ctx, hipMemcpyAsync(tmp.data(), src, sizeof(uint4) * n, hipMemcpyDeviceToHost,
-                                ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    int rc = read_root_belief(ctx, tree, h, n, tmp.data());
+    if (rc != POMCP_OK) return rc;
   }
   for (int i = 0; i < n; ++i) out[i] = (int32_t)tmp[i].w;
   return POMCP_OK;

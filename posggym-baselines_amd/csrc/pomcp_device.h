@@ -230,7 +230,8 @@ struct DevParams {
   uint32_t* want;       // [B] re-root: log id of the child to extract (0xFFFFFFFF: none)
   int4* want_info;      // [B] re-root: that child's {block, absorbing, code, found} (k_update)
   int32_t* cnt;         // [B] re-root: particles extracted into the new root belief
-  uint4* belief;        // [B][2][Nr] {t, v0, v1, 0}
+  uint4* belief;        // [B][Nr] {t, v0, v1, aux}: the root belief and the one being
+                        // built, one from each end (bel_at)
   uint4* path;          // [B][3 * kMaxPath] search path of the running simulation
   const double* logtab;
   int64_t logtab_n;
@@ -254,6 +255,17 @@ struct DevParams {
   int32_t* ovf_new;     // [B][H]
   OvfSlot* ovf_tmp;     // [B][H]
 };
+
+// Root belief region of a tree: Nr records holding the current root belief and
+// the next one (built by the re-root while the current one is still read by
+// the reinvigoration), one from each end: belief_sel 0 keeps particle i at
+// record i, belief_sel 1 at record Nr - 1 - i.  A re-root therefore needs
+// old + new particles <= Nr (checked: POMCP_E_ARENA), not two full buffers --
+// the update()-inclusive bench step (a few hundred root particles before, up to
+// one per simulation after) fits 65,536 trees in HBM.
+__host__ __device__ __forceinline__ int64_t bel_at(int sel, int64_t Nr, int64_t i) {
+  return sel ? Nr - 1 - i : i;
+}
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
@@ -368,7 +380,7 @@ struct LdsStream {
     const uint32_t lane = (uint32_t)lane_id();
     if (lane < kRngPage / 4) {
       uint32_t c[4] = {pg * (kRngPage / 4) + lane, 0u, stream, (uint32_t)(seed >> 32)};
-      philox4x32_10(c, (uint32_t)seed, tree);
+      philox4x32(c, (uint32_t)seed, tree);
       reinterpret_cast<uint4*>(page)[lane] = make_uint4(c[0], c[1], c[2], c[3]);
     }
   }

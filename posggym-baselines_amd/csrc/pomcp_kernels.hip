@@ -65,7 +65,7 @@ struct Tree {
     lane = lane_id();
     an = p.an + tree_base_lines(t, p.Nb, p.lines);
     ovf = p.ovf + (int64_t)t * p.H;
-    bel = p.belief + (int64_t)t * 2 * p.Nr;
+    bel = p.belief + (int64_t)t * p.Nr;
     const TreeHdr h = p.hdr[t];
     n_blocks = uni(h.n_blocks);
     n_log = uni(h.n_log);
@@ -152,8 +152,11 @@ struct Tree {
     return uniform_float(uniu(philox_word(seed, tkey, S_SELECT, c_select++)));
   }
 
-  __device__ uint4* root_belief() { return bel + (int64_t)bsel * p.Nr; }
-  __device__ uint4* other_belief() { return bel + (int64_t)(bsel ^ 1) * p.Nr; }
+  // record i of the root belief / of the belief being built (pomcp_device.h
+  // bel_at: one from each end of the tree's region); the room of the latter
+  __device__ uint4* rbel(int64_t i) { return bel + bel_at(bsel, p.Nr, i); }
+  __device__ uint4* obel(int64_t i) { return bel + bel_at(bsel ^ 1, p.Nr, i); }
+  __device__ int64_t obel_room() const { return p.Nr - (int64_t)bsize; }
 
   __device__ uint4 load_block(int blk) const {
     uint4 q = make_uint4(0, 0, 0, 0);
@@ -446,10 +449,9 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
       // _initial_update (mcts.py:175-227): root -> None -> obs node (visits 0)
       uint32_t s0, s1;
       if (!T.sample_agent_initial(obs, &s0, &s1)) T.err = POMCP_E_INVALID;   // probe
-      uint4* nb = T.other_belief();
       int n = 0;
       while (T.err == 0 && n < p.n_target) {
-        if (n >= p.Nr) {
+        if (n >= T.obel_room()) {
           T.err = POMCP_E_ARENA;
           break;
         }
@@ -460,7 +462,7 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
         if (p.tm && !p.tmt->no_mixture_draw)
           pid = uniform_int(uniu(philox_word(T.seed, T.tkey, S_MIXTURE, T.c_mix++)),
                             (uint32_t)p.tmt->n_other);
-        if (lane == 0) nb[n] = make_uint4(1u, s0, s1, pid);
+        if (lane == 0) *T.obel(n) = make_uint4(1u, s0, s1, pid);
         ++n;
       }
       if (T.err == 0) {
@@ -490,21 +492,19 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
         c.code = uni(wi.z);
         {
           // the child's belief: its particles from the log in insertion order,
-          // already gathered into the other belief buffer by k_compact_log
-          uint4* nb = T.other_belief();
+          // already gathered into the belief being built by k_compact_log
           int n = uni(p.cnt[tree]);
           // ObsNode.visits of the new root = its particle records (one per
           // arrival, mcts.py:358-371); the slot's count may be stale
           // (pomcp_device.h: cut-off arrivals, children with a block)
           const int visits = n;
-          if (n > p.Nr) T.err = POMCP_E_ARENA;
+          if (n > T.obel_room()) T.err = POMCP_E_ARENA;
           // _reinvigorate (mcts.py:651-700) -> BeliefRejectionSampler (belief.py:145-194)
           const int need = p.n_target - n;
           if (T.err == 0 && !c.absorbing && need > 0) {
-            if (n + 2 * need > p.Nr) {
+            if (n + 2 * need > T.obel_room()) {
               T.err = POMCP_E_ARENA;
             } else {
-              const uint4* pbel = T.root_belief();
               const double limit = p.limit_factor * (double)need;
               int got = 0, tries = 0, nrej = 0;
               // 64 tries per pass, one per lane: try i draws word (counter + i) of
@@ -524,7 +524,7 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
                 const uint32_t wm = Env::kStepDraws
                                         ? philox_word(T.seed, T.tkey, S_MODEL, T.c_model + (uint32_t)lane)
                                         : 0u;
-                const uint4 hp = pbel[uniform_int(wb, (uint32_t)T.bsize)];
+                const uint4 hp = *T.rbel(uniform_int(wb, (uint32_t)T.bsize));
                 // the other agent's action: uniform, or (type-based) by the
                 // particle's policy (OtherAgentMixturePolicy.sample_action)
                 const uint32_t ao = p.tm && !p.tmt->other_uniform
@@ -543,9 +543,9 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
                 const uint64_t rm = __ballot(run);
                 const uint64_t jm = __ballot(run && !acc);
                 const uint4 rec = make_uint4(hp.x + 1u, n0, n1, hp.w);
-                if (run && acc) nb[n + got + pa] = rec;
+                if (run && acc) *T.obel(n + got + pa) = rec;
                 const int rr = nrej + __popcll(jm & lt);
-                if (run && !acc && rr < need) nb[n + need + rr] = rec;
+                if (run && !acc && rr < need) *T.obel(n + need + rr) = rec;
                 const int ran = __popcll(rm);
                 got += __popcll(am & rm);
                 nrej = min(need, nrej + __popcll(jm));
@@ -566,8 +566,8 @@ __global__ __launch_bounds__(256) void k_update(DevParams p) {
               for (int q0 = 0; q0 < fill; q0 += kWave) {   // disjoint ranges: got < need
                 const int q2 = q0 + lane;
                 if (q2 < fill) {   // written by other lanes: read past the L1
-                  const uint64_t* src = reinterpret_cast<const uint64_t*>(nb + n + need + q2);
-                  uint64_t* dst = reinterpret_cast<uint64_t*>(nb + n + got + q2);
+                  const uint64_t* src = reinterpret_cast<const uint64_t*>(T.obel(n + need + q2));
+                  uint64_t* dst = reinterpret_cast<uint64_t*>(T.obel(n + got + q2));
                   dst[0] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                   dst[1] = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
@@ -636,10 +636,12 @@ __global__ __launch_bounds__(256) void k_compact(DevParams p) {
   TreeHdr h = p.hdr[tree];
   const int4 wi = p.want_info[tree];
   const bool on = uni(h.error) == 0 && uni(wi.w) != 0;
-  if (lane == 0) p.cnt[tree] = on ? 1 : 0;   // read by k_compact_log
+  const int nb = uni(h.n_blocks);
+  // read by k_compact_log: 0 = not re-rooted, else 1 + the blocks before the
+  // compaction (the entries of cmap it stages in LDS)
+  if (lane == 0) p.cnt[tree] = on ? 1 + nb : 0;
   if (!on) return;
   const int A = p.A;
-  const int nb = uni(h.n_blocks);
   const int R = uni(wi.x);   // the new root's block (-1: a leaf)
   Line* const an = p.an + tree_base_lines(tree, p.Nb, p.lines);
   const int64_t bstride = blk_stride_lines(p.lines);
@@ -877,7 +879,9 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
   __shared__ uint32_t want[kWave];  // the new root's log id per tree (k_reroot_child) ...
   __shared__ int32_t xcnt[kWave];   // ... its records extracted so far
   __shared__ uint32_t tval[kWave];
-  __shared__ int64_t xdst[kWave];
+  __shared__ int64_t xdst[kWave];   // the tree's belief region ...
+  __shared__ int32_t xsel[kWave];   // ... the end the new belief grows from ...
+  __shared__ int32_t xroom[kWave];  // ... and its room (the current belief holds the rest)
   __shared__ uint8_t xw[kLogRecs][kLogWaves][kWave];   // this pass's extracted records per
                                                       // sub-pass, wave and tree (<= 64)
   __shared__ int32_t made[kWave];   // children materialised per tree
@@ -908,9 +912,19 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
       *vcnt(q * T + t) = 0;
     }
   };
-  constexpr int kQ = kLogRecs * T;  // deferred-record queue: a pass's records always fit
-  __shared__ uint32_t q_at[kQ], q_nani[kQ], q_v0[kQ], q_v1[kQ], q_l[kQ];   // place, action
-                                    // node, state (the key and done follow), tree lane
+  // deferred-record queue: a pass's records always fit.  Only their places: the
+  // record is stored there with its relabelled action node (cut_base + new
+  // action node | lane) and the flush reads it back (state -> key and done)
+  constexpr int kQ = kLogRecs * T;
+  __shared__ uint32_t q_at[kQ];
+  // cmap (k_compact: old block -> new block, -1 dropped) of the wave's 64 trees,
+  // staged in LDS when their old blocks fit (the bench: ~64 x 171): the
+  // classification of a record then issues no global load, so its wait never
+  // includes the next pass's prefetched records (vmcnt completes in order)
+  constexpr int kCmapLds = 16384;
+  __shared__ int16_t cml[kCmapLds];
+  __shared__ int32_t cmo[kWave + 1];   // per tree lane: its first entry in cml
+  __shared__ int32_t cml_ok;
 #ifdef PB_CLOG_TIMING
   uint64_t clt[6] = {0, 0, 0, 0, 0, 0};
   uint64_t cl_last = __builtin_amdgcn_s_memtime();
@@ -922,16 +936,51 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
     kept[lane] = 0;
     made[lane] = 0;
     bad[lane] = 0;
-    act[lane] = mytree < p.B ? p.cnt[mytree] : 0;
+    const int c = mytree < p.B ? p.cnt[mytree] : 0;   // k_compact: 1 + old blocks, 0 = off
+    act[lane] = c > 0 ? 1 : 0;
+    const int nbo = c > 0 ? c - 1 : 0;
+    int inc = nbo;   // inclusive scan over the wave's trees
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const int y = __shfl_up(inc, d);
+      if (lane >= d) inc += y;
+    }
+    cmo[lane] = inc - nbo;
+    if (lane == kWave - 1) cmo[kWave] = inc;
+    const bool fit = __ballot(nbo > 32767) == 0ull && __shfl(inc, kWave - 1) <= kCmapLds;
+    if (lane == 0) cml_ok = fit ? 1 : 0;
     const bool valid = mytree < p.B;
     const TreeHdr h = p.hdr[valid ? mytree : 0];
     want[lane] = valid ? p.want[mytree] : 0xFFFFFFFFu;
     xcnt[lane] = 0;
     tval[lane] = (uint32_t)h.root_t + 1u;
-    xdst[lane] = ((int64_t)mytree * 2 + (h.belief_sel ^ 1)) * p.Nr;
+    xdst[lane] = (int64_t)mytree * p.Nr;
+    xsel[lane] = h.belief_sel ^ 1;
+    xroom[lane] = (int32_t)(p.Nr - (int64_t)h.belief_size);
   }
   vclear();
   __syncthreads();
+#ifdef PB_NO_CMAP_LDS   // A/B builds only: classify from the global cmap
+  const bool cml_on = false;
+#else
+  const bool cml_on = cml_ok != 0;
+#endif
+  if (cml_on) {   // entry e belongs to the tree lane L with cmo[L] <= e < cmo[L + 1]
+    for (int e = t; e < cmo[kWave]; e += T) {
+      int lo = 0, hi = kWave - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (cmo[mid] <= e) lo = mid;
+        else hi = mid - 1;
+      }
+      cml[e] = (int16_t)p.cmap[(int64_t)(sw * kWave + lo) * p.Nb + (e - cmo[lo])];
+    }
+  }
+  __syncthreads();
+  // the new block of old block b of tree lane l (tree = sw * 64 + l)
+  auto cm = [&](uint32_t l, int tr, uint32_t b) -> int {
+    return cml_on ? (int)cml[cmo[l] + (int)b] : p.cmap[(int64_t)tr * p.Nb + (int)b];
+  };
   // a thread's place among the workgroup's threads with f set (thread order);
   // every thread calls it
   auto wg_rank = [&](bool f, int* total) -> int {
@@ -1151,6 +1200,8 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
   // materialise the queue's qn records (log order), T per chunk; each record's
   // id word gets its child's id.  Every thread calls it.
   auto flush = [&](int qn) {
+    wg_fence();        // the queued records were stored by this workgroup: they land
+    __syncthreads();   // before the (L1-bypassing) reads below
     for (int c = 0; c < qn; c += T) {
       const int e = c + t;
       const bool m = e < qn;
@@ -1159,16 +1210,20 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
       int dn = 0;
       if (m) {   // the child's observation key and absorbing flag from the record's state
         at = q_at[e];
-        nani = q_nani[e];
-        ll = q_l[e];
-        const uint32_t v0 = q_v0[e], v1 = q_v1[e];
+        const uint32_t rid = ld_agent_u32(wl.id + at);
+        const uint32_t v0 = ld_agent_u32(wl.v0 + at), v1 = ld_agent_u32(wl.v1 + at);
+        ll = rid >> kIdBits;
+        nani = (rid & kIdMask) - p.cut_base;
         ok = Env::obs_key(sm, p.ego, v0, v1);
         dn = Env::done_of(p.ego, v0, v1);
       }
       int32_t nid = -1;
       bool keep = true;
       mat_block(m, sw * kWave + (int)ll, ll, nani, ok, dn, nid, keep);
-      if (m && keep) wl.id[at] = (uint32_t)nid | (ll << kIdBits);   // (else the tree has failed: E_ARENA)
+      // the overflow map is full (keep false): the tree has failed (bad[] ->
+      // POMCP_E_ARENA) and the record gets an id no node ever has (kIdMask), so
+      // it can never be read as a live deferred record
+      if (m) wl.id[at] = (keep ? (uint32_t)nid : kIdMask) | (ll << kIdBits);
     }
   };
   int qn = 0;   // queued deferred records (uniform over the workgroup)
@@ -1227,7 +1282,7 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
           if (id >= p.cut_base) {   // deferred record: its child is materialised below
             const uint32_t ani = id - p.cut_base;
             const uint32_t aq = divA(ani);
-            const int nb = p.cmap[(int64_t)tree[j] * p.Nb + (int)aq];
+            const int nb = cm(l[j], tree[j], aq);
             if (nb >= 0) {
               mat[j] = true;
               nani[j] = (uint32_t)nb * A + (ani - aq * A);   // (key and done: at the flush, dense)
@@ -1238,7 +1293,7 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
           } else if (id >= 1u) {
             const uint32_t ani = (id - 1u) / kSlots, k = (id - 1u) % kSlots;
             const uint32_t aq = divA(ani), ar = ani - aq * A;
-            const int nb = p.cmap[(int64_t)tree[j] * p.Nb + (int)aq];
+            const int nb = cm(l[j], tree[j], aq);
             if (nb >= 0) {
               nid[j] = (int32_t)(((uint32_t)nb * A + ar) * kSlots + k + 1u);
               uint4* const bp = reinterpret_cast<uint4*>(p.an + tree_base_lines(tree[j], p.Nb, p.lines) +
@@ -1277,6 +1332,7 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
           vh[j] = first ? h : -1;
         }
         if (keep[j] && !mat[j]) r[j].id = (uint32_t)nid[j] | (l[j] << kIdBits);
+        if (mat[j]) r[j].id = (p.cut_base + nani[j]) | (l[j] << kIdBits);   // (the flush reads it)
       }
       // (a count only: one LDS atomic per kept record -- a wave's records mostly
       // belong to distinct trees, lane = tree lane, so they seldom collide)
@@ -1312,7 +1368,8 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
         for (int jj = 0; jj < j; ++jj)
           for (int v = 0; v < kLogWaves; ++v) pos += xw[jj][v][lj];
         for (int v = 0; v < w; ++v) pos += xw[j][v][lj];
-        if (pos < p.Nr) p.belief[xdst[lj] + pos] = make_uint4(tval[lj], r[j].v0, r[j].v1, aux[j]);
+        if (pos < xroom[lj])   // (beyond: k_update fails the tree, POMCP_E_ARENA)
+          p.belief[xdst[lj] + bel_at(xsel[lj], p.Nr, pos)] = make_uint4(tval[lj], r[j].v0, r[j].v1, aux[j]);
       }
     }
 #pragma unroll
@@ -1351,14 +1408,7 @@ __global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
         const uint32_t at = out + (uint32_t)(tot + pre + __popcll(mk[j] & below));
         wl.store(at, r[j]);
         if (p.tm) wl.aux[at] = aux[j];
-        if (mat[j]) {
-          const int e = mt + mpre + __popcll(mm[j] & below);
-          q_at[e] = at;
-          q_nani[e] = nani[j];
-          q_v0[e] = r[j].v0;
-          q_v1[e] = r[j].v1;
-          q_l[e] = l[j];
-        }
+        if (mat[j]) q_at[mt + mpre + __popcll(mm[j] & below)] = at;
       }
       tot += tj;
       mt += mj;

@@ -184,7 +184,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   OvfSlot* const ovf = p.ovf + (int64_t)tt * p.H;
   PathEntry* const path = reinterpret_cast<PathEntry*>(p.path) + (int64_t)tt * kMaxPath;
   const TreeHdr* const h = p.hdr + tt;
-  const uint4* const rbel = p.belief + (int64_t)tt * 2 * p.Nr + (int64_t)h->belief_sel * p.Nr;
+  // the root belief: particle i at rbel[bdir * i] (pomcp_device.h bel_at)
+  const int bdir = h->belief_sel ? -1 : 1;
+  const uint4* const rbel = p.belief + (int64_t)tt * p.Nr + (h->belief_sel ? p.Nr - 1 : 0);
   int root_blk = h->root_blk, root_visits = h->root_visits;
   int n_blocks = h->n_blocks, n_log = h->n_log, n_nodes = h->n_nodes;
   const int bsize = h->belief_size, epoch = h->epoch, root_abs = h->root_abs;
@@ -239,7 +241,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
   auto spec_blocks = [&]() {   // the next simulation's, assuming this one draws 1..4 words
     const uint32_t cm = m_base + 4u, co = o_base + 4u;
     uint32_t bo[4] = {co >> 2, 0u, (uint32_t)(S_ACT_BASE + p.other), (uint32_t)(seed >> 32)};
-    philox4x32_10(bo, (uint32_t)seed, tkey);
+    philox4x32(bo, (uint32_t)seed, tkey);
     no0 = bo[0];
     no1 = bo[1];
     no2 = bo[2];
@@ -247,7 +249,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
     no_base = co;
     if constexpr (Env::kStepDraws) {
       uint32_t bm[4] = {cm >> 2, 0u, (uint32_t)S_MODEL, (uint32_t)(seed >> 32)};
-      philox4x32_10(bm, (uint32_t)seed, tkey);
+      philox4x32(bm, (uint32_t)seed, tkey);
       nm0 = bm[0];
       nm1 = bm[1];
       nm2 = bm[2];
@@ -263,14 +265,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
     const bool hit = co == no_base && (!Env::kStepDraws || c_mod == nm_base);
     if (!hit) {   // (divergent: the first simulation, or one that drew 0 or > 4 words)
       uint32_t bo[4] = {co >> 2, 0u, (uint32_t)(S_ACT_BASE + p.other), (uint32_t)(seed >> 32)};
-      philox4x32_10(bo, (uint32_t)seed, tkey);
+      philox4x32(bo, (uint32_t)seed, tkey);
       no0 = bo[0];
       no1 = bo[1];
       no2 = bo[2];
       no3 = bo[3];
       if constexpr (Env::kStepDraws) {
         uint32_t bm[4] = {c_mod >> 2, 0u, (uint32_t)S_MODEL, (uint32_t)(seed >> 32)};
-        philox4x32_10(bm, (uint32_t)seed, tkey);
+        philox4x32(bm, (uint32_t)seed, tkey);
         nm0 = bm[0];
         nm1 = bm[1];
         nm2 = bm[2];
@@ -631,7 +633,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
         if constexpr (TM != 0) rap[a] = reinterpret_cast<const double*>(rb + part_prior(A))[a];
       }
     }
-    pf = rbel[d_belief((uint32_t)bsize)];   // the first simulation's particle
+    pf = rbel[bdir * (int)d_belief((uint32_t)bsize)];   // the first simulation's particle
     la_bel();
   }
 
@@ -805,7 +807,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(POMCP_WAVES
 #ifdef POMCP_ABLATE_BELIEF   // ablation build only (tools/ablate.sh): no belief line per simulation
           pf.w += uniform_int(w_bel, (uint32_t)bsize) & 1u;
 #else
-          pf = rbel[uniform_int(w_bel, (uint32_t)bsize)];
+          pf = rbel[bdir * (int)uniform_int(w_bel, (uint32_t)bsize)];
 #endif
           pend_b = 0;
         }

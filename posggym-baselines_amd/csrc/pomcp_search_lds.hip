@@ -107,7 +107,7 @@ __device__ __forceinline__ void vs_fill(VStream& s, uint64_t seed, uint32_t tkey
   const uint32_t base = s.ctr & ~63u;
   const uint32_t i = (uint32_t)lane_id();
   uint32_t c[4] = {(base >> 2) + (i >> 2), 0u, sid, (uint32_t)(seed >> 32)};
-  philox4x32_10(c, (uint32_t)seed, tkey);
+  philox4x32(c, (uint32_t)seed, tkey);
   const uint32_t q = i & 3u;
   s.w = q == 0u ? c[0] : (q == 1u ? c[1] : (q == 2u ? c[2] : c[3]));
   s.base = base;
@@ -187,8 +187,9 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
   };
 
   const TreeHdr* const h = p.hdr + tree;
-  const uint4* const rbel =
-      p.belief + (int64_t)tree * 2 * p.Nr + (int64_t)uni(h->belief_sel) * p.Nr;
+  // the root belief: particle i at rbel[bdir * i] (pomcp_device.h bel_at)
+  const int bdir = uni(h->belief_sel) ? -1 : 1;
+  const uint4* const rbel = p.belief + (int64_t)tree * p.Nr + (uni(h->belief_sel) ? p.Nr - 1 : 0);
   int root_blk = uni(h->root_blk), root_visits = uni(h->root_visits);
   int n_blocks = uni(h->n_blocks), n_log = uni(h->n_log), n_nodes = uni(h->n_nodes);
   const int bsize = uni(h->belief_size), epoch = uni(h->epoch), root_abs = uni(h->root_abs);
@@ -247,7 +248,7 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
   for (int i = (int)threadIdx.x; i < ndp; i += (int)blockDim.x) dpw[i] = p.dpow[i];
   const bool bel_lds = bsize <= kLdsBelief;
   if (bel_lds)
-    for (int i = (int)threadIdx.x; i < bsize; i += (int)blockDim.x) bel[i] = rbel[i];
+    for (int i = (int)threadIdx.x; i < bsize; i += (int)blockDim.x) bel[i] = rbel[bdir * i];
   // the step streams are simulation-aligned (oracle/rng.py SIM_STREAMS): every
   // simulation starts the model's and both agents' action streams at a Philox
   // block boundary (counters rounded up to a multiple of 4)
@@ -276,7 +277,7 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
   auto logtab_now = [&](int n) {
     return *reinterpret_cast<const volatile double*>(p.logtab + (n < p.logtab_n ? n : 0));
   };
-  auto particle = [&](uint32_t i) { return bel_lds ? bel[i] : rbel[i]; };
+  auto particle = [&](uint32_t i) { return bel_lds ? bel[i] : rbel[bdir * (int)i]; };
   // the root's math.log(n): block b's entry when it holds n (the previous
   // simulation left it there), else the host table
   auto root_log = [&](int b, int n) {

@@ -11,7 +11,7 @@ import os
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.environ.get("POMCP_LIB_PATH") or os.path.join(LIB_DIR, "libpomcp_hip.so")
 
-POMCP_ABI_VERSION = 6
+POMCP_ABI_VERSION = 7
 POMCP_MAX_TYPE_POLICIES = 8
 POMCP_MAX_ACTIONS = 8
 POMCP_XREC_STATS = 6

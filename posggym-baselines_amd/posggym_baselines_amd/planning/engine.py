@@ -18,17 +18,18 @@ INT32_MAX = 2**31 - 1
 class Capacities:
     max_blocks: int           # expanded obs nodes (each A x 128 B action nodes)
     max_particles: int        # particle log records (16 B)
-    max_belief: int           # root belief records (16 B), two ping-pong buffers
+    max_belief: int           # root belief region (16 B records): the root belief and the
+                              # next one, one from each end (pomcp_device.h bel_at)
     overflow_slots: int       # obs children beyond 6 per action node (32 B)
     log_table_size: int
     discount_pow_size: int
 
     def bytes_per_tree(self, num_actions: int, type_based: bool = False) -> int:
         """HBM of one tree (pomcp_create): (A + 1 [+ 1]) x 128 B per block, 32 B
-        overflow entries, 12 [16] B particle records, two 16 B root beliefs."""
+        overflow entries, 12 [16] B particle records, the 16 B root belief region."""
         tm = 1 if type_based else 0
         return (self.max_blocks * (num_actions + 1 + tm) * 128 + self.overflow_slots * 32
-                + self.max_particles * (12 + 4 * tm) + 2 * self.max_belief * 16)
+                + self.max_particles * (12 + 4 * tm) + self.max_belief * 16)
 
 
 def _next_pow2(n: int) -> int:
@@ -62,7 +63,9 @@ def plan_capacities(config, step_limit: int, num_sims: int, searches: int = 1,
     else:
         nb = max_blocks
     np_ = total * min(levels, 64) + searches * 2 * n_target + 64
-    nr = (np_ + 2 * n_target + 64) if reroot else (4 * n_target + 64)
+    # the root belief region holds the root belief and the next (a re-root's
+    # extraction + reinvigoration), each at most a log's worth of particles
+    nr = 2 * (np_ + 2 * n_target + 64) if reroot else 2 * (4 * n_target + 64)
     return Capacities(
         max_blocks=nb, max_particles=np_, max_belief=nr, overflow_slots=ovf,
         log_table_size=total + 2, discount_pow_size=min(levels, 4096) + 2)

@@ -3,9 +3,13 @@ run_pomcp(update_step=True)): one search of 65,536 simulations from the
 synthetic PursuitEvasion-v1 / Driving-v1 roots, the environment's answer and
 update(); prints the distribution of the re-rooted belief sizes, blocks and log
 records in use before / after the re-root (sizes the arenas)."""
+import os
 import sys
 
 import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "posggym-baselines_amd"))
 
 
 def probe(env, B=1024, S=65536, seed=0):
