@@ -853,8 +853,12 @@ def main():
         base_cfg = TM_CFG
     # (no CPU leg for POTMMCP: the oracle has no restatement of it -- its parity
     # is pinned to the reference's own records)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not tm:
-        # before any GPU call: the worker processes are forked from this one
+    if rank == 0 and not args.no_cpu_baseline and not tm:
+        # before any GPU call: the worker processes are forked from this one.
+        # With N ranks rank 0 runs it before the process group forms (the other
+        # ranks wait in its rendezvous), so every line carries its CPU baseline;
+        # the timed steps start after run_pomcp's barrier, so it is never in the
+        # measured time
         procs = max(1, min(args.cpu_procs, os.cpu_count() or 1))
         sample = args.cpu_sample_sims if not args.deep else max(64, args.cpu_sample_sims // 8)
         cpu = cpu_baseline_parallel(sample, procs, args.seed, args.env, base_cfg)

@@ -13,7 +13,9 @@
  * (INTMCP.initialize's recursion, intmcp.py:950-994); nesting_level = 3:
  * four trees -- tree 0 the planner's (level 3), trees 1 and 2 the level-2 and
  * level-1 planners of the other agent and the planner's agent, tree 3 the
- * other agent's level-0 planner.  Paths relative to
+ * other agent's level-0 planner; in general nesting_level = L >= 2 keeps L + 1
+ * trees, tree k the level-(L - k) planner (of the planner's agent if k is
+ * even), up to INTMCP_MAX_TREES.  Paths relative to
  * posggym_baselines/planning/ in the reference.
  *
  * Same conventions as pomcp.h (plain pointers, POMCP_* status codes, a
@@ -30,10 +32,12 @@
 extern "C" {
 #endif
 
+#define INTMCP_MAX_TREES 6        /* nesting levels 0 .. 5: a tree per level */
+
 typedef struct intmcp_config {
   pomcp_config base;              /* MCTSConfig + model + tables (num_trees = planner pairs) */
   int32_t state_belief_only;      /* MCTSConfig.state_belief_only (test config: 0) */
-  int32_t nesting_level;          /* 0 to 3 (INTMCP.initialize's nesting_level) */
+  int32_t nesting_level;          /* 0 to INTMCP_MAX_TREES - 1 (INTMCP.initialize's nesting_level) */
   int64_t max_nodes;              /* obs nodes per tree */
   int64_t max_stats;              /* action-node statistics entries per tree (A per expanded node) */
   int64_t max_log;                /* particle log records per tree (16 B) */
@@ -127,7 +131,8 @@ int intmcp_get_mid_support(intmcp_ctx* ctx, int32_t pair, int32_t* entries, int3
 int intmcp_search_level(intmcp_ctx* ctx, int32_t level, int32_t sims, int32_t flags,
                         int32_t* actions_out);
 /* Arena counters of every pair: out[pair][tree][{nodes, log records, stats}]
- * for trees 0..3 (zeros for a tree the nesting level does not have), B x 12. */
+ * for trees 0 .. INTMCP_MAX_TREES - 1 (zeros for a tree the nesting level does
+ * not have), B x INTMCP_MAX_TREES x 3. */
 int intmcp_get_tree_counts(intmcp_ctx* ctx, int32_t* out);
 /* INTMCP.initialize's search_policies (intmcp.py:956-971): the search policy of
  * agent `agent` at nesting level `level` -- NULL: RandomSearchPolicy

@@ -32,8 +32,10 @@ from oracle.rng import S_ACT_BASE, S_BELIEF, S_SELECT, Streams, StreamRandom
 INF = float("inf")
 S_BELIEF_NESTED = 3   # the level-0 planner's random.Random(config.seed) (intmcp.py:66)
 S_BELIEF_MID = 5      # a middle planner's random.Random(config.seed): level l (1 <= l < the
-                      # nesting level) draws on S_BELIEF_MID + l - 1 (5, 6 at nesting level 3)
-MAX_NESTING = 3       # (streams 5..7 are free for middle levels; the engine builds 0-3)
+                      # nesting level) draws on S_BELIEF_MID + l - 1 for l <= 3 (5, 6, 7) and
+S_BELIEF_MID_HI = 16  # on S_BELIEF_MID_HI + l beyond (20, 21: clear of the action streams 8 + i;
+                      # csrc/philox.h belief_mid_stream)
+MAX_NESTING = 5       # (the engine builds nesting levels 0-5: include/intmcp.h INTMCP_MAX_TREES)
 
 
 def belief_stream(level: int, nesting_level: int) -> int:
@@ -43,7 +45,7 @@ def belief_stream(level: int, nesting_level: int) -> int:
         return S_BELIEF_NESTED
     if level == nesting_level:
         return S_BELIEF
-    return S_BELIEF_MID + level - 1
+    return S_BELIEF_MID + level - 1 if level <= 3 else S_BELIEF_MID_HI + level
 
 
 class _Tree:

@@ -1,4 +1,4 @@
-"""Counter-based RNG streams (Philox4x32-10) shared by oracle, harness and HIP.
+"""Counter-based RNG streams (Philox4x32-7) shared by oracle, harness and HIP.
 
 TEST INFRASTRUCTURE (see ``oracle/__init__.py``).
 
@@ -8,8 +8,9 @@ global ``random`` module (``mcts.py:496,532,555,571,581,590,600``), the
 gymnasium ``Discrete.sample()`` of each agent's action space
 (``search_policy.py:177``, ``other_policy.py:151``) and the model's own RNG.
 The build gives each family one *stream*: draw ``j`` of stream ``s`` under key
-``(seed, tree)`` is word ``j & 3`` of ``philox4x32_10(ctr=(j>>2 lo, j>>2 hi, s,
-seed_hi), key=(seed_lo, tree))``.  A uniform int in ``[0, n)`` is
+``(seed, tree)`` is word ``j & 3`` of ``philox4x32(ctr=(j>>2 lo, j>>2 hi, s,
+seed_hi), key=(seed_lo, tree))`` with ``PHILOX_ROUNDS`` = 7 rounds (rounds 1-5
+of the build used 10; ``csrc/philox.h`` gives the statistical argument).  A uniform int in ``[0, n)`` is
 ``(u32 * n) >> 32`` and a uniform float is ``u32 * 2**-32``.  The HIP kernels
 (``csrc/philox.h``) implement exactly this function.
 """
@@ -36,9 +37,12 @@ S_ENV_POLICY_BASE = 40  # harness: true (non-planning) agent i's random policy: 
 SIM_STREAMS = (S_MODEL, S_ACT_BASE, S_ACT_BASE + 1)
 
 
-def philox4x32_10(c0, c1, c2, c3, k0, k1):
-    """Random123 Philox4x32 with 10 rounds (pure Python ints)."""
-    for _ in range(10):
+PHILOX_ROUNDS = 7
+
+
+def philox4x32(c0, c1, c2, c3, k0, k1, rounds=PHILOX_ROUNDS):
+    """Random123 Philox4x32 with ``rounds`` rounds (pure Python ints)."""
+    for _ in range(rounds):
         p0 = _M0 * c0
         p1 = _M1 * c2
         c0, c1, c2, c3 = (
@@ -50,6 +54,11 @@ def philox4x32_10(c0, c1, c2, c3, k0, k1):
         k0 = (k0 + _W0) & MASK32
         k1 = (k1 + _W1) & MASK32
     return c0, c1, c2, c3
+
+
+def philox4x32_10(c0, c1, c2, c3, k0, k1):
+    """Philox4x32-10 (Random123's default; the known answers of the round function)."""
+    return philox4x32(c0, c1, c2, c3, k0, k1, rounds=10)
 
 
 class Streams:
@@ -79,7 +88,7 @@ class Streams:
         b = j >> 2
         cached = self._blk.get(stream)
         if cached is None or cached[0] != b:
-            words = philox4x32_10(b & MASK32, (b >> 32) & MASK32, stream, self._c3,
+            words = philox4x32(b & MASK32, (b >> 32) & MASK32, stream, self._c3,
                                   self._k0, self._k1)
             cached = (b, words)
             self._blk[stream] = cached

@@ -125,11 +125,15 @@ struct ISup {           // a materialised level-0 belief
 // one; nesting level 1: tree 0 (the planner's level-1 tree) and tree 1 (the
 // other agent's level-0 tree); level 2 (ImParams::nt = 3) adds a middle tree
 // (tree 1, level 1, the other agent), level 3 two (trees 1 and 2, levels 2
-// and 1).  Tree k models agent ego if k is even.  The bottom tree's beliefs
-// are the "support" (sup / supp); middle tree k's are msup[k - 1] /
-// msupp[k - 1].
-constexpr int kImMaxT = 4;
-constexpr int kImMaxMid = kImMaxT - 2;   // middle trees (nesting level 3: trees 1 and 2)
+// and 1), ... level L >= 2 L - 1 (trees 1 .. L - 1, levels L - 1 .. 1; built up
+// to nesting level 5).  Tree k models agent ego if k is even.  The bottom
+// tree's beliefs are the "support" (sup / supp); middle tree k's are
+// msup[k - 1] / msupp[k - 1].
+constexpr int kImMaxT = INTMCP_MAX_TREES;   // nesting levels 0 .. kImMaxT - 1
+constexpr int kImMaxMid = kImMaxT - 2;      // middle trees (nesting level 5: trees 1 .. 4)
+struct ImSims {                             // simulations per level of one k_im_searchN launch
+  int32_t s[kImMaxT];
+};
 struct IHdr {
   int32_t n_nodes[kImMaxT], n_stats[kImMaxT], n_log[kImMaxT];
   int32_t cur, root_sel, root_size, sup_sel, n_sup, sup_used, err, last_action;
@@ -140,8 +144,8 @@ struct IHdr {
   double mm_min[kImMaxT], mm_max[kImMaxT];
   uint64_t seed;
   uint32_t tree_key;
-  uint32_t ctr[8];      // belief (top), select, model, act0, act1, belief (level 0), belief
-                        // (middle trees 1, 2)
+  uint32_t ctr[6 + kImMaxMid];   // belief (top), select, model, act0, act1, belief (level 0),
+                                 // belief (middle trees 1 .. kImMaxMid)
 };
 
 struct ImParams {
@@ -232,7 +236,7 @@ __host__ __device__ __forceinline__ int im_order(uint32_t info, int k) { return 
 __device__ __forceinline__ bool im_has_stats(uint32_t info) { return (info & kImStatsBit) != 0u; }
 
 // One planner pair (lane): pointers, counters, RNG.  NT: trees per pair
-// (== ImParams::nt: 2, 3 at nesting level 2, 4 at level 3).
+// (== ImParams::nt: 2, else the nesting level + 1).
 template <class Env, int NT = 2>
 struct ImPair {
   using Model = typename Env::Model;
@@ -271,7 +275,7 @@ struct ImPair {
   // wave waits on a load anyway; draw() consumes it.  Each stream is consumed
   // in order, so results are unchanged; stored counters exclude a computed but
   // unconsumed word (la_pend).
-  uint32_t la_w[8];
+  uint32_t la_w[6 + kImMaxMid];
   uint32_t la_pend = 0u;
 #ifdef POMCP_PHASE_TIMING
   uint64_t pt[kImPhases] = {};
@@ -302,6 +306,7 @@ struct ImPair {
     dp = p.dpow;
   }
   static constexpr int kCtrs = NT > 2 ? 4 + NT : 6;   // RNG streams in use (slot 5 + k: middle tree k)
+  static_assert(kCtrs <= 6 + kImMaxMid, "IHdr::ctr holds every stream's counter");
   __device__ __forceinline__ uint32_t ctr_stored(int q) const { return h.ctr[q] - ((la_pend >> q) & 1u); }
   // intmcp.py:326-330 (_prune_traverse's clear_belief at every update): the
   // particles of nodes more than two steps behind the current one are dropped
@@ -446,12 +451,12 @@ struct ImPair {
     return philox_word(h.seed, h.tree_key, stream, h.ctr[slot]++);
   }
   // the stream of counter slot q: slot 5 + k is middle tree k's planner's,
-  // whose level is NT - 1 - k: S_BELIEF_MID + level - 1 (oracle/intmcp.py
+  // whose level is NT - 1 - k (philox.h belief_mid_stream, oracle/intmcp.py
   // belief_stream)
   static __device__ __forceinline__ constexpr uint32_t slot_stream(int q) {
     return q == 0 ? (uint32_t)S_BELIEF : q == 1 ? (uint32_t)S_SELECT : q == 2 ? (uint32_t)S_MODEL
            : q == 3 ? (uint32_t)S_ACT_BASE : q == 4 ? (uint32_t)S_ACT_BASE + 1u
-           : q == 5 ? (uint32_t)S_BELIEF_NESTED : (uint32_t)(S_BELIEF_MID + NT + 3 - q);
+           : q == 5 ? (uint32_t)S_BELIEF_NESTED : belief_mid_stream(NT + 4 - q);
   }
   __device__ __forceinline__ void la_fill() {
 #pragma unroll
@@ -469,8 +474,7 @@ struct ImPair {
   __device__ __forceinline__ uint32_t d_bel(int k, uint32_t n) {
     if (k == kBot) return uniform_int(draw(5, S_BELIEF_NESTED), n);
     if (k == 0) return uniform_int(draw(0, S_BELIEF), n);
-    if (NT > 3 && k == 2) return uniform_int(draw(7, slot_stream(7)), n);
-    return uniform_int(draw(6, slot_stream(6)), n);
+    return uniform_int(draw(5 + k, slot_stream(5 + k)), n);   // middle tree k
   }
   __device__ __forceinline__ uint32_t d_sel(uint32_t n) { return uniform_int(draw(1, S_SELECT), n); }
   __device__ __forceinline__ double d_sel_float() { return uniform_float(draw(1, S_SELECT)); }
@@ -2170,7 +2174,7 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
   P.store_search();
 }
 
-// INTMCP.get_action (intmcp.py:368-408) at nesting level NT - 1 = 2 or 3:
+// INTMCP.get_action (intmcp.py:368-408) at nesting level NT - 1 >= 2:
 // sims[l] simulations at level l = 0 .. NT - 1 in turn.  Every simulation
 // samples a root particle of the top planner (its stream); below the top it
 // dispatches down the levels (_nested_sim, intmcp.py:410-442): each middle
@@ -2179,8 +2183,7 @@ __global__ __launch_bounds__(64) void k_im_search(ImParams p, int sims0, int sim
 // level, which runs _simulate.  (Correctness first: a plain serial lane per
 // pair, no lookahead of the next particle.)
 template <class Env, int NT>
-__global__ __launch_bounds__(64) void k_im_searchN(ImParams p, int sims0, int sims1, int sims2,
-                                                   int sims3, int flags) {
+__global__ __launch_bounds__(64) void k_im_searchN(ImParams p, ImSims sims, int flags) {
   static_assert(NT >= 3 && NT <= kImMaxT, "a middle tree");
   constexpr int kB = NT - 1;
   __shared__ typename Env::Model sm;
@@ -2211,7 +2214,10 @@ __global__ __launch_bounds__(64) void k_im_searchN(ImParams p, int sims0, int si
   int action = 0;
   if (P.h.err == 0 && !im_absorbing(P.N(0, root).info) && P.N(0, root).t > 0) {
     const uint4* const rb = P.root_buf(P.h.root_sel);
-    if (sims0 + sims1 + sims2 + sims3 > 0) {   // the top planner's _nested_sim head (no draws)
+    int any = 0;
+#pragma unroll
+    for (int l = 0; l < NT; ++l) any += sims.s[l];
+    if (any > 0) {   // the top planner's _nested_sim head (no draws)
       P.traverse(0, root);
       if (im_nreg(P.N(0, root).info) == 0) P.expand(0, root);
       if (P.h.root_size == 0 || P.h.root_size < p.extra) P.fail(POMCP_E_UNSUPPORTED);
@@ -2219,7 +2225,7 @@ __global__ __launch_bounds__(64) void k_im_searchN(ImParams p, int sims0, int si
     const ISup* const t2 = P.sup_tab(P.h.sup_sel);
     const uint2* const q2s = P.sup_parts(P.h.sup_sel);
     for (int level = 0; level < NT && P.h.err == 0; ++level) {
-      const int num_sims = level == 0 ? sims0 : level == 1 ? sims1 : level == 2 ? sims2 : sims3;
+      const int num_sims = sims.s[level];
       if (level == kB && num_sims > 0) {   // the root's view, kept current by the backups
         P.rv_put(P.view(0, root));
         P.rv_root = root;

@@ -159,7 +159,7 @@ int intmcp_create(const intmcp_config* cfg, int32_t device, void* hip_stream, in
     return bad(POMCP_E_UNSUPPORTED, "I-NTMCP pucb reads self.action_space (intmcp.py:645): ucb / uniform only");
   if (c.ego_agent < 0 || c.ego_agent > 1 || c.num_trees < 1) return bad(POMCP_E_INVALID, "ego / pairs");
   if (cfg->nesting_level < 0 || cfg->nesting_level > kImMaxT - 1)
-    return bad(POMCP_E_UNSUPPORTED, "nesting levels 0 to 3");
+    return bad(POMCP_E_UNSUPPORTED, "nesting levels 0 to INTMCP_MAX_TREES - 1 (5)");
   if (c.depth_limit < 0 || c.step_limit < 0 || c.num_particles < 1) return bad(POMCP_E_INVALID, "limits");
   if (cfg->max_nodes < 2 || cfg->max_nodes >= (1ll << 28) || cfg->max_stats < c.num_actions ||
       cfg->max_log < 1 || cfg->hash_slots < 16 || (cfg->hash_slots & (cfg->hash_slots - 1)) ||
@@ -347,7 +347,11 @@ int intmcp_update(intmcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_k
       else hipLaunchKernelGGL((k_im_updateN<EnvDriving, NT, false>), ugrid, dim3(64), 0, ctx->stream, ctx->ip); \
     }                                                                                                       \
   } while (0)
-  if (ctx->ip.nt == 4) {   // nesting level 3
+  if (ctx->ip.nt == 6) {   // nesting level 5
+    IM_UPDATE_N(6);
+  } else if (ctx->ip.nt == 5) {   // nesting level 4
+    IM_UPDATE_N(5);
+  } else if (ctx->ip.nt == 4) {   // nesting level 3
     IM_UPDATE_N(4);
   } else if (ctx->ip.nt == 3) {   // nesting level 2
     IM_UPDATE_N(3);
@@ -386,7 +390,9 @@ int intmcp_search_levels(intmcp_ctx* ctx, int32_t level0_sims, int32_t level1_si
     return POMCP_E_INVALID;
   }
   if (ctx->ip.nt >= 3) {
-    const int32_t sims[kImMaxT] = {level0_sims, level1_sims, 0, 0};
+    int32_t sims[kImMaxT] = {};
+    sims[0] = level0_sims;
+    sims[1] = level1_sims;
     return im_searchN(ctx, sims, flags, actions_out);
   }
   IM_TRY(ctx, hipSetDevice(ctx->device));
@@ -410,14 +416,20 @@ static int im_searchN(intmcp_ctx* ctx, const int32_t sims[kImMaxT], int32_t flag
   IM_TRY(ctx, hipSetDevice(ctx->device));
   const dim3 grid(im_blocks(ctx->ip.B));
   const bool pe = ctx->cfg.base.env_id == POMCP_ENV_PURSUIT_EVASION;
-  const int s0 = sims[0], s1 = sims[1], s2 = sims[2], s3 = sims[3];
-  if (ctx->ip.nt == 4) {
-    if (pe) hipLaunchKernelGGL((k_im_searchN<EnvPursuitEvasion, 4>), grid, dim3(64), 0, ctx->stream, ctx->ip, s0, s1, s2, s3, (int)flags);
-    else hipLaunchKernelGGL((k_im_searchN<EnvDriving, 4>), grid, dim3(64), 0, ctx->stream, ctx->ip, s0, s1, s2, s3, (int)flags);
-  } else {
-    if (pe) hipLaunchKernelGGL((k_im_searchN<EnvPursuitEvasion, 3>), grid, dim3(64), 0, ctx->stream, ctx->ip, s0, s1, s2, 0, (int)flags);
-    else hipLaunchKernelGGL((k_im_searchN<EnvDriving, 3>), grid, dim3(64), 0, ctx->stream, ctx->ip, s0, s1, s2, 0, (int)flags);
+  ImSims s{};
+  for (int l = 0; l < ctx->ip.nt; ++l) s.s[l] = sims[l];
+#define IM_SEARCH_N(NT)                                                                                      \
+  do {                                                                                                       \
+    if (pe) hipLaunchKernelGGL((k_im_searchN<EnvPursuitEvasion, NT>), grid, dim3(64), 0, ctx->stream, ctx->ip, s, (int)flags); \
+    else hipLaunchKernelGGL((k_im_searchN<EnvDriving, NT>), grid, dim3(64), 0, ctx->stream, ctx->ip, s, (int)flags); \
+  } while (0)
+  switch (ctx->ip.nt) {   // a tree per nesting level
+    case 6: IM_SEARCH_N(6); break;
+    case 5: IM_SEARCH_N(5); break;
+    case 4: IM_SEARCH_N(4); break;
+    default: IM_SEARCH_N(3); break;
   }
+#undef IM_SEARCH_N
   IM_TRY(ctx, hipGetLastError());
   if (!actions_out) return POMCP_OK;
   int rc = im_fetch_hdr(ctx);
@@ -435,7 +447,7 @@ static int im_searchN(intmcp_ctx* ctx, const int32_t sims[kImMaxT], int32_t flag
 int intmcp_search(intmcp_ctx* ctx, int32_t num_sims, int32_t* actions_out) {
   if (!ctx || num_sims < 0) return POMCP_E_INVALID;
   if (ctx->ip.nt >= 3) {
-    int32_t sims[kImMaxT] = {0, 0, 0, 0};
+    int32_t sims[kImMaxT] = {};
     for (int l = 0; l < ctx->ip.nt; ++l) sims[l] = num_sims;
     return im_searchN(ctx, sims, kImBegin | kImFinal, actions_out);
   }
@@ -452,7 +464,7 @@ int intmcp_search_level(intmcp_ctx* ctx, int32_t level, int32_t sims, int32_t fl
     return POMCP_E_INVALID;
   }
   if (ctx->ip.nt >= 3) {
-    int32_t s[kImMaxT] = {0, 0, 0, 0};
+    int32_t s[kImMaxT] = {};
     s[level] = sims;
     return im_searchN(ctx, s, flags, actions_out);
   }
@@ -692,7 +704,7 @@ int intmcp_get_middle_support(intmcp_ctx* ctx, int32_t pair, int32_t tree, int32
                               int32_t capacity_particles, int32_t* n_particles) {
   if (!ctx || !n_entries || !n_particles || pair < 0 || pair >= ctx->ip.B) return POMCP_E_INVALID;
   if (tree < 1 || tree > ctx->ip.nt - 2) {
-    ctx->err = "get_middle_support: no middle tree " + std::to_string(tree) + " (nesting levels 2, 3)";
+    ctx->err = "get_middle_support: no middle tree " + std::to_string(tree) + " (nesting levels >= 2)";
     return POMCP_E_INVALID;
   }
   int rc = im_fetch_hdr(ctx);

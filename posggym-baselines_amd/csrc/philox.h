@@ -1,7 +1,14 @@
-// Philox4x32-10 counter-based RNG streams (host + device).
+// Philox4x32-7 counter-based RNG streams (host + device).
 //
 // Draw j of stream s under key (seed, tree) is word (j & 3) of
-// philox4x32(ctr = {j >> 2, 0, s, seed >> 32}, key = {seed & 0xffffffff, tree}).
+// philox4x32(ctr = {j >> 2, 0, s, seed >> 32}, key = {seed & 0xffffffff, tree}),
+// Random123's Philox4x32 with 7 rounds (round 6 of the build; rounds 1-5 used
+// 10).  Random123 (Salmon et al., SC'11) reports Philox4x32-7 passing TestU01's
+// BigCrush with no failures ("Crush-resistant": 7 is the fewest rounds that
+// do) and recommends 10 only as a safety margin; a planner's draws are
+// simulation noise, not cryptography.  7 rounds are 30% less Philox work in
+// k_search (10% of a simulation by phase timing: +3% measured); the Random123
+// known answers for 7 and 10 rounds pin the function (tests/test_oracle.py).
 // uniform int in [0, n) = (u32 * n) >> 32; uniform float = u32 * 2^-32.
 // This is the build's definition of "the reference's RNG" (SURVEY Appendix B):
 // every random draw on the hot path (planner Random(seed), global `random`,
@@ -31,10 +38,18 @@ enum Stream : uint32_t {
   S_ENV_POLICY_BASE = 40,
 };
 
+// I-NTMCP: the middle planner of level l (1 <= l < the nesting level) draws its
+// random.Random(seed) on S_BELIEF_MID + l - 1 for levels 1-3 (5, 6, 7) and on
+// 16 + l beyond (20, 21: clear of the agents' action streams 8 + i); the
+// oracle's belief_stream (oracle/intmcp.py) is the same map.
+PB_HD constexpr uint32_t belief_mid_stream(int level) {
+  return level <= 3 ? (uint32_t)S_BELIEF_MID + (uint32_t)level - 1u : 16u + (uint32_t)level;
+}
+
 // PB_PHILOX_ROUNDS: ablation builds only (tools/ablate.sh measures the RNG's
-// share of k_search); any other value breaks parity.
+// share of k_search); any other value breaks parity with oracle/rng.py.
 #ifndef PB_PHILOX_ROUNDS
-#define PB_PHILOX_ROUNDS 10
+#define PB_PHILOX_ROUNDS 7
 #endif
 PB_HD void philox4x32(uint32_t c[4], uint32_t k0, uint32_t k1) {
 #pragma unroll

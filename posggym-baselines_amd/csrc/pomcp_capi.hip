@@ -21,6 +21,7 @@
 #include "host_api.cpp"
 #include "pomcp_search.hip"
 #include "pomcp_search_lds.hip"
+#include "../../include/intmcp.h"   // (INTMCP_MAX_TREES)
 #include "intmcp.hip"
 #include "../../include/pomcp_debug.h"
 

@@ -866,7 +866,12 @@ __device__ __forceinline__ uint64_t ld_agent_u64(const uint64_t* p) {
   } while (0)
 #endif
 template <class Env>
-__global__ __launch_bounds__(64 * kLogWaves) void k_compact_log(DevParams p) {
+#ifdef PB_LOG_WPE   // A/B builds only: waves per SIMD the register allocation must allow
+#define PB_LOG_ATTR __attribute__((amdgpu_waves_per_eu(PB_LOG_WPE)))
+#else
+#define PB_LOG_ATTR
+#endif
+__global__ __launch_bounds__(64 * kLogWaves) PB_LOG_ATTR void k_compact_log(DevParams p) {
   __shared__ typename Env::Model sm;
   stage_model(p.model, sm);
   constexpr int T = 64 * kLogWaves;

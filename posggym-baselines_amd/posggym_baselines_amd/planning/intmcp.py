@@ -1,5 +1,5 @@
 """I-NTMCP drop-in: the reference's ``INTMCP`` API (``intmcp.py:22-994``) at
-nesting levels 0 to 3 with two agents, the planners' trees, beliefs and
+nesting levels 0 to 5 with two agents, the planners' trees, beliefs and
 generative model on the GPU (``include/intmcp.h``, ``csrc/intmcp.hip``).
 
 Public surface kept from the reference: ``INTMCP.initialize(model,
@@ -13,7 +13,7 @@ same device state), ``search_policies``, ``action_spaces``, ``step_limit``,
 ``BatchedINTMCP`` runs many independent planner pairs in one launch (BASELINE
 config 5: nested trees as a batched launch).
 
-Scope (DESIGN.md "I-NTMCP"): nesting levels 0 to 3, random or
+Scope (DESIGN.md "I-NTMCP"): nesting levels 0 to 5, random or
 fixed-distribution search policies (``RandomSearchPolicy`` /
 ``SearchPolicyWrapper(FixedDistributionPolicy)`` per level and agent: they draw
 the rollouts and the other agent's action at an unvisited history; the node
@@ -52,6 +52,8 @@ from posggym_baselines_amd.planning.utils import PlanningStatTracker
 INT32_MAX = 2**31 - 1
 # a node's device bytes: its 128 B line + six 32 B action records (csrc/intmcp.hip kImBlock)
 INTMCP_NODE_BYTES = 320
+MAX_TREES = 6                  # include/intmcp.h INTMCP_MAX_TREES: a tree per nesting level
+MAX_NESTING = MAX_TREES - 1
 
 
 @dataclass
@@ -170,8 +172,8 @@ class IntmcpEngine:
         self._emodel = engine_model(model)
         self.config = config
         self.num_pairs = int(num_pairs)
-        if nesting_level not in (0, 1, 2, 3):
-            raise NotImplementedError("the GPU I-NTMCP engine runs nesting levels 0 to 3")
+        if not 0 <= int(nesting_level) <= MAX_NESTING:
+            raise NotImplementedError(f"the GPU I-NTMCP engine runs nesting levels 0 to {MAX_NESTING}")
         self.nesting_level = int(nesting_level)
         self.ego = model.possible_agents.index(agent_id)
         self.A = model.action_spaces[agent_id].n
@@ -309,8 +311,8 @@ class IntmcpEngine:
         return out
 
     def tree_counts(self):
-        """[pairs][4 trees][nodes, log records, stats] (``intmcp_get_tree_counts``)."""
-        out = np.zeros((self.num_pairs, 4, 3), dtype=np.int32)
+        """[pairs][MAX_TREES][nodes, log records, stats] (``intmcp_get_tree_counts``)."""
+        out = np.zeros((self.num_pairs, MAX_TREES, 3), dtype=np.int32)
         self._check(self._lib.intmcp_get_tree_counts(self._ctx, out.ctypes.data_as(C.POINTER(C.c_int32))),
                     "get_tree_counts")
         return out
@@ -338,7 +340,7 @@ class IntmcpEngine:
         reinv = int(math.ceil(cfg.reinvigoration_sample_limit_factor * target)) + target
         reserve = 2 * reinv + 2 * target + 8        # plan_intmcp_capacities' per-update share
         room = INT32_MAX
-        if getattr(self, "nesting_level", 1) >= 2:   # 3 or 4 trees: intmcp_get_tree_counts
+        if getattr(self, "nesting_level", 1) >= 2:   # 3+ trees: intmcp_get_tree_counts
             cnt = self.tree_counts()
             for p in range(self.num_pairs):
                 for t in range(self.nesting_level + 1):
@@ -480,8 +482,8 @@ class INTMCP:
     def __init__(self, model, agent_id: str, config: MCTSConfig, nesting_level: int,
                  other_agent_policies=None, search_policies=None, *,
                  num_sims: Optional[int] = None):
-        if nesting_level not in (0, 1, 2, 3):
-            raise NotImplementedError("the GPU I-NTMCP engine runs nesting levels 0 to 3")
+        if not 0 <= int(nesting_level) <= MAX_NESTING:
+            raise NotImplementedError(f"the GPU I-NTMCP engine runs nesting levels 0 to {MAX_NESTING}")
         from posggym_baselines_amd.planning.ipomcp import search_policy_probs
         assert agent_id in model.possible_agents
         # {level: {agent: policy}} (INTMCP.initialize) or one {agent: policy}

@@ -125,6 +125,20 @@ INTMCP3_CASES = {
 }
 
 
+# I-NTMCP nesting_level=4 and 5: chains of five and six planners (the same
+# recursion, intmcp.py:949-994); search_time_limit = 0.1 * (nesting_level + 1).
+# Level 5's middle planners of levels 4 draw on the streams past the agents'
+# action streams (oracle/intmcp.py belief_stream).
+INTMCP4_CFG = dict(TEST_CFG, search_time_limit=0.5, state_belief_only=False)
+INTMCP5_CFG = dict(TEST_CFG, search_time_limit=0.6, state_belief_only=False)
+INTMCP45_CASES = {
+    # name: (nesting level, cfg overrides, num_sims, [(seed, env_seed)], ego, max_steps, env)
+    "intmcp4_ucb": (4, {}, 12, [(80, 80)], "0", 8, "Driving-v1"),
+    "intmcp4_pe": (4, {}, 10, [(81, 81)], "1", 10, "PursuitEvasion-v1"),
+    "intmcp5_ucb": (5, {}, 8, [(82, 82)], "1", 6, "Driving-v1"),
+}
+
+
 # I-NTMCP with caller-supplied search policies (intmcp.py:956-971):
 # {level: {agent: probs}} -> SearchPolicyWrapper(FixedDistributionPolicy) on
 # the agent's action stream, RandomSearchPolicy for the agents left out.
@@ -150,6 +164,9 @@ def run_intmcp_case(name):
     if name in INTMCP_SP_CASES:
         level, sp, num_sims, pairs, ego, max_steps, env = INTMCP_SP_CASES[name]
         over, base = {}, (INTMCP0_CFG, INTMCP_CFG, INTMCP2_CFG, INTMCP3_CFG)[level]
+    elif name in INTMCP45_CASES:
+        level, over, num_sims, pairs, ego, max_steps, env = INTMCP45_CASES[name]
+        base = INTMCP4_CFG if level == 4 else INTMCP5_CFG
     elif name in INTMCP3_CASES:
         over, num_sims, pairs, ego, max_steps, env = INTMCP3_CASES[name]
         base, level = INTMCP3_CFG, 3
@@ -442,7 +459,7 @@ def main(only=None, out_dir=HERE):
         n = sum(len(e["records"]) for e in data["episodes"])
         print(f"{name}: {len(data['episodes'])} episodes, {n} records")
     for name in (list(INTMCP_CASES) + list(INTMCP0_CASES) + list(INTMCP2_CASES)
-                 + list(INTMCP3_CASES) + list(INTMCP_SP_CASES) if only is None
+                 + list(INTMCP3_CASES) + list(INTMCP45_CASES) + list(INTMCP_SP_CASES) if only is None
                  else (only if isinstance(only, list) else ())):
         data = run_intmcp_case(name)
         _write(out_dir, name, data)

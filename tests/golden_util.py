@@ -48,6 +48,9 @@ INTMCP2_CASES = ["intmcp2_ucb", "intmcp2_ego1_uniform", "intmcp2_pe"]
 # I-NTMCP nesting_level=3 (make_golden.py INTMCP3_CASES): four trees
 INTMCP3_CASES = ["intmcp3_ucb", "intmcp3_pe"]
 
+# I-NTMCP nesting_level=4 / 5 (make_golden.py INTMCP45_CASES): five / six trees
+INTMCP45_CASES = ["intmcp4_ucb", "intmcp4_pe", "intmcp5_ucb"]
+
 
 def search_probs(data):
     """A golden's {level: {agent: probs}} with integer levels (None if absent)."""

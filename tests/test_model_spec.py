@@ -104,7 +104,7 @@ def test_intmcp_nesting2_capacities_and_headroom():
     target = cfg.num_particles + cfg.extra_particles
     reserve = 2 * (int(-(-cfg.reinvigoration_sample_limit_factor * target // 1)) + target) \
         + 2 * target + 8
-    counts = np.zeros((1, 4, 3), dtype=np.int32)
+    counts = np.zeros((1, M.MAX_TREES, 3), dtype=np.int32)
     counts[0, 2, 0] = 1000     # the level-0 tree holds the most nodes
     eng.tree_counts = lambda: counts
     assert eng.headroom() == (caps.max_nodes - 1000 - reserve) // L
@@ -134,7 +134,7 @@ def test_intmcp_nesting3_capacities_and_headroom():
     target = cfg.num_particles + cfg.extra_particles
     reserve = 2 * (int(-(-cfg.reinvigoration_sample_limit_factor * target // 1)) + target) \
         + 2 * target + 8
-    counts = np.zeros((1, 4, 3), dtype=np.int32)
+    counts = np.zeros((1, M.MAX_TREES, 3), dtype=np.int32)
     counts[0, 3, 1] = 2000     # the level-0 tree's log is the fullest
     eng.tree_counts = lambda: counts
     assert eng.headroom() == (caps.max_log - 2000 - reserve) // L

@@ -4,12 +4,18 @@ import pytest
 from golden_util import (EPISODE_CASES, IPOMCP_CASES, case_env, case_max_steps, cfg_kwargs, load,
                          search_probs)
 from oracle.pomcp import OracleConfig
-from oracle.rng import Streams, StreamRandom, philox4x32_10
+from oracle.rng import PHILOX_ROUNDS, Streams, StreamRandom, philox4x32, philox4x32_10
 from oracle.run import oracle_episode
 
 
 def test_philox_known_answers():
-    # Random123 kat_vectors for philox4x32_10
+    # Random123 kat_vectors for philox4x32 7 rounds (the build's streams since
+    # round 6, csrc/philox.h) ...
+    assert PHILOX_ROUNDS == 7
+    assert philox4x32(0, 0, 0, 0, 0, 0) == (0x5F6FB709, 0x0D893F64, 0x4F121F81, 0x4F730A48)
+    assert philox4x32(0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344,
+                      0xA4093822, 0x299F31D0) == (0x4DFCCABA, 0x190A87F0, 0xC47362BA, 0xB6B5242A)
+    # ... and for philox4x32_10 (the same round function run 10 rounds)
     assert philox4x32_10(0, 0, 0, 0, 0, 0) == (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)
     m = 0xFFFFFFFF
     assert philox4x32_10(m, m, m, m, m, m) == (0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD)
@@ -20,8 +26,8 @@ def test_philox_known_answers():
 def test_stream_layout():
     s = Streams(5, 3)
     words = [s.u32(1) for _ in range(6)]
-    b0 = philox4x32_10(0, 0, 1, 0, 5, 3)
-    b1 = philox4x32_10(1, 0, 1, 0, 5, 3)
+    b0 = philox4x32(0, 0, 1, 0, 5, 3)
+    b1 = philox4x32(1, 0, 1, 0, 5, 3)
     assert words == list(b0) + list(b1[:2])
     assert s.counters() == {1: 6}
     # randint is a multiply-shift of one word
@@ -78,7 +84,8 @@ def test_oracle_matches_reference_goldens(case):
                                   "intmcp0_deep", "intmcp0_pe", "intmcp_sp_ucb",
                                   "intmcp0_sp_ego1", "intmcp_sp_pe", "intmcp2_ucb",
                                   "intmcp2_ego1_uniform", "intmcp2_pe", "intmcp2_sp_ucb",
-                                  "intmcp3_ucb", "intmcp3_pe"])
+                                  "intmcp3_ucb", "intmcp3_pe", "intmcp4_ucb", "intmcp4_pe",
+                                  "intmcp5_ucb"])
 def test_intmcp_oracle_matches_reference_goldens(case):
     """I-NTMCP nesting 1 (BASELINE config 5) and nesting 0: the oracle
     restatement against the real reference planner's records (root children,
