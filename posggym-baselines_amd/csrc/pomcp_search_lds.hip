@@ -946,7 +946,9 @@ __global__ __launch_bounds__(64 * (NP + 1)) void k_search_lds(DevParams p, int n
   }
   // _final_action_selection (mcts.py:565-600) ends get_action; a search split
   // over several launches (final_sel = 0 for all but the last) draws it once
-  int action = -1;
+  // an absorbing root is not searched and get_action returns action_space[0]
+  // (mcts.py:270-272); -1 = no action (an error, or not the final launch)
+  int action = err == 0 && root_abs && final_sel ? 0 : -1;
   if (have && final_sel) {
     action = 0;
     uint32_t ties = 0;

@@ -503,9 +503,9 @@ def test_reinvigoration_many_particles(time_limit):
     S, K, B = 32, 3, 5
     seeds, exp = [], []
     s = 9100
-    while len(seeds) < B:
+    while len(seeds) < B:   # (a root that turned absorbing is not reinvigorated: skip)
         trace, recs = oracle_episode(cfg, S, s, tree=len(seeds), max_steps=K)
-        if trace["len"] >= K and all(r["searched"] for r in recs):
+        if trace["len"] >= K and all(r["searched"] and r.get("num_sims") for r in recs):
             seeds.append(s)
             exp.append(recs)
         s += 1
