@@ -546,7 +546,7 @@ def run_pomcp(dev, *, env, B, S, K, base_cfg, tm, steps, warmup, seed=0, max_blo
                                overflow_slots=1024)
         caps.max_belief = min(caps.max_belief, max(S, 2 * n_target) + n_target + 64)
         free = torch.cuda.mem_get_info(dev)[0]
-        while B > 1024 and caps.bytes_per_tree(A) * B > 0.92 * free:
+        while B > 1024 and caps.bytes_per_tree(A, reroot=True) * B > 0.92 * free:
             B //= 2
             note = f" (halved to fit {free / 2**30:.0f} GiB)"
     else:

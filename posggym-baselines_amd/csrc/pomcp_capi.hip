@@ -62,6 +62,12 @@ struct pomcp_ctx {
   // materialises those children (a record's absorbing flag must not race an
   // eager arrival's, mcts.py:370)
   bool defer_pending = false;
+  // the re-root's log scan: the streaming kernels (k_log_filter + the
+  // materialising pass) unless POMCP_LOG_SCAN=legacy (one workgroup per log,
+  // k_compact_log: A/B and fallback); the look-back tags' epoch
+  bool log_scan_legacy = false;
+  uint32_t lf_epoch = 0;
+  int lf_grid = 0;
 };
 
 // Wave-per-tree search (k_search_lds) for batches up to this many trees: one
@@ -406,6 +412,30 @@ static int ensure_compaction_scratch(pomcp_ctx* ctx) {
   d.ovf_new = reinterpret_cast<int32_t*>(p);
   if ((rc = dev_alloc(ctx, &p, sizeof(OvfSlot) * (size_t)(B * d.H))) != POMCP_OK) return rc;
   d.ovf_tmp = reinterpret_cast<OvfSlot*>(p);
+  if ((rc = dev_alloc(ctx, &p, sizeof(uint4) * (size_t)B)) != POMCP_OK) return rc;
+  d.scan_info = reinterpret_cast<uint4*>(p);
+  // the streaming scan's look-back records: every wave log's capacity in
+  // segments; zeroed (tag epoch 0 is never current)
+  const int waves = search_waves((int)B);
+  d.lf_nseg = (int32_t)((kWave * d.Np + kLfSeg - 1) / kLfSeg);
+  const size_t nd = sizeof(LfDesc) * (size_t)waves * (size_t)((d.lf_nseg + kLfChunk - 1) / kLfChunk);
+  if ((rc = dev_alloc(ctx, &p, nd)) != POMCP_OK) return rc;
+  d.lf_desc = reinterpret_cast<LfDesc*>(p);
+  if ((rc = dev_alloc(ctx, &p, 2 * sizeof(uint32_t))) != POMCP_OK) return rc;
+  d.lf_fail = reinterpret_cast<uint32_t*>(p);
+  HIP_TRY(ctx, hipMemsetAsync(d.lf_desc, 0, nd, ctx->stream));
+  ctx->lf_epoch = 0;
+  const char* ls = std::getenv("POMCP_LOG_SCAN");
+  ctx->log_scan_legacy = ls != nullptr && std::string(ls) == "legacy";
+  // the persistent grid: as many workgroups as are resident at once
+  int per_cu = 0, ncu = 0;
+  HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                   &per_cu, reinterpret_cast<const void*>(d.env == POMCP_ENV_PURSUIT_EVASION
+                                                              ? &k_log_filter<EnvPursuitEvasion>
+                                                              : &k_log_filter<EnvDriving>),
+                   kLfThreads, 0));
+  HIP_TRY(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+  ctx->lf_grid = (per_cu > 0 ? per_cu : 1) * (ncu > 0 ? ncu : 1);
   return POMCP_OK;
 }
 
@@ -434,15 +464,43 @@ int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_key
     if (rc != POMCP_OK) return rc;
     hipLaunchKernelGGL(k_compact, dim3(grid_blocks(B)), dim3(256), 0, ctx->stream, ctx->dp);
     HIP_TRY(ctx, hipGetLastError());
-    PB_ENV_LAUNCH(ctx, k_compact_log, dim3((unsigned)search_waves(B)), dim3(64 * kLogWaves),
-                  ctx->dp);
+    if (ctx->log_scan_legacy) {
+      PB_ENV_LAUNCH(ctx, k_compact_log, dim3((unsigned)search_waves(B)), dim3(64 * kLogWaves),
+                    ctx->dp);
+    } else {
+      // the streaming scan: the filter over every log's segments, then the
+      // materialising pass over the kept records
+      if (++ctx->lf_epoch >= (1u << 30)) {   // (tags hold 30 bits: start over on zeroed records)
+        HIP_TRY(ctx, hipMemsetAsync(ctx->dp.lf_desc, 0,
+                                    sizeof(LfDesc) * (size_t)search_waves(B) *
+                                        (size_t)((ctx->dp.lf_nseg + kLfChunk - 1) / kLfChunk),
+                                    ctx->stream));
+        ctx->lf_epoch = 1;
+      }
+      ctx->dp.lf_epoch = ctx->lf_epoch;
+      HIP_TRY(ctx, hipMemsetAsync(ctx->dp.lf_fail, 0, 2 * sizeof(uint32_t), ctx->stream));
+      PB_ENV_LAUNCH(ctx, k_log_filter, dim3((unsigned)ctx->lf_grid), dim3(kLfThreads), ctx->dp,
+                    search_waves(B));
+      HIP_TRY(ctx, hipGetLastError());
+      if (ctx->dp.env == POMCP_ENV_PURSUIT_EVASION)
+        hipLaunchKernelGGL((k_compact_log<EnvPursuitEvasion, true>), dim3((unsigned)search_waves(B)),
+                           dim3(64 * kMatWaves), 0, ctx->stream, ctx->dp);
+      else
+        hipLaunchKernelGGL((k_compact_log<EnvDriving, true>), dim3((unsigned)search_waves(B)),
+                           dim3(64 * kMatWaves), 0, ctx->stream, ctx->dp);
+    }
     HIP_TRY(ctx, hipGetLastError());
   }
   PB_ENV_LAUNCH(ctx, k_update, dim3(grid_blocks(B)), dim3(256), ctx->dp);
   HIP_TRY(ctx, hipGetLastError());
   HIP_TRY(ctx, hipMemcpyAsync(ctx->host_upd.data(), ctx->dp.upd_out, sizeof(int32_t) * 2 * B,
                               hipMemcpyDeviceToHost, ctx->stream));
+  uint32_t lf_fail = 0u;
+  if (reroot && !ctx->log_scan_legacy)
+    HIP_TRY(ctx, hipMemcpyAsync(&lf_fail, ctx->dp.lf_fail, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                ctx->stream));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  if (lf_fail != 0u) return fail(ctx, POMCP_E_HIP, "update: the log scan's look-back gave up");
   ctx->defer_pending = false;   // k_compact_log materialised the surviving deferred children
   if (root_absorbing_out)
     for (int t = 0; t < B; ++t) root_absorbing_out[t] = ctx->host_upd[2 * t];
@@ -994,9 +1052,6 @@ int pomcp_debug_exp(const double* x, int32_t n, double* out) {
 }
 
 
-// Debug: use only the first n (1..6) inline obs slots of every action node, so
-// the overflow map serves the rest (tests of that path: the models here rarely
-// give an action node more than 6 obs children).  Before the first search.
 // Debug: k_search's fast-selection margin (pomcp_debug.h); >= 1e-12 keeps
 // results exact, larger sends more selections to the exact FP64 scores
 // (counted in pomcp_root_stats.n_exact_selects).
@@ -1006,6 +1061,9 @@ int pomcp_debug_set_select_margin(pomcp_ctx* ctx, double rel) {
   return POMCP_OK;
 }
 
+// Debug: use only the first n (1..6) inline obs slots of every action node, so
+// the overflow map serves the rest (tests of that path: the models here rarely
+// give an action node more than 6 obs children).  Before the first search.
 int pomcp_debug_set_inline_slots(pomcp_ctx* ctx, int32_t n) {
   if (!ctx || n < 1 || n > kSlots) return POMCP_E_INVALID;
   ctx->dp.islots = n;

@@ -204,6 +204,17 @@ struct TreeHdr {
   uint32_t ctr_mix;    // type-based: S_MIXTURE draws (the other agent's policy per particle)
 };
 
+// Streaming re-root scan (k_log_filter, round 6): one look-back record per
+// segment of a search wave's log.  `tag` = epoch << 2 | state (1: the
+// segment's own counts published, 2: the counts through it); the counts are
+// stored write-through before the tag (MI355X guide: sc1 payload, drained,
+// then one sc1 flag store; the reader polls the tag with sc1 loads).
+struct alignas(16) LfDesc {
+  uint32_t tag, kept_agg, kept_inc, pad;
+  uint32_t ex_agg[64];   // extracted records of tree lane l in the segment ...
+  uint32_t ex_inc[64];   // ... and in the segments up to it
+};
+
 struct DevParams {
   int32_t B, A, ego, other, sel, depth_limit, step_limit, n_target, has_kb, ncells;
   double discount, c, pucb_f, limit_factor, kb_min, kb_max;
@@ -254,6 +265,16 @@ struct DevParams {
   int32_t* cpar;        // [B][Nb]
   int32_t* ovf_new;     // [B][H]
   OvfSlot* ovf_tmp;     // [B][H]
+  // the streaming re-root scan (k_log_filter / k_log_mat, pomcp_kernels.hip),
+  // allocated on the first re-root: per tree {want, 1 + old blocks (0: not
+  // re-rooted), end of the next belief << 31 | its room, t of the new root}
+  // (k_compact), the look-back records of every wave's log segments
+  uint4* scan_info;     // [B]
+  LfDesc* lf_desc;      // [waves][lf_nseg]
+  int32_t lf_nseg;      // segments per wave log (its capacity / kLfSeg)
+  uint32_t lf_epoch;    // this re-root's tag epoch (1, 2, ...; older tags are stale)
+  uint32_t* lf_fail;    // [2] a look-back wait that gave up (never expected: POMCP_E_HIP);
+                        // the segment claims of the running k_log_filter
 };
 
 // Root belief region of a tree: Nr records holding the current root belief and

@@ -411,6 +411,10 @@ __global__ __launch_bounds__(256) void k_reroot_child(DevParams p) {
 // 4 -> 16 waves 142 -> 130 ms (2 waves 237 ms, profiles/r5w_log_waves_ab.txt);
 // at 16 waves 4 -> 3 records 115 -> 107.6 ms with 128 VGPRs (the most 1,024
 // threads allow; 2 records 111 ms, profiles/r5zc_compact_log_ab.txt)
+// LDS: k_compact_log takes ~118-123 KB of static LDS at 16 waves (the visits
+// table / deferred-children hash, the places queue, the wave's cmap): it needs
+// gfx950's 160 KB per workgroup -- a target with 64 KB fails to compile (the
+// static allocation exceeds the limit), it cannot launch wrongly sized.
 #ifndef PB_LOG_WAVES   // A/B builds only
 #define PB_LOG_WAVES 16
 #endif
@@ -419,6 +423,19 @@ constexpr int kLogWaves = PB_LOG_WAVES;
 #define PB_LOG_RECS 3
 #endif
 constexpr int kLogRecs = PB_LOG_RECS;   // records per thread per pass
+// The streaming scan's materialising pass (k_compact_log<Env, true>): 8 waves,
+// so two of its workgroups share a CU (round 6 A/B: 16 -> 8 waves with two
+// per CU took the legacy scan's update 211 -> 177 ms,
+// profiles/r6c_philox7_and_logscan_ab.txt)
+#ifndef PB_MAT_WAVES   // A/B builds only
+#define PB_MAT_WAVES 8
+#endif
+constexpr int kMatWaves = PB_MAT_WAVES;
+// The streaming scan's segments (k_log_filter): 512 threads x 4 records
+constexpr int kLfThreads = 512;
+constexpr int kLfRecs = 4;
+constexpr int kLfSeg = kLfThreads * kLfRecs;
+constexpr int kLfChunk = 8;   // consecutive segments of one log per claim (and look-back record)
 
 // The lanes whose 6-bit key equals this lane's, among the active ones (a
 // match-any on the tree lane of a log record: 6 ballots).
@@ -638,8 +655,17 @@ __global__ __launch_bounds__(256) void k_compact(DevParams p) {
   const bool on = uni(h.error) == 0 && uni(wi.w) != 0;
   const int nb = uni(h.n_blocks);
   // read by k_compact_log: 0 = not re-rooted, else 1 + the blocks before the
-  // compaction (the entries of cmap it stages in LDS)
-  if (lane == 0) p.cnt[tree] = on ? 1 + nb : 0;
+  // compaction (the entries of cmap it stages in LDS); the streaming scan's
+  // per-tree record (DevParams::scan_info)
+  if (lane == 0) {
+    p.cnt[tree] = on ? 1 + nb : 0;
+    if (p.scan_info != nullptr) {
+      const uint32_t nsel = (uint32_t)(h.belief_sel ^ 1);
+      const uint32_t room = (uint32_t)(p.Nr - (int64_t)h.belief_size);   // (< 2^31: pomcp_create)
+      p.scan_info[tree] = make_uint4(p.want[tree], on ? 1u + (uint32_t)nb : 0u, (nsel << 31) | room,
+                                     (uint32_t)h.root_t + 1u);
+    }
+  }
   if (!on) return;
   const int A = p.A;
   const int R = uni(wi.x);   // the new root's block (-1: a leaf)
@@ -865,16 +891,22 @@ __device__ __forceinline__ uint64_t ld_agent_u64(const uint64_t* p) {
   do {               \
   } while (0)
 #endif
-template <class Env>
+// kMatOnly (the streaming scan's second kernel, k_log_filter below): the log
+// has been filtered and relabelled already; this pass only counts every
+// tree's records and materialises the deferred children of the re-rooted
+// trees in log order (records stay where they are: a queued place is the
+// record's own), the extracted counts come from the look-back records.
 #ifdef PB_LOG_WPE   // A/B builds only: waves per SIMD the register allocation must allow
 #define PB_LOG_ATTR __attribute__((amdgpu_waves_per_eu(PB_LOG_WPE)))
 #else
 #define PB_LOG_ATTR
 #endif
-__global__ __launch_bounds__(64 * kLogWaves) PB_LOG_ATTR void k_compact_log(DevParams p) {
+template <class Env, bool kMatOnly = false>
+__global__ __launch_bounds__(64 * (kMatOnly ? kMatWaves : kLogWaves)) PB_LOG_ATTR void k_compact_log(DevParams p) {
+  constexpr int LW = kMatOnly ? kMatWaves : kLogWaves;   // waves of the workgroup
   __shared__ typename Env::Model sm;
   stage_model(p.model, sm);
-  constexpr int T = 64 * kLogWaves;
+  constexpr int T = 64 * LW;
   const int sw = blockIdx.x;
   const int w = (int)(threadIdx.x >> 6);
   const int lane = lane_id();
@@ -887,11 +919,11 @@ __global__ __launch_bounds__(64 * kLogWaves) PB_LOG_ATTR void k_compact_log(DevP
   __shared__ int64_t xdst[kWave];   // the tree's belief region ...
   __shared__ int32_t xsel[kWave];   // ... the end the new belief grows from ...
   __shared__ int32_t xroom[kWave];  // ... and its room (the current belief holds the rest)
-  __shared__ uint8_t xw[kLogRecs][kLogWaves][kWave];   // this pass's extracted records per
+  __shared__ uint8_t xw[kLogRecs][LW][kWave];   // this pass's extracted records per
                                                       // sub-pass, wave and tree (<= 64)
   __shared__ int32_t made[kWave];   // children materialised per tree
   __shared__ int32_t bad[kWave];    // overflow map full
-  __shared__ int32_t wsum[kLogWaves];
+  __shared__ int32_t wsum[LW];
   __shared__ int32_t ovq[T];        // threads whose child goes to the overflow map, in order
   __shared__ int32_t ovres[T];      // per thread: its overflow entry (-1: map full)
   __shared__ uint32_t ovd[5][T];    // per thread: tree lane, action node, key lo / hi, done
@@ -963,12 +995,24 @@ __global__ __launch_bounds__(64 * kLogWaves) PB_LOG_ATTR void k_compact_log(DevP
     xsel[lane] = h.belief_sel ^ 1;
     xroom[lane] = (int32_t)(p.Nr - (int64_t)h.belief_size);
   }
+  // the streaming scan: the kept records and each tree's extracted count from
+  // the last segment's look-back record
+  uint32_t n_mat = 0u;
+  if constexpr (kMatOnly) {
+    const uint32_t n0 = p.wlog[sw];
+    if (n0 > 0u) {
+      const int nchunk = (p.lf_nseg + kLfChunk - 1) / kLfChunk;
+      const LfDesc& d = p.lf_desc[(int64_t)sw * nchunk + (int64_t)((n0 - 1u) / kLfSeg / kLfChunk)];
+      n_mat = d.kept_inc;
+      if (w == 0) xcnt[lane] = (int32_t)d.ex_inc[lane];
+    }
+  }
   vclear();
   __syncthreads();
 #ifdef PB_NO_CMAP_LDS   // A/B builds only: classify from the global cmap
   const bool cml_on = false;
 #else
-  const bool cml_on = cml_ok != 0;
+  const bool cml_on = !kMatOnly && cml_ok != 0;
 #endif
   if (cml_on) {   // entry e belongs to the tree lane L with cmo[L] <= e < cmo[L + 1]
     for (int e = t; e < cmo[kWave]; e += T) {
@@ -994,7 +1038,7 @@ __global__ __launch_bounds__(64 * kLogWaves) PB_LOG_ATTR void k_compact_log(DevP
     __syncthreads();
     int pre = 0, tot = 0;
 #pragma unroll
-    for (int v = 0; v < kLogWaves; ++v) {
+    for (int v = 0; v < LW; ++v) {
       pre += v < w ? wsum[v] : 0;
       tot += wsum[v];
     }
@@ -1003,7 +1047,7 @@ __global__ __launch_bounds__(64 * kLogWaves) PB_LOG_ATTR void k_compact_log(DevP
     return pre + __popcll(m & ((1ull << lane) - 1ull));
   };
   const WaveLog wl(p.plog, p.Np, sw, p.tm);
-  const uint32_t n = p.wlog[sw];
+  const uint32_t n = kMatOnly ? n_mat : p.wlog[sw];
   const uint32_t A = (uint32_t)p.A;
   // x / A by a multiply: amag = ceil(2^32 / A) is exact for x < 2^32 / A
   // (x < 2^26: node ids, pomcp_create; A <= 5)
@@ -1012,8 +1056,8 @@ __global__ __launch_bounds__(64 * kLogWaves) PB_LOG_ATTR void k_compact_log(DevP
   const int64_t bstride = blk_stride_lines(p.lines);
   constexpr int R = kLogRecs;
   const uint64_t below = (1ull << lane) - 1ull;
-  __shared__ int32_t ksum[R][kLogWaves];   // kept records per sub-pass and wave
-  __shared__ int32_t msum[R][kLogWaves];   // deferred records to materialise, likewise
+  __shared__ int32_t ksum[R][LW];   // kept records per sub-pass and wave
+  __shared__ int32_t msum[R][LW];   // deferred records to materialise, likewise
   // A deferred record's child, found or inserted (inline slots by CAS, else the
   // overflow map in log order), its absorbing flag set by the last arrival of
   // the chunk and its visits raised by the chunk's arrivals (one atomic per
@@ -1244,8 +1288,12 @@ __global__ __launch_bounds__(64 * kLogWaves) PB_LOG_ATTR void k_compact_log(DevP
     rn[j] = LogRec{0u, 0u, 0u};
     auxn[j] = 0u;
     if (i < n) {
-      rn[j] = wl.load(i);
-      if (p.tm) auxn[j] = wl.aux[i];
+      if constexpr (kMatOnly) {   // (ids only: the flush reads a deferred record's state)
+        rn[j].id = wl.id[i];
+      } else {
+        rn[j] = wl.load(i);
+        if (p.tm) auxn[j] = wl.aux[i];
+      }
     }
   }
   for (uint32_t base = 0; base < n; base += (uint32_t)(R * T)) {
@@ -1257,8 +1305,12 @@ __global__ __launch_bounds__(64 * kLogWaves) PB_LOG_ATTR void k_compact_log(DevP
       aux[j] = auxn[j];
       const uint32_t i2 = base + (uint32_t)((R + j) * T + t);
       if (i2 < n) {
-        rn[j] = wl.load(i2);
-        if (p.tm) auxn[j] = wl.aux[i2];
+        if constexpr (kMatOnly) {
+          rn[j].id = wl.id[i2];
+        } else {
+          rn[j] = wl.load(i2);
+          if (p.tm) auxn[j] = wl.aux[i2];
+        }
       }
     }
     bool keep[R], mat[R], ex[R];
@@ -1281,8 +1333,14 @@ __global__ __launch_bounds__(64 * kLogWaves) PB_LOG_ATTR void k_compact_log(DevP
       if (i < n) {
         l[j] = r[j].id >> kIdBits;
         const uint32_t id = r[j].id & kIdMask;
-        ex[j] = want[l[j]] == r[j].id;   // a record of the new root (never kept below)
         keep[j] = true;
+        if constexpr (kMatOnly) {   // filtered and relabelled by k_log_filter
+          if (act[l[j]] && id >= p.cut_base && id < kIdMask) {
+            mat[j] = true;
+            nani[j] = id - p.cut_base;
+          }
+        } else {
+        ex[j] = want[l[j]] == r[j].id;   // a record of the new root (never kept below)
         if (act[l[j]]) {
           if (id >= p.cut_base) {   // deferred record: its child is materialised below
             const uint32_t ani = id - p.cut_base;
@@ -1307,6 +1365,7 @@ __global__ __launch_bounds__(64 * kLogWaves) PB_LOG_ATTR void k_compact_log(DevP
             }
           }
           keep[j] = nid[j] >= 0 || mat[j];
+        }
         }
       }
       CL_CNT(0, i < n);
@@ -1336,8 +1395,10 @@ __global__ __launch_bounds__(64 * kLogWaves) PB_LOG_ATTR void k_compact_log(DevP
           atomicAdd(vcnt(h), 1);
           vh[j] = first ? h : -1;
         }
-        if (keep[j] && !mat[j]) r[j].id = (uint32_t)nid[j] | (l[j] << kIdBits);
-        if (mat[j]) r[j].id = (p.cut_base + nani[j]) | (l[j] << kIdBits);   // (the flush reads it)
+        if constexpr (!kMatOnly) {
+          if (keep[j] && !mat[j]) r[j].id = (uint32_t)nid[j] | (l[j] << kIdBits);
+          if (mat[j]) r[j].id = (p.cut_base + nani[j]) | (l[j] << kIdBits);   // (the flush reads it)
+        }
       }
       // (a count only: one LDS atomic per kept record -- a wave's records mostly
       // belong to distinct trees, lane = tree lane, so they seldom collide)
@@ -1371,7 +1432,7 @@ __global__ __launch_bounds__(64 * kLogWaves) PB_LOG_ATTR void k_compact_log(DevP
         const int lj = (int)l[j];
         int pos = xcnt[lj] + xr[j];
         for (int jj = 0; jj < j; ++jj)
-          for (int v = 0; v < kLogWaves; ++v) pos += xw[jj][v][lj];
+          for (int v = 0; v < LW; ++v) pos += xw[jj][v][lj];
         for (int v = 0; v < w; ++v) pos += xw[j][v][lj];
         if (pos < xroom[lj])   // (beyond: k_update fails the tree, POMCP_E_ARENA)
           p.belief[xdst[lj] + bel_at(xsel[lj], p.Nr, pos)] = make_uint4(tval[lj], r[j].v0, r[j].v1, aux[j]);
@@ -1385,13 +1446,13 @@ __global__ __launch_bounds__(64 * kLogWaves) PB_LOG_ATTR void k_compact_log(DevP
 #pragma unroll
       for (int j = 0; j < R; ++j)
 #pragma unroll
-        for (int v = 0; v < kLogWaves; ++v) xadd += xw[j][v][lane];
+        for (int v = 0; v < LW; ++v) xadd += xw[j][v][lane];
     }
     int mtot = 0;
 #pragma unroll
     for (int j = 0; j < R; ++j)
 #pragma unroll
-      for (int v = 0; v < kLogWaves; ++v) mtot += msum[j][v];
+      for (int v = 0; v < LW; ++v) mtot += msum[j][v];
     CL_MARK(4);
     if (qn + mtot > kQ) {   // (uniform) materialise the queue first
       __syncthreads();   // (the visits table's counts are read: mat_block reuses its LDS)
@@ -1403,16 +1464,18 @@ __global__ __launch_bounds__(64 * kLogWaves) PB_LOG_ATTR void k_compact_log(DevP
     for (int j = 0; j < R; ++j) {
       int pre = 0, tj = 0, mpre = 0, mj = 0;
 #pragma unroll
-      for (int v = 0; v < kLogWaves; ++v) {
+      for (int v = 0; v < LW; ++v) {
         pre += v < w ? ksum[j][v] : 0;
         tj += ksum[j][v];
         mpre += v < w ? msum[j][v] : 0;
         mj += msum[j][v];
       }
-      if (keep[j]) {
+      if (keep[j]) {   // (kMatOnly: every record is kept, so `at` is its own place)
         const uint32_t at = out + (uint32_t)(tot + pre + __popcll(mk[j] & below));
-        wl.store(at, r[j]);
-        if (p.tm) wl.aux[at] = aux[j];
+        if constexpr (!kMatOnly) {
+          wl.store(at, r[j]);
+          if (p.tm) wl.aux[at] = aux[j];
+        }
         if (mat[j]) q_at[mt + mpre + __popcll(mm[j] & below)] = at;
       }
       tot += tj;
@@ -1447,6 +1510,327 @@ __global__ __launch_bounds__(64 * kLogWaves) PB_LOG_ATTR void k_compact_log(DevP
       }
     }
     if (lane == 0) p.wlog[sw] = out;
+  }
+}
+
+// --------------------------------------------- the streaming re-root scan
+// (round 6) The re-root's scan of every search wave's log as two kernels.
+//
+// k_log_filter: the logs are cut into segments of kLfSeg records, processed by
+// a persistent grid that claims chunks of kLfChunk consecutive segments of one
+// log in increasing order (one atomic counter; chunk c is chunk c / waves of
+// wave c % waves), so every segment a segment waits for was claimed earlier by
+// a running workgroup: no deadlock whatever the residency.  A chunk's first
+// segment waits only for the previous chunk of its log, claimed `waves`
+// chunks earlier (long done); the others for the same workgroup's previous
+// segment (done).  Only a chunk publishes (its last segment: the counts
+// through it) and only a chunk's first segment looks back (at the previous
+// chunk's publication); within a chunk the workgroup carries the prefix, and
+// loads each segment's records while the previous one is being stored.  A segment classifies its records as k_compact_log
+// does (kept and relabelled; deferred, kept with its new action node; the new
+// root's, extracted; dropped), publishes its kept and per-tree extracted
+// counts and learns those of the segments before it by decoupled look-back
+// (LfDesc: write-through counts, then one write-through tag; the reader polls
+// the tag), then stores its kept records at their final places and the
+// extracted ones into the tree's next belief, and adds the kept records'
+// visits (an LDS table per segment, one atomic per node).  In place: a segment
+// publishes only after it has loaded all its records, a later segment stores
+// only after reading that publication, and every place lies below the storing
+// segment's own end -- no store lands on a record not yet read.  No workgroup
+// walks a whole log: one search wave's 12.6 M records (the bench) spread over
+// the whole GPU instead of one CU.
+// k_log_mat = k_compact_log<Env, true>: one workgroup per wave over the
+// compacted log (the kept records only, ~1/4): every tree's record count and
+// the deferred children materialised in log order.
+constexpr int kLfWaves = kLfThreads / kWave;
+constexpr int kLfV = 2 * kLfSeg;   // a segment's visits table (entries)
+constexpr int kLfVBits = kLfV == 4096 ? 12 : kLfV == 2048 ? 11 : -1;
+static_assert(kLfVBits > 0, "the visits table takes log2(kLfV) bits");
+constexpr int kLfSpin = 1 << 22;   // look-back polls before giving up (lf_fail[0])
+
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* q) {
+  return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(uint32_t* q, uint32_t v) {
+  __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <class Env>
+__global__ __launch_bounds__(kLfThreads) void k_log_filter(DevParams p, int nwaves) {
+  constexpr int T = kLfThreads, R = kLfRecs, NW = kLfWaves;
+  const int t = (int)threadIdx.x, w = t >> 6, lane = lane_id();
+  __shared__ uint4 si[kWave];               // scan_info of the chunk's 64 trees
+  __shared__ int32_t kc[R][NW];             // kept records per sub-pass and wave
+  __shared__ uint8_t xw[R][NW][kWave];      // extracted records per sub-pass, wave, tree lane
+  __shared__ uint16_t xq[R][NW][kWave];     // ... their exclusive prefix in the segment
+  __shared__ uint32_t xpre[kWave];          // per tree lane: extracted before the segment
+  __shared__ uint32_t kpre;                 // kept records before the segment
+  __shared__ uint32_t vkey[kLfV];           // the visits table: node id | tree lane ...
+  __shared__ int32_t vcnt[kLfV];            // ... and its kept records in this segment
+  __shared__ uint32_t claim;
+  // the log's cmap in LDS for the chunk (as k_compact_log: int16, when the 64
+  // trees' old blocks fit), so a record's classification issues no dependent
+  // global load
+  constexpr int kCm = 12288;
+  __shared__ int16_t cml[kCm];
+  __shared__ int32_t cmo[kWave + 1];
+  __shared__ int32_t cml_ok;
+  const uint32_t A = (uint32_t)p.A;
+  const uint64_t amag = (0x100000000ull + A - 1u) / A;   // x / A by a multiply (k_compact_log)
+  auto divA = [&](uint32_t x) -> uint32_t { return (uint32_t)(((uint64_t)x * amag) >> 32); };
+  const int64_t bstride = blk_stride_lines(p.lines);
+  const uint64_t below = (1ull << lane) - 1ull;
+  const uint32_t ep = p.lf_epoch & 0x3FFFFFFFu;
+  for (int i = t; i < kLfV; i += T) {
+    vkey[i] = 0xFFFFFFFFu;   // (ids < kIdMask: pomcp_create)
+    vcnt[i] = 0;
+  }
+  const int nchunk = (p.lf_nseg + kLfChunk - 1) / kLfChunk;   // chunks per log
+  const int64_t total = (int64_t)nwaves * nchunk;
+  for (;;) {
+    if (t == 0) claim = atomicAdd(p.lf_fail + 1, 1u);   // (lf_fail[1]: the claims)
+    __syncthreads();
+    const int64_t c = claim;
+    __syncthreads();   // (read before the next claim overwrites it)
+    if (c >= total) break;
+    const int sw = (int)(c % nwaves);
+    const int ch = (int)(c / nwaves);
+    const uint32_t n = p.wlog[sw];
+    const int s0 = ch * kLfChunk;
+    int s1 = s0 + kLfChunk < p.lf_nseg ? s0 + kLfChunk : p.lf_nseg;
+    const int sn = (int)((n + (uint32_t)kLfSeg - 1u) / (uint32_t)kLfSeg);   // the log's segments
+    if (s1 > sn) s1 = sn;
+    if (s0 >= s1) continue;   // (no such chunk: none waits for it)
+    const WaveLog wl(p.plog, p.Np, sw, p.tm);
+    if (w == 0) {
+      const int tr = sw * kWave + lane;
+      const uint4 inf = tr < p.B ? p.scan_info[tr] : make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
+      si[lane] = inf;
+      const int nbo = inf.y > 0u ? (int)inf.y - 1 : 0;   // the tree's old blocks
+      int inc = nbo;
+#pragma unroll
+      for (int d2 = 1; d2 < kWave; d2 <<= 1) {
+        const int y = __shfl_up(inc, d2);
+        if (lane >= d2) inc += y;
+      }
+      cmo[lane] = inc - nbo;
+      if (lane == kWave - 1) cmo[kWave] = inc;
+      const bool fit = __ballot(nbo > 32767) == 0ull && __shfl(inc, kWave - 1) <= kCm;
+      if (lane == 0) cml_ok = fit ? 1 : 0;
+    }
+    // the chunk's first segment's records (each later one is loaded during the
+    // previous one, after its dependent loads and before its stores)
+    LogRec rn[R];
+    uint32_t auxn[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const uint32_t i = (uint32_t)s0 * (uint32_t)kLfSeg + (uint32_t)(j * T + t);
+      rn[j] = LogRec{0u, 0u, 0u};
+      auxn[j] = 0u;
+      if (i < n) {
+        rn[j] = wl.load(i);
+        if (p.tm) auxn[j] = wl.aux[i];
+      }
+    }
+    __syncthreads();
+    const bool cml_on = cml_ok != 0;
+    if (cml_on) {   // entry e belongs to the tree lane L with cmo[L] <= e < cmo[L + 1]
+      for (int e = t; e < cmo[kWave]; e += T) {
+        int lo = 0, hi = kWave - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (cmo[mid] <= e) lo = mid;
+          else hi = mid - 1;
+        }
+        cml[e] = (int16_t)p.cmap[(int64_t)(sw * kWave + lo) * p.Nb + (e - cmo[lo])];
+      }
+    }
+    __syncthreads();
+    auto cm = [&](uint32_t ll, int tr, uint32_t b) -> int {
+      return cml_on ? (int)cml[cmo[ll] + (int)b] : p.cmap[(int64_t)tr * p.Nb + (int)b];
+    };
+    for (int sg = s0; sg < s1; ++sg) {
+      const uint32_t base = (uint32_t)sg * (uint32_t)kLfSeg;
+      LogRec r[R];
+      uint32_t aux[R];
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        r[j] = rn[j];
+        aux[j] = auxn[j];
+      }
+      // classification (k_compact_log's rules)
+      bool keep[R], ex[R];
+      uint32_t l[R];
+      int32_t* vis[R];
+      int vh[R];
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        const uint32_t i = base + (uint32_t)(j * T + t);
+        keep[j] = false;
+        ex[j] = false;
+        l[j] = 0u;
+        vis[j] = nullptr;
+        vh[j] = -1;
+        if (i < n) {
+          l[j] = r[j].id >> kIdBits;
+          const uint32_t id = r[j].id & kIdMask;
+          const int tree = sw * kWave + (int)l[j];
+          const uint4 inf = si[l[j]];
+          ex[j] = inf.x == r[j].id;   // a record of the new root (never kept)
+          keep[j] = true;
+          if (inf.y != 0u) {   // re-rooted: only the new root's subtree stays
+            int32_t nid = -1;
+            if (id >= p.cut_base) {   // deferred: kept with its relabelled action node
+              const uint32_t ani = id - p.cut_base, aq = divA(ani);
+              const int nb = cm(l[j], tree, aq);
+              keep[j] = nb >= 0;
+              if (nb >= 0) r[j].id = (p.cut_base + (uint32_t)nb * A + (ani - aq * A)) | (l[j] << kIdBits);
+            } else {
+              if (id >= p.ovf_base) {
+                nid = p.ovf_new[(int64_t)tree * p.H + (id - p.ovf_base)];
+                if (nid >= 0) vis[j] = &p.ovf[(int64_t)tree * p.H + ((uint32_t)nid - p.ovf_base)].visits;
+              } else if (id >= 1u) {
+                const uint32_t ani = (id - 1u) / kSlots, k = (id - 1u) % kSlots;
+                const uint32_t aq = divA(ani), ar = ani - aq * A;
+                const int nb = cm(l[j], tree, aq);
+                if (nb >= 0) {
+                  nid = (int32_t)(((uint32_t)nb * A + ar) * kSlots + k + 1u);
+                  uint4* const bp = reinterpret_cast<uint4*>(p.an + tree_base_lines(tree, p.Nb, p.lines) +
+                                                             (int64_t)nb * bstride);
+                  vis[j] = reinterpret_cast<int32_t*>(bp + part_slot((int)ar, (int)k)) + 3;
+                }
+              }
+              keep[j] = nid >= 0;
+              if (nid >= 0) r[j].id = (uint32_t)nid | (l[j] << kIdBits);
+            }
+          }
+        }
+      }
+      // the next segment's records, in flight from here (issued after this
+      // segment's dependent loads, before its stores: vmcnt retires in order)
+      if (sg + 1 < s1) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+          const uint32_t i = base + (uint32_t)kLfSeg + (uint32_t)(j * T + t);
+          rn[j] = LogRec{0u, 0u, 0u};
+          auxn[j] = 0u;
+          if (i < n) {
+            rn[j] = wl.load(i);
+            if (p.tm) auxn[j] = wl.aux[i];
+          }
+        }
+      }
+      // the kept records' nodes counted in the table (the entering thread adds
+      // them below); ranks: kept records in segment order (sub-pass, wave,
+      // lane), extracted records per tree lane likewise
+      uint64_t mk[R];
+      int xr[R];
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        if (vis[j] != nullptr) {
+          const uint32_t key = r[j].id;   // node id | tree lane (unique in the segment)
+          int h = (int)((key * 0x9E3779B1u) >> (32 - kLfVBits));
+          for (;;) {   // (a segment holds kLfSeg records: a free entry remains)
+            const uint32_t old = atomicCAS(&vkey[h], 0xFFFFFFFFu, key);
+            if (old == 0xFFFFFFFFu) vh[j] = h;
+            if (old == 0xFFFFFFFFu || old == key) break;
+            h = (h + 1) & (kLfV - 1);
+          }
+          atomicAdd(&vcnt[h], 1);
+        }
+        mk[j] = __ballot(keep[j]);
+        if (lane == 0) kc[j][w] = __popcll(mk[j]);
+        xw[j][w][lane] = 0;
+        xr[j] = 0;
+        if (__ballot(ex[j]) != 0ull) {
+          const uint64_t xs = same_lane_mask(l[j], ex[j]);
+          xr[j] = __popcll(xs & below);
+          asm volatile("" ::: "memory");   // (the zero lands first: one wave's LDS ops run in order)
+          if (ex[j] && (xs >> lane) == 1ull) xw[j][w][l[j]] = (uint8_t)__popcll(xs);
+        }
+      }
+      __syncthreads();
+      uint32_t xs_seg = 0u, ks_seg = 0u;   // (wave 0: this segment's counts)
+      if (w == 0) {
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+#pragma unroll
+          for (int v = 0; v < NW; ++v) {
+            xq[j][v][lane] = (uint16_t)xs_seg;
+            xs_seg += xw[j][v][lane];
+            ks_seg += (uint32_t)kc[j][v];
+          }
+        if (sg == s0) {   // the counts before the chunk: the previous chunk's publication
+          uint32_t kp = 0u, xp = 0u;
+          if (ch > 0) {
+            const LfDesc* const e = p.lf_desc + (int64_t)sw * nchunk + (ch - 1);
+            for (int spin = 0;; ++spin) {
+              const uint32_t tg = __builtin_amdgcn_readfirstlane(ld_sc1(&e->tag));
+              if (tg == (ep << 2 | 2u)) break;
+              if (spin >= kLfSpin) {   // (never expected: the previous chunk was claimed first)
+                if (lane == 0) atomicExch(p.lf_fail, 1);
+                break;
+              }
+              __builtin_amdgcn_s_sleep(2);
+            }
+            kp = ld_sc1(&e->kept_inc);
+            xp = ld_sc1(&e->ex_inc[lane]);
+          }
+          xpre[lane] = xp;
+          if (lane == 0) kpre = kp;
+        }
+      }
+      __syncthreads();
+      // stores: kept records at their final places, extracted ones into the
+      // tree's next belief ({root_t + 1, v0, v1, aux}, mcts.py:248-252), the
+      // visits one atomic per node
+      const uint32_t kp = kpre;
+      int pre = 0;
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        int pw = 0, tj = 0;
+#pragma unroll
+        for (int v = 0; v < NW; ++v) {
+          pw += v < w ? kc[j][v] : 0;
+          tj += kc[j][v];
+        }
+        if (keep[j]) {
+          const uint32_t at = kp + (uint32_t)(pre + pw + __popcll(mk[j] & below));
+          wl.store(at, r[j]);
+          if (p.tm) wl.aux[at] = aux[j];
+        }
+        if (ex[j]) {
+          const uint4 inf = si[l[j]];
+          const uint32_t pos = xpre[l[j]] + xq[j][w][l[j]] + (uint32_t)xr[j];
+          const uint32_t room = inf.z & 0x7FFFFFFFu;
+          if (pos < room)   // (beyond: k_update fails the tree, POMCP_E_ARENA)
+            p.belief[(int64_t)(sw * kWave + (int)l[j]) * p.Nr + bel_at((int)(inf.z >> 31), p.Nr, pos)] =
+                make_uint4(inf.w, r[j].v0, r[j].v1, aux[j]);
+        }
+        if (vh[j] >= 0) atomicAdd(vis[j], vcnt[vh[j]]);
+        pre += tj;
+      }
+      __syncthreads();   // (every count read: clear the table, advance the prefix)
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+        if (vh[j] >= 0) {
+          vkey[vh[j]] = 0xFFFFFFFFu;
+          vcnt[vh[j]] = 0;
+        }
+      if (w == 0) {
+        const uint32_t kn = kp + ks_seg, xn = xpre[lane] + xs_seg;
+        xpre[lane] = xn;
+        if (lane == 0) kpre = kn;
+        if (sg + 1 == s1) {   // the chunk's counts through its last segment, for the next chunk
+          LfDesc* const d = p.lf_desc + (int64_t)sw * nchunk + ch;
+          st_sc1(&d->ex_inc[lane], xn);
+          if (lane == 0) st_sc1(&d->kept_inc, kn);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (lane == 0) st_sc1(&d->tag, ep << 2 | 2u);
+        }
+      }
+      __syncthreads();
+    }
   }
 }
 

@@ -24,12 +24,21 @@ class Capacities:
     log_table_size: int
     discount_pow_size: int
 
-    def bytes_per_tree(self, num_actions: int, type_based: bool = False) -> int:
+    def bytes_per_tree(self, num_actions: int, type_based: bool = False,
+                       reroot: bool = False) -> int:
         """HBM of one tree (pomcp_create): (A + 1 [+ 1]) x 128 B per block, 32 B
-        overflow entries, 12 [16] B particle records, the 16 B root belief region."""
+        overflow entries, 12 [16] B particle records, the 16 B root belief region;
+        with ``reroot`` also the re-root's scratch (allocated on the first update
+        that re-roots: the block map / parents, the overflow rebuild, the scan's
+        per-tree record and its share of the look-back records, 528 B per 16,384
+        log records of its search wave)."""
         tm = 1 if type_based else 0
-        return (self.max_blocks * (num_actions + 1 + tm) * 128 + self.overflow_slots * 32
-                + self.max_particles * (12 + 4 * tm) + self.max_belief * 16)
+        b = (self.max_blocks * (num_actions + 1 + tm) * 128 + self.overflow_slots * 32
+             + self.max_particles * (12 + 4 * tm) + self.max_belief * 16)
+        if reroot:
+            b += (8 * self.max_blocks + 36 * self.overflow_slots + 16
+                  + -(-64 * self.max_particles // 16384) * 528 // 64 + 528)
+        return b
 
 
 def _next_pow2(n: int) -> int:
