@@ -423,6 +423,10 @@ static int ensure_compaction_scratch(pomcp_ctx* ctx) {
   d.lf_desc = reinterpret_cast<LfDesc*>(p);
   if ((rc = dev_alloc(ctx, &p, 2 * sizeof(uint32_t))) != POMCP_OK) return rc;
   d.lf_fail = reinterpret_cast<uint32_t*>(p);
+  if ((rc = dev_alloc(ctx, &p, sizeof(int16_t) * (size_t)waves * kCm16)) != POMCP_OK) return rc;
+  d.cm16 = reinterpret_cast<int16_t*>(p);
+  if ((rc = dev_alloc(ctx, &p, sizeof(int32_t) * (size_t)waves * kCm16Off)) != POMCP_OK) return rc;
+  d.cm16_off = reinterpret_cast<int32_t*>(p);
   HIP_TRY(ctx, hipMemsetAsync(d.lf_desc, 0, nd, ctx->stream));
   ctx->lf_epoch = 0;
   const char* ls = std::getenv("POMCP_LOG_SCAN");
@@ -479,6 +483,8 @@ int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_key
       }
       ctx->dp.lf_epoch = ctx->lf_epoch;
       HIP_TRY(ctx, hipMemsetAsync(ctx->dp.lf_fail, 0, 2 * sizeof(uint32_t), ctx->stream));
+      hipLaunchKernelGGL(k_pack_cmap, dim3((unsigned)search_waves(B)), dim3(256), 0, ctx->stream, ctx->dp);
+      HIP_TRY(ctx, hipGetLastError());
       PB_ENV_LAUNCH(ctx, k_log_filter, dim3((unsigned)ctx->lf_grid), dim3(kLfThreads), ctx->dp,
                     search_waves(B));
       HIP_TRY(ctx, hipGetLastError());

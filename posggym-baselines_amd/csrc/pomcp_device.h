@@ -270,7 +270,11 @@ struct DevParams {
   // re-rooted), end of the next belief << 31 | its room, t of the new root}
   // (k_compact), the look-back records of every wave's log segments
   uint4* scan_info;     // [B]
-  LfDesc* lf_desc;      // [waves][lf_nseg]
+  LfDesc* lf_desc;      // [waves][chunks per log]
+  // every log's block map packed for the filter (k_pack_cmap): per wave its 64
+  // trees' cmap entries as int16, back to back, and their offsets (+ a fit flag)
+  int16_t* cm16;        // [waves][kCm16]
+  int32_t* cm16_off;    // [waves][kCm16Off]: 65 offsets, fit flag
   int32_t lf_nseg;      // segments per wave log (its capacity / kLfSeg)
   uint32_t lf_epoch;    // this re-root's tag epoch (1, 2, ...; older tags are stale)
   uint32_t* lf_fail;    // [2] a look-back wait that gave up (never expected: POMCP_E_HIP);

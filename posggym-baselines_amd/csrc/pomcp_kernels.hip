@@ -435,7 +435,16 @@ constexpr int kMatWaves = PB_MAT_WAVES;
 constexpr int kLfThreads = 512;
 constexpr int kLfRecs = 4;
 constexpr int kLfSeg = kLfThreads * kLfRecs;
-constexpr int kLfChunk = 8;   // consecutive segments of one log per claim (and look-back record)
+// consecutive segments of one log per claim (and look-back record); round 6
+// A/B 8 -> 32: update 161 -> 149 ms (profiles/r6i_lf_chunk_ab.txt)
+#ifndef PB_LF_CHUNK   // A/B builds only
+#define PB_LF_CHUNK 32
+#endif
+constexpr int kLfChunk = PB_LF_CHUNK;
+// the packed block maps (DevParams::cm16): entries per log (the bench: 64 x
+// ~171 old blocks) and the offsets record
+constexpr int kCm16 = 12288;
+constexpr int kCm16Off = kWave + 2;
 
 // The lanes whose 6-bit key equals this lane's, among the active ones (a
 // match-any on the tree lane of a log record: 6 ballots).
@@ -958,7 +967,7 @@ __global__ __launch_bounds__(64 * (kMatOnly ? kMatWaves : kLogWaves)) PB_LOG_ATT
   // staged in LDS when their old blocks fit (the bench: ~64 x 171): the
   // classification of a record then issues no global load, so its wait never
   // includes the next pass's prefetched records (vmcnt completes in order)
-  constexpr int kCmapLds = 16384;
+  constexpr int kCmapLds = kMatOnly ? 8 : 16384;   // (kMatOnly classifies nothing)
   __shared__ int16_t cml[kCmapLds];
   __shared__ int32_t cmo[kWave + 1];   // per tree lane: its first entry in cml
   __shared__ int32_t cml_ok;
@@ -1251,6 +1260,15 @@ __global__ __launch_bounds__(64 * (kMatOnly ? kMatWaves : kLogWaves)) PB_LOG_ATT
   auto flush = [&](int qn) {
     wg_fence();        // the queued records were stored by this workgroup: they land
     __syncthreads();   // before the (L1-bypassing) reads below
+    // each chunk's records are read during the previous chunk (their wait is
+    // then the previous chunk's slot loads' own)
+    uint32_t n_rid = 0u, n_v0 = 0u, n_v1 = 0u;
+    if (t < qn) {
+      const uint32_t at0 = q_at[t];
+      n_rid = ld_agent_u32(wl.id + at0);
+      n_v0 = ld_agent_u32(wl.v0 + at0);
+      n_v1 = ld_agent_u32(wl.v1 + at0);
+    }
     for (int c = 0; c < qn; c += T) {
       const int e = c + t;
       const bool m = e < qn;
@@ -1259,12 +1277,17 @@ __global__ __launch_bounds__(64 * (kMatOnly ? kMatWaves : kLogWaves)) PB_LOG_ATT
       int dn = 0;
       if (m) {   // the child's observation key and absorbing flag from the record's state
         at = q_at[e];
-        const uint32_t rid = ld_agent_u32(wl.id + at);
-        const uint32_t v0 = ld_agent_u32(wl.v0 + at), v1 = ld_agent_u32(wl.v1 + at);
+        const uint32_t rid = n_rid, v0 = n_v0, v1 = n_v1;
         ll = rid >> kIdBits;
         nani = (rid & kIdMask) - p.cut_base;
         ok = Env::obs_key(sm, p.ego, v0, v1);
         dn = Env::done_of(p.ego, v0, v1);
+      }
+      if (e + T < qn) {
+        const uint32_t at1 = q_at[e + T];
+        n_rid = ld_agent_u32(wl.id + at1);
+        n_v0 = ld_agent_u32(wl.v0 + at1);
+        n_v1 = ld_agent_u32(wl.v1 + at1);
       }
       int32_t nid = -1;
       bool keep = true;
@@ -1514,6 +1537,43 @@ __global__ __launch_bounds__(64 * (kMatOnly ? kMatWaves : kLogWaves)) PB_LOG_ATT
 }
 
 // --------------------------------------------- the streaming re-root scan
+// k_pack_cmap: one workgroup per search wave packs its 64 trees' block maps
+// (k_compact's cmap, entries 0 .. old blocks - 1) as int16 back to back, with
+// the offsets and a fit flag, so that every k_log_filter chunk stages them in
+// LDS by one contiguous copy
+__global__ __launch_bounds__(256) void k_pack_cmap(DevParams p) {
+  const int sw = blockIdx.x;
+  const int t = (int)threadIdx.x, w = t >> 6, lane = lane_id();
+  __shared__ int32_t off[kWave + 1];
+  __shared__ int32_t ok;
+  if (w == 0) {
+    const int tr = sw * kWave + lane;
+    const uint32_t c = tr < p.B ? p.scan_info[tr].y : 0u;   // 1 + old blocks (0: not re-rooted)
+    const int nbo = c > 0u ? (int)c - 1 : 0;
+    int inc = nbo;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const int y = __shfl_up(inc, d);
+      if (lane >= d) inc += y;
+    }
+    off[lane] = inc - nbo;
+    if (lane == kWave - 1) off[kWave] = inc;
+    const bool fit = __ballot(nbo > 32767) == 0ull && __shfl(inc, kWave - 1) <= kCm16;
+    if (lane == 0) ok = fit ? 1 : 0;
+  }
+  __syncthreads();
+  int32_t* const o = p.cm16_off + (int64_t)sw * kCm16Off;
+  if (t <= kWave) o[t] = off[t];
+  if (t == kWave + 1) o[t] = ok;
+  if (!ok) return;
+  int16_t* const dst = p.cm16 + (int64_t)sw * kCm16;
+  for (int l = w; l < kWave; l += 4) {   // wave w: tree lanes w, w + 4, ...
+    const int32_t* const src = p.cmap + (int64_t)(sw * kWave + l) * p.Nb;
+    const int b0 = off[l], nb = off[l + 1] - b0;
+    for (int b = lane; b < nb; b += kWave) dst[b0 + b] = (int16_t)src[b];
+  }
+}
+
 // (round 6) The re-root's scan of every search wave's log as two kernels.
 //
 // k_log_filter: the logs are cut into segments of kLfSeg records, processed by
@@ -1571,10 +1631,9 @@ __global__ __launch_bounds__(kLfThreads) void k_log_filter(DevParams p, int nwav
   // the log's cmap in LDS for the chunk (as k_compact_log: int16, when the 64
   // trees' old blocks fit), so a record's classification issues no dependent
   // global load
-  constexpr int kCm = 12288;
-  __shared__ int16_t cml[kCm];
-  __shared__ int32_t cmo[kWave + 1];
-  __shared__ int32_t cml_ok;
+  constexpr int kCm = kCm16;
+  __shared__ __attribute__((aligned(16))) int16_t cml[kCm];
+  __shared__ int32_t cmo[kCm16Off];   // offsets per tree lane, [kWave + 1]: the fit flag
   const uint32_t A = (uint32_t)p.A;
   const uint64_t amag = (0x100000000ull + A - 1u) / A;   // x / A by a multiply (k_compact_log)
   auto divA = [&](uint32_t x) -> uint32_t { return (uint32_t)(((uint64_t)x * amag) >> 32); };
@@ -1604,20 +1663,9 @@ __global__ __launch_bounds__(kLfThreads) void k_log_filter(DevParams p, int nwav
     const WaveLog wl(p.plog, p.Np, sw, p.tm);
     if (w == 0) {
       const int tr = sw * kWave + lane;
-      const uint4 inf = tr < p.B ? p.scan_info[tr] : make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
-      si[lane] = inf;
-      const int nbo = inf.y > 0u ? (int)inf.y - 1 : 0;   // the tree's old blocks
-      int inc = nbo;
-#pragma unroll
-      for (int d2 = 1; d2 < kWave; d2 <<= 1) {
-        const int y = __shfl_up(inc, d2);
-        if (lane >= d2) inc += y;
-      }
-      cmo[lane] = inc - nbo;
-      if (lane == kWave - 1) cmo[kWave] = inc;
-      const bool fit = __ballot(nbo > 32767) == 0ull && __shfl(inc, kWave - 1) <= kCm;
-      if (lane == 0) cml_ok = fit ? 1 : 0;
+      si[lane] = tr < p.B ? p.scan_info[tr] : make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
     }
+    if (t < kCm16Off) cmo[t] = p.cm16_off[(int64_t)sw * kCm16Off + t];   // (k_pack_cmap)
     // the chunk's first segment's records (each later one is loaded during the
     // previous one, after its dependent loads and before its stores)
     LogRec rn[R];
@@ -1633,16 +1681,21 @@ __global__ __launch_bounds__(kLfThreads) void k_log_filter(DevParams p, int nwav
       }
     }
     __syncthreads();
-    const bool cml_on = cml_ok != 0;
-    if (cml_on) {   // entry e belongs to the tree lane L with cmo[L] <= e < cmo[L + 1]
-      for (int e = t; e < cmo[kWave]; e += T) {
-        int lo = 0, hi = kWave - 1;
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (cmo[mid] <= e) lo = mid;
-          else hi = mid - 1;
-        }
-        cml[e] = (int16_t)p.cmap[(int64_t)(sw * kWave + lo) * p.Nb + (e - cmo[lo])];
+    const bool cml_on = cmo[kWave + 1] != 0;
+    if (cml_on) {   // one contiguous copy, 8 entries per 16 B load, all loads issued first
+      constexpr int kPer = (kCm / 8 + T - 1) / T;
+      const int nq = (cmo[kWave] + 7) >> 3;
+      const uint4* const src = reinterpret_cast<const uint4*>(p.cm16 + (int64_t)sw * kCm);
+      uint4 v[kPer];
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) {
+        const int e = q * T + t;
+        v[q] = e < nq ? src[e] : make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) {
+        const int e = q * T + t;
+        if (e < nq) reinterpret_cast<uint4*>(cml)[e] = v[q];
       }
     }
     __syncthreads();

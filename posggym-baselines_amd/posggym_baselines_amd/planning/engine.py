@@ -30,14 +30,15 @@ class Capacities:
         overflow entries, 12 [16] B particle records, the 16 B root belief region;
         with ``reroot`` also the re-root's scratch (allocated on the first update
         that re-roots: the block map / parents, the overflow rebuild, the scan's
-        per-tree record and its share of the look-back records, 528 B per 16,384
-        log records of its search wave)."""
+        per-tree record, its share of the look-back records -- 528 B per 16,384
+        log records of its search wave, an upper bound -- and of its wave's
+        packed block map, 24,840 B)."""
         tm = 1 if type_based else 0
         b = (self.max_blocks * (num_actions + 1 + tm) * 128 + self.overflow_slots * 32
              + self.max_particles * (12 + 4 * tm) + self.max_belief * 16)
         if reroot:
             b += (8 * self.max_blocks + 36 * self.overflow_slots + 16
-                  + -(-64 * self.max_particles // 16384) * 528 // 64 + 528)
+                  + -(-64 * self.max_particles // 16384) * 528 // 64 + 528 + 389)
         return b
 
 
