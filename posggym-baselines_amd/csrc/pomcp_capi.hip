@@ -66,6 +66,7 @@ struct pomcp_ctx {
   // materialising pass) unless POMCP_LOG_SCAN=legacy (one workgroup per log,
   // k_compact_log: A/B and fallback); the look-back tags' epoch
   bool log_scan_legacy = false;
+  bool lf_packed_cmap = true;   // POMCP_LF_PACKED_CMAP=off: tests only
   uint32_t lf_epoch = 0;
   int lf_grid = 0;
 };
@@ -431,6 +432,10 @@ static int ensure_compaction_scratch(pomcp_ctx* ctx) {
   ctx->lf_epoch = 0;
   const char* ls = std::getenv("POMCP_LOG_SCAN");
   ctx->log_scan_legacy = ls != nullptr && std::string(ls) == "legacy";
+  // tests only: the filter classifies from the global block maps (the path of
+  // logs whose 64 trees' maps do not fit the packed table)
+  const char* pk = std::getenv("POMCP_LF_PACKED_CMAP");
+  ctx->lf_packed_cmap = !(pk != nullptr && std::string(pk) == "off");
   // the persistent grid: as many workgroups as are resident at once
   int per_cu = 0, ncu = 0;
   HIP_TRY(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -483,7 +488,8 @@ int pomcp_update(pomcp_ctx* ctx, const int32_t* actions, const uint64_t* obs_key
       }
       ctx->dp.lf_epoch = ctx->lf_epoch;
       HIP_TRY(ctx, hipMemsetAsync(ctx->dp.lf_fail, 0, 2 * sizeof(uint32_t), ctx->stream));
-      hipLaunchKernelGGL(k_pack_cmap, dim3((unsigned)search_waves(B)), dim3(256), 0, ctx->stream, ctx->dp);
+      hipLaunchKernelGGL(k_pack_cmap, dim3((unsigned)search_waves(B)), dim3(256), 0, ctx->stream, ctx->dp,
+                         ctx->lf_packed_cmap ? 1 : 0);
       HIP_TRY(ctx, hipGetLastError());
       PB_ENV_LAUNCH(ctx, k_log_filter, dim3((unsigned)ctx->lf_grid), dim3(kLfThreads), ctx->dp,
                     search_waves(B));

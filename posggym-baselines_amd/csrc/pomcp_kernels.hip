@@ -1540,8 +1540,9 @@ __global__ __launch_bounds__(64 * (kMatOnly ? kMatWaves : kLogWaves)) PB_LOG_ATT
 // k_pack_cmap: one workgroup per search wave packs its 64 trees' block maps
 // (k_compact's cmap, entries 0 .. old blocks - 1) as int16 back to back, with
 // the offsets and a fit flag, so that every k_log_filter chunk stages them in
-// LDS by one contiguous copy
-__global__ __launch_bounds__(256) void k_pack_cmap(DevParams p) {
+// LDS by one contiguous copy (when they do not fit, the filter reads the
+// global cmap)
+__global__ __launch_bounds__(256) void k_pack_cmap(DevParams p, int allow) {   // allow 0: tests only
   const int sw = blockIdx.x;
   const int t = (int)threadIdx.x, w = t >> 6, lane = lane_id();
   __shared__ int32_t off[kWave + 1];
@@ -1559,7 +1560,7 @@ __global__ __launch_bounds__(256) void k_pack_cmap(DevParams p) {
     off[lane] = inc - nbo;
     if (lane == kWave - 1) off[kWave] = inc;
     const bool fit = __ballot(nbo > 32767) == 0ull && __shfl(inc, kWave - 1) <= kCm16;
-    if (lane == 0) ok = fit ? 1 : 0;
+    if (lane == 0) ok = fit && allow ? 1 : 0;
   }
   __syncthreads();
   int32_t* const o = p.cm16_off + (int64_t)sw * kCm16Off;

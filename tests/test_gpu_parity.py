@@ -427,11 +427,20 @@ def test_wall_clock_search_mode():
     planner.close()
 
 
-def test_subtree_compaction_forced_small_arena():
+@pytest.mark.parametrize("scan", ["stream", "stream_global_cmap", "legacy"])
+def test_subtree_compaction_forced_small_arena(scan, monkeypatch):
     """Arenas sized for ~2 searches carry 8-step episodes: every update compacts
     the tree to the new root's subtree (k_compact / k_compact_log: blocks moved,
     overflow map rebuilt, particle log filtered and relabelled) and every tree
-    stays bit-exact with the oracle, whose tree is never compacted."""
+    stays bit-exact with the oracle, whose tree is never compacted.  In each
+    re-root scan: the streaming one (k_log_filter + the materialising pass), the
+    same with the filter classifying from the global block maps (the path of
+    logs whose maps do not fit the packed table), and the one-workgroup-per-log
+    k_compact_log (POMCP_LOG_SCAN=legacy)."""
+    if scan == "legacy":
+        monkeypatch.setenv("POMCP_LOG_SCAN", "legacy")
+    if scan == "stream_global_cmap":
+        monkeypatch.setenv("POMCP_LF_PACKED_CMAP", "off")
     from posggym_baselines_amd.planning.engine import plan_capacities
     from posggym_baselines_amd.planning import MCTSConfig
     from gpu_util import batched_episodes
