@@ -1083,7 +1083,10 @@ __global__ __launch_bounds__(64 * (kMatOnly ? kMatWaves : kLogWaves)) PB_LOG_ATT
       int32_t* vis = nullptr;
       uint32_t* flagw = nullptr;   // the word holding the child's absorbing flag ...
       uint32_t fbit = 0u;          // ... and its bit
+      int curf = 2;                // the flag as this thread last saw it (2: not known)
       bool need_ovf = false;
+      bool ovf_look = false;   // (diagnostics counter: looked up in the overflow map)
+      (void)ovf_look;
       if (mat) {   // inline slots, filled in order; concurrent inserts by CAS on the key
         const uint32_t nq = divA(nani);
         uint4* const sl0 = reinterpret_cast<uint4*>(p.an + tree_base_lines(tree, p.Nb, p.lines) +
@@ -1091,27 +1094,57 @@ __global__ __launch_bounds__(64 * (kMatOnly ? kMatWaves : kLogWaves)) PB_LOG_ATT
                            part_slot((int)(nani - nq * A), 0);
         const uint64_t nk = okey | kValidBit | ((uint64_t)done << 63);
         uint64_t kk[kSlots];
+#ifndef PB_MAT_EAGER_SLOTS
+        // slots 0-1 first, the others only when both hold other observations
+        // (valid slots are a prefix: an insert takes the first slot it saw
+        // empty); an unread slot is taken as empty and the CAS below checks it.
+        // Round 6 A/B: update 149 -> 137 ms at 65,536 PursuitEvasion roots (the
+        // pass is bound by its slot-line requests; 1 / 1-1 / 1-2 / 2-1 tiers
+        // within 1 ms, profiles/r6q_lazy_slots_ab.txt)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          kk[q] = q < p.islots ? ld_agent_u64(reinterpret_cast<const uint64_t*>(sl0 + q)) : kValidBit;
+        const bool more = ((kk[0] & kk[1]) & kValidBit) != 0ull && (kk[0] & kObsMask) != okey &&
+                          (kk[1] & kObsMask) != okey;
+#pragma unroll
+        for (int q = 2; q < kSlots; ++q)
+          kk[q] = q < p.islots ? (more ? ld_agent_u64(reinterpret_cast<const uint64_t*>(sl0 + q)) : 0ull)
+                               : kValidBit;
+#else   // A/B builds only: every slot read
 #pragma unroll
         for (int q = 0; q < kSlots; ++q)
           kk[q] = q < p.islots ? ld_agent_u64(reinterpret_cast<const uint64_t*>(sl0 + q)) : kValidBit;
+#endif
         int ks = -1;
 #pragma unroll
         for (int q = kSlots - 1; q >= 0; --q)
-          if ((kk[q] & kValidBit) != 0ull && (kk[q] & kObsMask) == okey) ks = q;
+          if ((kk[q] & kValidBit) != 0ull && (kk[q] & kObsMask) == okey) {
+            ks = q;
+            curf = (int)(kk[q] >> 63);
+          }
         for (int q = 0; ks < 0 && q < p.islots; ++q) {
           uint64_t exp = 0ull;
 #pragma unroll
           for (int e = 0; e < kSlots; ++e) exp = e == q ? kk[e] : exp;   // (selects: registers)
           if ((exp & kValidBit) != 0ull) continue;   // taken by another observation
-          const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long*>(sl0 + q),
-                                         (unsigned long long)exp, (unsigned long long)nk);
+          uint64_t old = atomicCAS(reinterpret_cast<unsigned long long*>(sl0 + q),
+                                   (unsigned long long)exp, (unsigned long long)nk);
+#ifndef PB_MAT_EAGER_SLOTS
+          if (old != exp && (old & kValidBit) == 0ull) {   // an unread empty slot's word was not 0
+            exp = old;
+            old = atomicCAS(reinterpret_cast<unsigned long long*>(sl0 + q), (unsigned long long)exp,
+                            (unsigned long long)nk);
+          }
+#endif
           if (old == exp) {   // inserted: a leaf child (no block), visits counted below
             __hip_atomic_store(reinterpret_cast<int32_t*>(sl0 + q) + 2, -1, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
             atomicAdd(&made[l], 1);
             ks = q;
+            curf = done;
           } else if ((old & kValidBit) != 0ull && (old & kObsMask) == okey) {
             ks = q;   // another thread of this pass inserted it
+            curf = (int)(old >> 63);
           }
         }
         if (ks >= 0) {
@@ -1120,6 +1153,7 @@ __global__ __launch_bounds__(64 * (kMatOnly ? kMatWaves : kLogWaves)) PB_LOG_ATT
           flagw = reinterpret_cast<uint32_t*>(sl0 + ks) + 1;
           fbit = 1u << 31;
         } else {
+          ovf_look = true;
           // an overflow child made by an earlier pass (or by the search): every
           // thread looks its own up (read-only probe in insertion order: a bucket
           // holding the key, else the first bucket with a free entry ends it)
@@ -1155,6 +1189,7 @@ __global__ __launch_bounds__(64 * (kMatOnly ? kMatWaves : kLogWaves)) PB_LOG_ATT
       // overflow map: the pass's records of NEW overflow children (and of the
       // ones inserted earlier in the same pass), in thread (= log) order, one at
       // a time, by wave 0 (its 16 lanes probe a bucket)
+      CL_CNT(5, ovf_look);
       CL_MARK(1);
       CL_CNT(2, need_ovf);
       int novf = 0;
@@ -1245,8 +1280,14 @@ __global__ __launch_bounds__(64 * (kMatOnly ? kMatWaves : kLogWaves)) PB_LOG_ATT
       }
       __syncthreads();
       if (flagw != nullptr && hl[h] == t) {
-        if (done) atomicOr(flagw, fbit);
-        else atomicAnd(flagw, ~fbit);
+        // an inline child's flag as the last arrival saw it is current (earlier
+        // chunks' atomics landed before its read, and only the last arrival of
+        // this chunk writes it): unchanged, no atomic
+#ifdef PB_MAT_ALWAYS_FLAG   // A/B builds only
+        curf = 2;
+#endif
+        if (done && curf != 1) atomicOr(flagw, fbit);
+        else if (!done && curf != 0) atomicAnd(flagw, ~fbit);
         atomicAdd(vis, hc[h]);
       }
       wg_fence();   // the chunk's inserts, flags and visits land before the next chunk's
@@ -1518,7 +1559,7 @@ __global__ __launch_bounds__(64 * (kMatOnly ? kMatWaves : kLogWaves)) PB_LOG_ATT
 #ifdef PB_CLOG_TIMING
   if (t == 0 && p.timing != nullptr) {
     for (int q = 0; q < 5; ++q) p.timing[sw * 16 + q] = clt[q];
-    for (int q = 0; q < 5; ++q) p.timing[sw * 16 + 8 + q] = clc[q];
+    for (int q = 0; q < 6; ++q) p.timing[sw * 16 + 8 + q] = clc[q];
   }
 #endif
   if (w == 0) {

@@ -20,7 +20,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "posggym-baselines_amd")]
 SECTIONS = ["classify (record, cmap)", "mat: slots + ovf lookup", "mat: serial ovf inserts",
             "mat: flags + fence", "visits, rank, store"]
-COUNTERS = ["records", "mat records", "serial ovf records", "flag records", "kept records"]
+COUNTERS = ["records", "mat records", "serial ovf records", "flag records", "kept records",
+            "overflow-map lookups"]
 
 
 def main():
